@@ -1,0 +1,143 @@
+/*
+ * rss_toeplitz.h -- C ABI of the MI355X (gfx950) RSS Toeplitz hashing engine.
+ *
+ * This is the drop-in boundary for the reference's hot path.  The reference
+ * (noamsto/rss_simulator_nvidia v0.0.2) is pure Python and has no FFI, so each
+ * entry point below names the Python function whose job it takes over; the
+ * Python mirror in rss_simulator_nvidia_amd/ binds them through ctypes
+ * (rss_simulator_nvidia_amd/_native.py) and INTEGRATION.md shows the ctypes stub
+ * a reference maintainer would add.
+ *
+ * Conventions
+ *   - plain C types only; buffers are caller-owned; nothing here allocates on
+ *     behalf of the caller except an rss_ctx (which owns its device scratch);
+ *   - every function returns RSS_OK (0) or a negative errno-style code and never
+ *     aborts; rss_last_error() returns a thread-local message for the last
+ *     failure on the calling thread;
+ *   - "device" entry points take device pointers and a hipStream_t passed as
+ *     void* (NULL = the legacy default stream) and are stream-ordered: they
+ *     enqueue work and return without synchronising;
+ *   - all arithmetic is integer and bit-exact to the reference.
+ */
+#ifndef RSS_TOEPLITZ_H
+#define RSS_TOEPLITZ_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RSS_ABI_VERSION 1
+
+/* status codes (negative errno values) */
+#define RSS_OK 0
+#define RSS_EIO (-5)      /* HIP runtime / device failure                         */
+#define RSS_ENOMEM (-12)  /* device or pinned allocation failed                   */
+#define RSS_EINVAL (-22)  /* bad argument (NULL, bad key length, zero htable ...) */
+#define RSS_ENODEV (-19)  /* no usable gfx950 device                              */
+
+/*
+ * One IPv4 4-tuple, packed to 12 bytes, 4-byte aligned.  The three host-order
+ * words are exactly the 96-bit big-endian Toeplitz input of
+ * rss_simulator/toeplitz.py:113-142 (__prepare_input_bytes): src_ip, dst_ip,
+ * then (src_port & 0xFFFF) << 16 | (dst_port & 0xFFFF).  Ports are masked to 16
+ * bits by the caller, matching toeplitz.py:138-141.
+ */
+typedef struct rss_tuple4 {
+    uint32_t sip;
+    uint32_t dip;
+    uint32_t ports;
+} rss_tuple4;
+
+#define RSS_KEY_MIN_BYTES 4
+#define RSS_KEY_MAX_BYTES 52
+#define RSS_INPUT_BITS 96
+#define RSS_NIBBLES (RSS_INPUT_BITS / 4)
+
+/*
+ * Prepared hash key.  window[i] is the 32-bit window the reference XORs in
+ * for input bit i (toeplitz.py:65-68 with __key_left_most_32bits :71-81 after i
+ * rotations by __shift_key :83-98), i.e. key bits [i, i+32) MSB-first.
+ * nibble_lut[t][v] is the XOR of the windows selected by the 4-bit value v at
+ * input nibble t (input bits 4t..4t+3), the table the device kernel replicates
+ * into LDS.  For len >= 16 only key bytes 0..15 influence any hash.
+ */
+typedef struct rss_key {
+    uint32_t len;                          /* key length in bytes (>= 4)     */
+    uint8_t bytes[RSS_KEY_MAX_BYTES];      /* first min(len, 52) key bytes   */
+    uint32_t window[RSS_INPUT_BITS];
+    uint32_t nibble_lut[RSS_NIBBLES][16];
+} rss_key;
+
+/*
+ * Replaces HashKey.__from_str's conversion result -> Toeplitz(key)
+ * (rss_simulator/hash_key.py:12-32, rss_simulator/toeplitz.py:8-15).  `key`
+ * holds `len` raw bytes, len >= 4.  The CLI's key regex admits only 40 or 52
+ * (hash_key.py:25-28), but Toeplitz(list) accepts any list of >= 4 bytes, and a
+ * key shorter than 16 bytes wraps during the rotation -- reproduced here.  Text
+ * parsing stays in the caller.
+ */
+int rss_key_prepare(const uint8_t* key, size_t len, rss_key* out);
+
+/* flags for rss_hash_device / rss_hash_host */
+#define RSS_FLAG_ACCUMULATE 1u  /* add into counts instead of overwriting them */
+
+/*
+ * Device-resident hot path.  Replaces, for n tuples at once:
+ *   Simulator.calc_hash          rss_simulator/simulator.py:74-92
+ *     -> Toeplitz.compute_hash    rss_simulator/toeplitz.py:46-69
+ *   Simulator.calc_queue_number  rss_simulator/simulator.py:94-98
+ *     (queue = hash % htable % nqueues)
+ *   the value_counts of Simulator.write_statistics  simulator.py:107-113
+ *     (counts[q] = number of tuples with queue q, for q < nqueues).
+ * d_tuples: n packed tuples in device memory.  d_hash, d_queue: n uint32 each
+ * or NULL to skip that output.  d_counts: nqueues uint64 or NULL; overwritten
+ * unless RSS_FLAG_ACCUMULATE.  htable >= 1, nqueues >= 1 (positive_int.py:27).
+ * Launched on `stream` (hipStream_t) on the calling thread's current device.
+ */
+int rss_hash_device(const rss_key* key, const rss_tuple4* d_tuples, size_t n,
+                    uint32_t htable, uint32_t nqueues, uint32_t* d_hash,
+                    uint32_t* d_queue, uint64_t* d_counts, uint32_t flags,
+                    void* stream);
+
+/*
+ * Synthetic input: tuple i (i = first_index .. first_index+n-1) is
+ *   r0 = mix64(seed + 2i), r1 = mix64(seed + 2i + 1)       (mod 2^64)
+ *   sip = r0 >> 32, dip = (uint32)r0, ports = (uint32)r1
+ * with mix64 the splitmix64 finaliser (gamma 0x9E3779B97F4A7C15).  The oracle
+ * restates the same generator, so any shard can be rebuilt on the host.
+ */
+int rss_generate_tuples(uint64_t seed, uint64_t first_index, size_t n,
+                        rss_tuple4* d_tuples, void* stream);
+
+/* Host-memory convenience path (CSV in -> CSV out): owns device buffers. */
+typedef struct rss_ctx rss_ctx;
+
+int rss_ctx_create(int device, rss_ctx** out);
+void rss_ctx_destroy(rss_ctx* ctx);
+
+/*
+ * Same contract as rss_hash_device but on host buffers: chunked
+ * H2D -> kernel -> D2H through pinned staging, synchronous on return.
+ * h_hash / h_queue / h_counts may be NULL.
+ */
+int rss_hash_host(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples,
+                  size_t n, uint32_t htable, uint32_t nqueues, uint32_t* h_hash,
+                  uint32_t* h_queue, uint64_t* h_counts, uint32_t flags);
+
+/* Number of visible gfx950 devices (0 when there is no GPU). */
+int rss_device_count(int* out);
+
+/* Thread-local message describing the last failure on this thread ("" if none). */
+const char* rss_last_error(void);
+
+/* RSS_ABI_VERSION of the loaded library. */
+int rss_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RSS_TOEPLITZ_H */

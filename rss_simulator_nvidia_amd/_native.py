@@ -1,0 +1,183 @@
+"""ctypes binding of the C ABI in ``include/rss_toeplitz.h``.
+
+The library (``librss_toeplitz.so``, built in-tree by ``__graft_entry__.build()`` /
+``make -C rss_simulator_nvidia_amd/csrc``) is the only compute path of this
+package: there is no CPU fallback.  Every entry point raises
+:class:`~rss_simulator_nvidia_amd.exceptions.NativeLibraryError` when the library
+is missing and :class:`~rss_simulator_nvidia_amd.exceptions.DeviceError` when the
+HIP runtime reports a failure (including "no gfx950 device").
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+from rss_simulator_nvidia_amd.exceptions import DeviceError, NativeLibraryError
+
+LIB_NAME = "librss_toeplitz.so"
+LIB_PATH = os.environ.get(
+    "RSS_TOEPLITZ_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME))
+
+ABI_VERSION = 1
+FLAG_ACCUMULATE = 1
+KEY_MIN_BYTES = 4
+
+# Every symbol include/rss_toeplitz.h declares (tests/test_native_abi.py checks them).
+EXPORTED_SYMBOLS = (
+    "rss_key_prepare", "rss_hash_device", "rss_generate_tuples", "rss_ctx_create",
+    "rss_ctx_destroy", "rss_hash_host", "rss_device_count", "rss_last_error",
+    "rss_abi_version",
+)
+
+
+class RssTuple4(ctypes.Structure):
+    """``rss_tuple4``: packed 12-byte IPv4 4-tuple."""
+    _fields_ = [("sip", ctypes.c_uint32), ("dip", ctypes.c_uint32), ("ports", ctypes.c_uint32)]
+
+
+class RssKey(ctypes.Structure):
+    """``rss_key``: prepared key (windows + nibble tables)."""
+    _fields_ = [
+        ("len", ctypes.c_uint32),
+        ("bytes", ctypes.c_uint8 * 52),
+        ("window", ctypes.c_uint32 * 96),
+        ("nibble_lut", (ctypes.c_uint32 * 16) * 24),
+    ]
+
+
+TUPLE_DTYPE = np.dtype([("sip", "<u4"), ("dip", "<u4"), ("ports", "<u4")])
+assert TUPLE_DTYPE.itemsize == ctypes.sizeof(RssTuple4) == 12
+
+_lock = threading.Lock()
+_lib = None
+
+
+def _bind(lib):
+    vp, sz, u32, u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint64
+    key_p = ctypes.POINTER(RssKey)
+    sigs = {
+        "rss_abi_version": ([], ctypes.c_int),
+        "rss_last_error": ([], ctypes.c_char_p),
+        "rss_key_prepare": ([ctypes.POINTER(ctypes.c_uint8), sz, key_p], ctypes.c_int),
+        "rss_device_count": ([ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+        "rss_hash_device": ([key_p, vp, sz, u32, u32, vp, vp, vp, u32, vp], ctypes.c_int),
+        "rss_generate_tuples": ([u64, u64, sz, vp, vp], ctypes.c_int),
+        "rss_ctx_create": ([ctypes.c_int, ctypes.POINTER(vp)], ctypes.c_int),
+        "rss_ctx_destroy": ([vp], None),
+        "rss_hash_host": ([vp, key_p, vp, sz, u32, u32, vp, vp, vp, u32], ctypes.c_int),
+    }
+    for name, (args, res) in sigs.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    return lib
+
+
+def load():
+    """Load (once) and return the native library; raise loudly if it is absent."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise NativeLibraryError(
+                    "HIP extension %s not found; build it with `python -c "
+                    "'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)" % LIB_PATH)
+            try:
+                lib = ctypes.CDLL(LIB_PATH)
+            except OSError as err:
+                raise NativeLibraryError("cannot load %s: %s" % (LIB_PATH, err))
+            lib = _bind(lib)
+            if lib.rss_abi_version() != ABI_VERSION:
+                raise NativeLibraryError("ABI mismatch: library %d, binding %d"
+                                         % (lib.rss_abi_version(), ABI_VERSION))
+            _lib = lib
+        return _lib
+
+
+def _check(rc, what):
+    if rc != 0:
+        msg = load().rss_last_error().decode("utf-8", "replace")
+        raise DeviceError("%s failed (%d): %s" % (what, rc, msg))
+
+
+def device_count():
+    out = ctypes.c_int(0)
+    _check(load().rss_device_count(ctypes.byref(out)), "rss_device_count")
+    return out.value
+
+
+def prepare_key(key_bytes):
+    """Build an :class:`RssKey` from raw key bytes (>= 4; the CLI admits 40 or 52)."""
+    raw = bytes(bytearray(int(b) & 0xFF for b in key_bytes))
+    if len(raw) < KEY_MIN_BYTES:
+        raise ValueError("hash key must hold at least %d bytes, got %d" % (KEY_MIN_BYTES, len(raw)))
+    key = RssKey()
+    buf = (ctypes.c_uint8 * len(raw)).from_buffer_copy(raw)
+    _check(load().rss_key_prepare(buf, len(raw), ctypes.byref(key)), "rss_key_prepare")
+    return key
+
+
+class HostContext:
+    """Owns an ``rss_ctx`` (device buffers + streams) for host-memory batches."""
+
+    def __init__(self, device=0):
+        self._lib = load()
+        self._ctx = ctypes.c_void_p()
+        _check(self._lib.rss_ctx_create(device, ctypes.byref(self._ctx)), "rss_ctx_create")
+        self.device = device
+
+    def close(self):
+        if self._ctx:
+            self._lib.rss_ctx_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def hash(self, key, tuples, htable, nqueues, want_hash=True, want_queue=True, want_counts=True):
+        """Hash packed tuples (structured ``TUPLE_DTYPE`` or uint32 (n, 3)) on the GPU.
+
+        Returns ``(hash_u32, queue_u32, counts_u64)``; disabled outputs are None.
+        """
+        arr = np.ascontiguousarray(tuples)
+        if arr.dtype != TUPLE_DTYPE:
+            arr = np.ascontiguousarray(arr, dtype=np.uint32).reshape(-1, 3)
+        n = len(arr)
+        h = np.empty(n, dtype=np.uint32) if want_hash else None
+        q = np.empty(n, dtype=np.uint32) if want_queue else None
+        c = np.zeros(nqueues, dtype=np.uint64) if want_counts else None
+        ptr = lambda a: a.ctypes.data if a is not None else None  # noqa: E731
+        _check(self._lib.rss_hash_host(self._ctx, ctypes.byref(key), ptr(arr), n, htable, nqueues,
+                                       ptr(h), ptr(q), ptr(c), 0), "rss_hash_host")
+        return h, q, c
+
+
+_default_ctx = None
+_ctx_lock = threading.Lock()
+
+
+def default_context():
+    """Process-wide HostContext on device ``$RSS_DEVICE`` (default 0), created on first use."""
+    global _default_ctx
+    with _ctx_lock:
+        if _default_ctx is None:
+            _default_ctx = HostContext(int(os.environ.get("RSS_DEVICE", "0")))
+        return _default_ctx
+
+
+# ------------------------------------------------------- device pointers ----
+def hash_device(key, tuples_ptr, n, htable, nqueues, hash_ptr=None, queue_ptr=None,
+                counts_ptr=None, flags=0, stream=None):
+    """Stream-ordered ``rss_hash_device`` on raw device pointers (ints)."""
+    _check(load().rss_hash_device(ctypes.byref(key), tuples_ptr, n, htable, nqueues, hash_ptr,
+                                  queue_ptr, counts_ptr, flags, stream), "rss_hash_device")
+
+
+def generate_device(seed, first_index, n, tuples_ptr, stream=None):
+    """Stream-ordered ``rss_generate_tuples`` into a device buffer of n * 12 bytes."""
+    _check(load().rss_generate_tuples(seed, first_index, n, tuples_ptr, stream),
+           "rss_generate_tuples")

@@ -1,0 +1,97 @@
+"""CSV columns -> packed 12-byte tuples, with the reference's parsing semantics.
+
+The reference converts each row inside ``Toeplitz.compute_hash``:
+
+* ``__ip_to_int`` (``rss_simulator/toeplitz.py:100-111``): ``ip.split(".")``, then
+  ``int(o0) << 24 | int(o1) << 16 | int(o2) << 8 | int(o3)`` on unbounded Python
+  ints -- octets are not range-checked, extra octets are ignored, fewer than four
+  raise ``IndexError``, ``int()`` tolerates surrounding whitespace;
+* ``__prepare_input_bytes`` (``toeplitz.py:127-142``): keeps bytes of that value,
+  i.e. the value modulo 2**32, and ``(p & 0xFF00) >> 8, p & 0xFF`` of each port,
+  i.e. the port modulo 2**16 (two's complement for negatives).
+
+:func:`pack_frame` reproduces this column-wise: a vectorised fast path for the
+common ``d.d.d.d`` / integer-port case and an exact per-element restatement for
+everything else (which also raises the same exception types as the reference).
+Divergence: the reference raises on the first bad ROW; this module converts column
+by column, so with several bad cells the reported one may differ (same exit).
+"""
+import numpy as np
+import pandas as pd
+
+from rss_simulator_nvidia_amd._native import TUPLE_DTYPE
+from rss_simulator_nvidia_amd.column_names import ColumnNames
+
+_DOTTED = r"[0-9]{1,3}\.[0-9]{1,3}\.[0-9]{1,3}\.[0-9]{1,3}"
+
+
+def ip_to_u32(ip):
+    """One address, exactly as ``toeplitz.py:110-111`` + the byte masks ``:130-137``."""
+    ip_num = ip.split(".")
+    value = int(ip_num[0]) << 24 | int(ip_num[1]) << 16 | int(ip_num[2]) << 8 | int(ip_num[3])
+    return value & 0xFFFFFFFF
+
+
+def port_to_u16(port):
+    """One port, exactly as ``toeplitz.py:138-141`` (``&`` semantics, so floats raise)."""
+    return ((port & 0xFF00) >> 8) << 8 | (port & 0x00FF)
+
+
+def ip_column(series):
+    """uint32 array for an address column (pandas Series)."""
+    n = len(series)
+    out = np.empty(n, dtype=np.uint32)
+    if n == 0:
+        return out
+    if series.dtype == object or pd.api.types.is_string_dtype(series.dtype):
+        try:
+            fast = series.str.fullmatch(_DOTTED).fillna(False).to_numpy(dtype=bool)
+        except AttributeError:  # the .str accessor refuses this column
+            fast = np.zeros(n, dtype=bool)
+        if fast.any():
+            parts = series[fast].str.split(".", expand=True).to_numpy(dtype=np.int64)
+            vals = (parts[:, 0] << 24) | (parts[:, 1] << 16) | (parts[:, 2] << 8) | parts[:, 3]
+            out[fast] = (vals & 0xFFFFFFFF).astype(np.uint32)
+        slow = np.flatnonzero(~fast)
+    else:
+        slow = np.arange(n)
+    values = series.to_numpy()
+    for i in slow:
+        out[i] = ip_to_u32(values[i])
+    return out
+
+
+def port_column(series):
+    """uint32 array (values < 2**16) for a port column (pandas Series)."""
+    kind = series.dtype.kind
+    if kind in "iub":
+        vals = series.to_numpy()
+        if kind == "u":
+            vals = vals.astype(np.uint64)
+            return (vals & np.uint64(0xFFFF)).astype(np.uint32)
+        return (vals.astype(np.int64) & 0xFFFF).astype(np.uint32)
+    values = series.to_numpy()
+    out = np.empty(len(values), dtype=np.uint32)
+    for i, v in enumerate(values):
+        out[i] = port_to_u16(v)
+    return out
+
+
+def pack_columns(sip, dip, sport, dport):
+    """Pack four equal-length arrays into the ``rss_tuple4`` layout."""
+    n = len(sip)
+    out = np.empty(n, dtype=TUPLE_DTYPE)
+    out["sip"] = np.asarray(sip, dtype=np.uint32)
+    out["dip"] = np.asarray(dip, dtype=np.uint32)
+    sp = np.asarray(sport).astype(np.uint32) & np.uint32(0xFFFF)
+    dp = np.asarray(dport).astype(np.uint32) & np.uint32(0xFFFF)
+    out["ports"] = (sp << np.uint32(16)) | dp
+    return out
+
+
+def pack_frame(df):
+    """Packed tuples for every row of a DataFrame holding the four input columns."""
+    return pack_columns(ip_column(df[ColumnNames.SRC_IP.value]),
+                        ip_column(df[ColumnNames.DST_IP.value]),
+                        port_column(df[ColumnNames.SRC_PORT.value]),
+                        port_column(df[ColumnNames.DST_PORT.value]))

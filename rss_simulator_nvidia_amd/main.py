@@ -1,0 +1,51 @@
+"""``rss-simulator`` command line -- drop-in for ``rss_simulator/main.py``.
+
+Same five flags, metavars, help texts, validation and exit codes as the
+reference (``main.py:10-64``): ``--key-file`` is parsed eagerly (bad key ->
+argparse error, exit 2), ``--htable-size`` / ``--num-queues`` must be >= 1,
+``--csv PATH`` writes statistics, otherwise the histogram is shown.
+"""
+from argparse import ArgumentParser
+
+from rss_simulator_nvidia_amd.arg_parse_types import PositiveInt
+from rss_simulator_nvidia_amd.arg_parse_types import arg_parse_type_decorator as apt_decorator
+from rss_simulator_nvidia_amd.hash_key import HashKey
+from rss_simulator_nvidia_amd.simulator import Simulator
+
+
+def build_parser():
+    """The reference's ArgumentParser (``main.py:17-50``)."""
+    parser = ArgumentParser(
+        prog="rss-simulator",
+        description="Simulate Nvidia's NIC RSS queue's distribution for Toeplitz hash function.",
+    )
+    parser.add_argument("--key-file", metavar="PATH", dest="key",
+                        type=apt_decorator(HashKey.from_file), required=True,
+                        help="File containing 40B hash key.")
+    parser.add_argument("--ips-file", metavar="PATH", required=True,
+                        help="csv containing source/destination IP and source/destination ports "
+                             "4 tupels entries.")
+    parser.add_argument("--htable-size", metavar="NUM", type=PositiveInt.parse, required=True,
+                        help="Positive number representing the hash-table size.")
+    parser.add_argument("--num-queues", metavar="NUM", type=PositiveInt.parse, required=True,
+                        help="Positive number representing number of queues.")
+    parser.add_argument("--csv", metavar="PATH", help="Write output to csv file.")
+    return parser
+
+
+def parse_args(argv=None):
+    """Parse script arguments (``main.py:10-51``)."""
+    return build_parser().parse_args(argv)
+
+
+def main(argv=None):
+    """Invoke the RSS simulator (``main.py:54-64``)."""
+    args = parse_args(argv)
+    rss_sim = Simulator(args.key, args.htable_size, args.num_queues)
+    rss_sim.load_ips_from_csv(args.ips_file)
+    rss_sim.calc_hash()
+    rss_sim.calc_queue_number()
+    if args.csv:
+        rss_sim.write_statistics(args.csv)
+    else:
+        rss_sim.show_histogram()

@@ -1,0 +1,144 @@
+"""RSS simulator driver -- drop-in for ``rss_simulator/simulator.py`` (``Simulator``).
+
+Public methods and their behaviour follow the reference:
+
+* ``load_ips_from_csv``  (``simulator.py:43-72``): ``pd.read_csv``, the same
+  ``ParseException`` messages (the unreadable-file message keeps the reference's
+  literal, unformatted ``'{csv}'``);
+* ``calc_hash``          (``simulator.py:74-92``): adds the int64 ``hash_result``
+  column.  Here the whole column is one kernel launch that also produces the
+  queue column and the per-queue histogram;
+* ``calc_queue_number``  (``simulator.py:94-98``): adds ``queue_number`` =
+  ``hash_result % htable % queues`` (computed by the same kernel pass);
+* ``write_statistics``   (``simulator.py:100-116``): ``queue_number,counts`` rows
+  for the non-empty queues (from the device histogram), then the full table,
+  then the same stdout line;
+* ``show_histogram``     (``simulator.py:118-172``): the per-queue bar chart with
+  the key / htable / queue caption (headless backends just render it).
+"""
+from __future__ import print_function
+
+import numpy as np
+import pandas as pd
+from pandas.errors import ParserError as pd_ParserError
+
+from rss_simulator_nvidia_amd.column_names import INPUT_COLUMNS, ColumnNames
+from rss_simulator_nvidia_amd.exceptions import ParseException
+from rss_simulator_nvidia_amd.ingest import pack_frame
+from rss_simulator_nvidia_amd.toeplitz import Toeplitz
+
+_HASH = ColumnNames.HASH_RESULT.value
+_QUEUE = ColumnNames.QUEUE_NUMBER.value
+
+
+class Simulator(object):
+    """RSS simulator class (``simulator.py:26``)."""
+
+    def __init__(self, hash_key, hash_table_size, queue_number):
+        """Key as ``List[int]``, hash-table size and number of queues (both >= 1)."""
+        self.__ip_df = None
+        self.__toeplitz = Toeplitz(hash_key)
+        self.__hash_table_size = hash_table_size
+        self.__queue_num = queue_number
+        self.__queues = None
+        self.__counts = None
+
+    @property
+    def data_frame(self):
+        """The working DataFrame (input columns + the columns added so far)."""
+        return self.__ip_df
+
+    @property
+    def queue_counts(self):
+        """uint64[num_queues] per-queue counts from the last ``calc_hash``."""
+        return self.__counts
+
+    def load_ips_from_csv(self, csv_path):
+        """Read the 4-tuple CSV; raise ParseException like ``simulator.py:54-71``."""
+        try:
+            df = pd.read_csv(csv_path)
+        except (UnicodeDecodeError, IOError, pd_ParserError):
+            msg = "Couldn't parse '{csv}' file, make sure it's a valid CSV encoded with 'utf-8'"
+            raise ParseException(msg)
+        expected = {col.value for col in INPUT_COLUMNS}
+        missing_columns = expected - set(df.columns.tolist())
+        if missing_columns:
+            raise ParseException("{csv} is missing columns: {cols}".format(
+                csv=csv_path, cols=", ".join(missing_columns)))
+        self.load_frame(df)
+
+    def load_frame(self, df):
+        """Use an in-memory DataFrame (same column contract as the CSV)."""
+        self.__ip_df = df
+        self.__queues = None
+        self.__counts = None
+
+    def calc_hash(self):
+        """Hash every row on the GPU and add the ``hash_result`` column."""
+        df = self.__ip_df
+        if len(df) == 0:
+            # the reference's DataFrame.apply on zero rows fails the same way
+            raise ValueError("Cannot set a DataFrame with multiple columns to the single column "
+                             "hash_result")
+        tuples = pack_frame(df)
+        h, q, c = self.__toeplitz.compute_queues(tuples, self.__hash_table_size, self.__queue_num)
+        df[_HASH] = h.astype(np.int64)
+        self.__queues = q
+        self.__counts = c
+
+    def calc_queue_number(self):
+        """Add ``queue_number`` = ``hash_result % htable % queues`` (``simulator.py:96-98``)."""
+        if self.__queues is None:
+            raise AttributeError("'DataFrame' object has no attribute 'hash_result'")
+        self.__ip_df[_QUEUE] = self.__queues.astype(np.int64)
+
+    def queue_count_rows(self):
+        """``[(queue, count)]`` for non-empty queues, ascending (value_counts().sort_index())."""
+        counts = self.__counts
+        nz = np.flatnonzero(counts)
+        return [(int(q), int(counts[q])) for q in nz]
+
+    def write_statistics(self, output):
+        """Write counts then the full table to ``output`` (``simulator.py:100-116``)."""
+        with open(output, "w") as f:
+            f.write("{},counts\n".format(_QUEUE))
+            for q, c in self.queue_count_rows():
+                f.write("{},{}\n".format(q, c))
+        self.__ip_df.to_csv(output, mode="a", index=False)
+        print("Wrote statistics to {csv}.".format(csv=output))
+
+    def histogram_caption(self):
+        """The caption lines of ``simulator.py:160-169``."""
+        hash_key = self.__toeplitz.hash_key_str()
+        key_str = "Hash Key: {}\n{}{}".format(hash_key[:94], " " * 17, hash_key[94:])
+        return "\n".join([
+            key_str,
+            "Hash Table Size: {}".format(self.__hash_table_size),
+            "Number Queues: {}".format(self.__queue_num),
+            "Number of Queues Chosen by Hash Function: {}".format(len(self.queue_count_rows())),
+        ])
+
+    def show_histogram(self, output=None):
+        """Per-queue bar chart + caption; ``plt.show()``, or save to ``output`` if given."""
+        import matplotlib.pyplot as plt
+        from matplotlib.ticker import MaxNLocator
+
+        counts = np.asarray(self.__counts, dtype=np.int64)
+        fig, ax = plt.subplots(figsize=(12, 8))
+        ax.bar(np.arange(self.__queue_num) + 0.5, counts, width=0.9, color="#86bf91", zorder=2)
+        for side in ("right", "top", "left"):
+            ax.spines[side].set_visible(False)
+        for tick in ax.get_yticks():
+            ax.axhline(y=tick, linestyle="dashed", alpha=0.8, color="#dddddd", zorder=1)
+        ax.set_title("Number of Unique Flows per Queue", weight="bold", size=16)
+        ax.set_xlabel("Queue Number", labelpad=20, weight="bold", size=12)
+        ax.set_ylabel("Number of Flows", labelpad=20, weight="bold", size=12)
+        ax.yaxis.set_major_locator(MaxNLocator(integer=True))
+        ax.set_xlim(0, self.__queue_num)
+        fig.text(0.04, 0.03, self.histogram_caption(), fontsize=12)
+        fig.subplots_adjust(bottom=0.27)
+        if output:
+            fig.savefig(output)
+            plt.close(fig)
+        else:
+            plt.show()
