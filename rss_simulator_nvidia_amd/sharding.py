@@ -1,0 +1,62 @@
+"""Multi-GPU data parallelism for the hot path: one process per GPU.
+
+Tuples are independent, so a batch is block-partitioned over ranks with no
+data-path communication; every rank hashes its shard on its own GPU and keeps its
+``hash_result`` / ``queue_number`` slice.  The only exchange step is the per-queue
+histogram: ``uint64[nqueues]`` summed with one all-reduce (RCCL over xGMI with the
+``nccl`` backend; ``gloo`` in the CPU tests).  That vector is <= 512 B at the
+benchmark configs, so the collective is latency-bound, not link-bound.
+
+The reference is single-process (``simulator.py:74-116``); this module is new.
+"""
+import torch
+import torch.distributed as dist
+
+
+def shard_range(n_total, rank, world):
+    """Contiguous block partition: ``(start, count)`` of rank's shard of ``n_total``.
+
+    The first ``n_total % world`` ranks get one extra tuple, so shards differ by at
+    most one and concatenate, in rank order, to the whole batch.
+    """
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError("bad rank %d for world %d" % (rank, world))
+    base, extra = divmod(int(n_total), world)
+    start = rank * base + min(rank, extra)
+    return start, base + (1 if rank < extra else 0)
+
+
+def world_info():
+    """``(rank, world)`` of the default process group, ``(0, 1)`` when not distributed."""
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+def allreduce_counts(counts, group=None):
+    """Sum per-queue counts over ranks in place (int64 tensor; uint64 bit pattern).
+
+    Counts are exact integers, so the reduced histogram equals the single-device
+    histogram of the whole batch bit for bit.
+    """
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=group)
+    return counts
+
+
+def hash_shard(key, tuples, n, htable, nqueues, hashes=None, queues=None, counts=None,
+               accumulate=False, group=None):
+    """Hash this rank's resident shard on the current device, then all-reduce counts.
+
+    ``tuples`` is a device tensor of at least ``3 * n`` int32 (packed ``rss_tuple4``);
+    ``hashes`` / ``queues`` (int32[n]) and ``counts`` (int64[nqueues]) may be None.
+    Everything is enqueued on torch's current stream.
+    """
+    from rss_simulator_nvidia_amd import _native
+    stream = torch.cuda.current_stream(tuples.device).cuda_stream
+    ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+    _native.hash_device(key, tuples.data_ptr(), n, htable, nqueues, ptr(hashes), ptr(queues),
+                        ptr(counts), _native.FLAG_ACCUMULATE if accumulate else 0, stream)
+    if counts is not None:
+        allreduce_counts(counts, group)
+    return hashes, queues, counts

@@ -1,0 +1,114 @@
+"""The C-ABI library builds, loads and exports everything include/rss_toeplitz.h
+declares; host-side entry points (key preparation, argument validation, device
+discovery) behave on a machine without a GPU.  No kernel is launched here."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from rss_simulator_nvidia_amd import _native
+from rss_simulator_nvidia_amd.exceptions import DeviceError
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "rss_toeplitz.h")
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(_native.LIB_PATH):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "rss_simulator_nvidia_amd", "csrc")],
+                       check=True)
+    return _native.load()
+
+
+def header_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(rss_[a-z_0-9]+)\s*\(", text)))
+
+
+def test_every_declared_symbol_is_exported(lib):
+    declared = header_functions()
+    assert set(declared) == set(_native.EXPORTED_SYMBOLS)
+    out = subprocess.run(["nm", "-D", "--defined-only", _native.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (rss_[a-z_0-9]+)$", out, flags=re.M))
+    assert set(declared) <= exported, set(declared) - exported
+
+
+def test_abi_version_matches_header(lib):
+    m = re.search(r"#define RSS_ABI_VERSION (\d+)", open(HEADER).read())
+    assert lib.rss_abi_version() == int(m.group(1)) == _native.ABI_VERSION
+
+
+def test_struct_layout_matches_c(tmp_path):
+    src = tmp_path / "layout.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "rss_toeplitz.h"\n'
+                   'int main(void){printf("%zu %zu %zu %zu %zu\\n", sizeof(rss_tuple4), '
+                   'sizeof(rss_key), offsetof(rss_key, bytes), offsetof(rss_key, window), '
+                   'offsetof(rss_key, nibble_lut));return 0;}\n')
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
+    K = _native.RssKey
+    assert got == [ctypes.sizeof(_native.RssTuple4), ctypes.sizeof(K), K.bytes.offset,
+                   K.window.offset, K.nibble_lut.offset]
+
+
+def test_key_prepare_matches_oracle_windows(lib, random_golden, oracle_lib):
+    rng = np.random.default_rng(5)
+    keys = list(random_golden["key_list"]) + [[int(x) for x in rng.integers(0, 256, n)]
+                                              for n in (4, 9, 15, 16, 33, 64, 200)]
+    for key in keys:
+        k = _native.prepare_key(key)
+        w = np.ctypeslib.as_array(k.window)
+        np.testing.assert_array_equal(w, oracle_lib.windows(key))
+        lut = np.ctypeslib.as_array(k.nibble_lut).reshape(24, 16)
+        for t in range(24):
+            for v in range(16):
+                x = 0
+                for j in range(4):
+                    if v & (8 >> j):
+                        x ^= int(w[4 * t + j])
+                assert lut[t, v] == x
+        assert k.len == len(key)
+
+
+def test_key_prepare_rejects_short_keys(lib):
+    with pytest.raises(ValueError):
+        _native.prepare_key([1, 2, 3])
+    key = _native.RssKey()
+    buf = (ctypes.c_uint8 * 3)(1, 2, 3)
+    assert lib.rss_key_prepare(buf, 3, ctypes.byref(key)) == -22
+    assert b">= 4 bytes" in lib.rss_last_error()
+
+
+def test_argument_validation_before_any_device_work(lib, example_key):
+    key = _native.prepare_key(example_key)
+    with pytest.raises(DeviceError, match="must be >= 1"):
+        _native.hash_device(key, 0, 16, 0, 24)
+    with pytest.raises(DeviceError, match="must be >= 1"):
+        _native.hash_device(key, 0, 16, 128, 0)
+    with pytest.raises(DeviceError, match="tuples is NULL"):
+        _native.hash_device(key, None, 16, 128, 24)
+    empty = _native.RssKey()
+    with pytest.raises(DeviceError, match="key not prepared"):
+        _native.hash_device(empty, 0, 16, 128, 24)
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="only meaningful without a GPU")
+def test_no_gpu_is_reported_not_faked(lib):
+    assert _native.device_count() == 0
+    with pytest.raises(DeviceError, match="no HIP device"):
+        _native.HostContext(0)
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    from rss_simulator_nvidia_amd.exceptions import NativeLibraryError
+    monkeypatch.setattr(_native, "LIB_PATH", str(tmp_path / "nope.so"))
+    monkeypatch.setattr(_native, "_lib", None)
+    with pytest.raises(NativeLibraryError, match="no CPU fallback"):
+        _native.load()

@@ -1,0 +1,65 @@
+"""Multi-rank path on CPU: world_size-2 ``gloo`` process group, tuple sharding and the
+count all-reduce (the per-shard compute is the oracle here; the GPU box and the
+driver's 8-GPU run exercise the same code with the HIP kernel and RCCL)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from rss_simulator_nvidia_amd.sharding import allreduce_counts, shard_range, world_info
+
+
+@pytest.mark.parametrize("n,world", [(0, 1), (10, 3), (7, 8), (2**28 + 5, 8), (1000, 2)])
+def test_shard_range_partitions(n, world):
+    spans = [shard_range(n, r, world) for r in range(world)]
+    assert spans[0][0] == 0
+    for (s0, c0), (s1, _) in zip(spans, spans[1:]):
+        assert s0 + c0 == s1
+    assert sum(c for _, c in spans) == n
+    assert max(c for _, c in spans) - min(c for _, c in spans) <= 1
+
+
+def test_shard_range_rejects_bad_rank():
+    with pytest.raises(ValueError):
+        shard_range(10, 2, 2)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, key, n_total, htable, nqueues, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle.oracle import OracleLib
+        lib = OracleLib()
+        assert world_info() == (rank, world)
+        start, count = shard_range(n_total, rank, world)
+        tup = lib.generate(0x5EED, start, count)
+        h, q, c = lib.run(key, tup, htable, nqueues, threads=1)
+        counts = torch.from_numpy(c.view(np.int64).copy())
+        allreduce_counts(counts)
+        np.save(os.path.join(out_dir, "h%d.npy" % rank), h)
+        np.save(os.path.join(out_dir, "c%d.npy" % rank), counts.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_sharded_counts_equal_single_process(world, tmp_path, oracle_lib, example_key):
+    n_total, htable, nqueues = 100003, 128, 24
+    mp.start_processes(_worker, args=(world, _free_port(), example_key, n_total, htable, nqueues,
+                                      str(tmp_path)), nprocs=world, start_method="spawn")
+    whole = oracle_lib.generate(0x5EED, 0, n_total)
+    h, _, c = oracle_lib.run(example_key, whole, htable, nqueues)
+    shards = np.concatenate([np.load(tmp_path / ("h%d.npy" % r)) for r in range(world)])
+    np.testing.assert_array_equal(shards, h)
+    for r in range(world):
+        np.testing.assert_array_equal(np.load(tmp_path / ("c%d.npy" % r)).view(np.uint64), c)
