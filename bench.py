@@ -27,7 +27,8 @@ EXAMPLE_KEY = ("23:0d:44:3d:8c:2c:6e:64:d4:1a:f3:44:49:9b:21:74:fd:1a:9d:c1:dd:7
                "51:66:85:7b:dc:48:a8:3e:55:08:c1:63:af:01:9d")
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 READ_BYTES = 12                # packed tuple
-WRITE_BYTES = 8                # u32 hash_result + u32 queue_number
+HASH_BYTES = 4                 # u32 hash_result
+QUEUE_BYTES = {"u8": 1, "u16": 2, "u32": 4}
 SEED = 0x5EED
 
 
@@ -39,6 +40,8 @@ def parse_args():
     p.add_argument("--tuples-per-gpu", type=int, default=1 << 28)
     p.add_argument("--htable", type=int, default=128)
     p.add_argument("--queues", type=int, default=24)
+    p.add_argument("--queue-width", choices=["auto", "u8", "u16", "u32"], default="auto",
+                   help="queue_number output dtype; auto = narrowest that holds every queue")
     p.add_argument("--cpu-sample", type=int, default=12000,
                    help="tuples for the CPU baseline (about 20 CPU-seconds)")
     p.add_argument("--cpu-procs", type=int, default=16,
@@ -124,12 +127,17 @@ def main():
 
     n = args.tuples_per_gpu
     H, Q = args.htable, args.queues
+    qw = args.queue_width
+    if qw == "auto":
+        qw = "u8" if Q <= 256 else ("u16" if Q <= 65536 else "u32")
+    qflag = {"u8": _native.FLAG_QUEUE_U8, "u16": _native.FLAG_QUEUE_U16, "u32": 0}[qw]
+    write_bytes = HASH_BYTES + QUEUE_BYTES[qw]
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
     key = _native.prepare_key(key_bytes)
     tuples = torch.empty(3 * n, dtype=torch.int32, device=dev)
     hashes = torch.empty(n, dtype=torch.int32, device=dev)
-    queues = torch.empty(n, dtype=torch.int32, device=dev)
+    queues = torch.empty(n, dtype=torch.int32, device=dev)  # big enough for any width
     counts = torch.zeros(Q, dtype=torch.int64, device=dev)
     _native.generate_device(SEED, rank * n, n, tuples.data_ptr(), sp)
     torch.cuda.synchronize()
@@ -137,12 +145,12 @@ def main():
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
 
-    def step(i=None, hash_ptr=hashes.data_ptr(), queue_ptr=queues.data_ptr()):
+    def step(i=None, hash_ptr=hashes.data_ptr(), queue_ptr=queues.data_ptr(), flags=qflag):
         counts.zero_()
         if i is not None:
             ev[i][0].record(stream)
         _native.hash_device(key, tuples.data_ptr(), n, H, Q, hash_ptr, queue_ptr,
-                            counts.data_ptr(), _native.FLAG_ACCUMULATE, sp)
+                            counts.data_ptr(), _native.FLAG_ACCUMULATE | flags, sp)
         if i is not None:
             ev[i][1].record(stream)
         if world > 1:
@@ -168,24 +176,30 @@ def main():
     if total != n * world:
         raise SystemExit("bench: per-queue counts sum to %d, expected %d" % (total, n * world))
 
-    # secondary line: counts-only mode (12 B/tuple, the HBM-read roofline)
-    co_ms = None
-    if rank == 0:
+    # secondary lines (rank 0, after the timed region): counts-only mode (12 B/tuple,
+    # the HBM-read roofline) and u32 queue outputs (20 B/tuple)
+    def kernel_ms_of(hash_ptr, queue_ptr, flags):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         reps = max(5, args.steps // 2)
-        step(None, None, None)
+        _native.hash_device(key, tuples.data_ptr(), n, H, Q, hash_ptr, queue_ptr,
+                            counts.data_ptr(), flags, sp)
         a.record(stream)
         for _ in range(reps):
-            _native.hash_device(key, tuples.data_ptr(), n, H, Q, None, None, counts.data_ptr(),
-                                _native.FLAG_ACCUMULATE, sp)
+            _native.hash_device(key, tuples.data_ptr(), n, H, Q, hash_ptr, queue_ptr,
+                                counts.data_ptr(), flags, sp)
         b.record(stream)
         torch.cuda.synchronize()
-        co_ms = a.elapsed_time(b) / reps
+        return a.elapsed_time(b) / reps
+
+    co_ms = u32_ms = None
+    if rank == 0:
+        co_ms = kernel_ms_of(None, None, 0)
+        u32_ms = kernel_ms_of(hashes.data_ptr(), queues.data_ptr(), 0)
 
     if rank == 0:
         value = n * world * args.steps / elapsed
         kernel_s = kernel_ms / 1e3
-        achieved = n * (READ_BYTES + WRITE_BYTES) / kernel_s / 1e9
+        achieved = n * (READ_BYTES + write_bytes) / kernel_s / 1e9
         traffic = load_traffic(args.profile_dir, n, H, Q)
         line = {
             "metric": METRIC,
@@ -203,11 +217,13 @@ def main():
             "config": {
                 "workload": "configs[2]: %d synthetic 4-tuples per GPU (x%d GPUs), key "
                             "example_input/hash_key.txt (40 B), htable=%d, queues=%d; outputs "
-                            "hash_result + queue_number + per-queue counts" % (n, world, H, Q),
+                            "hash_result (u32) + queue_number (%s) + per-queue counts (u64)"
+                            % (n, world, H, Q, qw),
                 "tuples_per_gpu": n,
                 "global_tuples": n * world,
                 "htable": H,
                 "queues": Q,
+                "queue_width": qw,
                 "parallelism": "tuple-sharded x%d, RCCL all-reduce of uint64[%d] counts"
                                % (world, Q),
             },
@@ -219,7 +235,7 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "kernel": "rss_toeplitz_kernel",
-                "bytes_per_tuple": READ_BYTES + WRITE_BYTES,
+                "bytes_per_tuple": READ_BYTES + write_bytes,
                 "kernel_ms": kernel_ms,
                 "kernel_ms_max_rank": kernel_ms_max,
             },
@@ -229,6 +245,11 @@ def main():
                 "tuples_per_s_per_gpu": n / (co_ms / 1e3),
                 "hbm_read_GBs": n * READ_BYTES / (co_ms / 1e3) / 1e9,
                 "hbm_read_frac": n * READ_BYTES / (co_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
+            },
+            "queue_u32": {
+                "kernel_ms": u32_ms,
+                "tuples_per_s_per_gpu": n / (u32_ms / 1e3),
+                "achieved_GBs": n * 20 / (u32_ms / 1e3) / 1e9,
             },
             "cpu_baseline": baseline,
         }

@@ -54,21 +54,19 @@ typedef struct rss_tuple4 {
 #define RSS_KEY_MIN_BYTES 4
 #define RSS_KEY_MAX_BYTES 52
 #define RSS_INPUT_BITS 96
-#define RSS_NIBBLES (RSS_INPUT_BITS / 4)
 
 /*
  * Prepared hash key.  window[i] is the 32-bit window the reference XORs in
  * for input bit i (toeplitz.py:65-68 with __key_left_most_32bits :71-81 after i
- * rotations by __shift_key :83-98), i.e. key bits [i, i+32) MSB-first.
- * nibble_lut[t][v] is the XOR of the windows selected by the 4-bit value v at
- * input nibble t (input bits 4t..4t+3), the table the device kernel replicates
- * into LDS.  For len >= 16 only key bytes 0..15 influence any hash.
+ * rotations by __shift_key :83-98), i.e. key bits [i, i+32) MSB-first (bit
+ * indices taken modulo 8*len, which only matters for keys shorter than 16
+ * bytes).  The device kernel expands the windows into its LDS lookup tables.
+ * For len >= 16 only key bytes 0..15 influence any hash.
  */
 typedef struct rss_key {
     uint32_t len;                          /* key length in bytes (>= 4)     */
     uint8_t bytes[RSS_KEY_MAX_BYTES];      /* first min(len, 52) key bytes   */
     uint32_t window[RSS_INPUT_BITS];
-    uint32_t nibble_lut[RSS_NIBBLES][16];
 } rss_key;
 
 /*
@@ -82,7 +80,9 @@ typedef struct rss_key {
 int rss_key_prepare(const uint8_t* key, size_t len, rss_key* out);
 
 /* flags for rss_hash_device / rss_hash_host */
-#define RSS_FLAG_ACCUMULATE 1u  /* add into counts instead of overwriting them */
+#define RSS_FLAG_ACCUMULATE 1u  /* add into counts instead of overwriting them      */
+#define RSS_FLAG_QUEUE_U16 2u   /* rss_hash_device: d_queue is uint16_t[n] (Q<=2^16) */
+#define RSS_FLAG_QUEUE_U8 4u    /* rss_hash_device: d_queue is uint8_t[n]  (Q<=256)  */
 
 /*
  * Device-resident hot path.  Replaces, for n tuples at once:
@@ -92,14 +92,18 @@ int rss_key_prepare(const uint8_t* key, size_t len, rss_key* out);
  *     (queue = hash % htable % nqueues)
  *   the value_counts of Simulator.write_statistics  simulator.py:107-113
  *     (counts[q] = number of tuples with queue q, for q < nqueues).
- * d_tuples: n packed tuples in device memory.  d_hash, d_queue: n uint32 each
- * or NULL to skip that output.  d_counts: nqueues uint64 or NULL; overwritten
- * unless RSS_FLAG_ACCUMULATE.  htable >= 1, nqueues >= 1 (positive_int.py:27).
- * Launched on `stream` (hipStream_t) on the calling thread's current device.
+ * d_tuples: n packed tuples in device memory.  d_hash: n uint32 or NULL.
+ * d_queue: n queue numbers or NULL -- uint32 by default, uint16 / uint8 with
+ * RSS_FLAG_QUEUE_U16 / RSS_FLAG_QUEUE_U8 (same values, narrower stores; the
+ * flag is rejected if nqueues does not fit).  d_counts: nqueues uint64 or NULL;
+ * overwritten unless RSS_FLAG_ACCUMULATE.  htable >= 1, nqueues >= 1
+ * (positive_int.py:27).  Launched on `stream` (hipStream_t) on the calling
+ * thread's current device.  Any alignment works; 16-byte aligned tuples/hashes
+ * (and 4/8/16-byte aligned u8/u16/u32 queues) take the 4-tuples-per-lane path.
  */
 int rss_hash_device(const rss_key* key, const rss_tuple4* d_tuples, size_t n,
                     uint32_t htable, uint32_t nqueues, uint32_t* d_hash,
-                    uint32_t* d_queue, uint64_t* d_counts, uint32_t flags,
+                    void* d_queue, uint64_t* d_counts, uint32_t flags,
                     void* stream);
 
 /*
@@ -121,7 +125,8 @@ void rss_ctx_destroy(rss_ctx* ctx);
 /*
  * Same contract as rss_hash_device but on host buffers: chunked
  * H2D -> kernel -> D2H through pinned staging, synchronous on return.
- * h_hash / h_queue / h_counts may be NULL.
+ * h_hash / h_queue (uint32) / h_counts may be NULL; only RSS_FLAG_ACCUMULATE
+ * is honoured.
  */
 int rss_hash_host(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples,
                   size_t n, uint32_t htable, uint32_t nqueues, uint32_t* h_hash,

@@ -21,6 +21,8 @@ LIB_PATH = os.environ.get(
 
 ABI_VERSION = 1
 FLAG_ACCUMULATE = 1
+FLAG_QUEUE_U16 = 2
+FLAG_QUEUE_U8 = 4
 KEY_MIN_BYTES = 4
 
 # Every symbol include/rss_toeplitz.h declares (tests/test_native_abi.py checks them).
@@ -37,12 +39,11 @@ class RssTuple4(ctypes.Structure):
 
 
 class RssKey(ctypes.Structure):
-    """``rss_key``: prepared key (windows + nibble tables)."""
+    """``rss_key``: prepared key (length, bytes, the 96 rotation windows)."""
     _fields_ = [
         ("len", ctypes.c_uint32),
         ("bytes", ctypes.c_uint8 * 52),
         ("window", ctypes.c_uint32 * 96),
-        ("nibble_lut", (ctypes.c_uint32 * 16) * 24),
     ]
 
 

@@ -7,13 +7,14 @@
 //   value_counts in write_statistics rss_simulator/simulator.py:107-113
 //
 // Kernel shape: one lane per tuple, 4 consecutive tuples per lane
-// per iteration (3 x dwordx4 loads, dwordx4 hash/queue stores), persistent
-// grid-stride launch of 2 x 1024-thread workgroups per CU.  The Toeplitz hash is
-// evaluated from 24 nibble tables (16 entries each, the XOR of the key windows a
-// 4-bit input value selects) replicated 32x in LDS so that lane l always reads
-// bank l: 24 conflict-free ds_read_b32 + ~48 VALU per tuple instead of the
-// reference's 96-step bit-serial loop.  The per-queue histogram is privatised per
-// lane column in LDS and folded into global uint64 counts once per workgroup.
+// per iteration (3 x dwordx4 loads, nontemporal hash/queue stores), persistent
+// grid-stride launch of one 1024-thread workgroup per CU.  The Toeplitz hash is
+// evaluated from 8 LDS tables of 4096 entries (the XOR of the key windows each
+// 12-bit slice of the input selects, 128 KiB, built per workgroup from the 96
+// windows): 8 ds_read_b32 + ~23 VALU per tuple instead of the reference's
+// 96-step bit-serial loop.  The per-queue histogram is privatised per lane
+// column in LDS and folded into global uint64 counts once per workgroup.
+// tools/kbench.hip holds the measured design space (4/6/8/12-bit tables).
 #include <hip/hip_runtime.h>
 
 #include <cstdarg>
@@ -51,22 +52,28 @@ int set_error(int code, const char* fmt, ...) {
 
 // ------------------------------------------------------------ constants -----
 constexpr int kBlock = 1024;            // threads per workgroup (16 waves)
-constexpr int kBlocksPerCU = 2;         // 2 x 16 waves = 32 waves/CU
-constexpr int kCopies = 32;             // LUT replicas: lane l reads bank (l & 31)
-constexpr uint32_t kLutDwords = RSS_NIBBLES * 16 * kCopies;  // 12288 dwords
-constexpr uint32_t kLutBytes = kLutDwords * 4;              // 48 KiB
-static_assert(kLutBytes == 48 * 1024, "LUT layout: 24 tables x 16 values x 32 replicas");
-constexpr uint32_t kBinBytesMax = 32 * 1024;                // histogram LDS budget
+constexpr int kBlocksPerCU = 1;         // the 128 KiB LUT admits one workgroup per CU
+constexpr int kChunkBits = 12;          // input bits per table lookup
+constexpr int kTables = RSS_INPUT_BITS / kChunkBits;        // 8
+constexpr uint32_t kTableEntries = 1u << kChunkBits;        // 4096
+constexpr uint32_t kLutDwords = kTables * kTableEntries;    // 32768
+constexpr uint32_t kLutBytes = kLutDwords * 4;              // 128 KiB
+constexpr uint32_t kLdsBytes = 160 * 1024;                  // gfx950 LDS per CU
+constexpr uint32_t kBinBytesMax = kLdsBytes - kLutBytes;    // 32 KiB for histogram bins
+constexpr int kBinCols = 32;            // private histogram columns (one per bank)
+static_assert(kLutBytes == 128 * 1024, "LUT layout: 8 tables x 4096 x u32");
+static_assert(kBlock * 4 == (int)kTableEntries, "LUT build maps 4 entries per thread per table");
 
 enum QueueMode { QM_MASK = 0, QM_FAST16 = 1, QM_FAST32 = 2 };
 enum HistMode { HIST_PRIVATE = 0, HIST_SHARED = 1, HIST_GLOBAL = 2, HIST_NONE = 3 };
+enum QueueWidth { QW_U32 = 0, QW_U16 = 1, QW_U8 = 2 };
 
-// Everything a launch needs, passed by value in the kernarg segment (1.6 KiB).
+// Everything a launch needs, passed by value in the kernarg segment.
 struct LaunchParams {
-    uint32_t lut[RSS_NIBBLES][16];
+    uint32_t window[RSS_INPUT_BITS];  // rss_key::window
     const rss_tuple4* tuples;
     uint32_t* hash_out;
-    uint32_t* queue_out;
+    void* queue_out;
     unsigned long long* counts;
     uint64_t n;
     uint64_t h_m64;     // ceil(2^64 / H) for the non-power-of-two htable path
@@ -80,29 +87,64 @@ struct LaunchParams {
 };
 
 // ------------------------------------------------------------- device -------
-// Toeplitz hash of one 96-bit input (w0 = src ip, w1 = dst ip, w2 = ports) from
-// the lane-replicated nibble tables.  Table t, value v, replica c lives at byte
-// t*2048 + v*128 + c*4 of the static LDS LUT, so the byte address is the nibble
-// moved to bits 7..10 OR the lane's replica offset (v_lshrrev + v_and_or_b32),
-// and the table offset folds into the ds_read_b32 immediate.  lane4 must be
-// opaque to the compiler (see rss_toeplitz_kernel): if it can prove the OR is
-// disjoint it rewrites it as an add and splits v_and_or_b32 into two ops.
-__device__ __forceinline__ uint32_t toeplitz_lut(const uint32_t* __restrict__ lut, uint32_t w0,
-                                                 uint32_t w1, uint32_t w2, uint32_t lane4) {
-    const char* base = reinterpret_cast<const char*>(lut);
-    uint32_t r[RSS_NIBBLES];
+// LUT: table t (input bits 12t .. 12t+11, MSB first) holds, for every 12-bit
+// value v, the XOR of the key windows whose input bit is set in v -- i.e. the
+// reference's inner loop (toeplitz.py:65-68) pre-summed over 12 bits.  Entry
+// (t, v) lives at LDS byte t*16384 + v*4.  One hash = 8 ds_read_b32 + 7 XOR.
+//
+// Build: thread `tid` owns v = hi*1024 + tid (hi = 0..3) of every table: the low
+// ten bits of v are its thread id, so it XORs their windows once per table and
+// derives the four entries from the two top-bit windows.
+__device__ __forceinline__ void build_lut(uint32_t* lut, const LaunchParams& p, uint32_t tid) {
 #pragma unroll
-    for (int t = 0; t < RSS_NIBBLES; ++t) {
-        const uint32_t w = t < 8 ? w0 : (t < 16 ? w1 : w2);
-        const int sh = 28 - 4 * (t & 7);  // nibble occupies bits sh..sh+3
-        const uint32_t moved = sh >= 7 ? (w >> (sh - 7)) : (w << (7 - sh));
-        const uint32_t off = (moved & 0x780u) | lane4;
-        r[t] = *reinterpret_cast<const uint32_t*>(base + t * 2048 + off);
+    for (int t = 0; t < kTables; ++t) {
+        const uint32_t* w = p.window + kChunkBits * t;  // w[j] <-> bit (11 - j) of v
+        uint32_t base = 0;
+#pragma unroll
+        for (int j = 2; j < kChunkBits; ++j) base ^= ((tid >> (11 - j)) & 1u) ? w[j] : 0u;
+        uint32_t* dst = lut + t * kTableEntries + tid;
+        dst[0 * kBlock] = base;
+        dst[1 * kBlock] = base ^ w[1];
+        dst[2 * kBlock] = base ^ w[0];
+        dst[3 * kBlock] = base ^ w[0] ^ w[1];
     }
-    uint32_t h = 0;
-#pragma unroll
-    for (int t = 0; t < RSS_NIBBLES; ++t) h ^= r[t];
-    return h;
+}
+
+// Byte address of chunk t's entry for the input words w0 = src ip, w1 = dst ip,
+// w2 = ports: the 12-bit value moved to bits 2..13 (shift or, for chunks 2 and 5
+// that straddle two words, the funnel shift v_alignbit_b32) and masked.  Tables
+// 4..7 sit above the 16-bit ds_read immediate, so their base 0x10000 is ORed in
+// by the same v_and_or_b32 from `hi` -- an opaque register holding 0x10000 (a
+// literal would cost a separate v_or).  Each address is 2 VALU ops.
+template <int kT>
+__device__ __forceinline__ uint32_t chunk_offset(uint32_t w0, uint32_t w1, uint32_t w2,
+                                                 uint32_t hi) {
+    constexpr uint32_t kMask = (kTableEntries - 1) << 2;  // 0x3FFC
+    if constexpr (kT == 0) return (w0 >> 18) & kMask;     // w0[31:20]
+    if constexpr (kT == 1) return (w0 >> 6) & kMask;      // w0[19:8]
+    if constexpr (kT == 2) return __builtin_amdgcn_alignbit(w0, w1, 26) & kMask;  // w0[7:0] w1[31:28]
+    if constexpr (kT == 3) return (w1 >> 14) & kMask;     // w1[27:16]
+    if constexpr (kT == 4) return ((w1 >> 2) & kMask) | hi;  // w1[15:4]
+    if constexpr (kT == 5) return (__builtin_amdgcn_alignbit(w1, w2, 22) & kMask) | hi;  // w1[3:0] w2[31:24]
+    if constexpr (kT == 6) return ((w2 >> 10) & kMask) | hi;  // w2[23:12]
+    return ((w2 << 2) & kMask) | hi;                          // w2[11:0]
+}
+
+template <int kT>
+__device__ __forceinline__ uint32_t lut_term(const char* lut, uint32_t w0, uint32_t w1, uint32_t w2,
+                                             uint32_t hi) {
+    constexpr uint32_t kImm = (kT & 3) * (kTableEntries * 4);  // fits the 16-bit offset
+    return *reinterpret_cast<const uint32_t*>(lut + kImm + chunk_offset<kT>(w0, w1, w2, hi));
+}
+
+// Toeplitz hash of one 96-bit input (toeplitz.py:46-69 over the bytes of :113-142).
+__device__ __forceinline__ uint32_t toeplitz_hash(const uint32_t* __restrict__ lut, uint32_t w0,
+                                                  uint32_t w1, uint32_t w2, uint32_t hi) {
+    const char* base = reinterpret_cast<const char*>(lut);
+    return (lut_term<0>(base, w0, w1, w2, hi) ^ lut_term<1>(base, w0, w1, w2, hi)) ^
+           (lut_term<2>(base, w0, w1, w2, hi) ^ lut_term<3>(base, w0, w1, w2, hi)) ^
+           (lut_term<4>(base, w0, w1, w2, hi) ^ lut_term<5>(base, w0, w1, w2, hi)) ^
+           (lut_term<6>(base, w0, w1, w2, hi) ^ lut_term<7>(base, w0, w1, w2, hi));
 }
 
 // hash % htable  (simulator.py:97, first modulo)
@@ -131,10 +173,10 @@ __device__ __forceinline__ uint32_t queue_of(uint32_t b, const LaunchParams& p) 
 }
 
 template <int kHist>
-__device__ __forceinline__ void count_queue(uint32_t* bins, uint32_t q, uint32_t lane,
+__device__ __forceinline__ void count_queue(uint32_t* bins, uint32_t q, uint32_t col,
                                             const LaunchParams& p) {
     if constexpr (kHist == HIST_PRIVATE) {
-        __hip_atomic_fetch_add(&bins[q * kCopies + lane], 1u, __ATOMIC_RELAXED,
+        __hip_atomic_fetch_add(&bins[q * kBinCols + col], 1u, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP);
     } else if constexpr (kHist == HIST_SHARED) {
         __hip_atomic_fetch_add(&bins[q], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -143,33 +185,69 @@ __device__ __forceinline__ void count_queue(uint32_t* bins, uint32_t q, uint32_t
     }
 }
 
-template <bool kHPow2, int kQMode, int kHist>
-__device__ __forceinline__ void one_tuple(const uint32_t* lds, uint32_t* bins, uint64_t i,
-                                          uint32_t lane, const LaunchParams& p) {
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(p.tuples) + 3 * i;
-    const uint32_t h = toeplitz_lut(lds, src[0], src[1], src[2], lane * 4);
-    const uint32_t q = queue_of<kQMode>(bucket_of<kHPow2>(h, p), p);
-    if (p.hash_out) p.hash_out[i] = h;
-    if (p.queue_out) p.queue_out[i] = q;
-    count_queue<kHist>(bins, q, lane, p);
+// Streaming outputs are written once and never re-read by this kernel: use
+// nontemporal stores so they do not displace the input stream in L2.
+template <typename T>
+__device__ __forceinline__ void stream_store(T* dst, T v) {
+    __builtin_nontemporal_store(v, dst);
 }
 
-template <bool kHPow2, int kQMode, int kHist, bool kVec4>
+template <int kQWidth>
+__device__ __forceinline__ void store_queue1(void* out, uint64_t i, uint32_t q) {
+    if constexpr (kQWidth == QW_U8) {
+        stream_store(static_cast<uint8_t*>(out) + i, (uint8_t)q);
+    } else if constexpr (kQWidth == QW_U16) {
+        stream_store(static_cast<uint16_t*>(out) + i, (uint16_t)q);
+    } else {
+        stream_store(static_cast<uint32_t*>(out) + i, q);
+    }
+}
+
+// four consecutive queues of group g (tuples 4g .. 4g+3) as one 4/8/16-byte store
+template <int kQWidth>
+__device__ __forceinline__ void store_queue4(void* out, uint64_t g, uint32_t q0, uint32_t q1,
+                                             uint32_t q2, uint32_t q3) {
+    if constexpr (kQWidth == QW_U8) {
+        stream_store(static_cast<uint32_t*>(out) + g, q0 | q1 << 8 | q2 << 16 | q3 << 24);
+    } else if constexpr (kQWidth == QW_U16) {
+        uint32_t* o = static_cast<uint32_t*>(out) + 2 * g;
+        stream_store(o, q0 | q1 << 16);
+        stream_store(o + 1, q2 | q3 << 16);
+    } else {
+        uint32_t* o = static_cast<uint32_t*>(out) + 4 * g;
+        stream_store(o, q0);
+        stream_store(o + 1, q1);
+        stream_store(o + 2, q2);
+        stream_store(o + 3, q3);
+    }
+}
+
+template <bool kHPow2, int kQMode, int kHist, int kQWidth>
+__device__ __forceinline__ void one_tuple(const uint32_t* lut, uint32_t* bins, uint64_t i,
+                                          uint32_t col, uint32_t hi, const LaunchParams& p) {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(p.tuples) + 3 * i;
+    const uint32_t h = toeplitz_hash(lut, src[0], src[1], src[2], hi);
+    const uint32_t q = queue_of<kQMode>(bucket_of<kHPow2>(h, p), p);
+    if (p.hash_out) stream_store(p.hash_out + i, h);
+    if (p.queue_out) store_queue1<kQWidth>(p.queue_out, i, q);
+    count_queue<kHist>(bins, q, col, p);
+}
+
+template <bool kHPow2, int kQMode, int kHist, int kQWidth, bool kVec4>
 __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams p) {
-    __shared__ uint32_t smem[kLutDwords];  // static: table offsets fold into ds_read
-    extern __shared__ uint32_t bins[];      // histogram bins, sized at launch
+    __shared__ uint32_t lut[kLutDwords];  // static: table offsets fold into ds_read
+    extern __shared__ uint32_t bins[];    // histogram bins, sized at launch
     const uint32_t tid = threadIdx.x;
 
-    // Prologue: replicate the 24x16 nibble table 32x (entry-major, replica-minor).
-    for (uint32_t e = tid; e < kLutDwords; e += kBlock) smem[e] = p.lut[e >> 9][(e >> 5) & 15];
+    build_lut(lut, p, tid);
     const uint32_t nbins =
-        kHist == HIST_PRIVATE ? p.Q * kCopies : (kHist == HIST_SHARED ? p.Q : 0u);
+        kHist == HIST_PRIVATE ? p.Q * kBinCols : (kHist == HIST_SHARED ? p.Q : 0u);
     for (uint32_t e = tid; e < nbins; e += kBlock) bins[e] = 0;
     __syncthreads();
 
-    const uint32_t lane = tid & (kCopies - 1);
-    uint32_t lane4 = lane * 4;
-    asm volatile("" : "+v"(lane4));  // hide the known-zero bits (see toeplitz_lut)
+    const uint32_t col = tid & (kBinCols - 1);
+    uint32_t hi = 4 * kTableEntries * 4;  // byte base of tables 4..7
+    asm volatile("" : "+v"(hi));          // keep it opaque (see chunk_offset)
     const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
     const uint64_t gstride = (uint64_t)gridDim.x * kBlock;
     uint64_t tail_begin = 0;
@@ -182,26 +260,31 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
             const uint4 a = src[3 * g + 0];
             const uint4 b = src[3 * g + 1];
             const uint4 c = src[3 * g + 2];
-            uint4 h, q;
-            h.x = toeplitz_lut(smem, a.x, a.y, a.z, lane4);
-            h.y = toeplitz_lut(smem, a.w, b.x, b.y, lane4);
-            h.z = toeplitz_lut(smem, b.z, b.w, c.x, lane4);
-            h.w = toeplitz_lut(smem, c.y, c.z, c.w, lane4);
-            q.x = queue_of<kQMode>(bucket_of<kHPow2>(h.x, p), p);
-            q.y = queue_of<kQMode>(bucket_of<kHPow2>(h.y, p), p);
-            q.z = queue_of<kQMode>(bucket_of<kHPow2>(h.z, p), p);
-            q.w = queue_of<kQMode>(bucket_of<kHPow2>(h.w, p), p);
-            if (p.hash_out) reinterpret_cast<uint4*>(p.hash_out)[g] = h;
-            if (p.queue_out) reinterpret_cast<uint4*>(p.queue_out)[g] = q;
-            count_queue<kHist>(bins, q.x, lane, p);
-            count_queue<kHist>(bins, q.y, lane, p);
-            count_queue<kHist>(bins, q.z, lane, p);
-            count_queue<kHist>(bins, q.w, lane, p);
+            const uint32_t h0 = toeplitz_hash(lut, a.x, a.y, a.z, hi);
+            const uint32_t h1 = toeplitz_hash(lut, a.w, b.x, b.y, hi);
+            const uint32_t h2 = toeplitz_hash(lut, b.z, b.w, c.x, hi);
+            const uint32_t h3 = toeplitz_hash(lut, c.y, c.z, c.w, hi);
+            const uint32_t q0 = queue_of<kQMode>(bucket_of<kHPow2>(h0, p), p);
+            const uint32_t q1 = queue_of<kQMode>(bucket_of<kHPow2>(h1, p), p);
+            const uint32_t q2 = queue_of<kQMode>(bucket_of<kHPow2>(h2, p), p);
+            const uint32_t q3 = queue_of<kQMode>(bucket_of<kHPow2>(h3, p), p);
+            if (p.hash_out) {
+                uint32_t* o = p.hash_out + 4 * g;
+                stream_store(o, h0);
+                stream_store(o + 1, h1);
+                stream_store(o + 2, h2);
+                stream_store(o + 3, h3);
+            }
+            if (p.queue_out) store_queue4<kQWidth>(p.queue_out, g, q0, q1, q2, q3);
+            count_queue<kHist>(bins, q0, col, p);
+            count_queue<kHist>(bins, q1, col, p);
+            count_queue<kHist>(bins, q2, col, p);
+            count_queue<kHist>(bins, q3, col, p);
         }
         tail_begin = ngroups << 2;
     }
     for (uint64_t i = tail_begin + gtid; i < p.n; i += gstride)
-        one_tuple<kHPow2, kQMode, kHist>(smem, bins, i, lane, p);
+        one_tuple<kHPow2, kQMode, kHist, kQWidth>(lut, bins, i, col, hi, p);
 
     // Epilogue: fold this workgroup's bins into the global uint64 counts.
     if constexpr (kHist == HIST_PRIVATE || kHist == HIST_SHARED) {
@@ -210,7 +293,8 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
             uint32_t s;
             if constexpr (kHist == HIST_PRIVATE) {
                 s = 0;
-                for (uint32_t c = 0; c < kCopies; ++c) s += bins[q * kCopies + ((c + q) & 31)];
+                for (uint32_t c = 0; c < kBinCols; ++c)
+                    s += bins[q * kBinCols + ((c + q) & (kBinCols - 1))];
             } else {
                 s = bins[q];
             }
@@ -263,28 +347,37 @@ int device_info(DeviceInfo* out) {
 
 using KernelFn = void (*)(const LaunchParams);
 
-template <bool kHPow2, int kQMode, int kHist>
+template <bool kHPow2, int kQMode, int kHist, int kQWidth>
 KernelFn pick_vec(bool vec4) {
-    return vec4 ? rss_toeplitz_kernel<kHPow2, kQMode, kHist, true>
-                : rss_toeplitz_kernel<kHPow2, kQMode, kHist, false>;
+    return vec4 ? rss_toeplitz_kernel<kHPow2, kQMode, kHist, kQWidth, true>
+                : rss_toeplitz_kernel<kHPow2, kQMode, kHist, kQWidth, false>;
+}
+
+template <bool kHPow2, int kQMode, int kHist>
+KernelFn pick_width(int qwidth, bool vec4) {
+    switch (qwidth) {
+        case QW_U8: return pick_vec<kHPow2, kQMode, kHist, QW_U8>(vec4);
+        case QW_U16: return pick_vec<kHPow2, kQMode, kHist, QW_U16>(vec4);
+        default: return pick_vec<kHPow2, kQMode, kHist, QW_U32>(vec4);
+    }
 }
 
 template <bool kHPow2, int kQMode>
-KernelFn pick_hist(int hist, bool vec4) {
+KernelFn pick_hist(int hist, int qwidth, bool vec4) {
     switch (hist) {
-        case HIST_PRIVATE: return pick_vec<kHPow2, kQMode, HIST_PRIVATE>(vec4);
-        case HIST_SHARED: return pick_vec<kHPow2, kQMode, HIST_SHARED>(vec4);
-        case HIST_GLOBAL: return pick_vec<kHPow2, kQMode, HIST_GLOBAL>(vec4);
-        default: return pick_vec<kHPow2, kQMode, HIST_NONE>(vec4);
+        case HIST_PRIVATE: return pick_width<kHPow2, kQMode, HIST_PRIVATE>(qwidth, vec4);
+        case HIST_SHARED: return pick_width<kHPow2, kQMode, HIST_SHARED>(qwidth, vec4);
+        case HIST_GLOBAL: return pick_width<kHPow2, kQMode, HIST_GLOBAL>(qwidth, vec4);
+        default: return pick_width<kHPow2, kQMode, HIST_NONE>(qwidth, vec4);
     }
 }
 
 template <bool kHPow2>
-KernelFn pick_queue(int qmode, int hist, bool vec4) {
+KernelFn pick_queue(int qmode, int hist, int qwidth, bool vec4) {
     switch (qmode) {
-        case QM_MASK: return pick_hist<kHPow2, QM_MASK>(hist, vec4);
-        case QM_FAST16: return pick_hist<kHPow2, QM_FAST16>(hist, vec4);
-        default: return pick_hist<kHPow2, QM_FAST32>(hist, vec4);
+        case QM_MASK: return pick_hist<kHPow2, QM_MASK>(hist, qwidth, vec4);
+        case QM_FAST16: return pick_hist<kHPow2, QM_FAST16>(hist, qwidth, vec4);
+        default: return pick_hist<kHPow2, QM_FAST32>(hist, qwidth, vec4);
     }
 }
 
@@ -297,7 +390,7 @@ uint64_t magic64(uint32_t d) { return UINT64_MAX / d + 1; }
 uint32_t magic32(uint32_t d) { return UINT32_MAX / d + 1; }
 
 int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32_t htable,
-                uint32_t nqueues, uint32_t* d_hash, uint32_t* d_queue, uint64_t* d_counts,
+                uint32_t nqueues, uint32_t* d_hash, void* d_queue, uint64_t* d_counts,
                 uint32_t flags, hipStream_t stream) {
     if (!key) return set_error(RSS_EINVAL, "rss_hash_device: key is NULL");
     if (key->len < RSS_KEY_MIN_BYTES)
@@ -306,16 +399,27 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
         return set_error(RSS_EINVAL, "rss_hash_device: htable (%u) and nqueues (%u) must be >= 1",
                          htable, nqueues);
     if (n && !d_tuples) return set_error(RSS_EINVAL, "rss_hash_device: tuples is NULL");
+    int qwidth = QW_U32;
+    if (flags & RSS_FLAG_QUEUE_U8) {
+        if (nqueues > 256)
+            return set_error(RSS_EINVAL, "rss_hash_device: RSS_FLAG_QUEUE_U8 needs nqueues <= 256");
+        qwidth = QW_U8;
+    } else if (flags & RSS_FLAG_QUEUE_U16) {
+        if (nqueues > 65536)
+            return set_error(RSS_EINVAL, "rss_hash_device: RSS_FLAG_QUEUE_U16 needs nqueues <= 65536");
+        qwidth = QW_U16;
+    }
     if (d_counts && !(flags & RSS_FLAG_ACCUMULATE))
         RSS_HIP_CHECK(hipMemsetAsync(d_counts, 0, sizeof(uint64_t) * nqueues, stream));
     if (n == 0) return RSS_OK;
 
     LaunchParams p;
     memset(&p, 0, sizeof p);
-    memcpy(p.lut, key->nibble_lut, sizeof p.lut);
+    memcpy(p.window, key->window, sizeof p.window);
     p.tuples = d_tuples;
     p.hash_out = d_hash;
     p.queue_out = d_queue;
+
     p.counts = reinterpret_cast<unsigned long long*>(d_counts);
     p.n = n;
     p.H = htable;
@@ -341,18 +445,22 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
     uint32_t bin_bytes = 0;
     if (!d_counts) {
         hist = HIST_NONE;
-    } else if ((uint64_t)nqueues * kCopies * 4 <= kBinBytesMax) {
+    } else if ((uint64_t)nqueues * kBinCols * 4 <= kBinBytesMax) {
         hist = HIST_PRIVATE;
-        bin_bytes = nqueues * kCopies * 4;
+        bin_bytes = nqueues * kBinCols * 4;
     } else if ((uint64_t)nqueues * 4 <= kBinBytesMax) {
         hist = HIST_SHARED;
         bin_bytes = nqueues * 4;
     } else {
         hist = HIST_GLOBAL;
     }
+    // the 4-tuples-per-lane body needs 16-B aligned tuples / hashes and a queue
+    // pointer aligned to the 4 queues it stores at once
+    const uintptr_t qalign = qwidth == QW_U8 ? 4 : (qwidth == QW_U16 ? 8 : 16);
     const bool vec4 = aligned16(d_tuples) && (!d_hash || aligned16(d_hash)) &&
-                      (!d_queue || aligned16(d_queue));
-    KernelFn fn = h_pow2 ? pick_queue<true>(qmode, hist, vec4) : pick_queue<false>(qmode, hist, vec4);
+                      (!d_queue || ((uintptr_t)d_queue % qalign) == 0);
+    KernelFn fn = h_pow2 ? pick_queue<true>(qmode, hist, qwidth, vec4)
+                         : pick_queue<false>(qmode, hist, qwidth, vec4);
 
     DeviceInfo info;
     int rc = device_info(&info);
@@ -361,7 +469,7 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
     const uint64_t want = (n + per_lane * kBlock - 1) / (per_lane * kBlock);
     const uint64_t cap = (uint64_t)info.cu_count * kBlocksPerCU;
     const unsigned grid = (unsigned)(want < cap ? want : cap);
-    const uint32_t shmem = bin_bytes;  // dynamic part; the 48 KiB LUT is static
+    const uint32_t shmem = bin_bytes;  // dynamic part; the 128 KiB LUT is static
     hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), shmem, stream, p);
     RSS_HIP_CHECK(hipGetLastError());
     return RSS_OK;
@@ -408,13 +516,6 @@ int rss_key_prepare(const uint8_t* key, size_t len, rss_key* out) {
         for (int j = 0; j < 32; ++j) w = (w << 1) | bit(((uint64_t)i + j) % nbits);
         out->window[i] = w;
     }
-    for (int t = 0; t < RSS_NIBBLES; ++t)
-        for (uint32_t v = 0; v < 16; ++v) {
-            uint32_t x = 0;
-            for (int j = 0; j < 4; ++j)
-                if (v & (8u >> j)) x ^= out->window[4 * t + j];
-            out->nibble_lut[t][v] = x;
-        }
     return RSS_OK;
 }
 
@@ -437,7 +538,7 @@ int rss_device_count(int* out) {
 }
 
 int rss_hash_device(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32_t htable,
-                    uint32_t nqueues, uint32_t* d_hash, uint32_t* d_queue, uint64_t* d_counts,
+                    uint32_t nqueues, uint32_t* d_hash, void* d_queue, uint64_t* d_counts,
                     uint32_t flags, void* stream) {
     return launch_hash(key, d_tuples, n, htable, nqueues, d_hash, d_queue, d_counts, flags,
                        static_cast<hipStream_t>(stream));
@@ -584,7 +685,7 @@ int rss_hash_host(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples, 
                                      hipMemcpyHostToDevice, s));
         rc = launch_hash(key, ctx->d_in[b], len, htable, nqueues, h_hash ? ctx->d_hash[b] : nullptr,
                          h_queue ? ctx->d_queue[b] : nullptr, ctx->d_counts[b],
-                         RSS_FLAG_ACCUMULATE, s);
+                         RSS_FLAG_ACCUMULATE, s);  // u32 queues on the host path
         if (rc) return rc;
         if (h_hash)
             RSS_HIP_CHECK(hipMemcpyAsync(ctx->h_hash[b], ctx->d_hash[b], len * 4,

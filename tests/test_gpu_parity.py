@@ -212,3 +212,36 @@ def test_256M_sweep_counts_and_digest(native, oracle_lib, example_key):
             want = np.bincount(((ho % H) % Q).astype(np.int64), minlength=Q).astype(np.uint64)
             np.testing.assert_array_equal(_u64(counts), want)
             assert int(want.sum()) == n
+
+
+@pytest.mark.parametrize("width,flag_name,dtype", [("u8", "FLAG_QUEUE_U8", np.uint8),
+                                                   ("u16", "FLAG_QUEUE_U16", np.uint16)])
+@pytest.mark.parametrize("H,Q", [(128, 24), (512, 256), (100, 7), (65536, 1000)])
+def test_narrow_queue_outputs(native, oracle_lib, example_key, width, flag_name, dtype, H, Q):
+    if width == "u8" and Q > 256:
+        pytest.skip("u8 holds at most 256 queues")
+    dev = torch.device("cuda:0")
+    s = torch.cuda.current_stream(dev).cuda_stream
+    n = 65537
+    key = native.prepare_key(example_key)
+    tup_host = oracle_lib.generate(H + Q, 0, n)
+    _, qo, co = oracle_lib.run(example_key, tup_host, H, Q)
+    raw = torch.from_numpy(tup_host.view(np.int32).reshape(-1)).to(dev)
+    item = np.dtype(dtype).itemsize
+    for offset in (0, item):  # aligned (4-tuple stores) and misaligned (scalar stores)
+        buf = torch.full((n * item + 64,), 0xAB, dtype=torch.uint8, device=dev)
+        counts = torch.empty(Q, dtype=torch.int64, device=dev)
+        native.hash_device(key, raw.data_ptr(), n, H, Q, None, buf.data_ptr() + offset,
+                           counts.data_ptr(), getattr(native, flag_name), s)
+        torch.cuda.synchronize()
+        got = buf.cpu().numpy()
+        np.testing.assert_array_equal(got[offset:offset + n * item].view(dtype), qo.astype(dtype))
+        assert (got[:offset] == 0xAB).all() and (got[offset + n * item:] == 0xAB).all()
+        np.testing.assert_array_equal(_u64(counts), co)
+
+
+def test_narrow_queue_rejects_overflowing_queue_count(native, example_key):
+    from rss_simulator_nvidia_amd.exceptions import DeviceError
+    key = native.prepare_key(example_key)
+    with pytest.raises(DeviceError, match="QUEUE_U8"):
+        native.hash_device(key, 0, 0, 1024, 257, None, None, None, native.FLAG_QUEUE_U8)

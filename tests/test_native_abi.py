@@ -49,13 +49,13 @@ def test_struct_layout_matches_c(tmp_path):
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "rss_toeplitz.h"\n'
                    'int main(void){printf("%zu %zu %zu %zu %zu\\n", sizeof(rss_tuple4), '
                    'sizeof(rss_key), offsetof(rss_key, bytes), offsetof(rss_key, window), '
-                   'offsetof(rss_key, nibble_lut));return 0;}\n')
+                   'offsetof(rss_key, len));return 0;}\n')
     exe = tmp_path / "layout"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
     K = _native.RssKey
     assert got == [ctypes.sizeof(_native.RssTuple4), ctypes.sizeof(K), K.bytes.offset,
-                   K.window.offset, K.nibble_lut.offset]
+                   K.window.offset, K.len.offset]
 
 
 def test_key_prepare_matches_oracle_windows(lib, random_golden, oracle_lib):
@@ -66,15 +66,8 @@ def test_key_prepare_matches_oracle_windows(lib, random_golden, oracle_lib):
         k = _native.prepare_key(key)
         w = np.ctypeslib.as_array(k.window)
         np.testing.assert_array_equal(w, oracle_lib.windows(key))
-        lut = np.ctypeslib.as_array(k.nibble_lut).reshape(24, 16)
-        for t in range(24):
-            for v in range(16):
-                x = 0
-                for j in range(4):
-                    if v & (8 >> j):
-                        x ^= int(w[4 * t + j])
-                assert lut[t, v] == x
         assert k.len == len(key)
+        assert bytes(k.bytes[:min(len(key), 52)]) == bytes(key[:52])
 
 
 def test_key_prepare_rejects_short_keys(lib):
@@ -94,6 +87,10 @@ def test_argument_validation_before_any_device_work(lib, example_key):
         _native.hash_device(key, 0, 16, 128, 0)
     with pytest.raises(DeviceError, match="tuples is NULL"):
         _native.hash_device(key, None, 16, 128, 24)
+    with pytest.raises(DeviceError, match="QUEUE_U8 needs nqueues <= 256"):
+        _native.hash_device(key, 0, 0, 1024, 257, None, None, None, _native.FLAG_QUEUE_U8)
+    with pytest.raises(DeviceError, match="QUEUE_U16 needs nqueues <= 65536"):
+        _native.hash_device(key, 0, 0, 2**20, 65537, None, None, None, _native.FLAG_QUEUE_U16)
     empty = _native.RssKey()
     with pytest.raises(DeviceError, match="key not prepared"):
         _native.hash_device(empty, 0, 16, 128, 24)

@@ -1,0 +1,295 @@
+// kbench.hip -- design-space microbenchmark for the Toeplitz kernel (tool, not product).
+//
+// Times, on 2^28 resident synthetic tuples (H = 128, Q = 24), on one MI355X:
+//   * memory ceilings: read-only (12 B/tuple) and read+write (20 B/tuple) streams
+//     with the same access shape as the product kernel;
+//   * LUT variants: chunk width B in {4, 6, 8} bits, LDS replicas R, workgroup
+//     size, tuples per lane per iteration, software prefetch, full vs counts-only;
+// and checks every variant's hash/queue/count output against the product kernel
+// (librss_toeplitz.so through the C ABI).
+//
+// build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include tools/kbench.hip \
+//          -L rss_simulator_nvidia_amd -lrss_toeplitz -o tools/kbench
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "rss_toeplitz.h"
+
+#define CK(x)                                                                              \
+    do {                                                                                   \
+        hipError_t e = (x);                                                                \
+        if (e != hipSuccess) {                                                             \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e)); \
+            exit(1);                                                                       \
+        }                                                                                  \
+    } while (0)
+
+struct Params {
+    const uint32_t* tuples;
+    uint32_t* hash_out;
+    uint32_t* queue_out;
+    unsigned long long* counts;
+    uint64_t n;
+    uint32_t Q, q_m32, h_mask;
+    uint32_t window[96];
+};
+
+// ------------------------------------------------------------ memory ceilings
+template <bool kWrite>
+__global__ __launch_bounds__(1024) void mem_ceiling(Params p) {
+    const uint4* src = reinterpret_cast<const uint4*>(p.tuples);
+    const uint64_t ng = p.n >> 2;
+    uint32_t acc = 0;
+    for (uint64_t g = (uint64_t)blockIdx.x * 1024 + threadIdx.x; g < ng; g += (uint64_t)gridDim.x * 1024) {
+        uint4 a = src[3 * g], b = src[3 * g + 1], c = src[3 * g + 2];
+        uint4 h = make_uint4(a.x ^ a.y ^ a.z, a.w ^ b.x ^ b.y, b.z ^ b.w ^ c.x, c.y ^ c.z ^ c.w);
+        if constexpr (kWrite) {
+            reinterpret_cast<uint4*>(p.hash_out)[g] = h;
+            reinterpret_cast<uint4*>(p.queue_out)[g] = make_uint4(h.x & 23, h.y & 23, h.z & 23, h.w & 23);
+        } else {
+            acc ^= h.x ^ h.y ^ h.z ^ h.w;
+        }
+    }
+    if (!kWrite && acc == 0x12345678u) p.counts[0] = acc;  // keep the loads alive
+}
+
+// ------------------------------------------------------------ LUT variants
+// chunk t covers input bits [t*B, t*B + B) of the 96-bit MSB-first string.
+template <int B>
+__device__ __forceinline__ uint32_t chunk_addr(const uint32_t (&w)[3], int t, uint32_t lane4,
+                                               int rshift) {
+    // returns (chunk value << rshift) | lane4, rshift = log2(R * 4)
+    const int s = t * B, wi = s >> 5, o = s & 31;
+    const uint32_t mask = ((1u << B) - 1) << rshift;
+    if (o + B <= 32) {
+        const int sh = 32 - o - B - rshift;  // right shift that lands the chunk at rshift
+        const uint32_t moved = sh >= 0 ? (w[wi] >> sh) : (w[wi] << -sh);
+        return (moved & mask) | lane4;
+    }
+    const uint32_t v = __builtin_amdgcn_alignbit(w[wi], w[wi + 1], 64 - o - B);
+    return ((v << rshift) & mask) | lane4;
+}
+
+template <int B, int R>
+__device__ __forceinline__ uint32_t hash_lut(const char* lds, const uint32_t (&w)[3], uint32_t lane4) {
+    constexpr int C = 96 / B, E = 1 << B;
+    constexpr int RS = R == 32 ? 7 : (R == 16 ? 6 : (R == 8 ? 5 : (R == 4 ? 4 : (R == 2 ? 3 : 2))));
+    constexpr int TB = E * R * 4;  // table bytes
+    uint32_t r[C];
+#pragma unroll
+    for (int t = 0; t < C; ++t)
+        r[t] = *reinterpret_cast<const uint32_t*>(lds + t * TB + chunk_addr<B>(w, t, lane4, RS));
+    uint32_t h = 0;
+#pragma unroll
+    for (int t = 0; t < C; ++t) h ^= r[t];
+    return h;
+}
+
+template <int B, int R, int BLOCK, bool kWrite, bool kPrefetch, bool kQ8 = false, bool kNT = false>
+__global__ __launch_bounds__(BLOCK) void lut_kernel(Params p) {
+    constexpr int C = 96 / B, E = 1 << B;
+    constexpr int DW = C * E * R;
+    __shared__ uint32_t lut[DW];
+    __shared__ uint32_t bins[64 * 32];
+    for (int e = threadIdx.x; e < DW; e += BLOCK) {
+        const int t = e / (E * R), v = (e / R) % E;
+        uint32_t x = 0;
+        for (int j = 0; j < B; ++j)
+            if (v & (1 << (B - 1 - j))) x ^= p.window[t * B + j];
+        lut[e] = x;
+    }
+    for (int e = threadIdx.x; e < (int)p.Q * 32; e += BLOCK) bins[e] = 0;
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 31;
+    uint32_t lane4 = (lane & (R - 1)) * 4;
+    asm volatile("" : "+v"(lane4));
+    const char* lds = reinterpret_cast<const char*>(lut);
+    const uint4* src = reinterpret_cast<const uint4*>(p.tuples);
+    const uint64_t ng = p.n >> 2;
+    const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+    uint64_t g = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    uint4 a, b, c;
+    if (kPrefetch && g < ng) { a = src[3 * g]; b = src[3 * g + 1]; c = src[3 * g + 2]; }
+    for (; g < ng; g += stride) {
+        if (!kPrefetch) { a = src[3 * g]; b = src[3 * g + 1]; c = src[3 * g + 2]; }
+        const uint32_t w0[3] = {a.x, a.y, a.z}, w1[3] = {a.w, b.x, b.y};
+        const uint32_t w2[3] = {b.z, b.w, c.x}, w3[3] = {c.y, c.z, c.w};
+        if (kPrefetch && g + stride < ng) {
+            a = src[3 * (g + stride)]; b = src[3 * (g + stride) + 1]; c = src[3 * (g + stride) + 2];
+        }
+        uint4 h, q;
+        h.x = hash_lut<B, R>(lds, w0, lane4);
+        h.y = hash_lut<B, R>(lds, w1, lane4);
+        h.z = hash_lut<B, R>(lds, w2, lane4);
+        h.w = hash_lut<B, R>(lds, w3, lane4);
+        q.x = __umulhi(p.q_m32 * (h.x & p.h_mask), p.Q);
+        q.y = __umulhi(p.q_m32 * (h.y & p.h_mask), p.Q);
+        q.z = __umulhi(p.q_m32 * (h.z & p.h_mask), p.Q);
+        q.w = __umulhi(p.q_m32 * (h.w & p.h_mask), p.Q);
+        if (kWrite) {
+            if (kNT) {
+                uint32_t* o = p.hash_out + 4 * g;
+                __builtin_nontemporal_store(h.x, o); __builtin_nontemporal_store(h.y, o + 1);
+                __builtin_nontemporal_store(h.z, o + 2); __builtin_nontemporal_store(h.w, o + 3);
+            } else {
+                reinterpret_cast<uint4*>(p.hash_out)[g] = h;
+            }
+            if (kQ8) {
+                reinterpret_cast<uint32_t*>(p.queue_out)[g] = q.x | q.y << 8 | q.z << 16 | q.w << 24;
+            } else if (kNT) {
+                uint32_t* o = p.queue_out + 4 * g;
+                __builtin_nontemporal_store(q.x, o); __builtin_nontemporal_store(q.y, o + 1);
+                __builtin_nontemporal_store(q.z, o + 2); __builtin_nontemporal_store(q.w, o + 3);
+            } else {
+                reinterpret_cast<uint4*>(p.queue_out)[g] = q;
+            }
+        }
+        atomicAdd(&bins[q.x * 32 + lane], 1u);
+        atomicAdd(&bins[q.y * 32 + lane], 1u);
+        atomicAdd(&bins[q.z * 32 + lane], 1u);
+        atomicAdd(&bins[q.w * 32 + lane], 1u);
+    }
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < p.Q; q += BLOCK) {
+        uint32_t s = 0;
+        for (int k = 0; k < 32; ++k) s += bins[q * 32 + ((k + q) & 31)];
+        if (s) atomicAdd(&p.counts[q], (unsigned long long)s);
+    }
+}
+
+// ------------------------------------------------------------------ harness
+static int g_cus = 256;
+
+template <typename F>
+static float time_ms(F launch, int reps) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    launch();
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(a));
+    for (int i = 0; i < reps; ++i) launch();
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    return ms / reps;
+}
+
+int main(int argc, char** argv) {
+    const uint64_t n = argc > 1 ? strtoull(argv[1], 0, 0) : (1ull << 28);
+    const int reps = argc > 2 ? atoi(argv[2]) : 20;
+    const uint32_t H = 128, Q = 24;
+    CK(hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, 0));
+    const uint8_t key_bytes[40] = {0x23, 0x0d, 0x44, 0x3d, 0x8c, 0x2c, 0x6e, 0x64, 0xd4, 0x1a,
+                                   0xf3, 0x44, 0x49, 0x9b, 0x21, 0x74, 0xfd, 0x1a, 0x9d, 0xc1,
+                                   0xdd, 0x76, 0x77, 0x37, 0x38, 0x51, 0x66, 0x85, 0x7b, 0xdc,
+                                   0x48, 0xa8, 0x3e, 0x55, 0x08, 0xc1, 0x63, 0xaf, 0x01, 0x9d};
+    rss_key key;
+    if (rss_key_prepare(key_bytes, 40, &key)) return 1;
+    uint32_t *tup, *h0, *q0, *h1, *q1;
+    unsigned long long *c0, *c1;
+    CK(hipMalloc(&tup, n * 12));
+    CK(hipMalloc(&h0, n * 4));
+    CK(hipMalloc(&q0, n * 4));
+    CK(hipMalloc(&h1, n * 4));
+    CK(hipMalloc(&q1, n * 4));
+    CK(hipMalloc(&c0, Q * 8));
+    CK(hipMalloc(&c1, Q * 8));
+    if (rss_generate_tuples(0x5EED, 0, n, (rss_tuple4*)tup, nullptr)) return 1;
+    CK(hipDeviceSynchronize());
+
+    auto prod = [&](bool write) {
+        if (rss_hash_device(&key, (rss_tuple4*)tup, n, H, Q, write ? h0 : nullptr, write ? q0 : nullptr,
+                            (uint64_t*)c0, 0, nullptr)) {
+            fprintf(stderr, "prod failed: %s\n", rss_last_error());
+            exit(1);
+        }
+    };
+    const double gb_r = n * 12.0 / 1e9, gb_rw = n * 20.0 / 1e9;
+    float t = time_ms([&] { prod(true); }, reps);
+    printf("%-40s %8.3f ms  %7.1f Gt/s  %6.0f GB/s\n", "product full", t, n / t / 1e6, gb_rw / t * 1e3);
+    t = time_ms([&] { prod(false); }, reps);
+    printf("%-40s %8.3f ms  %7.1f Gt/s  %6.0f GB/s\n", "product counts", t, n / t / 1e6, gb_r / t * 1e3);
+    prod(true);
+    CK(hipDeviceSynchronize());
+    std::vector<uint32_t> rh0(n), rq0(n), rh1(n), rq1(n);
+    std::vector<unsigned long long> rc0(Q), rc1(Q);
+    CK(hipMemcpy(rh0.data(), h0, n * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(rq0.data(), q0, n * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(rc0.data(), c0, Q * 8, hipMemcpyDeviceToHost));
+
+    Params p;
+    p.tuples = tup;
+    p.hash_out = h1;
+    p.queue_out = q1;
+    p.counts = c1;
+    p.n = n;
+    p.Q = Q;
+    p.q_m32 = 0xFFFFFFFFu / Q + 1;
+    p.h_mask = H - 1;
+    memcpy(p.window, key.window, sizeof p.window);
+
+    const char* filter = argc > 3 ? argv[3] : "";
+    for (int wpc : {1, 2}) {
+        if (!strstr("mem", filter)) break;
+        char name[64];
+        snprintf(name, sizeof name, "mem read-only grid=%dx", wpc);
+        t = time_ms([&] { hipLaunchKernelGGL(mem_ceiling<false>, dim3(g_cus * wpc), dim3(1024), 0, 0, p); }, reps);
+        printf("%-40s %8.3f ms  %7.1f Gt/s  %6.0f GB/s\n", name, t, n / t / 1e6, gb_r / t * 1e3);
+        snprintf(name, sizeof name, "mem read+write grid=%dx", wpc);
+        t = time_ms([&] { hipLaunchKernelGGL(mem_ceiling<true>, dim3(g_cus * wpc), dim3(1024), 0, 0, p); }, reps);
+        printf("%-40s %8.3f ms  %7.1f Gt/s  %6.0f GB/s\n", name, t, n / t / 1e6, gb_rw / t * 1e3);
+    }
+
+    auto run_variant = [&](const char* name, void (*k)(Params), int block, int wgs_per_cu, bool write,
+                           bool q8 = false) {
+        if (!strstr(name, filter)) return;
+        auto launch = [&] {
+            CK(hipMemsetAsync(c1, 0, Q * 8, 0));
+            hipLaunchKernelGGL(k, dim3(g_cus * wgs_per_cu), dim3(block), 0, 0, p);
+        };
+        p.hash_out = write ? h1 : nullptr;
+        p.queue_out = write ? q1 : nullptr;
+        CK(hipMemset(h1, 0, n * 4));
+        launch();
+        CK(hipDeviceSynchronize());
+        CK(hipGetLastError());
+        bool ok = true;
+        CK(hipMemcpy(rc1.data(), c1, Q * 8, hipMemcpyDeviceToHost));
+        ok = ok && rc1 == rc0;
+        if (write) {
+            CK(hipMemcpy(rh1.data(), h1, n * 4, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(rq1.data(), q1, n * 4, hipMemcpyDeviceToHost));
+            ok = ok && rh1 == rh0;
+            if (q8) {
+                const uint8_t* b = reinterpret_cast<const uint8_t*>(rq1.data());
+                for (uint64_t i = 0; i < n && ok; ++i) ok = b[i] == rq0[i];
+            } else {
+                ok = ok && rq1 == rq0;
+            }
+        }
+        const float tt = time_ms(launch, reps);
+        printf("%-40s %8.3f ms  %7.1f Gt/s  %6.0f GB/s  %s\n", name, tt, n / tt / 1e6,
+               (write ? gb_rw : gb_r) / tt * 1e3, ok ? "OK" : "MISMATCH");
+    };
+#define V(B, R, BL, WPC, PF)                                                                   \
+    run_variant("B" #B " R" #R " blk" #BL " x" #WPC " pf" #PF " full", lut_kernel<B, R, BL, true, PF>, BL, WPC, true); \
+    run_variant("B" #B " R" #R " blk" #BL " x" #WPC " pf" #PF " counts", lut_kernel<B, R, BL, false, PF>, BL, WPC, false);
+    V(4, 32, 1024, 2, false)
+    V(6, 32, 1024, 1, false)
+    V(8, 1, 1024, 2, false)
+    V(8, 2, 1024, 2, false)
+    V(8, 8, 1024, 1, false)
+    V(12, 1, 1024, 1, false)
+    V(8, 1, 512, 4, false)
+    V(8, 1, 256, 8, false)
+    run_variant("B8 R1 blk1024 x2 q8 full", lut_kernel<8, 1, 1024, true, false, true>, 1024, 2, true, true);
+    run_variant("B8 R1 blk1024 x2 nt full", lut_kernel<8, 1, 1024, true, false, false, true>, 1024, 2, true);
+    run_variant("B8 R1 blk1024 x2 q8nt full", lut_kernel<8, 1, 1024, true, false, true, true>, 1024, 2, true, true);
+    return 0;
+}
