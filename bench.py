@@ -86,15 +86,17 @@ def cpu_baseline(key, n_sample, procs):
                       % (n_sample, procs, dt)}
 
 
-def load_traffic(profile_dir, n, htable, queues):
-    """HBM bytes per launch from a committed rocprofv3 PMC summary, if one matches."""
+def load_traffic(profile_dir, n, htable, queues, queue_width):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_summarize.py)
+    when it was measured on this exact configuration, else None."""
     path = os.path.join(profile_dir, "pmc_traffic.json")
     try:
         with open(path) as f:
             rec = json.load(f)
     except (OSError, ValueError):
         return None
-    if rec.get("tuples") == n and rec.get("htable") == htable and rec.get("queues") == queues:
+    if (rec.get("tuples"), rec.get("htable"), rec.get("queues"), rec.get("queue_width")) == \
+            (n, htable, queues, queue_width):
         return rec.get("hbm_bytes_per_launch")
     return None
 
@@ -200,7 +202,7 @@ def main():
         value = n * world * args.steps / elapsed
         kernel_s = kernel_ms / 1e3
         achieved = n * (READ_BYTES + write_bytes) / kernel_s / 1e9
-        traffic = load_traffic(args.profile_dir, n, H, Q)
+        traffic = load_traffic(args.profile_dir, n, H, Q, qw)
         line = {
             "metric": METRIC,
             "value": value,
