@@ -57,6 +57,21 @@ __global__ __launch_bounds__(1024) void mem_ceiling(Params p) {
     if (!kWrite && acc == 0x12345678u) p.counts[0] = acc;  // keep the loads alive
 }
 
+// 12 B read + 4 B hash + 1 B queue written, nontemporal stores: the bench's byte mix
+__global__ __launch_bounds__(1024) void mem_ceiling_q8(Params p) {
+    const uint4* src = reinterpret_cast<const uint4*>(p.tuples);
+    const uint64_t ng = p.n >> 2;
+    for (uint64_t g = (uint64_t)blockIdx.x * 1024 + threadIdx.x; g < ng; g += (uint64_t)gridDim.x * 1024) {
+        uint4 a = src[3 * g], b = src[3 * g + 1], c = src[3 * g + 2];
+        uint32_t* o = p.hash_out + 4 * g;
+        __builtin_nontemporal_store(a.x ^ a.y ^ a.z, o);
+        __builtin_nontemporal_store(a.w ^ b.x ^ b.y, o + 1);
+        __builtin_nontemporal_store(b.z ^ b.w ^ c.x, o + 2);
+        __builtin_nontemporal_store(c.y ^ c.z ^ c.w, o + 3);
+        __builtin_nontemporal_store((a.x ^ c.w) & 0x17171717u, p.queue_out + g);
+    }
+}
+
 // ------------------------------------------------------------ LUT variants
 // chunk t covers input bits [t*B, t*B + B) of the 96-bit MSB-first string.
 template <int B>
@@ -161,6 +176,60 @@ __global__ __launch_bounds__(BLOCK) void lut_kernel(Params p) {
     }
 }
 
+
+// 8 consecutive tuples per lane: 96 B = 6 x dwordx4 in, 2 x dwordx4 hashes + dwordx2 u8 queues out
+template <bool kWrite>
+__global__ __launch_bounds__(1024) void lut12_tpl8(Params p) {
+    constexpr int C = 8, E = 4096;
+    __shared__ uint32_t lut[C * E];
+    __shared__ uint32_t bins[64 * 32];
+    for (int e = threadIdx.x; e < C * E; e += 1024) {
+        const int t = e / E, v = e % E;
+        uint32_t x = 0;
+        for (int j = 0; j < 12; ++j)
+            if (v & (1 << (11 - j))) x ^= p.window[t * 12 + j];
+        lut[e] = x;
+    }
+    for (int e = threadIdx.x; e < (int)p.Q * 32; e += 1024) bins[e] = 0;
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 31;
+    uint32_t lane4 = 0;
+    asm volatile("" : "+v"(lane4));
+    const char* lds = reinterpret_cast<const char*>(lut);
+    const uint4* src = reinterpret_cast<const uint4*>(p.tuples);
+    const uint64_t ng = p.n >> 3;
+    const uint64_t stride = (uint64_t)gridDim.x * 1024;
+    for (uint64_t g = (uint64_t)blockIdx.x * 1024 + threadIdx.x; g < ng; g += stride) {
+        uint4 v[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) v[k] = src[6 * g + k];
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(v);
+        uint32_t h[8], q[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t ww[3] = {w[3 * k], w[3 * k + 1], w[3 * k + 2]};
+            h[k] = hash_lut<12, 1>(lds, ww, lane4);
+            q[k] = __umulhi(p.q_m32 * (h[k] & p.h_mask), p.Q);
+        }
+        if (kWrite) {
+            uint32_t* o = p.hash_out + 8 * g;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) __builtin_nontemporal_store(h[k], o + k);
+            uint32_t* oq = p.queue_out + 2 * g;
+            __builtin_nontemporal_store(q[0] | q[1] << 8 | q[2] << 16 | q[3] << 24, oq);
+            __builtin_nontemporal_store(q[4] | q[5] << 8 | q[6] << 16 | q[7] << 24, oq + 1);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) atomicAdd(&bins[q[k] * 32 + lane], 1u);
+    }
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < p.Q; q += 1024) {
+        uint32_t s = 0;
+        for (int k = 0; k < 32; ++k) s += bins[q * 32 + ((k + q) & 31)];
+        if (s) atomicAdd(&p.counts[q], (unsigned long long)s);
+    }
+}
+
 // ------------------------------------------------------------------ harness
 static int g_cus = 256;
 
@@ -203,9 +272,9 @@ int main(int argc, char** argv) {
     if (rss_generate_tuples(0x5EED, 0, n, (rss_tuple4*)tup, nullptr)) return 1;
     CK(hipDeviceSynchronize());
 
-    auto prod = [&](bool write) {
+    auto prod = [&](bool write, uint32_t flags = 0) {
         if (rss_hash_device(&key, (rss_tuple4*)tup, n, H, Q, write ? h0 : nullptr, write ? q0 : nullptr,
-                            (uint64_t*)c0, 0, nullptr)) {
+                            (uint64_t*)c0, flags, nullptr)) {
             fprintf(stderr, "prod failed: %s\n", rss_last_error());
             exit(1);
         }
@@ -215,6 +284,8 @@ int main(int argc, char** argv) {
     printf("%-40s %8.3f ms  %7.1f Gt/s  %6.0f GB/s\n", "product full", t, n / t / 1e6, gb_rw / t * 1e3);
     t = time_ms([&] { prod(false); }, reps);
     printf("%-40s %8.3f ms  %7.1f Gt/s  %6.0f GB/s\n", "product counts", t, n / t / 1e6, gb_r / t * 1e3);
+    t = time_ms([&] { prod(true, RSS_FLAG_QUEUE_U8); }, reps);
+    printf("%-40s %8.3f ms  %7.1f Gt/s  %6.0f GB/s\n", "product full u8", t, n / t / 1e6, n * 17e-9 / t * 1e3);
     prod(true);
     CK(hipDeviceSynchronize());
     std::vector<uint32_t> rh0(n), rq0(n), rh1(n), rq1(n);
@@ -246,6 +317,15 @@ int main(int argc, char** argv) {
         printf("%-40s %8.3f ms  %7.1f Gt/s  %6.0f GB/s\n", name, t, n / t / 1e6, gb_rw / t * 1e3);
     }
 
+    if (strstr("memq8", filter)) {
+        p.hash_out = h1;
+        p.queue_out = q1;
+        for (int wpc : {1, 2}) {
+            t = time_ms([&] { hipLaunchKernelGGL(mem_ceiling_q8, dim3(g_cus * wpc), dim3(1024), 0, 0, p); }, reps);
+            printf("mem 12R+5W nt grid=%dx                   %8.3f ms  %7.1f Gt/s  %6.0f GB/s\n", wpc, t,
+                   n / t / 1e6, n * 17e-9 / t * 1e3);
+        }
+    }
     auto run_variant = [&](const char* name, void (*k)(Params), int block, int wgs_per_cu, bool write,
                            bool q8 = false) {
         if (!strstr(name, filter)) return;
@@ -288,6 +368,10 @@ int main(int argc, char** argv) {
     V(12, 1, 1024, 1, false)
     V(8, 1, 512, 4, false)
     V(8, 1, 256, 8, false)
+    run_variant("B12 tpl8 q8nt full", lut12_tpl8<true>, 1024, 1, true, true);
+    run_variant("B12 R1 blk1024 x1 pf q8nt full", lut_kernel<12, 1, 1024, true, true, true, true>, 1024, 1, true, true);
+    run_variant("B12 tpl8 counts", lut12_tpl8<false>, 1024, 1, false);
+    run_variant("B12 R1 blk1024 x1 q8nt full", lut_kernel<12, 1, 1024, true, false, true, true>, 1024, 1, true, true);
     run_variant("B8 R1 blk1024 x2 q8 full", lut_kernel<8, 1, 1024, true, false, true>, 1024, 2, true, true);
     run_variant("B8 R1 blk1024 x2 nt full", lut_kernel<8, 1, 1024, true, false, false, true>, 1024, 2, true);
     run_variant("B8 R1 blk1024 x2 q8nt full", lut_kernel<8, 1, 1024, true, false, true, true>, 1024, 2, true, true);
