@@ -37,6 +37,7 @@ extern "C" {
 #define RSS_ENOMEM (-12)  /* device or pinned allocation failed                   */
 #define RSS_EINVAL (-22)  /* bad argument (NULL, bad key length, zero htable ...) */
 #define RSS_ENODEV (-19)  /* no usable gfx950 device                              */
+#define RSS_ENOTSUP (-95) /* CSV not in the canonical fast-path form (use pandas)  */
 
 /*
  * One IPv4 4-tuple, packed to 12 bytes, 4-byte aligned.  The three host-order
@@ -131,6 +132,41 @@ void rss_ctx_destroy(rss_ctx* ctx);
 int rss_hash_host(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples,
                   size_t n, uint32_t htable, uint32_t nqueues, uint32_t* h_hash,
                   uint32_t* h_queue, uint64_t* h_counts, uint32_t flags);
+
+/*
+ * ---- CSV fast path (host, multi-threaded) ----
+ * Replaces pd.read_csv (rss_simulator/simulator.py:55) and the two to_csv calls
+ * of write_statistics (simulator.py:114-115) for CANONICAL files: header = the
+ * four columns src_ip,dst_ip,src_port,dst_port in any order and nothing else;
+ * rows = four unquoted fields, dotted-quad addresses with octets 0..255 and no
+ * leading zeros, ports 0..65535 in plain decimal; LF or CRLF; empty lines
+ * skipped; ASCII only.  pandas round-trips such fields unchanged, so the output
+ * is byte-identical to the reference's.  Any other file -> RSS_ENOTSUP: the
+ * caller must take the pandas path, which reproduces the reference's parsing
+ * and error behaviour.  `threads` <= 0 picks min(16, hardware threads).
+ */
+typedef struct rss_csv_layout {
+    uint8_t field_column[4]; /* field f of a row holds column field_column[f]:
+                                0 src_ip, 1 dst_ip, 2 src_port, 3 dst_port   */
+} rss_csv_layout;
+
+/* Parse the whole file image; RSS_EINVAL with *n_rows set if cap is too small. */
+int rss_csv_parse(const char* data, size_t len, rss_tuple4* tuples, size_t cap,
+                  size_t* n_rows, rss_csv_layout* layout, int threads);
+
+/* Upper bound of rss_csv_format's output size. */
+size_t rss_csv_format_bound(size_t n, uint32_t nqueues);
+
+/*
+ * Write the statistics file of write_statistics (simulator.py:100-115): the
+ * "queue_number,counts" rows of the non-empty queues, then the table with the
+ * input columns in input order plus hash_result,queue_number.  `cap` must be
+ * >= rss_csv_format_bound(n, nqueues).
+ */
+int rss_csv_format(const rss_tuple4* tuples, const uint32_t* hash, const uint32_t* queue,
+                   size_t n, const uint64_t* counts, uint32_t nqueues,
+                   const rss_csv_layout* layout, char* out, size_t cap, size_t* out_len,
+                   int threads);
 
 /* Number of visible gfx950 devices (0 when there is no GPU). */
 int rss_device_count(int* out);

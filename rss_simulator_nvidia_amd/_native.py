@@ -29,8 +29,9 @@ KEY_MIN_BYTES = 4
 EXPORTED_SYMBOLS = (
     "rss_key_prepare", "rss_hash_device", "rss_generate_tuples", "rss_ctx_create",
     "rss_ctx_destroy", "rss_hash_host", "rss_device_count", "rss_last_error",
-    "rss_abi_version",
+    "rss_abi_version", "rss_csv_parse", "rss_csv_format_bound", "rss_csv_format",
 )
+ENOTSUP = -95
 
 
 class RssTuple4(ctypes.Structure):
@@ -45,6 +46,11 @@ class RssKey(ctypes.Structure):
         ("bytes", ctypes.c_uint8 * 52),
         ("window", ctypes.c_uint32 * 96),
     ]
+
+
+class RssCsvLayout(ctypes.Structure):
+    """``rss_csv_layout``: which column each CSV field holds."""
+    _fields_ = [("field_column", ctypes.c_uint8 * 4)]
 
 
 TUPLE_DTYPE = np.dtype([("sip", "<u4"), ("dip", "<u4"), ("ports", "<u4")])
@@ -67,6 +73,11 @@ def _bind(lib):
         "rss_ctx_create": ([ctypes.c_int, ctypes.POINTER(vp)], ctypes.c_int),
         "rss_ctx_destroy": ([vp], None),
         "rss_hash_host": ([vp, key_p, vp, sz, u32, u32, vp, vp, vp, u32], ctypes.c_int),
+        "rss_csv_parse": ([vp, sz, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(RssCsvLayout),
+                           ctypes.c_int], ctypes.c_int),
+        "rss_csv_format_bound": ([sz, u32], sz),
+        "rss_csv_format": ([vp, vp, vp, sz, vp, u32, ctypes.POINTER(RssCsvLayout), vp, sz,
+                            ctypes.POINTER(sz), ctypes.c_int], ctypes.c_int),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(lib, name)
@@ -182,3 +193,41 @@ def generate_device(seed, first_index, n, tuples_ptr, stream=None):
     """Stream-ordered ``rss_generate_tuples`` into a device buffer of n * 12 bytes."""
     _check(load().rss_generate_tuples(seed, first_index, n, tuples_ptr, stream),
            "rss_generate_tuples")
+
+
+# ------------------------------------------------------------ CSV fast path --
+def csv_parse(data, threads=0):
+    """Parse a canonical 4-tuple CSV image (bytes / uint8 array).
+
+    Returns ``(tuples, layout)`` or ``None`` when the file is not canonical
+    (``RSS_ENOTSUP``): the caller then takes the pandas path.
+    """
+    buf = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+    lib = load()
+    cap = int(np.count_nonzero(buf == 10)) + 1
+    tuples = np.empty(cap, dtype=TUPLE_DTYPE)
+    n = ctypes.c_size_t(0)
+    layout = RssCsvLayout()
+    rc = lib.rss_csv_parse(buf.ctypes.data, len(buf), tuples.ctypes.data, cap, ctypes.byref(n),
+                           ctypes.byref(layout), threads)
+    if rc == ENOTSUP:
+        return None
+    _check(rc, "rss_csv_parse")
+    return tuples[:n.value], layout
+
+
+def csv_format(tuples, hashes, queues, counts, layout, threads=0):
+    """Statistics CSV bytes (write_statistics layout) as a uint8 array."""
+    lib = load()
+    n, nq = len(tuples), len(counts)
+    tuples = np.ascontiguousarray(tuples, dtype=TUPLE_DTYPE)
+    hashes = np.ascontiguousarray(hashes, dtype=np.uint32)
+    queues = np.ascontiguousarray(queues, dtype=np.uint32)
+    counts = np.ascontiguousarray(counts, dtype=np.uint64)
+    cap = lib.rss_csv_format_bound(n, nq)
+    out = np.empty(cap, dtype=np.uint8)
+    out_len = ctypes.c_size_t(0)
+    _check(lib.rss_csv_format(tuples.ctypes.data, hashes.ctypes.data, queues.ctypes.data, n,
+                              counts.ctypes.data, nq, ctypes.byref(layout), out.ctypes.data, cap,
+                              ctypes.byref(out_len), threads), "rss_csv_format")
+    return out[:out_len.value]

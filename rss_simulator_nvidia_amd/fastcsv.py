@@ -1,0 +1,52 @@
+"""CLI fast path for ``--csv`` runs.
+
+canonical CSV file --native parse (rss_csv_parse)--> rss_tuple4[n] --rss_hash_host
+(pinned, chunked H2D -> kernel -> D2H)--> hash/queue/counts --native format
+(rss_csv_format)--> statistics file, byte-identical to the reference's
+``write_statistics`` output (``rss_simulator/simulator.py:100-116``).
+
+Files outside the canonical form (see ``include/rss_toeplitz.h``) return False and
+the CLI takes the pandas path of :class:`~rss_simulator_nvidia_amd.simulator.Simulator`,
+which reproduces the reference's parsing rules and errors.  ``RSS_CSV_FASTPATH=0``
+disables this module (the GPU computes the hashes either way).
+"""
+import os
+import time
+
+import numpy as np
+
+from rss_simulator_nvidia_amd import _native
+
+
+def enabled():
+    return os.environ.get("RSS_CSV_FASTPATH", "1") != "0"
+
+
+def run_csv(hash_key, ips_file, htable, nqueues, output, threads=0, timings=None):
+    """Process ``ips_file`` into ``output``; False if the file needs the pandas path."""
+    t = [time.perf_counter()]
+    try:
+        data = np.fromfile(ips_file, dtype=np.uint8)
+    except (OSError, ValueError):
+        return False
+    t.append(time.perf_counter())
+    parsed = _native.csv_parse(data, threads)
+    if parsed is None:
+        return False
+    tuples, layout = parsed
+    t.append(time.perf_counter())
+    key = _native.prepare_key(hash_key)
+    h, q, c = _native.default_context().hash(key, tuples, htable, nqueues)
+    t.append(time.perf_counter())
+    out = _native.csv_format(tuples, h, q, c, layout, threads)
+    t.append(time.perf_counter())
+    out.tofile(output)
+    t.append(time.perf_counter())
+    if timings is not None:
+        for name, a, b in zip(("read", "parse", "gpu", "format", "write"), t, t[1:]):
+            timings[name] = b - a
+        timings["rows"] = len(tuples)
+        timings["bytes_in"] = len(data)
+        timings["bytes_out"] = len(out)
+    print("Wrote statistics to {csv}.".format(csv=output))
+    return True

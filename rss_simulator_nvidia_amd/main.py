@@ -3,10 +3,13 @@
 Same five flags, metavars, help texts, validation and exit codes as the
 reference (``main.py:10-64``): ``--key-file`` is parsed eagerly (bad key ->
 argparse error, exit 2), ``--htable-size`` / ``--num-queues`` must be >= 1,
-``--csv PATH`` writes statistics, otherwise the histogram is shown.
+``--csv PATH`` writes statistics, otherwise the histogram is shown.  Canonical CSVs
+take the native parse/format fast path (``fastcsv.py``); everything else the
+pandas path of ``Simulator``.
 """
 from argparse import ArgumentParser
 
+from rss_simulator_nvidia_amd import fastcsv
 from rss_simulator_nvidia_amd.arg_parse_types import PositiveInt
 from rss_simulator_nvidia_amd.arg_parse_types import arg_parse_type_decorator as apt_decorator
 from rss_simulator_nvidia_amd.hash_key import HashKey
@@ -41,6 +44,9 @@ def parse_args(argv=None):
 def main(argv=None):
     """Invoke the RSS simulator (``main.py:54-64``)."""
     args = parse_args(argv)
+    if args.csv and fastcsv.enabled() and fastcsv.run_csv(
+            args.key, args.ips_file, args.htable_size, args.num_queues, args.csv):
+        return  # canonical input: native CSV parse/format around the same GPU kernel
     rss_sim = Simulator(args.key, args.htable_size, args.num_queues)
     rss_sim.load_ips_from_csv(args.ips_file)
     rss_sim.calc_hash()

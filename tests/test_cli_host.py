@@ -1,23 +1,35 @@
 """CLI / CSV host logic on CPU: the reference's recorded runs replayed through main().
 
-The one device call (``Toeplitz.compute_queues``) is replaced by the oracle here so
-that argument parsing, key parsing, CSV ingest, error messages and the CSV writer
-are checked without a GPU.  tests/test_gpu_cli.py replays the same cases with the
-real HIP path.
+The one device call (``HostContext.hash``, used by both the native CSV fast path and
+the pandas path) is replaced by the oracle here so that argument parsing, key
+parsing, CSV ingest, error messages and both CSV writers are checked without a GPU.
+tests/test_gpu_cli.py replays the same cases with the real HIP path.
 """
 import numpy as np
 import pytest
 
 from cli_cases import check_edge, check_example, edge_params, example_params
-from rss_simulator_nvidia_amd.toeplitz import Toeplitz
+from rss_simulator_nvidia_amd import _native
 
 
-@pytest.fixture
-def oracle_device(monkeypatch, oracle_lib):
-    def compute_queues(self, tuples, htable, nqueues):
+class OracleContext:
+    """Stands in for _native.HostContext in CPU-only tests (test infrastructure)."""
+
+    def __init__(self, oracle_lib):
+        self.oracle_lib = oracle_lib
+        self.calls = 0
+
+    def hash(self, key, tuples, htable, nqueues, want_hash=True, want_queue=True,
+             want_counts=True):
+        self.calls += 1
         arr = np.stack([tuples["sip"], tuples["dip"], tuples["ports"]], axis=1)
-        return oracle_lib.run(self.hash_key, arr, htable, nqueues, threads=2)
-    monkeypatch.setattr(Toeplitz, "compute_queues", compute_queues)
+        return self.oracle_lib.run(list(key.bytes[:key.len]), arr, htable, nqueues, threads=2)
+
+
+@pytest.fixture(params=["fast", "pandas"])
+def oracle_device(request, monkeypatch, oracle_lib):
+    monkeypatch.setattr(_native, "default_context", lambda: OracleContext(oracle_lib))
+    monkeypatch.setenv("RSS_CSV_FASTPATH", "1" if request.param == "fast" else "0")
 
 
 @example_params

@@ -1,0 +1,78 @@
+"""End-to-end (host memory) rates for DESIGN.md §6 (tool, not product).
+
+1. CSV -> CSV through the CLI fast path (native parse, rss_hash_host = pinned chunked
+   H2D -> kernel -> D2H, native format), per stage;
+2. rss_hash_host alone on host-resident packed tuples (the PCIe-inclusive rate);
+3. the pandas CLI path (RSS_CSV_FASTPATH=0) on a smaller file, for comparison.
+Prints one JSON object.
+usage: python tools/e2e_bench.py [ROWS] [PANDAS_ROWS] [WORKDIR]
+"""
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+from bench import EXAMPLE_KEY  # noqa: E402
+from rss_simulator_nvidia_amd import _native, fastcsv  # noqa: E402
+from rss_simulator_nvidia_amd.main import main as cli_main  # noqa: E402
+
+rows = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 24
+pandas_rows = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 18
+work = sys.argv[3] if len(sys.argv) > 3 else "/tmp/rss_e2e"
+os.makedirs(work, exist_ok=True)
+gen = os.path.join(work, "gen_csv")
+subprocess.run(["gcc", "-O2", "-o", gen, os.path.join(ROOT, "tools", "gen_csv.c")], check=True)
+big, small = os.path.join(work, "big.csv"), os.path.join(work, "small.csv")
+subprocess.run([gen, str(rows), "12345", big], check=True)
+subprocess.run([gen, str(pandas_rows), "777", small], check=True)
+key = [int(x, 16) for x in EXAMPLE_KEY.split(":")]
+H, Q = 128, 24
+result = {"rows": rows, "htable": H, "queues": Q}
+
+# warm the device context, then the timed CSV -> CSV run (twice; report the second)
+_native.default_context()
+for _ in range(2):
+    t = {}
+    t0 = time.perf_counter()
+    assert fastcsv.run_csv(key, big, H, Q, os.path.join(work, "out_big.csv"), timings=t)
+    wall = time.perf_counter() - t0
+result["csv_fastpath"] = {"wall_s": wall, "rows_per_s": rows / wall,
+                          "stages_s": {k: v for k, v in t.items() if k in
+                                       ("read", "parse", "gpu", "format", "write")},
+                          "bytes_in": t["bytes_in"], "bytes_out": t["bytes_out"]}
+
+# rss_hash_host alone (PCIe-inclusive): packed tuples in host memory -> host outputs
+tuples = _native.csv_parse(np.fromfile(big, dtype=np.uint8))[0]
+ctx = _native.default_context()
+k = _native.prepare_key(key)
+ctx.hash(k, tuples[:1 << 20], H, Q)
+t0 = time.perf_counter()
+h, q, c = ctx.hash(k, tuples, H, Q)
+dt = time.perf_counter() - t0
+result["host_path"] = {"wall_s": dt, "tuples_per_s": rows / dt,
+                       "bytes_moved": rows * 20, "GB_per_s": rows * 20 / dt / 1e9,
+                       "note": "12 B/tuple H2D + 8 B/tuple D2H through pinned staging"}
+assert int(c.sum()) == rows
+
+# pandas path on the small file
+os.environ["RSS_CSV_FASTPATH"] = "0"
+t0 = time.perf_counter()
+cli_main(["--key-file", os.path.join(ROOT, "tests", "golden", "example_input", "hash_key.txt"),
+          "--ips-file", small, "--htable-size", str(H), "--num-queues", str(Q),
+          "--csv", os.path.join(work, "out_small_pandas.csv")])
+dt = time.perf_counter() - t0
+os.environ["RSS_CSV_FASTPATH"] = "1"
+cli_main(["--key-file", os.path.join(ROOT, "tests", "golden", "example_input", "hash_key.txt"),
+          "--ips-file", small, "--htable-size", str(H), "--num-queues", str(Q),
+          "--csv", os.path.join(work, "out_small_fast.csv")])
+same = open(os.path.join(work, "out_small_pandas.csv"), "rb").read() == \
+    open(os.path.join(work, "out_small_fast.csv"), "rb").read()
+result["csv_pandas_path"] = {"rows": pandas_rows, "wall_s": dt, "rows_per_s": pandas_rows / dt,
+                             "fast_path_output_identical": same}
+print(json.dumps(result))
