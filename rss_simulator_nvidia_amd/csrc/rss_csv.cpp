@@ -15,7 +15,6 @@
 #include <algorithm>
 #include <atomic>
 #include <cstring>
-#include <string>
 #include <thread>
 #include <vector>
 
@@ -54,49 +53,73 @@ bool parse_header(const char* b, const char* e, uint8_t field_column[4]) {
     return seen == 15;
 }
 
-// canonical unsigned decimal in [b, e): 1..max_digits digits, no leading zero
-inline bool parse_uint(const char* b, const char* e, int max_digits, uint32_t max_value, uint32_t& v) {
-    const long len = e - b;
-    if (len < 1 || len > max_digits || (len > 1 && *b == '0')) return false;
-    uint32_t x = 0;
-    for (const char* p = b; p < e; ++p) {
-        const unsigned d = (unsigned)(*p - '0');
-        if (d > 9) return false;
-        x = x * 10 + d;
+inline bool is_digit(const char* p, const char* e) { return p < e && (unsigned)(*p - '0') <= 9; }
+
+// Canonical unsigned decimal at p (1..kMaxDigits digits, no leading zero, <= kMax);
+// advances p past it.
+template <int kMaxDigits, uint32_t kMax>
+inline bool scan_uint(const char*& p, const char* e, uint32_t& v) {
+    if (!is_digit(p, e)) return false;
+    uint32_t x = (uint32_t)(*p++ - '0');
+    if (x == 0) {
+        v = 0;
+        return !is_digit(p, e);
     }
-    if (x > max_value) return false;
+    for (int k = 1; k < kMaxDigits && is_digit(p, e); ++k) x = x * 10 + (uint32_t)(*p++ - '0');
+    if (is_digit(p, e) || x > kMax) return false;
     v = x;
     return true;
 }
 
-inline bool parse_ip(const char* b, const char* e, uint32_t& out) {
+inline bool scan_ip(const char*& p, const char* e, uint32_t& out) {
     uint32_t ip = 0;
     for (int k = 0; k < 4; ++k) {
-        const char* dot = k < 3 ? static_cast<const char*>(memchr(b, '.', e - b)) : e;
-        if (!dot) return false;
         uint32_t octet;
-        if (!parse_uint(b, dot, 3, 255, octet)) return false;
+        if (!scan_uint<3, 255>(p, e, octet)) return false;
         ip = ip << 8 | octet;
-        b = dot + 1;
+        if (k < 3) {
+            if (p >= e || *p != '.') return false;
+            ++p;
+        }
     }
     out = ip;
     return true;
 }
 
-bool parse_row(const char* b, const char* e, const uint8_t field_column[4], rss_tuple4& t) {
+// One data row starting at p; on success p points past its line end ("\n", "\r\n"
+// or end of input).
+inline bool scan_row(const char*& p, const char* e, const uint8_t field_column[4], rss_tuple4& t) {
     uint32_t v[4];
     for (int f = 0; f < 4; ++f) {
-        const char* comma = f < 3 ? static_cast<const char*>(memchr(b, ',', e - b)) : e;
-        if (!comma) return false;
         const int col = field_column[f];
-        const bool ok = col < 2 ? parse_ip(b, comma, v[col]) : parse_uint(b, comma, 5, 65535, v[col]);
-        if (!ok) return false;  // also rejects a fifth field (',' inside the last one)
-        b = comma + 1;
+        if (!(col < 2 ? scan_ip(p, e, v[col]) : scan_uint<5, 65535>(p, e, v[col]))) return false;
+        if (f < 3) {
+            if (p >= e || *p != ',') return false;
+            ++p;
+        }
+    }
+    if (p < e && *p == '\r') ++p;
+    if (p < e) {
+        if (*p != '\n') return false;
+        ++p;
     }
     t.sip = v[0];
     t.dip = v[1];
     t.ports = v[2] << 16 | v[3];
     return true;
+}
+
+// If p starts an empty line ("\n", "\r\n", or a final "\r"), skip it.
+inline bool skip_empty_line(const char*& p, const char* e) {
+    if (*p == '\n') {
+        ++p;
+        return true;
+    }
+    if (*p == '\r' && (p + 1 == e || p[1] == '\n')) {
+        p += (p + 1 == e) ? 1 : 2;
+        return true;
+    }
+    return false;
 }
 
 // Split [b, e) into up to `parts` ranges that start at line starts.
@@ -113,28 +136,45 @@ std::vector<const char*> split_lines(const char* b, const char* e, int parts) {
     return cuts;
 }
 
-// Calls fn(line_begin, line_end_without_cr) for each non-empty line of [b, e).
-template <typename F>
-bool for_each_line(const char* b, const char* e, F&& fn) {
-    while (b < e) {
-        const char* nl = static_cast<const char*>(memchr(b, '\n', e - b));
-        const char* end = nl ? nl : e;
-        const char* t = trim_cr(b, end);
-        if (t > b && !fn(b, t)) return false;
-        b = nl ? nl + 1 : e;
-    }
-    return true;
-}
+const char kDigits2[201] =
+    "00010203040506070809101112131415161718192021222324252627282930313233343536373839"
+    "40414243444546474849505152535455565758596061626364656667686970717273747576777879"
+    "8081828384858687888990919293949596979899";
+
+inline size_t uint_len(uint64_t v);
 
 inline char* put_uint(char* p, uint64_t v) {
-    char tmp[24];
-    int n = 0;
-    do {
-        tmp[n++] = (char)('0' + v % 10);
-        v /= 10;
-    } while (v);
-    while (n) *p++ = tmp[--n];
-    return p;
+    const size_t len = uint_len(v);
+    char* w = p + len;
+    while (v >= 100) {
+        const unsigned r = (unsigned)(v % 100);
+        v /= 100;
+        w -= 2;
+        memcpy(w, kDigits2 + 2 * r, 2);
+    }
+    if (v >= 10) {
+        w -= 2;
+        memcpy(w, kDigits2 + 2 * v, 2);
+    } else {
+        *--w = (char)('0' + v);
+    }
+    return p + len;
+}
+
+inline size_t uint_len(uint64_t v) {
+    size_t n = 1;
+    while (v >= 10000) {
+        v /= 10000;
+        n += 4;
+    }
+    return n + (v >= 10) + (v >= 100) + (v >= 1000);
+}
+
+inline size_t octet_len(uint32_t v) { return v >= 100 ? 3 : (v >= 10 ? 2 : 1); }
+
+inline size_t ip_len(uint32_t ip) {
+    return octet_len(ip >> 24) + octet_len((ip >> 16) & 0xFF) + octet_len((ip >> 8) & 0xFF) +
+           octet_len(ip & 0xFF) + 3;
 }
 
 inline char* put_ip(char* p, uint32_t ip) {
@@ -165,40 +205,47 @@ int rss_csv_parse(const char* data, size_t len, rss_tuple4* tuples, size_t cap, 
     if (!parse_header(data, hend, layout->field_column)) return RSS_ENOTSUP;
     const char* body = nl ? nl + 1 : end;
     if (body >= end) return RSS_ENOTSUP;  // no data rows: the pandas path raises
-    for (const char* p = data; p < end; ++p)  // ASCII only: pandas decodes utf-8
-        if ((unsigned char)*p >= 0x80) return RSS_ENOTSUP;
+    // (no separate ASCII check: rows accept only digits . , \r \n, the header only
+    // the four column names, so any non-ASCII byte already fails the scan)
 
     const int nt = pick_threads(threads, (end - body) / 32);
     const std::vector<const char*> cuts = split_lines(body, end, nt);
     const int parts = (int)cuts.size() - 1;
-    std::vector<size_t> rows(parts + 1, 0);
+    // one scanning pass per range into a local buffer, then a parallel gather
+    std::vector<std::vector<rss_tuple4>> local(parts);
+    std::atomic<bool> ok{true};
     std::vector<std::thread> pool;
     for (int k = 0; k < parts; ++k)
         pool.emplace_back([&, k] {
-            size_t c = 0;
-            for_each_line(cuts[k], cuts[k + 1], [&](const char*, const char*) { ++c; return true; });
-            rows[k + 1] = c;
+            const char* p = cuts[k];
+            const char* e = cuts[k + 1];
+            std::vector<rss_tuple4>& out = local[k];
+            out.reserve((size_t)std::count(p, e, '\n') + 1);
+            rss_tuple4 t;
+            while (p < e) {
+                if (skip_empty_line(p, e)) continue;
+                if (!scan_row(p, e, layout->field_column, t)) {
+                    ok = false;
+                    return;
+                }
+                out.push_back(t);
+                if ((out.size() & 4095) == 0 && !ok.load(std::memory_order_relaxed)) return;
+            }
         });
     for (auto& t : pool) t.join();
     pool.clear();
-    for (int k = 0; k < parts; ++k) rows[k + 1] += rows[k];
-    if (rows[parts] == 0) return RSS_ENOTSUP;
-    if (rows[parts] > cap || !tuples) {
-        *n_rows = rows[parts];
-        return RSS_EINVAL;  // caller's buffer is too small; *n_rows says how many
-    }
-    std::atomic<bool> ok{true};
+    if (!ok) return RSS_ENOTSUP;
+    std::vector<size_t> off(parts + 1, 0);
+    for (int k = 0; k < parts; ++k) off[k + 1] = off[k] + local[k].size();
+    *n_rows = off[parts];
+    if (off[parts] == 0) return RSS_ENOTSUP;
+    if (off[parts] > cap || !tuples) return RSS_EINVAL;  // *n_rows says how many are needed
     for (int k = 0; k < parts; ++k)
         pool.emplace_back([&, k] {
-            rss_tuple4* out = tuples + rows[k];
-            const bool good = for_each_line(cuts[k], cuts[k + 1], [&](const char* b, const char* e) {
-                return ok.load(std::memory_order_relaxed) && parse_row(b, e, layout->field_column, *out++);
-            });
-            if (!good) ok = false;
+            if (!local[k].empty())
+                memcpy(tuples + off[k], local[k].data(), local[k].size() * sizeof(rss_tuple4));
         });
     for (auto& t : pool) t.join();
-    if (!ok) return RSS_ENOTSUP;
-    *n_rows = rows[parts];
     return RSS_OK;
 }
 
@@ -230,18 +277,41 @@ int rss_csv_format(const rss_tuple4* tuples, const uint32_t* hash, const uint32_
     memcpy(p, "hash_result,queue_number\n", 25);
     p += 25;
 
+    // two passes over row ranges: exact byte count per range, then every thread
+    // formats straight into its slice of `out` (no staging copy)
     const int nt = pick_threads(threads, n);
-    std::vector<std::string> parts(nt);
+    std::vector<size_t> off(nt + 1, 0);
+    auto row_fields = [&](size_t i, uint32_t col[4]) {
+        const rss_tuple4& t = tuples[i];
+        col[0] = t.sip;
+        col[1] = t.dip;
+        col[2] = t.ports >> 16;
+        col[3] = t.ports & 0xFFFF;
+    };
     std::vector<std::thread> pool;
     for (int k = 0; k < nt; ++k)
         pool.emplace_back([&, k] {
             const size_t a = n * k / nt, b = n * (k + 1) / nt;
-            std::string& s = parts[k];
-            s.resize((b - a) * kMaxRowBytes);
-            char* w = &s[0];
+            size_t bytes = 0;
             for (size_t i = a; i < b; ++i) {
-                const rss_tuple4& t = tuples[i];
-                const uint32_t col[4] = {t.sip, t.dip, t.ports >> 16, t.ports & 0xFFFF};
+                uint32_t col[4];
+                row_fields(i, col);
+                bytes += ip_len(col[0]) + ip_len(col[1]) + uint_len(col[2]) + uint_len(col[3]) +
+                         uint_len(hash[i]) + uint_len(queue[i]) + 6;
+            }
+            off[k + 1] = bytes;
+        });
+    for (auto& t : pool) t.join();
+    pool.clear();
+    off[0] = (size_t)(p - out);
+    for (int k = 0; k < nt; ++k) off[k + 1] += off[k];
+    for (int k = 0; k < nt; ++k)
+        pool.emplace_back([&, k] {
+            const size_t a = n * k / nt, b = n * (k + 1) / nt;
+            char* w = out + off[k];
+            for (size_t i = a; i < b; ++i) {
+                uint32_t col[4];
+                row_fields(i, col);
                 for (int f = 0; f < 4; ++f) {
                     const int c = layout->field_column[f];
                     w = c < 2 ? put_ip(w, col[c]) : put_uint(w, col[c]);
@@ -252,14 +322,7 @@ int rss_csv_format(const rss_tuple4* tuples, const uint32_t* hash, const uint32_
                 w = put_uint(w, queue[i]);
                 *w++ = '\n';
             }
-            s.resize(w - &s[0]);
         });
-    for (auto& t : pool) t.join();
-    pool.clear();
-    std::vector<size_t> off(nt + 1, (size_t)(p - out));
-    for (int k = 0; k < nt; ++k) off[k + 1] = off[k] + parts[k].size();
-    for (int k = 0; k < nt; ++k)
-        pool.emplace_back([&, k] { memcpy(out + off[k], parts[k].data(), parts[k].size()); });
     for (auto& t : pool) t.join();
     *out_len = off[nt];
     return RSS_OK;
