@@ -2,8 +2,10 @@
 
 One step = one pass of the hot path (Toeplitz hash -> htable index -> queue
 modulo -> per-queue histogram, all outputs written) over this rank's resident
-shard of synthetic tuples, followed by the RCCL all-reduce of the per-queue
-count vector when N > 1.  Weak scaling: every rank owns ``--tuples-per-gpu``
+shard of synthetic tuples (zero counts + one kernel launch; ``--graph`` replays the
+pair as a captured HIP graph), followed, when N > 1, by the RCCL all-reduce of the
+per-queue count vector, issued async so it overlaps the next step (double-buffered
+counts).  Weak scaling: every rank owns ``--tuples-per-gpu``
 tuples (default 2**28, BASELINE configs[2]) of one global splitmix64 stream.
 
     python bench.py [--gpus N --steps K --warmup W]
@@ -47,6 +49,11 @@ def parse_args():
     p.add_argument("--cpu-procs", type=int, default=16,
                    help="worker processes for the CPU baseline (the box's CPU share)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                   help="nccl = RCCL over xGMI; gloo only to rehearse N>1 on one GPU")
+    p.add_argument("--graph", action="store_true",
+                   help="replay each step as a captured HIP graph (measured: no gain over "
+                        "eager launches at 2**28 tuples per step)")
     p.add_argument("--profile-dir", default=os.path.join(ROOT, "profiles"),
                    help="where committed rocprofv3 PMC summaries (traffic) are looked up")
     return p.parse_args()
@@ -118,14 +125,22 @@ def main():
 
     from rss_simulator_nvidia_amd import _native
 
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # RSS_BENCH_DEVICE pins every rank to one device (rehearsing N>1 on a 1-GPU box)
+    dev_index = int(os.environ.get("RSS_BENCH_DEVICE", local_rank))
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     def barrier():
         if world > 1:
-            dist.barrier(device_ids=[local_rank])
+            if args.dist_backend == "nccl":
+                dist.barrier(device_ids=[dev_index])
+            else:
+                dist.barrier()
 
     n = args.tuples_per_gpu
     H, Q = args.htable, args.queues
@@ -144,59 +159,96 @@ def main():
     _native.generate_device(SEED, rank * n, n, tuples.data_ptr(), sp)
     torch.cuda.synchronize()
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
+    # Two count buffers: step i hashes into counts[i % 2] while the RCCL all-reduce of
+    # step i-1's buffer (async, on the collective stream) overlaps it.
+    counts2 = [counts, torch.zeros(Q, dtype=torch.int64, device=dev)]
 
-    def step(i=None, hash_ptr=hashes.data_ptr(), queue_ptr=queues.data_ptr(), flags=qflag):
-        counts.zero_()
-        if i is not None:
-            ev[i][0].record(stream)
-        _native.hash_device(key, tuples.data_ptr(), n, H, Q, hash_ptr, queue_ptr,
-                            counts.data_ptr(), _native.FLAG_ACCUMULATE | flags, sp)
-        if i is not None:
-            ev[i][1].record(stream)
+    def body(c):
+        c.zero_()
+        _native.hash_device(key, tuples.data_ptr(), n, H, Q, hashes.data_ptr(), queues.data_ptr(),
+                            c.data_ptr(), _native.FLAG_ACCUMULATE | qflag,
+                            torch.cuda.current_stream(dev).cuda_stream)
+
+    graphs = None
+    if args.graph:
+        try:  # capture zero + hash per buffer once; replay = one graph launch per step
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(stream)
+            with torch.cuda.stream(side):
+                body(counts2[0])
+            stream.wait_stream(side)
+            graphs = []
+            for c in counts2:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    body(c)
+                graphs.append(g)
+        except Exception as err:  # eager fallback keeps the same work per step
+            print("bench: graph capture unavailable (%s); launching eagerly" % err, file=sys.stderr)
+            graphs = None
+
+    pending = [None, None]
+
+    def step(i):
+        b = i & 1
+        if pending[b] is not None:
+            pending[b].wait()  # buffer b's previous all-reduce must finish before reuse
+        if graphs is not None:
+            graphs[b].replay()
+        else:
+            body(counts2[b])
         if world > 1:
-            dist.all_reduce(counts)  # RCCL over xGMI: the one exchange step
+            pending[b] = dist.all_reduce(counts2[b], async_op=True)  # RCCL over xGMI
 
-    for _ in range(args.warmup):
-        step()
+    def drain():
+        for b in (0, 1):
+            if pending[b] is not None:
+                pending[b].wait()
+                pending[b] = None
+
+    for i in range(args.warmup):
+        step(i)
+    drain()
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i)
+    drain()
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
-    kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    last = counts2[(args.steps - 1) & 1]
+
+    # kernel-only timing (HIP events on the launch stream), for roofline.achieved
+    def kernel_ms_of(hash_ptr, queue_ptr, flags, reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        _native.hash_device(key, tuples.data_ptr(), n, H, Q, hash_ptr, queue_ptr,
+                            counts.data_ptr(), flags | _native.FLAG_ACCUMULATE, sp)
+        a.record(stream)
+        for _ in range(reps):
+            _native.hash_device(key, tuples.data_ptr(), n, H, Q, hash_ptr, queue_ptr,
+                                counts.data_ptr(), flags | _native.FLAG_ACCUMULATE, sp)
+        b.record(stream)
+        torch.cuda.synchronize()
+        return a.elapsed_time(b) / reps
+
+    total = int(last.sum().item())
+    if total != n * world:
+        raise SystemExit("bench: per-queue counts sum to %d, expected %d" % (total, n * world))
+    kernel_ms = kernel_ms_of(hashes.data_ptr(), queues.data_ptr(), qflag, args.steps)
     stats = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(stats, op=dist.ReduceOp.MAX)
     elapsed, kernel_ms_max = float(stats[0]), float(stats[1])
 
-    total = int(counts.sum().item())
-    if total != n * world:
-        raise SystemExit("bench: per-queue counts sum to %d, expected %d" % (total, n * world))
-
     # secondary lines (rank 0, after the timed region): counts-only mode (12 B/tuple,
     # the HBM-read roofline) and u32 queue outputs (20 B/tuple)
-    def kernel_ms_of(hash_ptr, queue_ptr, flags):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        reps = max(5, args.steps // 2)
-        _native.hash_device(key, tuples.data_ptr(), n, H, Q, hash_ptr, queue_ptr,
-                            counts.data_ptr(), flags, sp)
-        a.record(stream)
-        for _ in range(reps):
-            _native.hash_device(key, tuples.data_ptr(), n, H, Q, hash_ptr, queue_ptr,
-                                counts.data_ptr(), flags, sp)
-        b.record(stream)
-        torch.cuda.synchronize()
-        return a.elapsed_time(b) / reps
-
     co_ms = u32_ms = None
     if rank == 0:
-        co_ms = kernel_ms_of(None, None, 0)
-        u32_ms = kernel_ms_of(hashes.data_ptr(), queues.data_ptr(), 0)
+        reps = max(5, args.steps // 2)
+        co_ms = kernel_ms_of(None, None, 0, reps)
+        u32_ms = kernel_ms_of(hashes.data_ptr(), queues.data_ptr(), 0, reps)
 
     if rank == 0:
         value = n * world * args.steps / elapsed
@@ -226,8 +278,11 @@ def main():
                 "htable": H,
                 "queues": Q,
                 "queue_width": qw,
-                "parallelism": "tuple-sharded x%d, RCCL all-reduce of uint64[%d] counts"
-                               % (world, Q),
+                "parallelism": "tuple-sharded x%d, %s all-reduce of uint64[%d] counts "
+                               "(async, overlapped with the next step)"
+                               % (world, "RCCL" if args.dist_backend == "nccl" else "gloo", Q),
+                "step": "hipGraph replay (zero counts + hash kernel)" if graphs is not None
+                        else "eager launches (zero counts + hash kernel)",
             },
             "roofline": {
                 "bound": "hbm",

@@ -72,6 +72,43 @@ __global__ __launch_bounds__(1024) void mem_ceiling_q8(Params p) {
     }
 }
 
+// store-shape probes for the 12R+5W mix: kMode 0 = plain stores, 1 = hash only (12R+4W),
+// 2 = queue bytes gathered through LDS into one 16-B store per lane every 4th group
+template <int kMode>
+__global__ __launch_bounds__(1024) void mem_probe(Params p) {
+    __shared__ uint32_t stage[1024];
+    const uint4* src = reinterpret_cast<const uint4*>(p.tuples);
+    const uint64_t ng = p.n >> 2;
+    const uint64_t stride = (uint64_t)gridDim.x * 1024;
+    for (uint64_t g = (uint64_t)blockIdx.x * 1024 + threadIdx.x; g < ng; g += stride) {
+        uint4 a = src[3 * g], b = src[3 * g + 1], c = src[3 * g + 2];
+        uint4 h = make_uint4(a.x ^ a.y ^ a.z, a.w ^ b.x ^ b.y, b.z ^ b.w ^ c.x, c.y ^ c.z ^ c.w);
+        const uint32_t qw = (a.x ^ c.w) & 0x17171717u;
+        if (kMode == 0) {
+            reinterpret_cast<uint4*>(p.hash_out)[g] = h;
+            p.queue_out[g] = qw;
+        } else if (kMode == 1) {
+            uint32_t* o = p.hash_out + 4 * g;
+            __builtin_nontemporal_store(h.x, o); __builtin_nontemporal_store(h.y, o + 1);
+            __builtin_nontemporal_store(h.z, o + 2); __builtin_nontemporal_store(h.w, o + 3);
+        } else {
+            uint32_t* o = p.hash_out + 4 * g;
+            __builtin_nontemporal_store(h.x, o); __builtin_nontemporal_store(h.y, o + 1);
+            __builtin_nontemporal_store(h.z, o + 2); __builtin_nontemporal_store(h.w, o + 3);
+            // lane l of each group of 4 lanes gathers the 16 queue bytes of lanes 4k..4k+3
+            stage[threadIdx.x] = qw;
+            __builtin_amdgcn_wave_barrier();
+            if ((threadIdx.x & 3) == 0) {
+                const uint32_t* s4 = stage + threadIdx.x;
+                uint32_t* oq = p.queue_out + g;  // g is 4-aligned for lane%4 == 0
+                __builtin_nontemporal_store(s4[0], oq); __builtin_nontemporal_store(s4[1], oq + 1);
+                __builtin_nontemporal_store(s4[2], oq + 2); __builtin_nontemporal_store(s4[3], oq + 3);
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+}
+
 // ------------------------------------------------------------ LUT variants
 // chunk t covers input bits [t*B, t*B + B) of the 96-bit MSB-first string.
 template <int B>
@@ -325,6 +362,22 @@ int main(int argc, char** argv) {
             printf("mem 12R+5W nt grid=%dx                   %8.3f ms  %7.1f Gt/s  %6.0f GB/s\n", wpc, t,
                    n / t / 1e6, n * 17e-9 / t * 1e3);
         }
+    }
+    if (strstr("memprobe", filter)) {
+        p.hash_out = h1;
+        p.queue_out = q1;
+        const char* names[3] = {"mem 12R+5W plain stores", "mem 12R+4W (hash only, nt)",
+                                "mem 12R+5W nt, queue via LDS x4"};
+        void (*ks[3])(Params) = {mem_probe<0>, mem_probe<1>, mem_probe<2>};
+        const double bytes[3] = {17e-9, 16e-9, 17e-9};
+        for (int m = 0; m < 3; ++m) {
+            t = time_ms([&] { hipLaunchKernelGGL(ks[m], dim3(g_cus), dim3(1024), 0, 0, p); }, reps);
+            printf("%-40s %8.3f ms  %7.1f Gt/s  %6.0f GB/s\n", names[m], t, n / t / 1e6, n * bytes[m] / t * 1e3);
+        }
+        t = time_ms([&] { hipLaunchKernelGGL(mem_ceiling_q8, dim3(g_cus), dim3(1024), 0, 0, p); }, reps);
+        printf("%-40s %8.3f ms  %7.1f Gt/s  %6.0f GB/s\n", "mem 12R+5W nt (as product)", t, n / t / 1e6, n * 17e-9 / t * 1e3);
+        t = time_ms([&] { hipLaunchKernelGGL(mem_ceiling<false>, dim3(g_cus), dim3(1024), 0, 0, p); }, reps);
+        printf("%-40s %8.3f ms  %7.1f Gt/s  %6.0f GB/s\n", "mem 12R", t, n / t / 1e6, n * 12e-9 / t * 1e3);
     }
     auto run_variant = [&](const char* name, void (*k)(Params), int block, int wgs_per_cu, bool write,
                            bool q8 = false) {
