@@ -50,3 +50,19 @@ def run_csv(hash_key, ips_file, htable, nqueues, output, threads=0, timings=None
         timings["bytes_out"] = len(out)
     print("Wrote statistics to {csv}.".format(csv=output))
     return True
+
+
+def run_counts(hash_key, ips_file, htable, nqueues, threads=0):
+    """Per-queue counts of a canonical file via the counts-only kernel (12 B/tuple);
+    None if the file needs the pandas path."""
+    try:
+        data = np.fromfile(ips_file, dtype=np.uint8)
+    except (OSError, ValueError):
+        return None
+    parsed = _native.csv_parse(data, threads)
+    if parsed is None:
+        return None
+    key = _native.prepare_key(hash_key)
+    _, _, counts = _native.default_context().hash(key, parsed[0], htable, nqueues,
+                                                  want_hash=False, want_queue=False)
+    return counts

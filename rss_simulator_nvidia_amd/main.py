@@ -7,13 +7,15 @@ argparse error, exit 2), ``--htable-size`` / ``--num-queues`` must be >= 1,
 take the native parse/format fast path (``fastcsv.py``); everything else the
 pandas path of ``Simulator``.
 """
+import argparse
 from argparse import ArgumentParser
 
-from rss_simulator_nvidia_amd import fastcsv
+from rss_simulator_nvidia_amd import fastcsv, histogram
 from rss_simulator_nvidia_amd.arg_parse_types import PositiveInt
 from rss_simulator_nvidia_amd.arg_parse_types import arg_parse_type_decorator as apt_decorator
 from rss_simulator_nvidia_amd.hash_key import HashKey
 from rss_simulator_nvidia_amd.simulator import Simulator
+from rss_simulator_nvidia_amd.toeplitz import Toeplitz
 
 
 def build_parser():
@@ -33,6 +35,8 @@ def build_parser():
     parser.add_argument("--num-queues", metavar="NUM", type=PositiveInt.parse, required=True,
                         help="Positive number representing number of queues.")
     parser.add_argument("--csv", metavar="PATH", help="Write output to csv file.")
+    # additive (not in the reference): save the histogram instead of opening a window
+    parser.add_argument("--histogram-png", metavar="PATH", help=argparse.SUPPRESS)
     return parser
 
 
@@ -47,6 +51,12 @@ def main(argv=None):
     if args.csv and fastcsv.enabled() and fastcsv.run_csv(
             args.key, args.ips_file, args.htable_size, args.num_queues, args.csv):
         return  # canonical input: native CSV parse/format around the same GPU kernel
+    if not args.csv and fastcsv.enabled():
+        counts = fastcsv.run_counts(args.key, args.ips_file, args.htable_size, args.num_queues)
+        if counts is not None:  # histogram mode needs the per-queue counts only
+            histogram.show(counts, Toeplitz(args.key).hash_key_str(), args.htable_size,
+                           args.num_queues, args.histogram_png)
+            return
     rss_sim = Simulator(args.key, args.htable_size, args.num_queues)
     rss_sim.load_ips_from_csv(args.ips_file)
     rss_sim.calc_hash()
@@ -54,4 +64,4 @@ def main(argv=None):
     if args.csv:
         rss_sim.write_statistics(args.csv)
     else:
-        rss_sim.show_histogram()
+        rss_sim.show_histogram(args.histogram_png)

@@ -14,7 +14,7 @@ Public methods and their behaviour follow the reference:
   for the non-empty queues (from the device histogram), then the full table,
   then the same stdout line;
 * ``show_histogram``     (``simulator.py:118-172``): the per-queue bar chart with
-  the key / htable / queue caption (headless backends just render it).
+  the key / htable / queue caption (``histogram.py``; ``output=`` saves a PNG).
 """
 from __future__ import print_function
 
@@ -22,6 +22,7 @@ import numpy as np
 import pandas as pd
 from pandas.errors import ParserError as pd_ParserError
 
+from rss_simulator_nvidia_amd import histogram
 from rss_simulator_nvidia_amd.column_names import INPUT_COLUMNS, ColumnNames
 from rss_simulator_nvidia_amd.exceptions import ParseException
 from rss_simulator_nvidia_amd.ingest import pack_frame
@@ -109,36 +110,10 @@ class Simulator(object):
 
     def histogram_caption(self):
         """The caption lines of ``simulator.py:160-169``."""
-        hash_key = self.__toeplitz.hash_key_str()
-        key_str = "Hash Key: {}\n{}{}".format(hash_key[:94], " " * 17, hash_key[94:])
-        return "\n".join([
-            key_str,
-            "Hash Table Size: {}".format(self.__hash_table_size),
-            "Number Queues: {}".format(self.__queue_num),
-            "Number of Queues Chosen by Hash Function: {}".format(len(self.queue_count_rows())),
-        ])
+        return histogram.caption(self.__toeplitz.hash_key_str(), self.__hash_table_size,
+                                 self.__queue_num, self.__counts)
 
     def show_histogram(self, output=None):
-        """Per-queue bar chart + caption; ``plt.show()``, or save to ``output`` if given."""
-        import matplotlib.pyplot as plt
-        from matplotlib.ticker import MaxNLocator
-
-        counts = np.asarray(self.__counts, dtype=np.int64)
-        fig, ax = plt.subplots(figsize=(12, 8))
-        ax.bar(np.arange(self.__queue_num) + 0.5, counts, width=0.9, color="#86bf91", zorder=2)
-        for side in ("right", "top", "left"):
-            ax.spines[side].set_visible(False)
-        for tick in ax.get_yticks():
-            ax.axhline(y=tick, linestyle="dashed", alpha=0.8, color="#dddddd", zorder=1)
-        ax.set_title("Number of Unique Flows per Queue", weight="bold", size=16)
-        ax.set_xlabel("Queue Number", labelpad=20, weight="bold", size=12)
-        ax.set_ylabel("Number of Flows", labelpad=20, weight="bold", size=12)
-        ax.yaxis.set_major_locator(MaxNLocator(integer=True))
-        ax.set_xlim(0, self.__queue_num)
-        fig.text(0.04, 0.03, self.histogram_caption(), fontsize=12)
-        fig.subplots_adjust(bottom=0.27)
-        if output:
-            fig.savefig(output)
-            plt.close(fig)
-        else:
-            plt.show()
+        """Per-queue bar chart + caption (``simulator.py:118-172``); PNG if ``output``."""
+        histogram.show(self.__counts, self.__toeplitz.hash_key_str(), self.__hash_table_size,
+                       self.__queue_num, output)

@@ -17,6 +17,8 @@ Fixtures written (all data; no reference source is copied):
 * ``one_hot.npz``                -- the 96 one-hot inputs + all-zero + all-ones (F4).
 * ``edge/*.csv`` + ``edge_cases.json`` -- CLI edge cases (F4): inputs, exit codes,
   stdout, last stderr line and output CSV bytes.
+* ``histogram.json``             -- histogram mode (``show_histogram``) with ``plt.show``
+  patched out: bar heights / positions, caption text, title and axis labels.
 
 Run:  PYTHONDONTWRITEBYTECODE=1 MPLBACKEND=Agg python tests/golden/make_golden.py
 """
@@ -238,6 +240,33 @@ def gen_edge():
         json.dump(results, f, indent=1, sort_keys=True)
 
 
+def gen_histogram(Simulator):
+    """Histogram mode (simulator.py:118-172) with plt.show patched out: the figure's bar
+    heights, bin edges, caption text, title and axis labels for a few configs."""
+    import matplotlib.pyplot as plt
+    ex_key = [int(x, 16) for x in open(os.path.join(HERE, "example_input/hash_key.txt")).read().split(":")]
+    out = {}
+    plt.show = lambda *a, **k: None
+    for h, q in [(128, 24), (100, 7), (512, 64), (128, 1)]:
+        plt.close("all")
+        sim = Simulator(list(ex_key), h, q)
+        sim.load_ips_from_csv(os.path.join(HERE, "example_input/ips.csv"))
+        sim.calc_hash()
+        sim.calc_queue_number()
+        sim.show_histogram()
+        fig = plt.gcf()
+        ax = fig.axes[0]
+        bars = [p for p in ax.patches]
+        out["%d,%d" % (h, q)] = {
+            "heights": [float(b.get_height()) for b in bars],
+            "lefts": [float(b.get_x()) for b in bars],
+            "caption": [t.get_text() for t in fig.texts],
+            "title": ax.get_title(), "xlabel": ax.get_xlabel(), "ylabel": ax.get_ylabel(),
+        }
+    with open(os.path.join(HERE, "histogram.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+
+
 def main(parts):
     Toeplitz, Simulator, _ = import_reference()
     if "example" in parts:
@@ -250,7 +279,9 @@ def main(parts):
         gen_edge()
     if "random" in parts:
         gen_random(Toeplitz, Simulator)
+    if "histogram" in parts:
+        gen_histogram(Simulator)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1:] or ["example", "kat", "one_hot", "edge", "random"])
+    main(sys.argv[1:] or ["example", "kat", "one_hot", "edge", "random", "histogram"])
