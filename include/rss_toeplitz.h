@@ -117,6 +117,18 @@ int rss_hash_device(const rss_key* key, const rss_tuple4* d_tuples, size_t n,
 int rss_generate_tuples(uint64_t seed, uint64_t first_index, size_t n,
                         rss_tuple4* d_tuples, void* stream);
 
+/*
+ * Key search (the reference's random_hash_key,
+ * hash_key.py:53-60, is the candidate generator this evaluates at scale): for
+ * each of nkeys keys, the per-queue counts of the same n device-resident tuples.
+ * d_windows: nkeys x 96 uint32 in device memory, key k's rss_key::window at
+ * k*96.  d_counts: nkeys x nqueues uint64, row k = key k, overwritten.  One
+ * launch; each workgroup builds one key's tables and histograms a slice.
+ */
+int rss_key_search_device(const uint32_t* d_windows, size_t nkeys,
+                          const rss_tuple4* d_tuples, size_t n, uint32_t htable,
+                          uint32_t nqueues, uint64_t* d_counts, void* stream);
+
 /* Host-memory convenience path (CSV in -> CSV out): owns device buffers. */
 typedef struct rss_ctx rss_ctx;
 
@@ -167,6 +179,12 @@ int rss_csv_format(const rss_tuple4* tuples, const uint32_t* hash, const uint32_
                    size_t n, const uint64_t* counts, uint32_t nqueues,
                    const rss_csv_layout* layout, char* out, size_t cap, size_t* out_len,
                    int threads);
+
+/* rss_key_search_device on host buffers (keys: nkeys prepared keys; h_counts:
+ * nkeys x nqueues uint64).  Synchronous. */
+int rss_key_search_host(rss_ctx* ctx, const rss_key* keys, size_t nkeys,
+                        const rss_tuple4* h_tuples, size_t n, uint32_t htable,
+                        uint32_t nqueues, uint64_t* h_counts);
 
 /* Number of visible gfx950 devices (0 when there is no GPU). */
 int rss_device_count(int* out);

@@ -30,6 +30,7 @@ EXPORTED_SYMBOLS = (
     "rss_key_prepare", "rss_hash_device", "rss_generate_tuples", "rss_ctx_create",
     "rss_ctx_destroy", "rss_hash_host", "rss_device_count", "rss_last_error",
     "rss_abi_version", "rss_csv_parse", "rss_csv_format_bound", "rss_csv_format",
+    "rss_key_search_device", "rss_key_search_host",
 )
 ENOTSUP = -95
 
@@ -76,6 +77,8 @@ def _bind(lib):
         "rss_csv_parse": ([vp, sz, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(RssCsvLayout),
                            ctypes.c_int], ctypes.c_int),
         "rss_csv_format_bound": ([sz, u32], sz),
+        "rss_key_search_device": ([vp, sz, vp, sz, u32, u32, vp, vp], ctypes.c_int),
+        "rss_key_search_host": ([vp, vp, sz, vp, sz, u32, u32, vp], ctypes.c_int),
         "rss_csv_format": ([vp, vp, vp, sz, vp, u32, ctypes.POINTER(RssCsvLayout), vp, sz,
                             ctypes.POINTER(sz), ctypes.c_int], ctypes.c_int),
     }
@@ -168,6 +171,19 @@ class HostContext:
         return h, q, c
 
 
+    def key_search(self, keys, tuples, htable, nqueues):
+        """Per-queue counts (uint64[len(keys), nqueues]) of ``tuples`` under each prepared key."""
+        arr = np.ascontiguousarray(tuples)
+        if arr.dtype != TUPLE_DTYPE:
+            arr = np.ascontiguousarray(arr, dtype=np.uint32).reshape(-1, 3)
+        karr = (RssKey * len(keys))(*keys)
+        out = np.zeros((len(keys), nqueues), dtype=np.uint64)
+        _check(self._lib.rss_key_search_host(self._ctx, karr, len(keys), arr.ctypes.data, len(arr),
+                                             htable, nqueues, out.ctypes.data),
+               "rss_key_search_host")
+        return out
+
+
 _default_ctx = None
 _ctx_lock = threading.Lock()
 
@@ -187,6 +203,13 @@ def hash_device(key, tuples_ptr, n, htable, nqueues, hash_ptr=None, queue_ptr=No
     """Stream-ordered ``rss_hash_device`` on raw device pointers (ints)."""
     _check(load().rss_hash_device(ctypes.byref(key), tuples_ptr, n, htable, nqueues, hash_ptr,
                                   queue_ptr, counts_ptr, flags, stream), "rss_hash_device")
+
+
+def key_search_device(windows_ptr, nkeys, tuples_ptr, n, htable, nqueues, counts_ptr,
+                      stream=None):
+    """Stream-ordered ``rss_key_search_device`` on raw device pointers (ints)."""
+    _check(load().rss_key_search_device(windows_ptr, nkeys, tuples_ptr, n, htable, nqueues,
+                                        counts_ptr, stream), "rss_key_search_device")
 
 
 def generate_device(seed, first_index, n, tuples_ptr, stream=None):

@@ -84,6 +84,7 @@ struct LaunchParams {
     uint32_t q_m32;     // ceil(2^32 / Q): exact b % Q for b, Q < 2^16
     uint32_t pad_;
     uint64_t q_m64;     // ceil(2^64 / Q): exact b % Q for any 32-bit b, Q
+    const uint32_t* key_windows;  // key search: nkeys x 96 windows in device memory
 };
 
 // ------------------------------------------------------------- device -------
@@ -95,10 +96,11 @@ struct LaunchParams {
 // Build: thread `tid` owns v = hi*1024 + tid (hi = 0..3) of every table: the low
 // ten bits of v are its thread id, so it XORs their windows once per table and
 // derives the four entries from the two top-bit windows.
-__device__ __forceinline__ void build_lut(uint32_t* lut, const LaunchParams& p, uint32_t tid) {
+__device__ __forceinline__ void build_lut(uint32_t* lut, const uint32_t* __restrict__ window,
+                                          uint32_t tid) {
 #pragma unroll
     for (int t = 0; t < kTables; ++t) {
-        const uint32_t* w = p.window + kChunkBits * t;  // w[j] <-> bit (11 - j) of v
+        const uint32_t* w = window + kChunkBits * t;  // w[j] <-> bit (11 - j) of v
         uint32_t base = 0;
 #pragma unroll
         for (int j = 2; j < kChunkBits; ++j) base ^= ((tid >> (11 - j)) & 1u) ? w[j] : 0u;
@@ -239,7 +241,7 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
     extern __shared__ uint32_t bins[];    // histogram bins, sized at launch
     const uint32_t tid = threadIdx.x;
 
-    build_lut(lut, p, tid);
+    build_lut(lut, p.window, tid);
     const uint32_t nbins =
         kHist == HIST_PRIVATE ? p.Q * kBinCols : (kHist == HIST_SHARED ? p.Q : 0u);
     for (uint32_t e = tid; e < nbins; e += kBlock) bins[e] = 0;
@@ -299,6 +301,65 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
                 s = bins[q];
             }
             if (s) atomicAdd(&p.counts[q], (unsigned long long)s);
+        }
+    }
+}
+
+// Key search: per-queue counts of the same tuples under many
+// keys.  blockIdx.y selects the key: each workgroup builds that key's LUT from
+// p.key_windows and histograms its grid-stride share of the tuples into
+// counts[key * Q .. key * Q + Q).  No per-tuple outputs; with the tuples resident
+// in the 256 MiB Infinity Cache the re-reads per key stay on die.
+template <bool kHPow2, int kQMode, int kHist, bool kVec4>
+__global__ __launch_bounds__(kBlock) void rss_key_search_kernel(const LaunchParams p) {
+    __shared__ uint32_t lut[kLutDwords];
+    extern __shared__ uint32_t bins[];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t key = blockIdx.y;
+    build_lut(lut, p.key_windows + (size_t)RSS_INPUT_BITS * key, tid);
+    const uint32_t nbins =
+        kHist == HIST_PRIVATE ? p.Q * kBinCols : (kHist == HIST_SHARED ? p.Q : 0u);
+    for (uint32_t e = tid; e < nbins; e += kBlock) bins[e] = 0;
+    __syncthreads();
+
+    LaunchParams q = p;  // per-key counts row
+    q.counts = p.counts + (size_t)key * p.Q;
+    const uint32_t col = tid & (kBinCols - 1);
+    uint32_t hi = 4 * kTableEntries * 4;
+    asm volatile("" : "+v"(hi));
+    const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
+    const uint64_t gstride = (uint64_t)gridDim.x * kBlock;
+    uint64_t tail_begin = 0;
+    if constexpr (kVec4) {
+        const uint4* __restrict__ src = reinterpret_cast<const uint4*>(p.tuples);
+        const uint64_t ngroups = p.n >> 2;
+        for (uint64_t g = gtid; g < ngroups; g += gstride) {
+            const uint4 a = src[3 * g + 0];
+            const uint4 b = src[3 * g + 1];
+            const uint4 c = src[3 * g + 2];
+            count_queue<kHist>(bins, queue_of<kQMode>(bucket_of<kHPow2>(toeplitz_hash(lut, a.x, a.y, a.z, hi), q), q), col, q);
+            count_queue<kHist>(bins, queue_of<kQMode>(bucket_of<kHPow2>(toeplitz_hash(lut, a.w, b.x, b.y, hi), q), q), col, q);
+            count_queue<kHist>(bins, queue_of<kQMode>(bucket_of<kHPow2>(toeplitz_hash(lut, b.z, b.w, c.x, hi), q), q), col, q);
+            count_queue<kHist>(bins, queue_of<kQMode>(bucket_of<kHPow2>(toeplitz_hash(lut, c.y, c.z, c.w, hi), q), q), col, q);
+        }
+        tail_begin = ngroups << 2;
+    }
+    for (uint64_t i = tail_begin + gtid; i < p.n; i += gstride) {
+        const uint32_t* t = reinterpret_cast<const uint32_t*>(p.tuples) + 3 * i;
+        count_queue<kHist>(bins, queue_of<kQMode>(bucket_of<kHPow2>(toeplitz_hash(lut, t[0], t[1], t[2], hi), q), q), col, q);
+    }
+    if constexpr (kHist == HIST_PRIVATE || kHist == HIST_SHARED) {
+        __syncthreads();
+        for (uint32_t k = tid; k < p.Q; k += kBlock) {
+            uint32_t s;
+            if constexpr (kHist == HIST_PRIVATE) {
+                s = 0;
+                for (uint32_t c = 0; c < kBinCols; ++c)
+                    s += bins[k * kBinCols + ((c + k) & (kBinCols - 1))];
+            } else {
+                s = bins[k];
+            }
+            if (s) atomicAdd(&q.counts[k], (unsigned long long)s);
         }
     }
 }
@@ -389,6 +450,104 @@ bool aligned16(const void* ptr) { return ((uintptr_t)ptr & 15u) == 0; }
 uint64_t magic64(uint32_t d) { return UINT64_MAX / d + 1; }
 uint32_t magic32(uint32_t d) { return UINT32_MAX / d + 1; }
 
+// Modulo strategy (mask / exact 16-bit magic / exact 64-bit magic) and histogram
+// placement (private LDS columns / shared LDS bins / global atomics) for H and Q.
+// Returns whether H is a power of two.
+bool setup_modes(LaunchParams* p, uint32_t htable, uint32_t nqueues, bool want_counts, int* qmode,
+                 int* hist, uint32_t* bin_bytes) {
+    p->H = htable;
+    p->Q = nqueues;
+    p->h_mask = htable - 1;
+    p->h_m64 = magic64(htable);
+    if (nqueues >= htable) {  // bucket < htable <= nqueues: remainder is the bucket itself
+        *qmode = QM_MASK;
+        p->q_mask = 0xFFFFFFFFu;
+    } else if (is_pow2(nqueues)) {
+        *qmode = QM_MASK;
+        p->q_mask = nqueues - 1;
+    } else if (htable <= 65536u) {  // bucket < 2^16 and nqueues < htable <= 2^16
+        *qmode = QM_FAST16;
+        p->q_m32 = magic32(nqueues);
+    } else {
+        *qmode = QM_FAST32;
+        p->q_m64 = magic64(nqueues);
+    }
+    *bin_bytes = 0;
+    if (!want_counts) {
+        *hist = HIST_NONE;
+    } else if ((uint64_t)nqueues * kBinCols * 4 <= kBinBytesMax) {
+        *hist = HIST_PRIVATE;
+        *bin_bytes = nqueues * kBinCols * 4;
+    } else if ((uint64_t)nqueues * 4 <= kBinBytesMax) {
+        *hist = HIST_SHARED;
+        *bin_bytes = nqueues * 4;
+    } else {
+        *hist = HIST_GLOBAL;
+    }
+    return is_pow2(htable);
+}
+
+template <bool kHPow2, int kQMode, int kHist>
+KernelFn pick_search_vec(bool vec4) {
+    return vec4 ? rss_key_search_kernel<kHPow2, kQMode, kHist, true>
+                : rss_key_search_kernel<kHPow2, kQMode, kHist, false>;
+}
+
+template <bool kHPow2, int kQMode>
+KernelFn pick_search_hist(int hist, bool vec4) {
+    switch (hist) {
+        case HIST_PRIVATE: return pick_search_vec<kHPow2, kQMode, HIST_PRIVATE>(vec4);
+        case HIST_SHARED: return pick_search_vec<kHPow2, kQMode, HIST_SHARED>(vec4);
+        default: return pick_search_vec<kHPow2, kQMode, HIST_GLOBAL>(vec4);
+    }
+}
+
+template <bool kHPow2>
+KernelFn pick_search(int qmode, int hist, bool vec4) {
+    switch (qmode) {
+        case QM_MASK: return pick_search_hist<kHPow2, QM_MASK>(hist, vec4);
+        case QM_FAST16: return pick_search_hist<kHPow2, QM_FAST16>(hist, vec4);
+        default: return pick_search_hist<kHPow2, QM_FAST32>(hist, vec4);
+    }
+}
+
+int launch_search(const uint32_t* d_windows, size_t nkeys, const rss_tuple4* d_tuples, size_t n,
+                  uint32_t htable, uint32_t nqueues, uint64_t* d_counts, hipStream_t stream) {
+    if (!d_windows || !d_counts || nkeys == 0)
+        return set_error(RSS_EINVAL, "rss_key_search_device: windows/counts NULL or no keys");
+    if (htable < 1 || nqueues < 1)
+        return set_error(RSS_EINVAL,
+                         "rss_key_search_device: htable (%u) and nqueues (%u) must be >= 1",
+                         htable, nqueues);
+    if (n && !d_tuples) return set_error(RSS_EINVAL, "rss_key_search_device: tuples is NULL");
+    RSS_HIP_CHECK(hipMemsetAsync(d_counts, 0, sizeof(uint64_t) * nqueues * nkeys, stream));
+    if (n == 0) return RSS_OK;
+    LaunchParams p;
+    memset(&p, 0, sizeof p);
+    p.tuples = d_tuples;
+    p.n = n;
+    int qmode, hist;
+    uint32_t bin_bytes;
+    const bool h_pow2 = setup_modes(&p, htable, nqueues, true, &qmode, &hist, &bin_bytes);
+    const bool vec4 = aligned16(d_tuples);
+    KernelFn fn = h_pow2 ? pick_search<true>(qmode, hist, vec4) : pick_search<false>(qmode, hist, vec4);
+    DeviceInfo info;
+    int rc = device_info(&info);
+    if (rc) return rc;
+    // ~256K tuples per workgroup amortise its 128 KiB LUT build (~2 us)
+    const uint64_t slices = (n + (1u << 18) - 1) >> 18;
+    const unsigned gx = (unsigned)(slices < (uint64_t)info.cu_count ? slices : info.cu_count);
+    constexpr size_t kMaxKeysPerLaunch = 65535;  // grid.y limit
+    for (size_t k0 = 0; k0 < nkeys; k0 += kMaxKeysPerLaunch) {
+        const size_t kn = nkeys - k0 < kMaxKeysPerLaunch ? nkeys - k0 : kMaxKeysPerLaunch;
+        p.key_windows = d_windows + k0 * RSS_INPUT_BITS;
+        p.counts = reinterpret_cast<unsigned long long*>(d_counts + k0 * nqueues);
+        hipLaunchKernelGGL(fn, dim3(gx, (unsigned)kn), dim3(kBlock), bin_bytes, stream, p);
+        RSS_HIP_CHECK(hipGetLastError());
+    }
+    return RSS_OK;
+}
+
 int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32_t htable,
                 uint32_t nqueues, uint32_t* d_hash, void* d_queue, uint64_t* d_counts,
                 uint32_t flags, hipStream_t stream) {
@@ -422,38 +581,10 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
 
     p.counts = reinterpret_cast<unsigned long long*>(d_counts);
     p.n = n;
-    p.H = htable;
-    p.Q = nqueues;
-    const bool h_pow2 = is_pow2(htable);
-    p.h_mask = htable - 1;
-    p.h_m64 = magic64(htable);
-    int qmode;
-    if (nqueues >= htable) {  // bucket < htable <= nqueues: remainder is the bucket itself
-        qmode = QM_MASK;
-        p.q_mask = 0xFFFFFFFFu;
-    } else if (is_pow2(nqueues)) {
-        qmode = QM_MASK;
-        p.q_mask = nqueues - 1;
-    } else if (htable <= 65536u) {  // bucket < 2^16 and nqueues < htable <= 2^16
-        qmode = QM_FAST16;
-        p.q_m32 = magic32(nqueues);
-    } else {
-        qmode = QM_FAST32;
-        p.q_m64 = magic64(nqueues);
-    }
-    int hist;
-    uint32_t bin_bytes = 0;
-    if (!d_counts) {
-        hist = HIST_NONE;
-    } else if ((uint64_t)nqueues * kBinCols * 4 <= kBinBytesMax) {
-        hist = HIST_PRIVATE;
-        bin_bytes = nqueues * kBinCols * 4;
-    } else if ((uint64_t)nqueues * 4 <= kBinBytesMax) {
-        hist = HIST_SHARED;
-        bin_bytes = nqueues * 4;
-    } else {
-        hist = HIST_GLOBAL;
-    }
+    int qmode, hist;
+    uint32_t bin_bytes;
+    const bool h_pow2 = setup_modes(&p, htable, nqueues, d_counts != nullptr, &qmode, &hist,
+                                    &bin_bytes);
     // the 4-tuples-per-lane body needs 16-B aligned tuples / hashes and a queue
     // pointer aligned to the 4 queues it stores at once
     const uintptr_t qalign = qwidth == QW_U8 ? 4 : (qwidth == QW_U16 ? 8 : 16);
@@ -542,6 +673,13 @@ int rss_hash_device(const rss_key* key, const rss_tuple4* d_tuples, size_t n, ui
                     uint32_t flags, void* stream) {
     return launch_hash(key, d_tuples, n, htable, nqueues, d_hash, d_queue, d_counts, flags,
                        static_cast<hipStream_t>(stream));
+}
+
+int rss_key_search_device(const uint32_t* d_windows, size_t nkeys, const rss_tuple4* d_tuples,
+                          size_t n, uint32_t htable, uint32_t nqueues, uint64_t* d_counts,
+                          void* stream) {
+    return launch_search(d_windows, nkeys, d_tuples, n, htable, nqueues, d_counts,
+                         static_cast<hipStream_t>(stream));
 }
 
 int rss_generate_tuples(uint64_t seed, uint64_t first_index, size_t n, rss_tuple4* d_tuples,
@@ -710,6 +848,54 @@ int rss_hash_host(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples, 
         }
     }
     return RSS_OK;
+}
+
+int rss_key_search_host(rss_ctx* ctx, const rss_key* keys, size_t nkeys,
+                        const rss_tuple4* h_tuples, size_t n, uint32_t htable, uint32_t nqueues,
+                        uint64_t* h_counts) {
+    if (!ctx || !keys || !h_counts || nkeys == 0)
+        return set_error(RSS_EINVAL, "rss_key_search_host: NULL argument or no keys");
+    if (n && !h_tuples) return set_error(RSS_EINVAL, "rss_key_search_host: tuples is NULL");
+    RSS_HIP_CHECK(hipSetDevice(ctx->device));
+    std::vector<uint32_t> windows(nkeys * RSS_INPUT_BITS);
+    for (size_t k = 0; k < nkeys; ++k) {
+        if (keys[k].len < RSS_KEY_MIN_BYTES)
+            return set_error(RSS_EINVAL, "rss_key_search_host: key %zu not prepared", k);
+        memcpy(&windows[k * RSS_INPUT_BITS], keys[k].window, sizeof keys[k].window);
+    }
+    uint32_t* d_w = nullptr;
+    rss_tuple4* d_t = nullptr;
+    uint64_t* d_c = nullptr;
+    hipStream_t s = ctx->stream[0];
+    auto cleanup = [&] {
+        (void)hipFree(d_w);
+        (void)hipFree(d_t);
+        (void)hipFree(d_c);
+    };
+    int rc = RSS_OK;
+    hipError_t e = hipMalloc(&d_w, windows.size() * sizeof(uint32_t));
+    if (e == hipSuccess && n) e = hipMalloc(&d_t, n * sizeof(rss_tuple4));
+    if (e == hipSuccess) e = hipMalloc(&d_c, nkeys * nqueues * sizeof(uint64_t));
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(d_w, windows.data(), windows.size() * sizeof(uint32_t),
+                           hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && n)
+        e = hipMemcpyAsync(d_t, h_tuples, n * sizeof(rss_tuple4), hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) {
+        cleanup();
+        return set_error(e == hipErrorOutOfMemory ? RSS_ENOMEM : RSS_EIO, "rss_key_search_host: %s",
+                         hipGetErrorString(e));
+    }
+    rc = launch_search(d_w, nkeys, d_t, n, htable, nqueues, d_c, s);
+    if (rc == RSS_OK) {
+        e = hipMemcpyAsync(h_counts, d_c, nkeys * nqueues * sizeof(uint64_t),
+                           hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess)
+            rc = set_error(RSS_EIO, "rss_key_search_host: %s", hipGetErrorString(e));
+    }
+    cleanup();
+    return rc;
 }
 
 }  // extern "C"

@@ -22,8 +22,14 @@ class OracleContext:
     def hash(self, key, tuples, htable, nqueues, want_hash=True, want_queue=True,
              want_counts=True):
         self.calls += 1
-        arr = np.stack([tuples["sip"], tuples["dip"], tuples["ports"]], axis=1)
+        if tuples.dtype.names:
+            arr = np.stack([tuples["sip"], tuples["dip"], tuples["ports"]], axis=1)
+        else:
+            arr = np.asarray(tuples, dtype=np.uint32).reshape(-1, 3)
         return self.oracle_lib.run(list(key.bytes[:key.len]), arr, htable, nqueues, threads=2)
+
+    def key_search(self, keys, tuples, htable, nqueues):
+        return np.stack([self.hash(k, tuples, htable, nqueues)[2] for k in keys])
 
 
 @pytest.fixture(params=["fast", "pandas"])

@@ -1,0 +1,62 @@
+"""GPU parity for key search: every key's per-queue counts == the single-key kernel
+and the oracle, across modulo / histogram modes, ragged sizes and misaligned input."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def native():
+    from rss_simulator_nvidia_amd import _native
+    if not torch.cuda.is_available():
+        pytest.fail("gpu tests need a gfx950 device")
+    return _native
+
+
+@pytest.mark.parametrize("H,Q,n", [(128, 24, 100003), (512, 64, 65536), (100, 7, 4097),
+                                   (65536, 1000, 30001), (100000, 7, 20000), (50000, 10000, 9999),
+                                   (1, 1, 5), (128, 24, 0)])
+def test_key_search_matches_oracle(native, oracle_lib, H, Q, n):
+    from rss_simulator_nvidia_amd import keysearch
+    keys = keysearch.random_keys(19, seed=H + Q) + [[int(x) for x in range(52)]]
+    tuples = oracle_lib.generate(H * 7 + n, 0, n)
+    counts = native.HostContext(0).key_search([native.prepare_key(k) for k in keys], tuples, H, Q)
+    assert counts.shape == (len(keys), Q)
+    for k, key in enumerate(keys):
+        _, _, c = oracle_lib.run(key, tuples, H, Q)
+        np.testing.assert_array_equal(counts[k], c)
+
+
+def test_key_search_device_api_misaligned(native, oracle_lib):
+    from rss_simulator_nvidia_amd import keysearch
+    dev = torch.device("cuda:0")
+    s = torch.cuda.current_stream(dev).cuda_stream
+    keys = keysearch.random_keys(70, seed=1)
+    n, H, Q = 123457, 128, 24
+    host = oracle_lib.generate(3, 0, n)
+    raw = torch.from_numpy(host.view(np.int32).reshape(-1)).to(dev)
+    shifted = torch.empty(3 * n + 1, dtype=torch.int32, device=dev)
+    shifted[1:] = raw
+    windows = torch.from_numpy(np.stack([np.ctypeslib.as_array(native.prepare_key(k).window)
+                                         for k in keys]).astype(np.uint32).view(np.int32)).to(dev)
+    for src in (raw, shifted[1:]):
+        counts = torch.full((len(keys), Q), 5, dtype=torch.int64, device=dev)
+        native.key_search_device(windows.data_ptr(), len(keys), src.data_ptr(), n, H, Q,
+                                 counts.data_ptr(), s)
+        torch.cuda.synchronize()
+        got = counts.cpu().numpy().view(np.uint64)
+        for k in (0, 17, 69):
+            np.testing.assert_array_equal(got[k], oracle_lib.run(keys[k], host, H, Q)[2])
+        assert (got.sum(axis=1) == n).all()
+
+
+def test_search_end_to_end_improves_on_example_key(native, oracle_lib, example_key):
+    from rss_simulator_nvidia_amd import keysearch
+    tuples = oracle_lib.generate(11, 0, 200000)
+    ranked = keysearch.search(tuples, 128, 24, n_keys=256, seed=2, top=3, extra_keys=[example_key])
+    base = keysearch.balance(oracle_lib.run(example_key, tuples, 128, 24)[2], 128, 24)
+    assert ranked[0]["max_load"] <= base["max_load"][0]
+    np.testing.assert_array_equal(ranked[0]["counts"],
+                                  oracle_lib.run(ranked[0]["key"], tuples, 128, 24)[2])
