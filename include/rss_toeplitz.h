@@ -80,6 +80,25 @@ typedef struct rss_key {
  */
 int rss_key_prepare(const uint8_t* key, size_t len, rss_key* out);
 
+/*
+ * Field selection (the reference's planned "select what
+ * will be the fields used for the RSS function", docs/rss_general_explaination.md:14-18,
+ * i.e. ethtool's rx-flow-hash s/d/f/n).  The hash input becomes the concatenation
+ * of the selected fields in the order src_ip, dst_ip, src_port, dst_port.  Since
+ * Toeplitz is linear in the input bits, that equals hashing the full 12-byte tuple
+ * with window[i] replaced by the window of bit i's position in the concatenation
+ * (0 for unselected bits): the kernel is unchanged.  Apply once, after
+ * rss_key_prepare.  RSS_FIELDS_IP is the "IPv4 only" hash of the Microsoft RSS
+ * verification suite.
+ */
+#define RSS_FIELD_SRC_IP 1u
+#define RSS_FIELD_DST_IP 2u
+#define RSS_FIELD_SRC_PORT 4u
+#define RSS_FIELD_DST_PORT 8u
+#define RSS_FIELDS_IP (RSS_FIELD_SRC_IP | RSS_FIELD_DST_IP)
+#define RSS_FIELDS_ALL 15u
+int rss_key_select_fields(rss_key* key, uint32_t fields);
+
 /* flags for rss_hash_device / rss_hash_host */
 #define RSS_FLAG_ACCUMULATE 1u  /* add into counts instead of overwriting them      */
 #define RSS_FLAG_QUEUE_U16 2u   /* rss_hash_device: d_queue is uint16_t[n] (Q<=2^16) */
@@ -128,6 +147,31 @@ int rss_generate_tuples(uint64_t seed, uint64_t first_index, size_t n,
 int rss_key_search_device(const uint32_t* d_windows, size_t nkeys,
                           const rss_tuple4* d_tuples, size_t n, uint32_t htable,
                           uint32_t nqueues, uint64_t* d_counts, void* stream);
+
+/*
+ * IPv6.  36-byte input = src addr (16 B) | dst addr (16 B) |
+ * src port | dst port, the layout of the Microsoft RSS IPv6 hash; stored as nine
+ * host-order words whose big-endian bytes are that input (w[0..3] src, w[4..7]
+ * dst, w[8] = sport << 16 | dport).  288 input bits use key bits up to 319, which
+ * a 40-byte key covers without wrapping.  Fields for rss_key6_select_fields use
+ * the same RSS_FIELD_* bits (RSS_FIELDS_IP = the "IPv6 only" hash).  Queue outputs
+ * are uint32 (RSS_FLAG_QUEUE_U8/U16 are rejected).
+ */
+#define RSS_INPUT6_BITS 288
+typedef struct rss_tuple6 {
+    uint32_t w[9];
+} rss_tuple6;
+
+typedef struct rss_key6 {
+    uint32_t len;
+    uint32_t window[RSS_INPUT6_BITS];
+} rss_key6;
+
+int rss_key6_prepare(const uint8_t* key, size_t len, rss_key6* out);
+int rss_key6_select_fields(rss_key6* key, uint32_t fields);
+int rss_hash6_device(const rss_key6* key, const rss_tuple6* d_tuples, size_t n,
+                     uint32_t htable, uint32_t nqueues, uint32_t* d_hash, uint32_t* d_queue,
+                     uint64_t* d_counts, uint32_t flags, void* stream);
 
 /* Host-memory convenience path (CSV in -> CSV out): owns device buffers. */
 typedef struct rss_ctx rss_ctx;
@@ -185,6 +229,11 @@ int rss_csv_format(const rss_tuple4* tuples, const uint32_t* hash, const uint32_
 int rss_key_search_host(rss_ctx* ctx, const rss_key* keys, size_t nkeys,
                         const rss_tuple4* h_tuples, size_t n, uint32_t htable,
                         uint32_t nqueues, uint64_t* h_counts);
+
+/* rss_hash6_device on host buffers (synchronous). */
+int rss_hash6_host(rss_ctx* ctx, const rss_key6* key, const rss_tuple6* h_tuples, size_t n,
+                   uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
+                   uint64_t* h_counts, uint32_t flags);
 
 /* Number of visible gfx950 devices (0 when there is no GPU). */
 int rss_device_count(int* out);

@@ -88,6 +88,16 @@ def compute_hash_u32(key, sip, dip, ports):
     return result
 
 
+FIELD_BYTES = ((1, 0, 4), (2, 4, 4), (4, 8, 2), (8, 10, 2))  # (mask bit, offset, size)
+
+
+def select_fields_bytes(sip, dip, ports, fields):
+    """The hash input for a field mask: selected fields of the 12-byte tuple, concatenated."""
+    full = (int(sip).to_bytes(4, "big") + int(dip).to_bytes(4, "big") +
+            int(ports).to_bytes(4, "big"))
+    return b"".join(full[o:o + n] for bit, o, n in FIELD_BYTES if fields & bit)
+
+
 # ---------------------------------------------------------------- batches ----
 def windows(key):
     """window[i] = key bits [i, i + 32), MSB first (closed form of the rotation)."""
@@ -107,6 +117,21 @@ def hash_batch_np(key, tuples):
         bit = (word >> np.uint32(31 - (i & 31))) & np.uint32(1)
         h ^= bit * w[i]
     return h
+
+
+def hash_words_np(windows, words):
+    """Closed form for any input length: XOR of windows[i] over the set input bits i of
+    big-endian-valued uint32 words (shape (n, len(windows) // 32))."""
+    words = np.asarray(words, dtype=np.uint32)
+    h = np.zeros(len(words), dtype=np.uint32)
+    for i in range(len(windows)):
+        bit = (words[:, i >> 5] >> np.uint32(31 - (i & 31))) & np.uint32(1)
+        h ^= bit * np.uint32(windows[i])
+    return h
+
+
+def words_to_bytes(row):
+    return b"".join(int(w).to_bytes(4, "big") for w in row)
 
 
 def queue_and_counts(hashes, htable, nqueues):
@@ -161,6 +186,10 @@ class OracleLib:
         lib.oracle_run.argtypes = [u8p, ctypes.c_size_t, u32p, ctypes.c_size_t, ctypes.c_uint32,
                                    ctypes.c_uint32, u32p, u32p, u64p, ctypes.c_int]
         lib.oracle_run.restype = ctypes.c_int
+        lib.oracle_windows_n.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, u32p]
+        lib.oracle_windows_n.restype = ctypes.c_int
+        lib.oracle_hash_bytes.argtypes = [u8p, ctypes.c_size_t, u8p, ctypes.c_size_t]
+        lib.oracle_hash_bytes.restype = ctypes.c_uint32
         lib.oracle_generate.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t, u32p]
         lib.oracle_generate.restype = None
         self._lib = lib
@@ -181,6 +210,19 @@ class OracleLib:
     def hash_rotating(self, key, sip, dip, sport, dport):
         k, n = self._key(key)
         return self._lib.oracle_hash_rotating(k, n, sip, dip, sport, dport)
+
+    def windows_n(self, key, nbits):
+        k, n = self._key(key)
+        out = np.zeros(nbits, dtype=np.uint32)
+        if self._lib.oracle_windows_n(k, n, nbits, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))):
+            raise ValueError("bad key length %d" % n)
+        return out
+
+    def hash_bytes(self, key, data):
+        """Literal rotating-key Toeplitz over an arbitrary byte string."""
+        k, n = self._key(key)
+        d = (ctypes.c_uint8 * max(1, len(data)))(*bytearray(data))
+        return self._lib.oracle_hash_bytes(k, n, d, len(data))
 
     def run(self, key, tuples, htable, nqueues, threads=None, want_hash=True, want_queue=True):
         """Returns (hash, queue, counts) for packed tuples of shape (n, 3)."""

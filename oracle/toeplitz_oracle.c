@@ -58,6 +58,18 @@ int oracle_windows(const uint8_t* key, size_t len, uint32_t* window96) {
     return 0;
 }
 
+/* The first nbits windows (any input length, e.g. 288 for IPv6). */
+int oracle_windows_n(const uint8_t* key, size_t len, int nbits, uint32_t* window) {
+    if (len < 4 || len > ORACLE_KEY_MAX || nbits < 0) return -22;
+    uint8_t k[ORACLE_KEY_MAX];
+    memcpy(k, key, len);
+    for (int i = 0; i < nbits; ++i) {
+        window[i] = key_left_most_32bits(k);
+        shift_key(k, len);
+    }
+    return 0;
+}
+
 /* 12 big-endian input bytes (toeplitz.py:127-142); ports masked to 16 bits. */
 static void prepare_input_bytes(uint32_t sip, uint32_t dip, uint32_t sport, uint32_t dport,
                                 uint8_t* b) {
@@ -79,6 +91,24 @@ uint32_t oracle_hash_rotating(const uint8_t* key, size_t len, uint32_t sip, uint
     for (int byte = 0; byte < 12; ++byte)
         for (int bit = 7; bit >= 0; --bit) {
             if ((in[byte] >> bit) & 1) result ^= key_left_most_32bits(k);
+            shift_key(k, len);
+        }
+    return result;
+}
+
+/*
+ * The same literal loop over an arbitrary byte string (field selection and IPv6
+ * inputs: the reference's algorithm applied to other inputs; pinned by the
+ * Microsoft RSS verification suite's "IPv4 only" and IPv6 vectors).
+ */
+uint32_t oracle_hash_bytes(const uint8_t* key, size_t len, const uint8_t* data, size_t nbytes) {
+    uint8_t k[ORACLE_KEY_MAX];
+    if (len < 4 || len > ORACLE_KEY_MAX) return 0;
+    memcpy(k, key, len);
+    uint32_t result = 0;
+    for (size_t byte = 0; byte < nbytes; ++byte)
+        for (int bit = 7; bit >= 0; --bit) {
+            if ((data[byte] >> bit) & 1) result ^= key_left_most_32bits(k);
             shift_key(k, len);
         }
     return result;

@@ -30,8 +30,11 @@ EXPORTED_SYMBOLS = (
     "rss_key_prepare", "rss_hash_device", "rss_generate_tuples", "rss_ctx_create",
     "rss_ctx_destroy", "rss_hash_host", "rss_device_count", "rss_last_error",
     "rss_abi_version", "rss_csv_parse", "rss_csv_format_bound", "rss_csv_format",
-    "rss_key_search_device", "rss_key_search_host",
+    "rss_key_search_device", "rss_key_search_host", "rss_key_select_fields",
+    "rss_key6_prepare", "rss_key6_select_fields", "rss_hash6_device", "rss_hash6_host",
 )
+FIELD_SRC_IP, FIELD_DST_IP, FIELD_SRC_PORT, FIELD_DST_PORT = 1, 2, 4, 8
+FIELDS_IP, FIELDS_ALL = 3, 15
 ENOTSUP = -95
 
 
@@ -49,6 +52,16 @@ class RssKey(ctypes.Structure):
     ]
 
 
+class RssKey6(ctypes.Structure):
+    """``rss_key6``: prepared key for the 288-bit IPv6 input."""
+    _fields_ = [("len", ctypes.c_uint32), ("window", ctypes.c_uint32 * 288)]
+
+
+class RssTuple6(ctypes.Structure):
+    """``rss_tuple6``: IPv6 4-tuple as nine big-endian-valued words."""
+    _fields_ = [("w", ctypes.c_uint32 * 9)]
+
+
 class RssCsvLayout(ctypes.Structure):
     """``rss_csv_layout``: which column each CSV field holds."""
     _fields_ = [("field_column", ctypes.c_uint8 * 4)]
@@ -56,6 +69,8 @@ class RssCsvLayout(ctypes.Structure):
 
 TUPLE_DTYPE = np.dtype([("sip", "<u4"), ("dip", "<u4"), ("ports", "<u4")])
 assert TUPLE_DTYPE.itemsize == ctypes.sizeof(RssTuple4) == 12
+TUPLE6_DTYPE = np.dtype([("sip", "<u4", (4,)), ("dip", "<u4", (4,)), ("ports", "<u4")])
+assert TUPLE6_DTYPE.itemsize == ctypes.sizeof(RssTuple6) == 36
 
 _lock = threading.Lock()
 _lib = None
@@ -78,6 +93,14 @@ def _bind(lib):
                            ctypes.c_int], ctypes.c_int),
         "rss_csv_format_bound": ([sz, u32], sz),
         "rss_key_search_device": ([vp, sz, vp, sz, u32, u32, vp, vp], ctypes.c_int),
+        "rss_key_select_fields": ([key_p, u32], ctypes.c_int),
+        "rss_key6_prepare": ([ctypes.POINTER(ctypes.c_uint8), sz, ctypes.POINTER(RssKey6)],
+                             ctypes.c_int),
+        "rss_key6_select_fields": ([ctypes.POINTER(RssKey6), u32], ctypes.c_int),
+        "rss_hash6_device": ([ctypes.POINTER(RssKey6), vp, sz, u32, u32, vp, vp, vp, u32, vp],
+                             ctypes.c_int),
+        "rss_hash6_host": ([vp, ctypes.POINTER(RssKey6), vp, sz, u32, u32, vp, vp, vp, u32],
+                           ctypes.c_int),
         "rss_key_search_host": ([vp, vp, sz, vp, sz, u32, u32, vp], ctypes.c_int),
         "rss_csv_format": ([vp, vp, vp, sz, vp, u32, ctypes.POINTER(RssCsvLayout), vp, sz,
                             ctypes.POINTER(sz), ctypes.c_int], ctypes.c_int),
@@ -122,14 +145,47 @@ def device_count():
     return out.value
 
 
-def prepare_key(key_bytes):
-    """Build an :class:`RssKey` from raw key bytes (>= 4; the CLI admits 40 or 52)."""
+def parse_fields(spec):
+    """ethtool-style field letters -> mask: s src ip, d dst ip, f src port, n dst port."""
+    bits = {"s": FIELD_SRC_IP, "d": FIELD_DST_IP, "f": FIELD_SRC_PORT, "n": FIELD_DST_PORT}
+    if not spec or any(c not in bits for c in spec) or len(set(spec)) != len(spec):
+        raise ValueError("hash fields must be distinct letters of 'sdfn', got %r" % (spec,))
+    mask = 0
+    for c in spec:
+        mask |= bits[c]
+    return mask
+
+
+def prepare_key(key_bytes, fields=FIELDS_ALL):
+    """Build an :class:`RssKey` from raw key bytes (>= 4; the CLI admits 40 or 52).
+
+    ``fields`` (mask or 'sdfn' letters) selects the hashed fields; the default hashes
+    the whole 4-tuple as the reference does."""
     raw = bytes(bytearray(int(b) & 0xFF for b in key_bytes))
     if len(raw) < KEY_MIN_BYTES:
         raise ValueError("hash key must hold at least %d bytes, got %d" % (KEY_MIN_BYTES, len(raw)))
     key = RssKey()
     buf = (ctypes.c_uint8 * len(raw)).from_buffer_copy(raw)
     _check(load().rss_key_prepare(buf, len(raw), ctypes.byref(key)), "rss_key_prepare")
+    if isinstance(fields, str):
+        fields = parse_fields(fields)
+    if fields != FIELDS_ALL:
+        _check(load().rss_key_select_fields(ctypes.byref(key), fields), "rss_key_select_fields")
+    return key
+
+
+def prepare_key6(key_bytes, fields=FIELDS_ALL):
+    """Build an :class:`RssKey6` (IPv6 input) from raw key bytes; optional field mask."""
+    raw = bytes(bytearray(int(b) & 0xFF for b in key_bytes))
+    if len(raw) < KEY_MIN_BYTES:
+        raise ValueError("hash key must hold at least %d bytes, got %d" % (KEY_MIN_BYTES, len(raw)))
+    key = RssKey6()
+    buf = (ctypes.c_uint8 * len(raw)).from_buffer_copy(raw)
+    _check(load().rss_key6_prepare(buf, len(raw), ctypes.byref(key)), "rss_key6_prepare")
+    if isinstance(fields, str):
+        fields = parse_fields(fields)
+    if fields != FIELDS_ALL:
+        _check(load().rss_key6_select_fields(ctypes.byref(key), fields), "rss_key6_select_fields")
     return key
 
 
@@ -171,6 +227,21 @@ class HostContext:
         return h, q, c
 
 
+    def hash6(self, key6, tuples6, htable, nqueues, want_hash=True, want_queue=True,
+              want_counts=True):
+        """IPv6 batch (``TUPLE6_DTYPE`` or uint32 (n, 9)) -> (hash, queue, counts)."""
+        arr = np.ascontiguousarray(tuples6)
+        if arr.dtype != TUPLE6_DTYPE:
+            arr = np.ascontiguousarray(arr, dtype=np.uint32).reshape(-1, 9)
+        n = len(arr)
+        h = np.empty(n, dtype=np.uint32) if want_hash else None
+        q = np.empty(n, dtype=np.uint32) if want_queue else None
+        c = np.zeros(nqueues, dtype=np.uint64) if want_counts else None
+        ptr = lambda a: a.ctypes.data if a is not None else None  # noqa: E731
+        _check(self._lib.rss_hash6_host(self._ctx, ctypes.byref(key6), ptr(arr), n, htable,
+                                        nqueues, ptr(h), ptr(q), ptr(c), 0), "rss_hash6_host")
+        return h, q, c
+
     def key_search(self, keys, tuples, htable, nqueues):
         """Per-queue counts (uint64[len(keys), nqueues]) of ``tuples`` under each prepared key."""
         arr = np.ascontiguousarray(tuples)
@@ -203,6 +274,13 @@ def hash_device(key, tuples_ptr, n, htable, nqueues, hash_ptr=None, queue_ptr=No
     """Stream-ordered ``rss_hash_device`` on raw device pointers (ints)."""
     _check(load().rss_hash_device(ctypes.byref(key), tuples_ptr, n, htable, nqueues, hash_ptr,
                                   queue_ptr, counts_ptr, flags, stream), "rss_hash_device")
+
+
+def hash6_device(key6, tuples_ptr, n, htable, nqueues, hash_ptr=None, queue_ptr=None,
+                 counts_ptr=None, flags=0, stream=None):
+    """Stream-ordered ``rss_hash6_device`` on raw device pointers (ints)."""
+    _check(load().rss_hash6_device(ctypes.byref(key6), tuples_ptr, n, htable, nqueues, hash_ptr,
+                                   queue_ptr, counts_ptr, flags, stream), "rss_hash6_device")
 
 
 def key_search_device(windows_ptr, nkeys, tuples_ptr, n, htable, nqueues, counts_ptr,

@@ -364,6 +364,147 @@ __global__ __launch_bounds__(kBlock) void rss_key_search_kernel(const LaunchPara
     }
 }
 
+// ------------------------------------------------------------- IPv6 -------
+// 36-byte input: nine big-endian words, 288 bits.  The 12-bit
+// tables would need 384 KiB, so IPv6 uses 36 byte-slice tables (256 entries each,
+// 36 KiB -- two 1024-thread workgroups per CU): 36 ds_read_b32 + 71 VALU per tuple.
+constexpr int kWords6 = RSS_INPUT6_BITS / 32;              // 9
+constexpr int kTables6 = RSS_INPUT6_BITS / 8;              // 36
+constexpr uint32_t kLut6Dwords = kTables6 * 256;           // 9216
+constexpr uint32_t kBinBytesMax6 = 32 * 1024;
+constexpr int kBlocksPerCU6 = 2;
+
+struct LaunchParams6 {
+    uint32_t window[RSS_INPUT6_BITS];
+    const rss_tuple6* tuples;
+    uint32_t* hash_out;
+    uint32_t* queue_out;
+    unsigned long long* counts;
+    uint64_t n;
+    uint64_t h_m64;
+    uint32_t h_mask, H, Q, q_mask, q_m32, pad_;
+    uint64_t q_m64;
+};
+
+__device__ __forceinline__ void build_lut6(uint32_t* lut, const uint32_t* __restrict__ window,
+                                           uint32_t tid) {
+    for (uint32_t e = tid; e < kLut6Dwords; e += kBlock) {
+        const uint32_t* w = window + 8 * (e >> 8);  // w[j] <-> bit (7 - j) of the byte
+        const uint32_t v = e & 255;
+        uint32_t x = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x ^= ((v >> (7 - j)) & 1u) ? w[j] : 0u;
+        lut[e] = x;
+    }
+}
+
+__device__ __forceinline__ uint32_t toeplitz_hash6(const uint32_t* __restrict__ lut,
+                                                   const uint32_t (&w)[kWords6]) {
+    const char* base = reinterpret_cast<const char*>(lut);
+    uint32_t h = 0;
+#pragma unroll
+    for (int k = 0; k < kWords6; ++k) {
+        // byte j (MSB first) of word k -> table 4k + j at byte offset (4k + j) * 1024;
+        // folding each word's four terms right away bounds the live registers
+        const uint32_t o0 = (w[k] >> 22) & 0x3FCu, o1 = (w[k] >> 14) & 0x3FCu;
+        const uint32_t o2 = (w[k] >> 6) & 0x3FCu, o3 = (w[k] << 2) & 0x3FCu;
+        h ^= *reinterpret_cast<const uint32_t*>(base + (4 * k + 0) * 1024 + o0) ^
+             *reinterpret_cast<const uint32_t*>(base + (4 * k + 1) * 1024 + o1) ^
+             *reinterpret_cast<const uint32_t*>(base + (4 * k + 2) * 1024 + o2) ^
+             *reinterpret_cast<const uint32_t*>(base + (4 * k + 3) * 1024 + o3);
+    }
+    return h;
+}
+
+template <bool kHPow2, int kQMode, int kHist, bool kVec4>
+__global__ __launch_bounds__(kBlock, 8) void rss_toeplitz6_kernel(const LaunchParams6 p6) {
+    __shared__ uint32_t lut[kLut6Dwords];
+    extern __shared__ uint32_t bins[];
+    const uint32_t tid = threadIdx.x;
+    build_lut6(lut, p6.window, tid);
+    // the modulo / histogram helpers read these LaunchParams fields only
+    LaunchParams p;
+    p.counts = p6.counts;
+    p.h_m64 = p6.h_m64;
+    p.h_mask = p6.h_mask;
+    p.H = p6.H;
+    p.Q = p6.Q;
+    p.q_mask = p6.q_mask;
+    p.q_m32 = p6.q_m32;
+    p.q_m64 = p6.q_m64;
+    const uint32_t nbins =
+        kHist == HIST_PRIVATE ? p.Q * kBinCols : (kHist == HIST_SHARED ? p.Q : 0u);
+    for (uint32_t e = tid; e < nbins; e += kBlock) bins[e] = 0;
+    __syncthreads();
+    const uint32_t col = tid & (kBinCols - 1);
+    const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
+    const uint64_t gstride = (uint64_t)gridDim.x * kBlock;
+    uint64_t tail_begin = 0;
+    if constexpr (kVec4) {
+        // 4 consecutive tuples per lane: 144 B = 9 x dwordx4, 16-B aligned
+        const uint4* __restrict__ src = reinterpret_cast<const uint4*>(p6.tuples);
+        const uint64_t ngroups = p6.n >> 2;
+        for (uint64_t g = gtid; g < ngroups; g += gstride) {
+            uint32_t v[4 * kWords6];
+#pragma unroll
+            for (int k = 0; k < kWords6; ++k) {
+                const uint4 x = src[kWords6 * g + k];
+                v[4 * k] = x.x;
+                v[4 * k + 1] = x.y;
+                v[4 * k + 2] = x.z;
+                v[4 * k + 3] = x.w;
+            }
+            uint32_t h[4], q[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                uint32_t w[kWords6];
+#pragma unroll
+                for (int k = 0; k < kWords6; ++k) w[k] = v[kWords6 * t + k];
+                h[t] = toeplitz_hash6(lut, w);
+                q[t] = queue_of<kQMode>(bucket_of<kHPow2>(h[t], p), p);
+            }
+            if (p6.hash_out) {
+                uint32_t* o = p6.hash_out + 4 * g;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) stream_store(o + t, h[t]);
+            }
+            if (p6.queue_out) {
+                uint32_t* o = p6.queue_out + 4 * g;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) stream_store(o + t, q[t]);
+            }
+#pragma unroll
+            for (int t = 0; t < 4; ++t) count_queue<kHist>(bins, q[t], col, p);
+        }
+        tail_begin = ngroups << 2;
+    }
+    for (uint64_t i = tail_begin + gtid; i < p6.n; i += gstride) {
+        const uint32_t* t = p6.tuples[i].w;
+        uint32_t w[kWords6];
+#pragma unroll
+        for (int k = 0; k < kWords6; ++k) w[k] = t[k];
+        const uint32_t h = toeplitz_hash6(lut, w);
+        const uint32_t q = queue_of<kQMode>(bucket_of<kHPow2>(h, p), p);
+        if (p6.hash_out) stream_store(p6.hash_out + i, h);
+        if (p6.queue_out) stream_store(p6.queue_out + i, q);
+        count_queue<kHist>(bins, q, col, p);
+    }
+    if constexpr (kHist == HIST_PRIVATE || kHist == HIST_SHARED) {
+        __syncthreads();
+        for (uint32_t k = tid; k < p.Q; k += kBlock) {
+            uint32_t s;
+            if constexpr (kHist == HIST_PRIVATE) {
+                s = 0;
+                for (uint32_t c = 0; c < kBinCols; ++c)
+                    s += bins[k * kBinCols + ((c + k) & (kBinCols - 1))];
+            } else {
+                s = bins[k];
+            }
+            if (s) atomicAdd(&p.counts[k], (unsigned long long)s);
+        }
+    }
+}
+
 __device__ __forceinline__ uint64_t mix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;
     x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -606,6 +747,114 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
     return RSS_OK;
 }
 
+using KernelFn6 = void (*)(const LaunchParams6);
+
+template <bool kHPow2, int kQMode, int kHist>
+KernelFn6 pick6_vec(bool vec4) {
+    return vec4 ? rss_toeplitz6_kernel<kHPow2, kQMode, kHist, true>
+                : rss_toeplitz6_kernel<kHPow2, kQMode, kHist, false>;
+}
+
+template <bool kHPow2, int kQMode>
+KernelFn6 pick6_hist(int hist, bool vec4) {
+    switch (hist) {
+        case HIST_PRIVATE: return pick6_vec<kHPow2, kQMode, HIST_PRIVATE>(vec4);
+        case HIST_SHARED: return pick6_vec<kHPow2, kQMode, HIST_SHARED>(vec4);
+        case HIST_GLOBAL: return pick6_vec<kHPow2, kQMode, HIST_GLOBAL>(vec4);
+        default: return pick6_vec<kHPow2, kQMode, HIST_NONE>(vec4);
+    }
+}
+
+template <bool kHPow2>
+KernelFn6 pick6(int qmode, int hist, bool vec4) {
+    switch (qmode) {
+        case QM_MASK: return pick6_hist<kHPow2, QM_MASK>(hist, vec4);
+        case QM_FAST16: return pick6_hist<kHPow2, QM_FAST16>(hist, vec4);
+        default: return pick6_hist<kHPow2, QM_FAST32>(hist, vec4);
+    }
+}
+
+int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint32_t htable,
+                 uint32_t nqueues, uint32_t* d_hash, uint32_t* d_queue, uint64_t* d_counts,
+                 uint32_t flags, hipStream_t stream) {
+    if (!key || key->len < RSS_KEY_MIN_BYTES)
+        return set_error(RSS_EINVAL, "rss_hash6_device: key NULL or not prepared");
+    if (htable < 1 || nqueues < 1)
+        return set_error(RSS_EINVAL, "rss_hash6_device: htable (%u) and nqueues (%u) must be >= 1",
+                         htable, nqueues);
+    if (n && !d_tuples) return set_error(RSS_EINVAL, "rss_hash6_device: tuples is NULL");
+    if (flags & (RSS_FLAG_QUEUE_U8 | RSS_FLAG_QUEUE_U16))
+        return set_error(RSS_EINVAL, "rss_hash6_device: IPv6 queues are uint32 only");
+    if (d_counts && !(flags & RSS_FLAG_ACCUMULATE))
+        RSS_HIP_CHECK(hipMemsetAsync(d_counts, 0, sizeof(uint64_t) * nqueues, stream));
+    if (n == 0) return RSS_OK;
+    LaunchParams tmp;  // reuse the IPv4 mode selection
+    memset(&tmp, 0, sizeof tmp);
+    int qmode, hist;
+    uint32_t bin_bytes;
+    const bool h_pow2 = setup_modes(&tmp, htable, nqueues, d_counts != nullptr, &qmode, &hist,
+                                    &bin_bytes);
+    if (bin_bytes > kBinBytesMax6) {  // keep two workgroups per CU: fall back to shared bins
+        hist = (uint64_t)nqueues * 4 <= kBinBytesMax6 ? HIST_SHARED : HIST_GLOBAL;
+        bin_bytes = hist == HIST_SHARED ? nqueues * 4 : 0;
+    }
+    LaunchParams6 p;
+    memset(&p, 0, sizeof p);
+    memcpy(p.window, key->window, sizeof p.window);
+    p.tuples = d_tuples;
+    p.hash_out = d_hash;
+    p.queue_out = d_queue;
+    p.counts = reinterpret_cast<unsigned long long*>(d_counts);
+    p.n = n;
+    p.h_m64 = tmp.h_m64;
+    p.h_mask = tmp.h_mask;
+    p.H = tmp.H;
+    p.Q = tmp.Q;
+    p.q_mask = tmp.q_mask;
+    p.q_m32 = tmp.q_m32;
+    p.q_m64 = tmp.q_m64;
+    const bool vec4 = aligned16(d_tuples) && (!d_hash || aligned16(d_hash)) &&
+                      (!d_queue || aligned16(d_queue));
+    KernelFn6 fn = h_pow2 ? pick6<true>(qmode, hist, vec4) : pick6<false>(qmode, hist, vec4);
+    DeviceInfo info;
+    int rc = device_info(&info);
+    if (rc) return rc;
+    const uint64_t per_lane = vec4 ? 4 : 1;
+    const uint64_t want = (n + per_lane * kBlock - 1) / (per_lane * kBlock);
+    const uint64_t cap = (uint64_t)info.cu_count * kBlocksPerCU6;
+    const unsigned grid = (unsigned)(want < cap ? want : cap);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), bin_bytes, stream, p);
+    RSS_HIP_CHECK(hipGetLastError());
+    return RSS_OK;
+}
+
+// window remap for field selection over a tuple of `nfields` fields
+void remap_windows(uint32_t* window, int nbits, const int* start, const int* width, int nfields,
+                   uint32_t fields) {
+    std::vector<uint32_t> out(nbits, 0);
+    int pos = 0;
+    for (int f = 0; f < nfields; ++f) {
+        if (!(fields & (1u << f))) continue;
+        for (int b = 0; b < width[f]; ++b) out[start[f] + b] = window[pos + b];
+        pos += width[f];
+    }
+    memcpy(window, out.data(), sizeof(uint32_t) * nbits);
+}
+
+void rotation_windows(const uint8_t* key, size_t len, uint32_t* window, int nbits) {
+    // after i one-bit rotations of the whole key (toeplitz.py:83-98) its leftmost 32 bits
+    // are key bits (i + j) mod 8*len, j = 0..31
+    const uint64_t kbits = (uint64_t)len * 8;
+    for (int i = 0; i < nbits; ++i) {
+        uint32_t w = 0;
+        for (int j = 0; j < 32; ++j) {
+            const uint64_t b = ((uint64_t)i + j) % kbits;
+            w = (w << 1) | ((key[b >> 3] >> (7 - (b & 7))) & 1u);
+        }
+        window[i] = w;
+    }
+}
+
 }  // namespace
 
 // ------------------------------------------------------------ C ABI ---------
@@ -637,17 +886,96 @@ int rss_key_prepare(const uint8_t* key, size_t len, rss_key* out) {
     memset(out, 0, sizeof *out);
     out->len = (uint32_t)len;
     memcpy(out->bytes, key, len < RSS_KEY_MAX_BYTES ? len : RSS_KEY_MAX_BYTES);
-    // After i one-bit rotations of the whole key (toeplitz.py:83-98) its leftmost
-    // 32 bits are key bits (i + j) mod 8*len, j = 0..31.  For len >= 16 bytes the
-    // index never wraps and only bytes 0..15 matter.
-    const uint64_t nbits = (uint64_t)len * 8;
-    auto bit = [&](uint64_t b) -> uint32_t { return (key[b >> 3] >> (7 - (b & 7))) & 1u; };
-    for (int i = 0; i < RSS_INPUT_BITS; ++i) {
-        uint32_t w = 0;
-        for (int j = 0; j < 32; ++j) w = (w << 1) | bit(((uint64_t)i + j) % nbits);
-        out->window[i] = w;
-    }
+    // For len >= 16 bytes the rotation never wraps and only bytes 0..15 matter.
+    rotation_windows(key, len, out->window, RSS_INPUT_BITS);
     return RSS_OK;
+}
+
+int rss_key_select_fields(rss_key* key, uint32_t fields) {
+    if (!key || key->len < RSS_KEY_MIN_BYTES)
+        return set_error(RSS_EINVAL, "rss_key_select_fields: key not prepared");
+    if (fields == 0 || (fields & ~RSS_FIELDS_ALL))
+        return set_error(RSS_EINVAL, "rss_key_select_fields: bad field mask 0x%x", fields);
+    // field f spans input bits [start[f], start[f] + width[f]) of the full tuple
+    static const int kStart[4] = {0, 32, 64, 80}, kWidth[4] = {32, 32, 16, 16};
+    remap_windows(key->window, RSS_INPUT_BITS, kStart, kWidth, 4, fields);
+    return RSS_OK;
+}
+
+int rss_key6_prepare(const uint8_t* key, size_t len, rss_key6* out) {
+    if (!key || !out) return set_error(RSS_EINVAL, "rss_key6_prepare: NULL argument");
+    if (len < RSS_KEY_MIN_BYTES)
+        return set_error(RSS_EINVAL, "rss_key6_prepare: key must hold >= %d bytes, got %zu",
+                         RSS_KEY_MIN_BYTES, len);
+    memset(out, 0, sizeof *out);
+    out->len = (uint32_t)len;
+    rotation_windows(key, len, out->window, RSS_INPUT6_BITS);
+    return RSS_OK;
+}
+
+int rss_key6_select_fields(rss_key6* key, uint32_t fields) {
+    if (!key || key->len < RSS_KEY_MIN_BYTES)
+        return set_error(RSS_EINVAL, "rss_key6_select_fields: key not prepared");
+    if (fields == 0 || (fields & ~RSS_FIELDS_ALL))
+        return set_error(RSS_EINVAL, "rss_key6_select_fields: bad field mask 0x%x", fields);
+    static const int kStart[4] = {0, 128, 256, 272}, kWidth[4] = {128, 128, 16, 16};
+    remap_windows(key->window, RSS_INPUT6_BITS, kStart, kWidth, 4, fields);
+    return RSS_OK;
+}
+
+int rss_hash6_device(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint32_t htable,
+                     uint32_t nqueues, uint32_t* d_hash, uint32_t* d_queue, uint64_t* d_counts,
+                     uint32_t flags, void* stream) {
+    return launch_hash6(key, d_tuples, n, htable, nqueues, d_hash, d_queue, d_counts, flags,
+                        static_cast<hipStream_t>(stream));
+}
+
+int rss_hash6_host(rss_ctx* ctx, const rss_key6* key, const rss_tuple6* h_tuples, size_t n,
+                   uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
+                   uint64_t* h_counts, uint32_t flags) {
+    if (!ctx) return set_error(RSS_EINVAL, "rss_hash6_host: ctx is NULL");
+    if (n && !h_tuples) return set_error(RSS_EINVAL, "rss_hash6_host: tuples is NULL");
+    RSS_HIP_CHECK(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream[0];
+    rss_tuple6* d_t = nullptr;
+    uint32_t *d_h = nullptr, *d_q = nullptr;
+    uint64_t* d_c = nullptr;
+    auto cleanup = [&] {
+        (void)hipFree(d_t);
+        (void)hipFree(d_h);
+        (void)hipFree(d_q);
+        (void)hipFree(d_c);
+    };
+    hipError_t e = hipSuccess;
+    if (n) e = hipMalloc(&d_t, n * sizeof(rss_tuple6));
+    if (e == hipSuccess && n && h_hash) e = hipMalloc(&d_h, n * 4);
+    if (e == hipSuccess && n && h_queue) e = hipMalloc(&d_q, n * 4);
+    if (e == hipSuccess && h_counts) e = hipMalloc(&d_c, nqueues * 8);
+    if (e == hipSuccess && n)
+        e = hipMemcpyAsync(d_t, h_tuples, n * sizeof(rss_tuple6), hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) {
+        cleanup();
+        return set_error(e == hipErrorOutOfMemory ? RSS_ENOMEM : RSS_EIO, "rss_hash6_host: %s",
+                         hipGetErrorString(e));
+    }
+    int rc = launch_hash6(key, d_t, n, htable, nqueues, d_h, d_q, d_c,
+                          0u, s);  // device counts start at 0; accumulation happens on the host
+    if (rc == RSS_OK) {
+        if (d_h) e = hipMemcpyAsync(h_hash, d_h, n * 4, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess && d_q) e = hipMemcpyAsync(h_queue, d_q, n * 4, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess && d_c) {
+            std::vector<uint64_t> tmp(nqueues);
+            e = hipMemcpyAsync(tmp.data(), d_c, nqueues * 8, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e == hipSuccess)
+                for (uint32_t q = 0; q < nqueues; ++q)
+                    h_counts[q] = (flags & RSS_FLAG_ACCUMULATE ? h_counts[q] : 0) + tmp[q];
+        }
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = set_error(RSS_EIO, "rss_hash6_host: %s", hipGetErrorString(e));
+    }
+    cleanup();
+    return rc;
 }
 
 int rss_device_count(int* out) {

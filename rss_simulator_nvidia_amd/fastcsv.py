@@ -22,7 +22,8 @@ def enabled():
     return os.environ.get("RSS_CSV_FASTPATH", "1") != "0"
 
 
-def run_csv(hash_key, ips_file, htable, nqueues, output, threads=0, timings=None):
+def run_csv(hash_key, ips_file, htable, nqueues, output, threads=0, timings=None,
+            fields=_native.FIELDS_ALL):
     """Process ``ips_file`` into ``output``; False if the file needs the pandas path."""
     t = [time.perf_counter()]
     try:
@@ -35,7 +36,7 @@ def run_csv(hash_key, ips_file, htable, nqueues, output, threads=0, timings=None
         return False
     tuples, layout = parsed
     t.append(time.perf_counter())
-    key = _native.prepare_key(hash_key)
+    key = _native.prepare_key(hash_key, fields)
     h, q, c = _native.default_context().hash(key, tuples, htable, nqueues)
     t.append(time.perf_counter())
     out = _native.csv_format(tuples, h, q, c, layout, threads)
@@ -52,7 +53,7 @@ def run_csv(hash_key, ips_file, htable, nqueues, output, threads=0, timings=None
     return True
 
 
-def run_counts(hash_key, ips_file, htable, nqueues, threads=0):
+def run_counts(hash_key, ips_file, htable, nqueues, threads=0, fields=_native.FIELDS_ALL):
     """Per-queue counts of a canonical file via the counts-only kernel (12 B/tuple);
     None if the file needs the pandas path."""
     try:
@@ -62,7 +63,7 @@ def run_counts(hash_key, ips_file, htable, nqueues, threads=0):
     parsed = _native.csv_parse(data, threads)
     if parsed is None:
         return None
-    key = _native.prepare_key(hash_key)
+    key = _native.prepare_key(hash_key, fields)
     _, _, counts = _native.default_context().hash(key, parsed[0], htable, nqueues,
                                                   want_hash=False, want_queue=False)
     return counts

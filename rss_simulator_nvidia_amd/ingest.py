@@ -19,7 +19,7 @@ by column, so with several bad cells the reported one may differ (same exit).
 import numpy as np
 import pandas as pd
 
-from rss_simulator_nvidia_amd._native import TUPLE_DTYPE
+from rss_simulator_nvidia_amd._native import TUPLE6_DTYPE, TUPLE_DTYPE
 from rss_simulator_nvidia_amd.column_names import ColumnNames
 
 _DOTTED = r"[0-9]{1,3}\.[0-9]{1,3}\.[0-9]{1,3}\.[0-9]{1,3}"
@@ -95,3 +95,32 @@ def pack_frame(df):
                         ip_column(df[ColumnNames.DST_IP.value]),
                         port_column(df[ColumnNames.SRC_PORT.value]),
                         port_column(df[ColumnNames.DST_PORT.value]))
+
+
+# ------------------------------------------------------------------ IPv6 -----
+def ipv6_words(ip):
+    """An IPv6 address (any ``ipaddress`` text form) as four big-endian-valued words."""
+    import ipaddress
+    packed = ipaddress.IPv6Address(ip.strip() if isinstance(ip, str) else ip).packed
+    return [int.from_bytes(packed[4 * k:4 * k + 4], "big") for k in range(4)]
+
+
+def ipv6_column(series):
+    """uint32[n, 4] for an IPv6 address column; ValueError on a non-IPv6 cell."""
+    values = series.to_numpy()
+    out = np.empty((len(values), 4), dtype=np.uint32)
+    for i, v in enumerate(values):
+        out[i] = ipv6_words(v)
+    return out
+
+
+def pack_frame6(df):
+    """``rss_tuple6`` rows for a DataFrame whose address columns hold IPv6 addresses."""
+    n = len(df)
+    out = np.empty(n, dtype=TUPLE6_DTYPE)
+    out["sip"] = ipv6_column(df[ColumnNames.SRC_IP.value])
+    out["dip"] = ipv6_column(df[ColumnNames.DST_IP.value])
+    sp = port_column(df[ColumnNames.SRC_PORT.value])
+    dp = port_column(df[ColumnNames.DST_PORT.value])
+    out["ports"] = (sp << np.uint32(16)) | dp
+    return out

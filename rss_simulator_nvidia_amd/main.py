@@ -10,12 +10,17 @@ pandas path of ``Simulator``.
 import argparse
 from argparse import ArgumentParser
 
-from rss_simulator_nvidia_amd import fastcsv, histogram
+from rss_simulator_nvidia_amd import _native, fastcsv, histogram
 from rss_simulator_nvidia_amd.arg_parse_types import PositiveInt
 from rss_simulator_nvidia_amd.arg_parse_types import arg_parse_type_decorator as apt_decorator
 from rss_simulator_nvidia_amd.hash_key import HashKey
 from rss_simulator_nvidia_amd.simulator import Simulator
 from rss_simulator_nvidia_amd.toeplitz import Toeplitz
+
+
+def _fields_arg(text):
+    _native.parse_fields(text)
+    return text
 
 
 def build_parser():
@@ -35,8 +40,16 @@ def build_parser():
     parser.add_argument("--num-queues", metavar="NUM", type=PositiveInt.parse, required=True,
                         help="Positive number representing number of queues.")
     parser.add_argument("--csv", metavar="PATH", help="Write output to csv file.")
-    # additive (not in the reference): save the histogram instead of opening a window
+    # Additive options (not in the reference).  They are
+    # kept out of usage/--help so the reference's argparse messages stay byte-identical:
+    #   --histogram-png PATH  save the histogram instead of opening a window
+    #   --hash-fields FIELDS  hashed fields, ethtool letters: s src ip, d dst ip,
+    #                         f src port, n dst port (default sdfn = whole 4-tuple)
+    #   --ipv6                address columns hold IPv6 addresses (36-byte input)
     parser.add_argument("--histogram-png", metavar="PATH", help=argparse.SUPPRESS)
+    parser.add_argument("--hash-fields", metavar="FIELDS", default="sdfn",
+                        type=apt_decorator(_fields_arg), help=argparse.SUPPRESS)
+    parser.add_argument("--ipv6", action="store_true", help=argparse.SUPPRESS)
     return parser
 
 
@@ -48,16 +61,18 @@ def parse_args(argv=None):
 def main(argv=None):
     """Invoke the RSS simulator (``main.py:54-64``)."""
     args = parse_args(argv)
-    if args.csv and fastcsv.enabled() and fastcsv.run_csv(
-            args.key, args.ips_file, args.htable_size, args.num_queues, args.csv):
+    fast = fastcsv.enabled() and not args.ipv6
+    if args.csv and fast and fastcsv.run_csv(args.key, args.ips_file, args.htable_size,
+                                             args.num_queues, args.csv, fields=args.hash_fields):
         return  # canonical input: native CSV parse/format around the same GPU kernel
-    if not args.csv and fastcsv.enabled():
-        counts = fastcsv.run_counts(args.key, args.ips_file, args.htable_size, args.num_queues)
+    if not args.csv and fast:
+        counts = fastcsv.run_counts(args.key, args.ips_file, args.htable_size, args.num_queues,
+                                    fields=args.hash_fields)
         if counts is not None:  # histogram mode needs the per-queue counts only
             histogram.show(counts, Toeplitz(args.key).hash_key_str(), args.htable_size,
                            args.num_queues, args.histogram_png)
             return
-    rss_sim = Simulator(args.key, args.htable_size, args.num_queues)
+    rss_sim = Simulator(args.key, args.htable_size, args.num_queues, args.hash_fields, args.ipv6)
     rss_sim.load_ips_from_csv(args.ips_file)
     rss_sim.calc_hash()
     rss_sim.calc_queue_number()

@@ -25,7 +25,7 @@ from pandas.errors import ParserError as pd_ParserError
 from rss_simulator_nvidia_amd import histogram
 from rss_simulator_nvidia_amd.column_names import INPUT_COLUMNS, ColumnNames
 from rss_simulator_nvidia_amd.exceptions import ParseException
-from rss_simulator_nvidia_amd.ingest import pack_frame
+from rss_simulator_nvidia_amd.ingest import pack_frame, pack_frame6
 from rss_simulator_nvidia_amd.toeplitz import Toeplitz
 
 _HASH = ColumnNames.HASH_RESULT.value
@@ -35,10 +35,14 @@ _QUEUE = ColumnNames.QUEUE_NUMBER.value
 class Simulator(object):
     """RSS simulator class (``simulator.py:26``)."""
 
-    def __init__(self, hash_key, hash_table_size, queue_number):
-        """Key as ``List[int]``, hash-table size and number of queues (both >= 1)."""
+    def __init__(self, hash_key, hash_table_size, queue_number, hash_fields=None, ipv6=False):
+        """Key as ``List[int]``, hash-table size and number of queues (both >= 1).
+
+        Additive options: ``hash_fields`` (mask or ``'sdfn'``
+        letters) selects the hashed fields; ``ipv6`` reads IPv6 address columns."""
         self.__ip_df = None
-        self.__toeplitz = Toeplitz(hash_key)
+        self.__toeplitz = Toeplitz(hash_key, hash_fields or "sdfn")
+        self.__ipv6 = ipv6
         self.__hash_table_size = hash_table_size
         self.__queue_num = queue_number
         self.__queues = None
@@ -81,8 +85,12 @@ class Simulator(object):
             # the reference's DataFrame.apply on zero rows fails the same way
             raise ValueError("Cannot set a DataFrame with multiple columns to the single column "
                              "hash_result")
-        tuples = pack_frame(df)
-        h, q, c = self.__toeplitz.compute_queues(tuples, self.__hash_table_size, self.__queue_num)
+        if self.__ipv6:
+            h, q, c = self.__toeplitz.compute_queues6(pack_frame6(df), self.__hash_table_size,
+                                                      self.__queue_num)
+        else:
+            h, q, c = self.__toeplitz.compute_queues(pack_frame(df), self.__hash_table_size,
+                                                     self.__queue_num)
         df[_HASH] = h.astype(np.int64)
         self.__queues = q
         self.__counts = c

@@ -16,10 +16,15 @@ from rss_simulator_nvidia_amd.ingest import ip_to_u32, pack_columns
 class Toeplitz(object):
     """Toeplitz RSS-hash related functionality (``toeplitz.py:5``)."""
 
-    def __init__(self, hash_key=None):
-        """Initialise with a key (``List[int]``); a random 40-byte key if None/empty."""
+    def __init__(self, hash_key=None, fields=_native.FIELDS_ALL):
+        """Initialise with a key (``List[int]``); a random 40-byte key if None/empty.
+
+        ``fields`` (additive): field mask or ethtool letters ``'sdfn'`` selecting the
+        hashed fields; the default hashes the whole 4-tuple like the reference."""
         self.__hash_key = hash_key if hash_key else HashKey.random_hash_key()
+        self.__fields = fields
         self.__prepared = None
+        self.__prepared6 = None
 
     @property
     def hash_key(self):
@@ -30,6 +35,7 @@ class Toeplitz(object):
     def hash_key(self, hash_key):
         self.__hash_key = hash_key
         self.__prepared = None
+        self.__prepared6 = None
 
     def hash_key_str(self):
         """Colon-separated two-digit hex (``toeplitz.py:37-44``)."""
@@ -39,8 +45,15 @@ class Toeplitz(object):
     def prepared_key(self):
         """The :class:`rss_simulator_nvidia_amd._native.RssKey` for this key (cached)."""
         if self.__prepared is None:
-            self.__prepared = _native.prepare_key(self.__hash_key)
+            self.__prepared = _native.prepare_key(self.__hash_key, self.__fields)
         return self.__prepared
+
+    @property
+    def prepared_key6(self):
+        """The :class:`rss_simulator_nvidia_amd._native.RssKey6` (IPv6 input) for this key."""
+        if self.__prepared6 is None:
+            self.__prepared6 = _native.prepare_key6(self.__hash_key, self.__fields)
+        return self.__prepared6
 
     def compute_hash(self, src_ip, dst_ip, src_port, dst_port):
         """Hash one 4-tuple (``toeplitz.py:46-69``); IPs are dotted strings."""
@@ -63,3 +76,8 @@ class Toeplitz(object):
         """
         return _native.default_context().hash(self.prepared_key, np.asarray(tuples),
                                               hash_table_size, queue_number)
+
+    def compute_queues6(self, tuples6, hash_table_size, queue_number):
+        """IPv6 counterpart of :meth:`compute_queues` (``rss_tuple6`` rows)."""
+        return _native.default_context().hash6(self.prepared_key6, np.asarray(tuples6),
+                                               hash_table_size, queue_number)

@@ -102,8 +102,11 @@ def gen_kat(Toeplitz):
     t = Toeplitz(key)
     vecs = []
     for s, d, sp, dp in MS_VECTORS:
+        # "hash_ip_only": the reference with both ports 0 = the 8-byte (src, dst) input,
+        # the verification suite's "IPv4 only" column
         vecs.append({"src_ip": s, "dst_ip": d, "src_port": sp, "dst_port": dp,
-                     "hash": t.compute_hash(s, d, sp, dp)})
+                     "hash": t.compute_hash(s, d, sp, dp),
+                     "hash_ip_only": t.compute_hash(s, d, 0, 0)})
     with open(os.path.join(HERE, "ms_kat.json"), "w") as f:
         json.dump({"key": key_text(key), "vectors": vecs}, f, indent=1)
 
