@@ -32,6 +32,7 @@ EXPORTED_SYMBOLS = (
     "rss_abi_version", "rss_csv_parse", "rss_csv_format_bound", "rss_csv_format",
     "rss_key_search_device", "rss_key_search_host", "rss_key_select_fields",
     "rss_key6_prepare", "rss_key6_select_fields", "rss_hash6_device", "rss_hash6_host",
+    "rss_pcap_parse",
 )
 FIELD_SRC_IP, FIELD_DST_IP, FIELD_SRC_PORT, FIELD_DST_PORT = 1, 2, 4, 8
 FIELDS_IP, FIELDS_ALL = 3, 15
@@ -94,6 +95,8 @@ def _bind(lib):
         "rss_csv_format_bound": ([sz, u32], sz),
         "rss_key_search_device": ([vp, sz, vp, sz, u32, u32, vp, vp], ctypes.c_int),
         "rss_key_select_fields": ([key_p, u32], ctypes.c_int),
+        "rss_pcap_parse": ([vp, sz, vp, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)],
+                           ctypes.c_int),
         "rss_key6_prepare": ([ctypes.POINTER(ctypes.c_uint8), sz, ctypes.POINTER(RssKey6)],
                              ctypes.c_int),
         "rss_key6_select_fields": ([ctypes.POINTER(RssKey6), u32], ctypes.c_int),
@@ -332,3 +335,20 @@ def csv_format(tuples, hashes, queues, counts, layout, threads=0):
                               counts.ctypes.data, nq, ctypes.byref(layout), out.ctypes.data, cap,
                               ctypes.byref(out_len), threads), "rss_csv_format")
     return out[:out_len.value]
+
+
+# ------------------------------------------------------------------ pcap ----
+def pcap_parse(data):
+    """Classic pcap image -> ``(tuples, protocols, skipped)`` or None if not pcap."""
+    buf = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+    lib = load()
+    cap = len(buf) // 36 + 1  # a record holds >= 16 B header + 20 B IPv4 header
+    tuples = np.empty(cap, dtype=TUPLE_DTYPE)
+    protos = np.empty(cap, dtype=np.uint8)
+    n, skipped = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    rc = lib.rss_pcap_parse(buf.ctypes.data, len(buf), tuples.ctypes.data, protos.ctypes.data, cap,
+                            ctypes.byref(n), ctypes.byref(skipped))
+    if rc == ENOTSUP:
+        return None
+    _check(rc, "rss_pcap_parse")
+    return tuples[:n.value], protos[:n.value], skipped.value

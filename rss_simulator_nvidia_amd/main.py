@@ -10,9 +10,10 @@ pandas path of ``Simulator``.
 import argparse
 from argparse import ArgumentParser
 
-from rss_simulator_nvidia_amd import _native, fastcsv, histogram
+from rss_simulator_nvidia_amd import _native, fastcsv, histogram, pcap
 from rss_simulator_nvidia_amd.arg_parse_types import PositiveInt
 from rss_simulator_nvidia_amd.arg_parse_types import arg_parse_type_decorator as apt_decorator
+from rss_simulator_nvidia_amd.exceptions import ParseException
 from rss_simulator_nvidia_amd.hash_key import HashKey
 from rss_simulator_nvidia_amd.simulator import Simulator
 from rss_simulator_nvidia_amd.toeplitz import Toeplitz
@@ -21,6 +22,27 @@ from rss_simulator_nvidia_amd.toeplitz import Toeplitz
 def _fields_arg(text):
     _native.parse_fields(text)
     return text
+
+
+def _l4_arg(text):
+    pcap.parse_l4(text)
+    return text
+
+
+def run_pcap(args):
+    """--pcap: unique IPv4 flows of a capture -> the same kernel -> CSV or histogram."""
+    tuples, _, _ = pcap.read_flows(args.ips_file, args.pcap_l4)
+    if len(tuples) == 0:
+        raise ParseException("%s holds no IPv4 packets" % args.ips_file)
+    key = _native.prepare_key(args.key, args.hash_fields)
+    h, q, c = _native.default_context().hash(key, tuples, args.htable_size, args.num_queues)
+    key_str = Toeplitz(args.key).hash_key_str()
+    if args.csv:
+        out = _native.csv_format(tuples, h, q, c, _native.RssCsvLayout((0, 1, 2, 3)))
+        out.tofile(args.csv)
+        print("Wrote statistics to {csv}.".format(csv=args.csv))
+    else:
+        histogram.show(c, key_str, args.htable_size, args.num_queues, args.histogram_png)
 
 
 def build_parser():
@@ -50,6 +72,11 @@ def build_parser():
     parser.add_argument("--hash-fields", metavar="FIELDS", default="sdfn",
                         type=apt_decorator(_fields_arg), help=argparse.SUPPRESS)
     parser.add_argument("--ipv6", action="store_true", help=argparse.SUPPRESS)
+    #   --pcap                --ips-file is a classic pcap capture (unique IPv4 flows)
+    #   --pcap-l4 LIST        protocols whose ports are hashed (tcp,udp,sctp | none)
+    parser.add_argument("--pcap", action="store_true", help=argparse.SUPPRESS)
+    parser.add_argument("--pcap-l4", metavar="LIST", default="all",
+                        type=apt_decorator(_l4_arg), help=argparse.SUPPRESS)
     return parser
 
 
@@ -61,6 +88,8 @@ def parse_args(argv=None):
 def main(argv=None):
     """Invoke the RSS simulator (``main.py:54-64``)."""
     args = parse_args(argv)
+    if args.pcap:
+        return run_pcap(args)
     fast = fastcsv.enabled() and not args.ipv6
     if args.csv and fast and fastcsv.run_csv(args.key, args.ips_file, args.htable_size,
                                              args.num_queues, args.csv, fields=args.hash_fields):

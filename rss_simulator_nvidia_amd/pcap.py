@@ -1,0 +1,49 @@
+"""pcap input (the reference's planned "Use pcap as input",
+``docs/rss_general_explaination.md:19``).
+
+``read_flows`` turns a capture into the flow list the simulator hashes: one 4-tuple
+per IPv4 packet (``rss_pcap_parse``), optionally restricted to the L4 protocols whose
+ports take part in the hash (ethtool ``rx-flow-hash`` style: e.g. only UDP -- the
+reference's "Only on UDPs"), then de-duplicated to unique flows in first-seen
+order, the unit the reference's histogram counts ("Number of Unique Flows per
+Queue", ``simulator.py:152``).
+"""
+import numpy as np
+
+from rss_simulator_nvidia_amd import _native
+from rss_simulator_nvidia_amd.exceptions import ParseException
+
+PROTOCOLS = {"tcp": 6, "udp": 17, "sctp": 132}
+
+
+def parse_l4(spec):
+    """'tcp,udp' -> {6, 17}; 'none' -> set()."""
+    if spec in (None, "", "all"):
+        return set(PROTOCOLS.values())
+    if spec == "none":
+        return set()
+    try:
+        return {PROTOCOLS[p] for p in spec.split(",")}
+    except KeyError:
+        raise ValueError("L4 protocols must be a comma list of tcp, udp, sctp (or none)")
+
+
+def read_flows(path, l4=None, unique=True):
+    """Packed 4-tuples of a capture's IPv4 packets -> (tuples, protocols, skipped packets)."""
+    try:
+        data = np.fromfile(path, dtype=np.uint8)
+    except OSError as err:
+        raise ParseException("Couldn't read pcap file %s: %s" % (path, err))
+    parsed = _native.pcap_parse(data)
+    if parsed is None:
+        raise ParseException("%s is not a classic pcap file" % path)
+    tuples, protos, skipped = parsed
+    keep = parse_l4(l4)
+    if keep != set(PROTOCOLS.values()):
+        tuples = tuples.copy()
+        tuples["ports"][~np.isin(protos, list(keep))] = 0
+    if unique and len(tuples):
+        _, first = np.unique(tuples, return_index=True)
+        order = np.sort(first)
+        tuples, protos = tuples[order], protos[order]
+    return tuples, protos, skipped

@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 
 from cli_cases import check_edge, check_example, edge_params, example_params
+from oracle import oracle as o
 from rss_simulator_nvidia_amd import _native
 
 
@@ -26,7 +27,10 @@ class OracleContext:
             arr = np.stack([tuples["sip"], tuples["dip"], tuples["ports"]], axis=1)
         else:
             arr = np.asarray(tuples, dtype=np.uint32).reshape(-1, 3)
-        return self.oracle_lib.run(list(key.bytes[:key.len]), arr, htable, nqueues, threads=2)
+        # the prepared key's own windows (field selection remaps them), closed form
+        h = o.hash_words_np(np.ctypeslib.as_array(key.window), arr)
+        q, c = o.queue_and_counts(h, htable, nqueues)
+        return h, q, c
 
     def key_search(self, keys, tuples, htable, nqueues):
         return np.stack([self.hash(k, tuples, htable, nqueues)[2] for k in keys])

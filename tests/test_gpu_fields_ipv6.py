@@ -123,3 +123,35 @@ def test_cli_ipv6_and_fields(tmp_path, golden_dir, oracle_lib, capsys):
         want = [oracle_lib.hash_bytes(key, o.words_to_bytes(w)[:nbytes]) for w in words]
         assert table.hash_result.tolist() == want
         assert table.queue_number.tolist() == [h % 128 % 24 for h in want]
+
+
+def test_cli_pcap_gpu(tmp_path, golden_dir, oracle_lib, capsys):
+    """20K-packet synthetic capture (Ethernet/VLAN, TCP/UDP/ICMP, repeats) through --pcap."""
+    from cli_cases import run_main
+    from pcap_builder import ether, ipv4, l4, pcap_file
+    from rss_simulator_nvidia_amd import pcap
+    rng = np.random.default_rng(9)
+    pk = []
+    for i in range(20000):
+        a, b = tuple(int(x) for x in rng.integers(0, 256, 4)), tuple(int(x) for x in rng.integers(0, 256, 4))
+        proto = (6, 17, 1)[i % 3]
+        body = l4(int(rng.integers(0, 65536)), int(rng.integers(0, 65536))) if proto != 1 else b"\x00" * 20
+        pk.append(ether(ipv4(a, b, proto, body), vlans=[(0x8100, 5)] if i % 5 == 0 else ()))
+        if i % 7 == 0:
+            pk.append(pk[-1])  # repeated packet of the same flow
+    path = tmp_path / "cap.pcap"
+    path.write_bytes(pcap_file(pk))
+    out = tmp_path / "out.csv"
+    key_file = os.path.join(golden_dir, "example_input", "hash_key.txt")
+    status, so, _, exc = run_main(["--key-file", key_file, "--ips-file", str(path), "--pcap",
+                                   "--htable-size", "512", "--num-queues", "16", "--csv", str(out),
+                                   "--pcap-l4", "udp"], capsys)
+    assert status == 0, exc
+    key = [int(x, 16) for x in open(key_file).read().split(":")]
+    t, _, _ = pcap.read_flows(str(path), "udp")
+    assert len(t) == 20000
+    h, q, c = oracle_lib.run(key, np.stack([t["sip"], t["dip"], t["ports"]], axis=1), 512, 16)
+    lines = out.read_text().splitlines()
+    body = lines[lines.index("src_ip,dst_ip,src_port,dst_port,hash_result,queue_number") + 1:]
+    assert [int(x.split(",")[4]) for x in body] == h.tolist()
+    assert lines[1:17] == ["%d,%d" % (i, c[i]) for i in range(16) if c[i]]

@@ -1,0 +1,116 @@
+"""pcap input (row f4), host side: the native parser against captures built by
+tests/pcap_builder.py with known tuples; flow de-duplication; L4 selection; the CLI
+(device call replaced by the oracle).  The capture format is new to this build (the
+reference only plans it), so parsing parity is against the constructed expectations;
+the hashes of the extracted tuples are pinned like every other input."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as o
+from pcap_builder import ether, ipv4, l4, pcap_file, sll
+from rss_simulator_nvidia_amd import _native, pcap
+from rss_simulator_nvidia_amd.main import main
+from test_cli_host import OracleContext
+
+A, B, C = (10, 0, 0, 1), (192, 168, 1, 20), (8, 8, 8, 8)
+
+
+def u32(ip):
+    return ip[0] << 24 | ip[1] << 16 | ip[2] << 8 | ip[3]
+
+
+def packets_and_expected():
+    pk, want = [], []
+    pk.append(ether(ipv4(A, B, 6, l4(1234, 80))))                      # TCP
+    want.append((u32(A), u32(B), 1234 << 16 | 80, 6))
+    pk.append(ether(ipv4(B, A, 17, l4(53, 40000)), vlans=[(0x8100, 7)]))  # UDP, VLAN
+    want.append((u32(B), u32(A), 53 << 16 | 40000, 17))
+    pk.append(ether(ipv4(A, C, 1, b"\x08\x00" + b"\x00" * 30)))        # ICMP: ports 0
+    want.append((u32(A), u32(C), 0, 1))
+    pk.append(ether(ipv4(A, B, 17, l4(1, 2), frag=0x2000)))            # first fragment
+    want.append((u32(A), u32(B), 0, 17))
+    pk.append(ether(ipv4(A, B, 17, b"\x00" * 8, frag=0x0010)))         # later fragment
+    want.append((u32(A), u32(B), 0, 17))
+    pk.append(ether(ipv4(C, A, 132, l4(9, 10)), vlans=[(0x88A8, 1), (0x8100, 2)]))  # SCTP QinQ
+    want.append((u32(C), u32(A), 9 << 16 | 10, 132))
+    pk.append(ether(ipv4(A, B, 6, l4(5, 6), ihl_words=7)))             # IP options
+    want.append((u32(A), u32(B), 5 << 16 | 6, 6))
+    pk.append(ether(b"\x60" + b"\x00" * 60, ethertype=0x86DD))         # IPv6: skipped
+    pk.append(ether(b"\x00" * 28, ethertype=0x0806))                   # ARP: skipped
+    pk.append(ether(ipv4(A, B, 6, b"\x00\x01")))                       # truncated TCP: skipped
+    pk.append(ether(ipv4(A, B, 6, l4(1234, 80))))                      # duplicate flow
+    want.append((u32(A), u32(B), 1234 << 16 | 80, 6))
+    return pk, want, 3
+
+
+def as_rows(tuples, protos):
+    return [(int(t["sip"]), int(t["dip"]), int(t["ports"]), int(p)) for t, p in zip(tuples, protos)]
+
+
+@pytest.mark.parametrize("big_endian,nanos", [(False, False), (True, False), (False, True)])
+def test_parse_ethernet(big_endian, nanos):
+    pk, want, skipped = packets_and_expected()
+    got = _native.pcap_parse(pcap_file(pk, big_endian=big_endian, nanos=nanos))
+    assert got is not None
+    assert as_rows(got[0], got[1]) == want and got[2] == skipped
+
+
+def test_parse_cooked_and_raw():
+    pk = [sll(ipv4(A, B, 17, l4(7, 8))), sll(b"\x00" * 40, ethertype=0x86DD)]
+    t, p, s = _native.pcap_parse(pcap_file(pk, linktype=113))
+    assert as_rows(t, p) == [(u32(A), u32(B), 7 << 16 | 8, 17)] and s == 1
+    for lt in (101, 228):
+        t, p, s = _native.pcap_parse(pcap_file([ipv4(C, B, 6, l4(1, 2))], linktype=lt))
+        assert as_rows(t, p) == [(u32(C), u32(B), 1 << 16 | 2, 6)] and s == 0
+
+
+def test_truncated_file_and_non_pcap():
+    pk, want, _ = packets_and_expected()
+    t, p, _ = _native.pcap_parse(pcap_file(pk, truncate_last=5))
+    assert as_rows(t, p) == want[:-1]
+    assert _native.pcap_parse(b"src_ip,dst_ip,src_port,dst_port\n" * 3) is None
+    assert _native.pcap_parse(b"\x0a\x0d\x0d\x0a" + b"\x00" * 40) is None  # pcapng
+    assert _native.pcap_parse(pcap_file(pk, linktype=147)) is None
+
+
+def test_read_flows_unique_and_l4(tmp_path):
+    pk, want, _ = packets_and_expected()
+    path = tmp_path / "c.pcap"
+    path.write_bytes(pcap_file(pk))
+    t, p, s = pcap.read_flows(str(path))
+    uniq = []
+    for w in want:
+        if w[:3] not in [u[:3] for u in uniq]:
+            uniq.append(w)
+    assert [r[:3] for r in as_rows(t, p)] == [u[:3] for u in uniq]
+    t, p, _ = pcap.read_flows(str(path), "udp")
+    rows = as_rows(t, p)
+    assert all(r[2] == 0 for r in rows if r[3] != 17)
+    assert (u32(B), u32(A), 53 << 16 | 40000, 17) in rows
+    with pytest.raises(ValueError):
+        pcap.parse_l4("icmp")
+
+
+@pytest.mark.parametrize("fields", ["sdfn", "sd"])
+def test_cli_pcap_csv(fields, tmp_path, monkeypatch, oracle_lib, golden_dir, capsys):
+    monkeypatch.setattr(_native, "default_context", lambda: OracleContext(oracle_lib))
+    pk, _, _ = packets_and_expected()
+    path = tmp_path / "c.pcap"
+    path.write_bytes(pcap_file(pk))
+    out = tmp_path / "out.csv"
+    key_file = os.path.join(golden_dir, "example_input", "hash_key.txt")
+    main(["--key-file", key_file, "--ips-file", str(path), "--pcap", "--htable-size", "128",
+          "--num-queues", "24", "--csv", str(out), "--hash-fields", fields])
+    assert capsys.readouterr().out == "Wrote statistics to %s.\n" % out
+    key = [int(x, 16) for x in open(key_file).read().split(":")]
+    t, _, _ = pcap.read_flows(str(path))
+    mask = _native.parse_fields(fields)
+    want_h = [oracle_lib.hash_bytes(key, o.select_fields_bytes(r["sip"], r["dip"], r["ports"], mask))
+              for r in t]
+    lines = out.read_text().splitlines()
+    body = lines[lines.index("src_ip,dst_ip,src_port,dst_port,hash_result,queue_number") + 1:]
+    assert [int(x.split(",")[4]) for x in body] == want_h
+    assert [int(x.split(",")[5]) for x in body] == [h % 128 % 24 for h in want_h]
+    assert body[0].startswith("10.0.0.1,192.168.1.20,1234,80,")
