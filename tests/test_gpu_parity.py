@@ -245,3 +245,62 @@ def test_narrow_queue_rejects_overflowing_queue_count(native, example_key):
     key = native.prepare_key(example_key)
     with pytest.raises(DeviceError, match="QUEUE_U8"):
         native.hash_device(key, 0, 0, 1024, 257, None, None, None, native.FLAG_QUEUE_U8)
+
+
+def test_graph_capture_and_replay(native, oracle_lib, example_key):
+    """rss_hash_device is stream-ordered and capture-safe: capture zero + hash in a HIP
+    graph, replay it on changing inputs, results match the oracle each time."""
+    dev = torch.device("cuda:0")
+    n, H, Q = 300001, 512, 24
+    key = native.prepare_key(example_key)
+    tuples = torch.empty(3 * n, dtype=torch.int32, device=dev)
+    hashes = torch.empty(n, dtype=torch.int32, device=dev)
+    queues = torch.empty(n, dtype=torch.uint8, device=dev)
+    counts = torch.empty(Q, dtype=torch.int64, device=dev)
+
+    def body():
+        counts.zero_()
+        native.hash_device(key, tuples.data_ptr(), n, H, Q, hashes.data_ptr(), queues.data_ptr(),
+                           counts.data_ptr(), native.FLAG_ACCUMULATE | native.FLAG_QUEUE_U8,
+                           torch.cuda.current_stream(dev).cuda_stream)
+
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        body()
+    torch.cuda.current_stream(dev).wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        body()
+    for seed in (1, 2, 3):
+        host = oracle_lib.generate(seed, 0, n)
+        tuples.copy_(torch.from_numpy(host.view(np.int32).reshape(-1)))
+        g.replay()
+        torch.cuda.synchronize()
+        ho, qo, co = oracle_lib.run(example_key, host, H, Q)
+        np.testing.assert_array_equal(_u32(hashes), ho)
+        np.testing.assert_array_equal(queues.cpu().numpy(), qo.astype(np.uint8))
+        np.testing.assert_array_equal(_u64(counts), co)
+
+
+def test_concurrent_streams_and_keys(native, oracle_lib, example_key):
+    """Two keys on two streams at once (independent launches share nothing)."""
+    dev = torch.device("cuda:0")
+    n = 1 << 20
+    keys = [example_key, list(range(40))]
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    host = oracle_lib.generate(5, 0, n)
+    tuples = torch.from_numpy(host.view(np.int32).reshape(-1)).to(dev)
+    outs = []
+    for k, s in zip(keys, streams):
+        h = torch.empty(n, dtype=torch.int32, device=dev)
+        c = torch.empty(24, dtype=torch.int64, device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        native.hash_device(native.prepare_key(k), tuples.data_ptr(), n, 128, 24, h.data_ptr(),
+                           None, c.data_ptr(), 0, s.cuda_stream)
+        outs.append((h, c))
+    torch.cuda.synchronize()
+    for k, (h, c) in zip(keys, outs):
+        ho, _, co = oracle_lib.run(k, host, 128, 24)
+        np.testing.assert_array_equal(_u32(h), ho)
+        np.testing.assert_array_equal(_u64(c), co)
