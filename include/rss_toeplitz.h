@@ -127,6 +127,18 @@ int rss_hash_device(const rss_key* key, const rss_tuple4* d_tuples, size_t n,
                     void* stream);
 
 /*
+ * Indirection table (RETA; `ethtool -X equal N / weight ...`, which the reference's
+ * docs cite, docs/rss_general_explaination.md:9-11): queue = reta[hash % htable]
+ * instead of (hash % htable) % nqueues.  reta: host array of htable entries, each
+ * < nqueues; htable <= 1024.  The reference's mapping is the table reta[b] = b %
+ * nqueues ("equal").  Everything else as rss_hash_device / rss_hash_host.
+ */
+int rss_hash_device_reta(const rss_key* key, const rss_tuple4* d_tuples, size_t n,
+                         uint32_t htable, const uint32_t* reta, uint32_t nqueues,
+                         uint32_t* d_hash, void* d_queue, uint64_t* d_counts, uint32_t flags,
+                         void* stream);
+
+/*
  * Synthetic input: tuple i (i = first_index .. first_index+n-1) is
  *   r0 = mix64(seed + 2i), r1 = mix64(seed + 2i + 1)       (mod 2^64)
  *   sip = r0 >> 32, dip = (uint32)r0, ports = (uint32)r1
@@ -247,6 +259,10 @@ int rss_hash6_host(rss_ctx* ctx, const rss_key6* key, const rss_tuple6* h_tuples
  */
 int rss_pcap_parse(const uint8_t* data, size_t len, rss_tuple4* tuples, uint8_t* protocols,
                    size_t cap, size_t* n_out, size_t* skipped);
+
+int rss_hash_host_reta(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples, size_t n,
+                       uint32_t htable, const uint32_t* reta, uint32_t nqueues, uint32_t* h_hash,
+                       uint32_t* h_queue, uint64_t* h_counts, uint32_t flags);
 
 /* Number of visible gfx950 devices (0 when there is no GPU). */
 int rss_device_count(int* out);

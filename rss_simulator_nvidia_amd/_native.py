@@ -32,7 +32,7 @@ EXPORTED_SYMBOLS = (
     "rss_abi_version", "rss_csv_parse", "rss_csv_format_bound", "rss_csv_format",
     "rss_key_search_device", "rss_key_search_host", "rss_key_select_fields",
     "rss_key6_prepare", "rss_key6_select_fields", "rss_hash6_device", "rss_hash6_host",
-    "rss_pcap_parse",
+    "rss_pcap_parse", "rss_hash_device_reta", "rss_hash_host_reta",
 )
 FIELD_SRC_IP, FIELD_DST_IP, FIELD_SRC_PORT, FIELD_DST_PORT = 1, 2, 4, 8
 FIELDS_IP, FIELDS_ALL = 3, 15
@@ -95,6 +95,8 @@ def _bind(lib):
         "rss_csv_format_bound": ([sz, u32], sz),
         "rss_key_search_device": ([vp, sz, vp, sz, u32, u32, vp, vp], ctypes.c_int),
         "rss_key_select_fields": ([key_p, u32], ctypes.c_int),
+        "rss_hash_device_reta": ([key_p, vp, sz, u32, vp, u32, vp, vp, vp, u32, vp], ctypes.c_int),
+        "rss_hash_host_reta": ([vp, key_p, vp, sz, u32, vp, u32, vp, vp, vp, u32], ctypes.c_int),
         "rss_pcap_parse": ([vp, sz, vp, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)],
                            ctypes.c_int),
         "rss_key6_prepare": ([ctypes.POINTER(ctypes.c_uint8), sz, ctypes.POINTER(RssKey6)],
@@ -212,10 +214,13 @@ class HostContext:
         except Exception:
             pass
 
-    def hash(self, key, tuples, htable, nqueues, want_hash=True, want_queue=True, want_counts=True):
+    def hash(self, key, tuples, htable, nqueues, want_hash=True, want_queue=True, want_counts=True,
+             reta=None):
         """Hash packed tuples (structured ``TUPLE_DTYPE`` or uint32 (n, 3)) on the GPU.
 
-        Returns ``(hash_u32, queue_u32, counts_u64)``; disabled outputs are None.
+        ``reta`` (optional, ``htable`` queue ids) maps buckets to queues instead of
+        ``bucket % nqueues``.  Returns ``(hash_u32, queue_u32, counts_u64)``; disabled
+        outputs are None.
         """
         arr = np.ascontiguousarray(tuples)
         if arr.dtype != TUPLE_DTYPE:
@@ -225,8 +230,17 @@ class HostContext:
         q = np.empty(n, dtype=np.uint32) if want_queue else None
         c = np.zeros(nqueues, dtype=np.uint64) if want_counts else None
         ptr = lambda a: a.ctypes.data if a is not None else None  # noqa: E731
-        _check(self._lib.rss_hash_host(self._ctx, ctypes.byref(key), ptr(arr), n, htable, nqueues,
-                                       ptr(h), ptr(q), ptr(c), 0), "rss_hash_host")
+        if reta is None:
+            _check(self._lib.rss_hash_host(self._ctx, ctypes.byref(key), ptr(arr), n, htable,
+                                           nqueues, ptr(h), ptr(q), ptr(c), 0), "rss_hash_host")
+        else:
+            table = np.ascontiguousarray(reta, dtype=np.uint32)
+            if len(table) != htable:
+                raise ValueError("indirection table has %d entries, htable is %d"
+                                 % (len(table), htable))
+            _check(self._lib.rss_hash_host_reta(self._ctx, ctypes.byref(key), ptr(arr), n, htable,
+                                                table.ctypes.data, nqueues, ptr(h), ptr(q), ptr(c),
+                                                0), "rss_hash_host_reta")
         return h, q, c
 
 
@@ -277,6 +291,17 @@ def hash_device(key, tuples_ptr, n, htable, nqueues, hash_ptr=None, queue_ptr=No
     """Stream-ordered ``rss_hash_device`` on raw device pointers (ints)."""
     _check(load().rss_hash_device(ctypes.byref(key), tuples_ptr, n, htable, nqueues, hash_ptr,
                                   queue_ptr, counts_ptr, flags, stream), "rss_hash_device")
+
+
+def hash_device_reta(key, tuples_ptr, n, htable, reta, nqueues, hash_ptr=None, queue_ptr=None,
+                     counts_ptr=None, flags=0, stream=None):
+    """Stream-ordered ``rss_hash_device_reta`` (``reta``: host sequence of htable queue ids)."""
+    table = np.ascontiguousarray(reta, dtype=np.uint32)
+    if len(table) != htable:
+        raise ValueError("indirection table has %d entries, htable is %d" % (len(table), htable))
+    _check(load().rss_hash_device_reta(ctypes.byref(key), tuples_ptr, n, htable,
+                                       table.ctypes.data, nqueues, hash_ptr, queue_ptr,
+                                       counts_ptr, flags, stream), "rss_hash_device_reta")
 
 
 def hash6_device(key6, tuples_ptr, n, htable, nqueues, hash_ptr=None, queue_ptr=None,

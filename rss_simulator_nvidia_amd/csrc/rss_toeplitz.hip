@@ -64,7 +64,8 @@ constexpr int kBinCols = 32;            // private histogram columns (one per ba
 static_assert(kLutBytes == 128 * 1024, "LUT layout: 8 tables x 4096 x u32");
 static_assert(kBlock * 4 == (int)kTableEntries, "LUT build maps 4 entries per thread per table");
 
-enum QueueMode { QM_MASK = 0, QM_FAST16 = 1, QM_FAST32 = 2 };
+enum QueueMode { QM_MASK = 0, QM_FAST16 = 1, QM_FAST32 = 2, QM_TABLE = 3 };
+constexpr uint32_t kRetaMax = 1024;  // indirection-table entries carried in the kernarg
 enum HistMode { HIST_PRIVATE = 0, HIST_SHARED = 1, HIST_GLOBAL = 2, HIST_NONE = 3 };
 enum QueueWidth { QW_U32 = 0, QW_U16 = 1, QW_U8 = 2 };
 
@@ -85,6 +86,7 @@ struct LaunchParams {
     uint32_t pad_;
     uint64_t q_m64;     // ceil(2^64 / Q): exact b % Q for any 32-bit b, Q
     const uint32_t* key_windows;  // key search: nkeys x 96 windows in device memory
+    uint16_t reta[kRetaMax];      // QM_TABLE: queue of bucket b (ethtool -X indirection)
 };
 
 // ------------------------------------------------------------- device -------
@@ -174,6 +176,17 @@ __device__ __forceinline__ uint32_t queue_of(uint32_t b, const LaunchParams& p) 
     }
 }
 
+// queue of a bucket: the modulo modes above, or the indirection table copied to LDS
+template <int kQMode>
+__device__ __forceinline__ uint32_t queue_lookup(uint32_t b, const LaunchParams& p,
+                                                 const uint32_t* reta_lds) {
+    if constexpr (kQMode == QM_TABLE) {
+        return reta_lds[b];
+    } else {
+        return queue_of<kQMode>(b, p);
+    }
+}
+
 template <int kHist>
 __device__ __forceinline__ void count_queue(uint32_t* bins, uint32_t q, uint32_t col,
                                             const LaunchParams& p) {
@@ -226,10 +239,11 @@ __device__ __forceinline__ void store_queue4(void* out, uint64_t g, uint32_t q0,
 
 template <bool kHPow2, int kQMode, int kHist, int kQWidth>
 __device__ __forceinline__ void one_tuple(const uint32_t* lut, uint32_t* bins, uint64_t i,
-                                          uint32_t col, uint32_t hi, const LaunchParams& p) {
+                                          uint32_t col, uint32_t hi, const uint32_t* reta_lds,
+                                          const LaunchParams& p) {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(p.tuples) + 3 * i;
     const uint32_t h = toeplitz_hash(lut, src[0], src[1], src[2], hi);
-    const uint32_t q = queue_of<kQMode>(bucket_of<kHPow2>(h, p), p);
+    const uint32_t q = queue_lookup<kQMode>(bucket_of<kHPow2>(h, p), p, reta_lds);
     if (p.hash_out) stream_store(p.hash_out + i, h);
     if (p.queue_out) store_queue1<kQWidth>(p.queue_out, i, q);
     count_queue<kHist>(bins, q, col, p);
@@ -245,6 +259,9 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
     const uint32_t nbins =
         kHist == HIST_PRIVATE ? p.Q * kBinCols : (kHist == HIST_SHARED ? p.Q : 0u);
     for (uint32_t e = tid; e < nbins; e += kBlock) bins[e] = 0;
+    uint32_t* reta_lds = bins + nbins;  // QM_TABLE: H entries after the bins
+    if constexpr (kQMode == QM_TABLE)
+        for (uint32_t e = tid; e < p.H; e += kBlock) reta_lds[e] = p.reta[e];
     __syncthreads();
 
     const uint32_t col = tid & (kBinCols - 1);
@@ -266,10 +283,10 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
             const uint32_t h1 = toeplitz_hash(lut, a.w, b.x, b.y, hi);
             const uint32_t h2 = toeplitz_hash(lut, b.z, b.w, c.x, hi);
             const uint32_t h3 = toeplitz_hash(lut, c.y, c.z, c.w, hi);
-            const uint32_t q0 = queue_of<kQMode>(bucket_of<kHPow2>(h0, p), p);
-            const uint32_t q1 = queue_of<kQMode>(bucket_of<kHPow2>(h1, p), p);
-            const uint32_t q2 = queue_of<kQMode>(bucket_of<kHPow2>(h2, p), p);
-            const uint32_t q3 = queue_of<kQMode>(bucket_of<kHPow2>(h3, p), p);
+            const uint32_t q0 = queue_lookup<kQMode>(bucket_of<kHPow2>(h0, p), p, reta_lds);
+            const uint32_t q1 = queue_lookup<kQMode>(bucket_of<kHPow2>(h1, p), p, reta_lds);
+            const uint32_t q2 = queue_lookup<kQMode>(bucket_of<kHPow2>(h2, p), p, reta_lds);
+            const uint32_t q3 = queue_lookup<kQMode>(bucket_of<kHPow2>(h3, p), p, reta_lds);
             if (p.hash_out) {
                 uint32_t* o = p.hash_out + 4 * g;
                 stream_store(o, h0);
@@ -286,7 +303,7 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
         tail_begin = ngroups << 2;
     }
     for (uint64_t i = tail_begin + gtid; i < p.n; i += gstride)
-        one_tuple<kHPow2, kQMode, kHist, kQWidth>(lut, bins, i, col, hi, p);
+        one_tuple<kHPow2, kQMode, kHist, kQWidth>(lut, bins, i, col, hi, reta_lds, p);
 
     // Epilogue: fold this workgroup's bins into the global uint64 counts.
     if constexpr (kHist == HIST_PRIVATE || kHist == HIST_SHARED) {
@@ -579,6 +596,7 @@ KernelFn pick_queue(int qmode, int hist, int qwidth, bool vec4) {
     switch (qmode) {
         case QM_MASK: return pick_hist<kHPow2, QM_MASK>(hist, qwidth, vec4);
         case QM_FAST16: return pick_hist<kHPow2, QM_FAST16>(hist, qwidth, vec4);
+        case QM_TABLE: return pick_hist<kHPow2, QM_TABLE>(hist, qwidth, vec4);
         default: return pick_hist<kHPow2, QM_FAST32>(hist, qwidth, vec4);
     }
 }
@@ -595,7 +613,7 @@ uint32_t magic32(uint32_t d) { return UINT32_MAX / d + 1; }
 // placement (private LDS columns / shared LDS bins / global atomics) for H and Q.
 // Returns whether H is a power of two.
 bool setup_modes(LaunchParams* p, uint32_t htable, uint32_t nqueues, bool want_counts, int* qmode,
-                 int* hist, uint32_t* bin_bytes) {
+                 int* hist, uint32_t* bin_bytes, uint32_t bin_budget = kBinBytesMax) {
     p->H = htable;
     p->Q = nqueues;
     p->h_mask = htable - 1;
@@ -616,10 +634,10 @@ bool setup_modes(LaunchParams* p, uint32_t htable, uint32_t nqueues, bool want_c
     *bin_bytes = 0;
     if (!want_counts) {
         *hist = HIST_NONE;
-    } else if ((uint64_t)nqueues * kBinCols * 4 <= kBinBytesMax) {
+    } else if ((uint64_t)nqueues * kBinCols * 4 <= bin_budget) {
         *hist = HIST_PRIVATE;
         *bin_bytes = nqueues * kBinCols * 4;
-    } else if ((uint64_t)nqueues * 4 <= kBinBytesMax) {
+    } else if ((uint64_t)nqueues * 4 <= bin_budget) {
         *hist = HIST_SHARED;
         *bin_bytes = nqueues * 4;
     } else {
@@ -691,7 +709,7 @@ int launch_search(const uint32_t* d_windows, size_t nkeys, const rss_tuple4* d_t
 
 int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32_t htable,
                 uint32_t nqueues, uint32_t* d_hash, void* d_queue, uint64_t* d_counts,
-                uint32_t flags, hipStream_t stream) {
+                uint32_t flags, hipStream_t stream, const uint32_t* reta = nullptr) {
     if (!key) return set_error(RSS_EINVAL, "rss_hash_device: key is NULL");
     if (key->len < RSS_KEY_MIN_BYTES)
         return set_error(RSS_EINVAL, "rss_hash_device: key not prepared (len=%u)", key->len);
@@ -699,6 +717,15 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
         return set_error(RSS_EINVAL, "rss_hash_device: htable (%u) and nqueues (%u) must be >= 1",
                          htable, nqueues);
     if (n && !d_tuples) return set_error(RSS_EINVAL, "rss_hash_device: tuples is NULL");
+    if (reta) {
+        if (htable > kRetaMax)
+            return set_error(RSS_EINVAL, "rss_hash_device_reta: htable %u exceeds %u entries",
+                             htable, kRetaMax);
+        for (uint32_t b = 0; b < htable; ++b)
+            if (reta[b] >= nqueues)
+                return set_error(RSS_EINVAL, "rss_hash_device_reta: reta[%u] = %u >= nqueues %u",
+                                 b, reta[b], nqueues);
+    }
     int qwidth = QW_U32;
     if (flags & RSS_FLAG_QUEUE_U8) {
         if (nqueues > 256)
@@ -724,8 +751,13 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
     p.n = n;
     int qmode, hist;
     uint32_t bin_bytes;
+    const uint32_t reta_bytes = reta ? htable * 4 : 0;
     const bool h_pow2 = setup_modes(&p, htable, nqueues, d_counts != nullptr, &qmode, &hist,
-                                    &bin_bytes);
+                                    &bin_bytes, kBinBytesMax - reta_bytes);
+    if (reta) {
+        qmode = QM_TABLE;
+        for (uint32_t b = 0; b < htable; ++b) p.reta[b] = (uint16_t)reta[b];
+    }
     // the 4-tuples-per-lane body needs 16-B aligned tuples / hashes and a queue
     // pointer aligned to the 4 queues it stores at once
     const uintptr_t qalign = qwidth == QW_U8 ? 4 : (qwidth == QW_U16 ? 8 : 16);
@@ -741,7 +773,7 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
     const uint64_t want = (n + per_lane * kBlock - 1) / (per_lane * kBlock);
     const uint64_t cap = (uint64_t)info.cu_count * kBlocksPerCU;
     const unsigned grid = (unsigned)(want < cap ? want : cap);
-    const uint32_t shmem = bin_bytes;  // dynamic part; the 128 KiB LUT is static
+    const uint32_t shmem = bin_bytes + reta_bytes;  // dynamic part; the 128 KiB LUT is static
     hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), shmem, stream, p);
     RSS_HIP_CHECK(hipGetLastError());
     return RSS_OK;
@@ -1003,6 +1035,14 @@ int rss_hash_device(const rss_key* key, const rss_tuple4* d_tuples, size_t n, ui
                        static_cast<hipStream_t>(stream));
 }
 
+int rss_hash_device_reta(const rss_key* key, const rss_tuple4* d_tuples, size_t n,
+                         uint32_t htable, const uint32_t* reta, uint32_t nqueues, uint32_t* d_hash,
+                         void* d_queue, uint64_t* d_counts, uint32_t flags, void* stream) {
+    if (!reta) return set_error(RSS_EINVAL, "rss_hash_device_reta: reta is NULL");
+    return launch_hash(key, d_tuples, n, htable, nqueues, d_hash, d_queue, d_counts, flags,
+                       static_cast<hipStream_t>(stream), reta);
+}
+
 int rss_key_search_device(const uint32_t* d_windows, size_t nkeys, const rss_tuple4* d_tuples,
                           size_t n, uint32_t htable, uint32_t nqueues, uint64_t* d_counts,
                           void* stream) {
@@ -1110,9 +1150,28 @@ static int ctx_reserve(rss_ctx* ctx, size_t chunk, uint32_t nqueues) {
     return RSS_OK;
 }
 
+static int hash_host_impl(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples, size_t n,
+                          uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
+                          uint64_t* h_counts, uint32_t flags, const uint32_t* reta);
+
 int rss_hash_host(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples, size_t n,
                   uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
                   uint64_t* h_counts, uint32_t flags) {
+    return hash_host_impl(ctx, key, h_tuples, n, htable, nqueues, h_hash, h_queue, h_counts, flags,
+                          nullptr);
+}
+
+int rss_hash_host_reta(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples, size_t n,
+                       uint32_t htable, const uint32_t* reta, uint32_t nqueues, uint32_t* h_hash,
+                       uint32_t* h_queue, uint64_t* h_counts, uint32_t flags) {
+    if (!reta) return set_error(RSS_EINVAL, "rss_hash_host_reta: reta is NULL");
+    return hash_host_impl(ctx, key, h_tuples, n, htable, nqueues, h_hash, h_queue, h_counts, flags,
+                          reta);
+}
+
+static int hash_host_impl(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples, size_t n,
+                          uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
+                          uint64_t* h_counts, uint32_t flags, const uint32_t* reta) {
     if (!ctx) return set_error(RSS_EINVAL, "rss_hash_host: ctx is NULL");
     if (n && !h_tuples) return set_error(RSS_EINVAL, "rss_hash_host: tuples is NULL");
     if (htable < 1 || nqueues < 1)
@@ -1151,7 +1210,7 @@ int rss_hash_host(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples, 
                                      hipMemcpyHostToDevice, s));
         rc = launch_hash(key, ctx->d_in[b], len, htable, nqueues, h_hash ? ctx->d_hash[b] : nullptr,
                          h_queue ? ctx->d_queue[b] : nullptr, ctx->d_counts[b],
-                         RSS_FLAG_ACCUMULATE, s);  // u32 queues on the host path
+                         RSS_FLAG_ACCUMULATE, s, reta);  // u32 queues on the host path
         if (rc) return rc;
         if (h_hash)
             RSS_HIP_CHECK(hipMemcpyAsync(ctx->h_hash[b], ctx->d_hash[b], len * 4,

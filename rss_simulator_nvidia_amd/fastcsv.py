@@ -23,7 +23,7 @@ def enabled():
 
 
 def run_csv(hash_key, ips_file, htable, nqueues, output, threads=0, timings=None,
-            fields=_native.FIELDS_ALL):
+            fields=_native.FIELDS_ALL, reta=None):
     """Process ``ips_file`` into ``output``; False if the file needs the pandas path."""
     t = [time.perf_counter()]
     try:
@@ -37,7 +37,7 @@ def run_csv(hash_key, ips_file, htable, nqueues, output, threads=0, timings=None
     tuples, layout = parsed
     t.append(time.perf_counter())
     key = _native.prepare_key(hash_key, fields)
-    h, q, c = _native.default_context().hash(key, tuples, htable, nqueues)
+    h, q, c = _native.default_context().hash(key, tuples, htable, nqueues, reta=reta)
     t.append(time.perf_counter())
     out = _native.csv_format(tuples, h, q, c, layout, threads)
     t.append(time.perf_counter())
@@ -53,7 +53,8 @@ def run_csv(hash_key, ips_file, htable, nqueues, output, threads=0, timings=None
     return True
 
 
-def run_counts(hash_key, ips_file, htable, nqueues, threads=0, fields=_native.FIELDS_ALL):
+def run_counts(hash_key, ips_file, htable, nqueues, threads=0, fields=_native.FIELDS_ALL,
+               reta=None):
     """Per-queue counts of a canonical file via the counts-only kernel (12 B/tuple);
     None if the file needs the pandas path."""
     try:
@@ -65,5 +66,5 @@ def run_counts(hash_key, ips_file, htable, nqueues, threads=0, fields=_native.FI
         return None
     key = _native.prepare_key(hash_key, fields)
     _, _, counts = _native.default_context().hash(key, parsed[0], htable, nqueues,
-                                                  want_hash=False, want_queue=False)
+                                                  want_hash=False, want_queue=False, reta=reta)
     return counts

@@ -10,7 +10,7 @@ pandas path of ``Simulator``.
 import argparse
 from argparse import ArgumentParser
 
-from rss_simulator_nvidia_amd import _native, fastcsv, histogram, pcap
+from rss_simulator_nvidia_amd import _native, fastcsv, histogram, pcap, reta
 from rss_simulator_nvidia_amd.arg_parse_types import PositiveInt
 from rss_simulator_nvidia_amd.arg_parse_types import arg_parse_type_decorator as apt_decorator
 from rss_simulator_nvidia_amd.exceptions import ParseException
@@ -29,13 +29,29 @@ def _l4_arg(text):
     return text
 
 
-def run_pcap(args):
+def indirection_table(args):
+    """The --reta-weights / --reta-file table, validated, or None (reference mapping)."""
+    if args.reta_weights is not None and args.reta_file is not None:
+        raise ValueError("give either --reta-weights or --reta-file")
+    if args.reta_weights is not None:
+        if len(args.reta_weights) != args.num_queues:
+            raise ValueError("--reta-weights needs one weight per queue (%d)" % args.num_queues)
+        table = reta.weights(args.htable_size, args.reta_weights)
+    elif args.reta_file is not None:
+        table = args.reta_file
+    else:
+        return None
+    return reta.validate(table, args.htable_size, args.num_queues)
+
+
+def run_pcap(args, table):
     """--pcap: unique IPv4 flows of a capture -> the same kernel -> CSV or histogram."""
     tuples, _, _ = pcap.read_flows(args.ips_file, args.pcap_l4)
     if len(tuples) == 0:
         raise ParseException("%s holds no IPv4 packets" % args.ips_file)
     key = _native.prepare_key(args.key, args.hash_fields)
-    h, q, c = _native.default_context().hash(key, tuples, args.htable_size, args.num_queues)
+    h, q, c = _native.default_context().hash(key, tuples, args.htable_size, args.num_queues,
+                                             reta=table)
     key_str = Toeplitz(args.key).hash_key_str()
     if args.csv:
         out = _native.csv_format(tuples, h, q, c, _native.RssCsvLayout((0, 1, 2, 3)))
@@ -77,6 +93,12 @@ def build_parser():
     parser.add_argument("--pcap", action="store_true", help=argparse.SUPPRESS)
     parser.add_argument("--pcap-l4", metavar="LIST", default="all",
                         type=apt_decorator(_l4_arg), help=argparse.SUPPRESS)
+    #   --reta-weights W,..   ethtool -X weight table over --htable-size buckets
+    #   --reta-file PATH      explicit indirection table (one queue id per bucket)
+    parser.add_argument("--reta-weights", metavar="W,...", type=apt_decorator(reta.parse_weights),
+                        help=argparse.SUPPRESS)
+    parser.add_argument("--reta-file", metavar="PATH", type=apt_decorator(reta.load),
+                        help=argparse.SUPPRESS)
     return parser
 
 
@@ -88,20 +110,23 @@ def parse_args(argv=None):
 def main(argv=None):
     """Invoke the RSS simulator (``main.py:54-64``)."""
     args = parse_args(argv)
+    table = indirection_table(args)
     if args.pcap:
-        return run_pcap(args)
+        return run_pcap(args, table)
     fast = fastcsv.enabled() and not args.ipv6
     if args.csv and fast and fastcsv.run_csv(args.key, args.ips_file, args.htable_size,
-                                             args.num_queues, args.csv, fields=args.hash_fields):
+                                             args.num_queues, args.csv, fields=args.hash_fields,
+                                             reta=table):
         return  # canonical input: native CSV parse/format around the same GPU kernel
     if not args.csv and fast:
         counts = fastcsv.run_counts(args.key, args.ips_file, args.htable_size, args.num_queues,
-                                    fields=args.hash_fields)
+                                    fields=args.hash_fields, reta=table)
         if counts is not None:  # histogram mode needs the per-queue counts only
             histogram.show(counts, Toeplitz(args.key).hash_key_str(), args.htable_size,
                            args.num_queues, args.histogram_png)
             return
-    rss_sim = Simulator(args.key, args.htable_size, args.num_queues, args.hash_fields, args.ipv6)
+    rss_sim = Simulator(args.key, args.htable_size, args.num_queues, args.hash_fields, args.ipv6,
+                        table)
     rss_sim.load_ips_from_csv(args.ips_file)
     rss_sim.calc_hash()
     rss_sim.calc_queue_number()

@@ -35,14 +35,19 @@ _QUEUE = ColumnNames.QUEUE_NUMBER.value
 class Simulator(object):
     """RSS simulator class (``simulator.py:26``)."""
 
-    def __init__(self, hash_key, hash_table_size, queue_number, hash_fields=None, ipv6=False):
+    def __init__(self, hash_key, hash_table_size, queue_number, hash_fields=None, ipv6=False,
+                 reta=None):
         """Key as ``List[int]``, hash-table size and number of queues (both >= 1).
 
         Additive options: ``hash_fields`` (mask or ``'sdfn'``
-        letters) selects the hashed fields; ``ipv6`` reads IPv6 address columns."""
+        letters) selects the hashed fields; ``ipv6`` reads IPv6 address columns; ``reta``
+        (``hash_table_size`` queue ids) replaces ``bucket % queue_number``."""
         self.__ip_df = None
         self.__toeplitz = Toeplitz(hash_key, hash_fields or "sdfn")
         self.__ipv6 = ipv6
+        self.__reta = reta
+        if reta is not None and ipv6:
+            raise ValueError("indirection tables are supported for IPv4 input only")
         self.__hash_table_size = hash_table_size
         self.__queue_num = queue_number
         self.__queues = None
@@ -90,7 +95,7 @@ class Simulator(object):
                                                       self.__queue_num)
         else:
             h, q, c = self.__toeplitz.compute_queues(pack_frame(df), self.__hash_table_size,
-                                                     self.__queue_num)
+                                                     self.__queue_num, self.__reta)
         df[_HASH] = h.astype(np.int64)
         self.__queues = q
         self.__counts = c

@@ -69,13 +69,12 @@ class Toeplitz(object):
                                                   want_queue=False, want_counts=False)
         return h
 
-    def compute_queues(self, tuples, hash_table_size, queue_number):
-        """Hash + ``hash % htable % queues`` + per-queue counts in one kernel pass.
-
-        Returns ``(hash_u32[n], queue_u32[n], counts_u64[queue_number])``.
+    def compute_queues(self, tuples, hash_table_size, queue_number, reta=None):
+        """Hash + ``hash % htable % queues`` (or ``reta[hash % htable]``) + per-queue counts
+        in one kernel pass.  Returns ``(hash_u32[n], queue_u32[n], counts_u64[queue_number])``.
         """
         return _native.default_context().hash(self.prepared_key, np.asarray(tuples),
-                                              hash_table_size, queue_number)
+                                              hash_table_size, queue_number, reta=reta)
 
     def compute_queues6(self, tuples6, hash_table_size, queue_number):
         """IPv6 counterpart of :meth:`compute_queues` (``rss_tuple6`` rows)."""

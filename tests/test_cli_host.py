@@ -21,7 +21,7 @@ class OracleContext:
         self.calls = 0
 
     def hash(self, key, tuples, htable, nqueues, want_hash=True, want_queue=True,
-             want_counts=True):
+             want_counts=True, reta=None):
         self.calls += 1
         if tuples.dtype.names:
             arr = np.stack([tuples["sip"], tuples["dip"], tuples["ports"]], axis=1)
@@ -29,7 +29,11 @@ class OracleContext:
             arr = np.asarray(tuples, dtype=np.uint32).reshape(-1, 3)
         # the prepared key's own windows (field selection remaps them), closed form
         h = o.hash_words_np(np.ctypeslib.as_array(key.window), arr)
-        q, c = o.queue_and_counts(h, htable, nqueues)
+        if reta is None:
+            q, c = o.queue_and_counts(h, htable, nqueues)
+        else:
+            q = np.asarray(reta, dtype=np.uint32)[h % htable]
+            c = np.bincount(q, minlength=nqueues).astype(np.uint64)
         return h, q, c
 
     def key_search(self, keys, tuples, htable, nqueues):
