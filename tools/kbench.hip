@@ -109,6 +109,48 @@ __global__ __launch_bounds__(1024) void mem_probe(Params p) {
     }
 }
 
+// read-policy / traversal probes: kNT = nontemporal loads, kChunk = each workgroup
+// streams one contiguous slice instead of grid-stride, kWrite = 12R+5W (nt stores)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+template <bool kNT, bool kChunk, bool kWrite>
+__global__ __launch_bounds__(1024) void mem_stream(Params p) {
+    const u32x4* src = reinterpret_cast<const u32x4*>(p.tuples);
+    const uint64_t ng = p.n >> 2;
+    uint64_t g0, g1, step;
+    if (kChunk) {
+        const uint64_t per = (ng + gridDim.x - 1) / gridDim.x;
+        g0 = (uint64_t)blockIdx.x * per + threadIdx.x;
+        g1 = min(ng, (uint64_t)(blockIdx.x + 1) * per);
+        step = 1024;
+    } else {
+        g0 = (uint64_t)blockIdx.x * 1024 + threadIdx.x;
+        g1 = ng;
+        step = (uint64_t)gridDim.x * 1024;
+    }
+    uint32_t acc = 0;
+    for (uint64_t g = g0; g < g1; g += step) {
+        u32x4 a, b, c;
+        if (kNT) {
+            a = __builtin_nontemporal_load(src + 3 * g);
+            b = __builtin_nontemporal_load(src + 3 * g + 1);
+            c = __builtin_nontemporal_load(src + 3 * g + 2);
+        } else {
+            a = src[3 * g]; b = src[3 * g + 1]; c = src[3 * g + 2];
+        }
+        const uint32_t h0 = a.x ^ a.y ^ a.z, h1 = a.w ^ b.x ^ b.y, h2 = b.z ^ b.w ^ c.x,
+                       h3 = c.y ^ c.z ^ c.w;
+        if (kWrite) {
+            uint32_t* o = p.hash_out + 4 * g;
+            __builtin_nontemporal_store(h0, o); __builtin_nontemporal_store(h1, o + 1);
+            __builtin_nontemporal_store(h2, o + 2); __builtin_nontemporal_store(h3, o + 3);
+            __builtin_nontemporal_store((a.x ^ c.w) & 0x17171717u, p.queue_out + g);
+        } else {
+            acc ^= h0 ^ h1 ^ h2 ^ h3;
+        }
+    }
+    if (!kWrite && acc == 0x12345678u) p.counts[0] = acc;
+}
+
 // ------------------------------------------------------------ LUT variants
 // chunk t covers input bits [t*B, t*B + B) of the 96-bit MSB-first string.
 template <int B>
@@ -378,6 +420,27 @@ int main(int argc, char** argv) {
         printf("%-40s %8.3f ms  %7.1f Gt/s  %6.0f GB/s\n", "mem 12R+5W nt (as product)", t, n / t / 1e6, n * 17e-9 / t * 1e3);
         t = time_ms([&] { hipLaunchKernelGGL(mem_ceiling<false>, dim3(g_cus), dim3(1024), 0, 0, p); }, reps);
         printf("%-40s %8.3f ms  %7.1f Gt/s  %6.0f GB/s\n", "mem 12R", t, n / t / 1e6, n * 12e-9 / t * 1e3);
+    }
+    if (strstr("stream", filter)) {
+        p.hash_out = h1;
+        p.queue_out = q1;
+        struct SV { const char* name; void (*k)(Params); double bytes; };
+        const SV sv[8] = {
+            {"stream 12R plain grid-stride", mem_stream<false, false, false>, 12e-9},
+            {"stream 12R nt grid-stride", mem_stream<true, false, false>, 12e-9},
+            {"stream 12R plain chunked", mem_stream<false, true, false>, 12e-9},
+            {"stream 12R nt chunked", mem_stream<true, true, false>, 12e-9},
+            {"stream 12R+5W plain-ld grid-stride", mem_stream<false, false, true>, 17e-9},
+            {"stream 12R+5W nt-ld grid-stride", mem_stream<true, false, true>, 17e-9},
+            {"stream 12R+5W plain-ld chunked", mem_stream<false, true, true>, 17e-9},
+            {"stream 12R+5W nt-ld chunked", mem_stream<true, true, true>, 17e-9}};
+        for (int wpc : {1, 2}) {
+            for (const SV& v : sv) {
+                t = time_ms([&] { hipLaunchKernelGGL(v.k, dim3(g_cus * wpc), dim3(1024), 0, 0, p); }, reps);
+                printf("%-36s x%d %8.3f ms  %7.1f Gt/s  %6.0f GB/s\n", v.name, wpc, t, n / t / 1e6,
+                       n * v.bytes / t * 1e3);
+            }
+        }
     }
     auto run_variant = [&](const char* name, void (*k)(Params), int block, int wgs_per_cu, bool write,
                            bool q8 = false) {
