@@ -54,9 +54,42 @@ def parse_args():
     p.add_argument("--graph", action="store_true",
                    help="replay each step as a captured HIP graph (measured: no gain over "
                         "eager launches at 2**28 tuples per step)")
+    p.add_argument("--distribution", choices=["uniform", "flow"], default="uniform",
+                   help="uniform = splitmix64 over all 96 bits (SURVEY.md 8d); flow = the "
+                        "example_input/ips.csv shape: one IP pair, sequential source ports")
     p.add_argument("--profile-dir", default=os.path.join(ROOT, "profiles"),
                    help="where committed rocprofv3 PMC summaries (traffic) are looked up")
     return p.parse_args()
+
+
+# ---------------------------------------------------------- flow-like input ---
+# SURVEY.md 8(d)'s second distribution, shaped like example_input/ips.csv (3.3.3.1 ->
+# 3.3.3.2, source ports counting up from 5201, destination port 5001): tuple i has source
+# port (5201 + i) mod 2**16 and, so that 2**28 tuples stay distinct, source address
+# 3.3.3.1 + i // 2**16.
+FLOW_SIP, FLOW_DIP, FLOW_SPORT, FLOW_DPORT = 0x03030301, 0x03030302, 5201, 5001
+
+
+def flow_np(first, n):
+    import numpy as np
+    i = np.arange(first, first + n, dtype=np.uint64)
+    t = np.empty((n, 3), dtype=np.uint32)
+    t[:, 0] = ((FLOW_SIP + (i >> np.uint64(16))) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    t[:, 1] = FLOW_DIP
+    t[:, 2] = (((FLOW_SPORT + i) & np.uint64(0xFFFF)) << np.uint64(16)).astype(np.uint32) | FLOW_DPORT
+    return t
+
+
+def flow_device(torch, tuples, first, n, dev):
+    """flow_np(first, n) written into the int32 view ``tuples`` on the device (untimed)."""
+    t = tuples.view(n, 3)
+    chunk = 1 << 26
+    for c0 in range(0, n, chunk):
+        c1 = min(n, c0 + chunk)
+        i = torch.arange(first + c0, first + c1, dtype=torch.int64, device=dev)
+        t[c0:c1, 0] = ((FLOW_SIP + (i >> 16)) & 0xFFFFFFFF).to(torch.int32)
+        t[c0:c1, 1] = FLOW_DIP
+        t[c0:c1, 2] = ((((FLOW_SPORT + i) & 0xFFFF) << 16) | FLOW_DPORT).to(torch.int32)
 
 
 # ------------------------------------------------------------ CPU baseline ----
@@ -66,7 +99,7 @@ def _port_worker(args):
     return [compute_hash_port(key, s, d, sp, dp) for s, d, sp, dp in rows]
 
 
-def cpu_baseline(key, n_sample, procs):
+def cpu_baseline(key, n_sample, procs, distribution="uniform"):
     """Time the pure-Python restatement of the reference's per-tuple path (``oracle``).
 
     Runs BEFORE the GPU is touched (fork-safe).  The sample is the first
@@ -76,7 +109,7 @@ def cpu_baseline(key, n_sample, procs):
     import multiprocessing as mp
 
     from oracle.oracle import generate_np
-    tup = generate_np(SEED, 0, n_sample)
+    tup = generate_np(SEED, 0, n_sample) if distribution == "uniform" else flow_np(0, n_sample)
     dotted = lambda v: "%d.%d.%d.%d" % ((v >> 24) & 255, (v >> 16) & 255, (v >> 8) & 255, v & 255)  # noqa
     rows = [(dotted(int(s)), dotted(int(d)), int(p) >> 16, int(p) & 0xFFFF) for s, d, p in tup]
     procs = max(1, min(procs, n_sample))
@@ -118,7 +151,7 @@ def main():
 
     baseline = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        baseline = cpu_baseline(key_bytes, args.cpu_sample, args.cpu_procs)
+        baseline = cpu_baseline(key_bytes, args.cpu_sample, args.cpu_procs, args.distribution)
 
     import torch
     import torch.distributed as dist
@@ -156,7 +189,10 @@ def main():
     hashes = torch.empty(n, dtype=torch.int32, device=dev)
     queues = torch.empty(n, dtype=torch.int32, device=dev)  # big enough for any width
     counts = torch.zeros(Q, dtype=torch.int64, device=dev)
-    _native.generate_device(SEED, rank * n, n, tuples.data_ptr(), sp)
+    if args.distribution == "uniform":
+        _native.generate_device(SEED, rank * n, n, tuples.data_ptr(), sp)
+    else:
+        flow_device(torch, tuples, rank * n, n, dev)
     torch.cuda.synchronize()
 
     # Two count buffers: step i hashes into counts[i % 2] while the RCCL all-reduce of
@@ -267,12 +303,16 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u32",
-            "data": "synthetic: splitmix64 IPv4 4-tuples generated on device, resident in HBM",
+            "data": ("synthetic: splitmix64 IPv4 4-tuples generated on device, resident in HBM"
+                     if args.distribution == "uniform" else
+                     "synthetic flow-like IPv4 4-tuples (example_input/ips.csv shape: one IP "
+                     "pair, sequential source ports) generated on device, resident in HBM"),
             "config": {
                 "workload": "configs[2]: %d synthetic 4-tuples per GPU (x%d GPUs), key "
                             "example_input/hash_key.txt (40 B), htable=%d, queues=%d; outputs "
                             "hash_result (u32) + queue_number (%s) + per-queue counts (u64)"
                             % (n, world, H, Q, qw),
+                "distribution": args.distribution,
                 "tuples_per_gpu": n,
                 "global_tuples": n * world,
                 "htable": H,

@@ -304,3 +304,27 @@ def test_concurrent_streams_and_keys(native, oracle_lib, example_key):
         ho, _, co = oracle_lib.run(k, host, 128, 24)
         np.testing.assert_array_equal(_u32(h), ho)
         np.testing.assert_array_equal(_u64(c), co)
+
+
+@pytest.mark.parametrize("H,Q", [(128, 24), (512, 64), (65536, 1000)])
+def test_flow_like_distribution_vs_oracle(native, oracle_lib, example_key, H, Q):
+    """SURVEY.md 8(d)'s flow-like input (bench.py --distribution flow: one IP pair,
+    sequential source ports), built on the device exactly as the bench builds it."""
+    import bench
+    n = (1 << 22) + 7
+    dev = torch.device("cuda:0")
+    s = torch.cuda.current_stream(dev).cuda_stream
+    tuples = torch.empty(3 * n, dtype=torch.int32, device=dev)
+    bench.flow_device(torch, tuples, 12345, n, dev)
+    hashes = torch.empty(n, dtype=torch.int32, device=dev)
+    queues = torch.empty(n, dtype=torch.int32, device=dev)
+    counts = torch.empty(Q, dtype=torch.int64, device=dev)
+    native.hash_device(native.prepare_key(example_key), tuples.data_ptr(), n, H, Q,
+                       hashes.data_ptr(), queues.data_ptr(), counts.data_ptr(), 0, s)
+    torch.cuda.synchronize()
+    host = bench.flow_np(12345, n)
+    np.testing.assert_array_equal(_u32(tuples).reshape(n, 3), host)
+    ho, qo, co = oracle_lib.run(example_key, host, H, Q, threads=16)
+    np.testing.assert_array_equal(_u32(hashes), ho)
+    np.testing.assert_array_equal(_u32(queues), qo)
+    np.testing.assert_array_equal(_u64(counts), co)
