@@ -90,11 +90,37 @@ struct LaunchParams {
 };
 
 // ------------------------------------------------------------- device -------
-// LUT: table t (input bits 12t .. 12t+11, MSB first) holds, for every 12-bit
-// value v, the XOR of the key windows whose input bit is set in v -- i.e. the
-// reference's inner loop (toeplitz.py:65-68) pre-summed over 12 bits.  Entry
-// (t, v) lives at LDS byte t*16384 + v*4.  One hash = 8 ds_read_b32 + 7 XOR.
+// LUT: eight tables, each indexed by 12 of the 96 input bits; entry v of table t
+// holds the XOR of the key windows of the input bits set in v -- the reference's
+// inner loop (toeplitz.py:65-68) pre-summed over 12 bits.  Toeplitz is linear in
+// the input bits, so any partition of the 96 bits into tables gives the exact hash.
+// Entry (t, v) lives at LDS byte t*16384 + v*4.  One hash = 8 ds_read_b32 + 7 XOR.
 //
+// Partition (words w0 = src ip, w1 = dst ip, w2 = sport << 16 | dport, bit 0 = LSB):
+//   t0: w0[31:24] | w2[15:12] << 8     t1: w1[31:24] | w2[31:28] << 8
+//   t2: w0[11:0]   t3: w1[11:0]   t4: w0[23:12]   t5: w1[23:12]
+//   t6: w2[11:0] (dport)          t7: w2[27:16] (sport)
+// Every field's least significant bits -- the ones that vary from flow to flow in
+// real traffic (sequential ports, neighbouring hosts) -- are the LOW bits of a table
+// index, i.e. they select the LDS bank ((addr/4) mod 32 for ds_read_b32).  Slicing
+// the MSB-first bit string in order instead puts e.g. sport[7:0] at index bits 4..11:
+// on flow-like input (one IP pair, sequential source ports) every lane of a wave
+// then reads a different entry of ONE bank, a 32-way conflict (measured: 55 % more
+// SQ_LDS_BANK_CONFLICT cycles and 16 % longer counts-only launches than uniform input).
+
+// Input bit (toeplitz.py:65-68 order: 0 = MSB of the source ip) that feeds bit b of
+// table t's index.  Word k bit i is input bit 32k + 31 - i.
+__host__ __device__ constexpr int slice_bit(int t, int b) {
+    return t == 0 ? (b < 8 ? 7 - b : 91 - b)      // w0[24+b] ; w2[4+b]
+         : t == 1 ? (b < 8 ? 39 - b : 75 - b)     // w1[24+b] ; w2[20+b]
+         : t == 2 ? 31 - b                        // w0[b]
+         : t == 3 ? 63 - b                        // w1[b]
+         : t == 4 ? 19 - b                        // w0[12+b]
+         : t == 5 ? 51 - b                        // w1[12+b]
+         : t == 6 ? 95 - b                        // w2[b]
+                  : 79 - b;                       // w2[16+b]
+}
+
 // Build: thread `tid` owns v = hi*1024 + tid (hi = 0..3) of every table: the low
 // ten bits of v are its thread id, so it XORs their windows once per table and
 // derives the four entries from the two top-bit windows.
@@ -102,36 +128,35 @@ __device__ __forceinline__ void build_lut(uint32_t* lut, const uint32_t* __restr
                                           uint32_t tid) {
 #pragma unroll
     for (int t = 0; t < kTables; ++t) {
-        const uint32_t* w = window + kChunkBits * t;  // w[j] <-> bit (11 - j) of v
         uint32_t base = 0;
 #pragma unroll
-        for (int j = 2; j < kChunkBits; ++j) base ^= ((tid >> (11 - j)) & 1u) ? w[j] : 0u;
+        for (int b = 0; b < 10; ++b) base ^= ((tid >> b) & 1u) ? window[slice_bit(t, b)] : 0u;
+        const uint32_t w10 = window[slice_bit(t, 10)], w11 = window[slice_bit(t, 11)];
         uint32_t* dst = lut + t * kTableEntries + tid;
         dst[0 * kBlock] = base;
-        dst[1 * kBlock] = base ^ w[1];
-        dst[2 * kBlock] = base ^ w[0];
-        dst[3 * kBlock] = base ^ w[0] ^ w[1];
+        dst[1 * kBlock] = base ^ w10;
+        dst[2 * kBlock] = base ^ w11;
+        dst[3 * kBlock] = base ^ w10 ^ w11;
     }
 }
 
-// Byte address of chunk t's entry for the input words w0 = src ip, w1 = dst ip,
-// w2 = ports: the 12-bit value moved to bits 2..13 (shift or, for chunks 2 and 5
-// that straddle two words, the funnel shift v_alignbit_b32) and masked.  Tables
-// 4..7 sit above the 16-bit ds_read immediate, so their base 0x10000 is ORed in
-// by the same v_and_or_b32 from `hi` -- an opaque register holding 0x10000 (a
-// literal would cost a separate v_or).  Each address is 2 VALU ops.
+// Byte address of table t's entry for (w0, w1, w2): the index moved to bits 2..13 and
+// masked -- 2 VALU ops for the one-field tables 2..7, 4 for the two-field tables 0..1.
+// Tables 4..7 sit above the 16-bit ds_read immediate, so their base 0x10000 is ORed
+// in by the same v_and_or_b32 from `hi` -- an opaque register holding 0x10000 (a
+// literal would cost a separate v_or).
 template <int kT>
 __device__ __forceinline__ uint32_t chunk_offset(uint32_t w0, uint32_t w1, uint32_t w2,
                                                  uint32_t hi) {
     constexpr uint32_t kMask = (kTableEntries - 1) << 2;  // 0x3FFC
-    if constexpr (kT == 0) return (w0 >> 18) & kMask;     // w0[31:20]
-    if constexpr (kT == 1) return (w0 >> 6) & kMask;      // w0[19:8]
-    if constexpr (kT == 2) return __builtin_amdgcn_alignbit(w0, w1, 26) & kMask;  // w0[7:0] w1[31:28]
-    if constexpr (kT == 3) return (w1 >> 14) & kMask;     // w1[27:16]
-    if constexpr (kT == 4) return ((w1 >> 2) & kMask) | hi;  // w1[15:4]
-    if constexpr (kT == 5) return (__builtin_amdgcn_alignbit(w1, w2, 22) & kMask) | hi;  // w1[3:0] w2[31:24]
-    if constexpr (kT == 6) return ((w2 >> 10) & kMask) | hi;  // w2[23:12]
-    return ((w2 << 2) & kMask) | hi;                          // w2[11:0]
+    if constexpr (kT == 0) return ((w0 >> 22) & 0x3FCu) | ((w2 >> 2) & 0x3C00u);
+    if constexpr (kT == 1) return ((w1 >> 22) & 0x3FCu) | ((w2 >> 18) & 0x3C00u);
+    if constexpr (kT == 2) return (w0 << 2) & kMask;
+    if constexpr (kT == 3) return (w1 << 2) & kMask;
+    if constexpr (kT == 4) return ((w0 >> 10) & kMask) | hi;
+    if constexpr (kT == 5) return ((w1 >> 10) & kMask) | hi;
+    if constexpr (kT == 6) return ((w2 << 2) & kMask) | hi;
+    return ((w2 >> 14) & kMask) | hi;
 }
 
 template <int kT>

@@ -1,5 +1,6 @@
 """Key-search throughput (tool, not product): K random keys x n resident flows, one launch.
-Prints key-tuple evaluations per second.  usage: python tools/keysearch_bench.py [K] [n]"""
+Prints key-tuple evaluations per second.
+usage: python tools/keysearch_bench.py [K] [n] [uniform|flow]"""
 import json
 import os
 import sys
@@ -14,6 +15,7 @@ from rss_simulator_nvidia_amd import _native, keysearch  # noqa: E402
 
 K = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 20
+dist = sys.argv[3] if len(sys.argv) > 3 else "uniform"
 H, Q = 128, 24
 dev = torch.device("cuda:0")
 s = torch.cuda.current_stream(dev).cuda_stream
@@ -22,7 +24,11 @@ win = np.stack([np.ctypeslib.as_array(_native.prepare_key(k).window) for k in ke
 windows = torch.from_numpy(win.astype(np.uint32).view(np.int32)).to(dev)
 tuples = torch.empty(3 * n, dtype=torch.int32, device=dev)
 counts = torch.empty((K, Q), dtype=torch.int64, device=dev)
-_native.generate_device(1, 0, n, tuples.data_ptr(), s)
+if dist == "flow":
+    import bench  # noqa: E402
+    bench.flow_device(torch, tuples, 0, n, dev)
+else:
+    _native.generate_device(1, 0, n, tuples.data_ptr(), s)
 run = lambda: _native.key_search_device(windows.data_ptr(), K, tuples.data_ptr(), n, H, Q,  # noqa
                                         counts.data_ptr(), s)
 run()
@@ -36,6 +42,6 @@ b.record()
 torch.cuda.synchronize()
 ms = a.elapsed_time(b) / reps
 assert int(counts.sum()) == K * n
-print(json.dumps({"keys": K, "flows": n, "htable": H, "queues": Q, "ms": ms,
+print(json.dumps({"distribution": dist, "keys": K, "flows": n, "htable": H, "queues": Q, "ms": ms,
                   "key_tuple_evals_per_s": K * n / (ms / 1e3),
                   "keys_per_s": K / (ms / 1e3)}))
