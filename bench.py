@@ -352,6 +352,7 @@ def main():
         }
         print(json.dumps(line), flush=True)
     if world > 1:
+        barrier()  # ranks leave together (rank 0 ran the secondary timings alone)
         dist.destroy_process_group()
 
 

@@ -407,14 +407,37 @@ __global__ __launch_bounds__(kBlock) void rss_key_search_kernel(const LaunchPara
 }
 
 // ------------------------------------------------------------- IPv6 -------
-// 36-byte input: nine big-endian words, 288 bits.  The 12-bit
-// tables would need 384 KiB, so IPv6 uses 36 byte-slice tables (256 entries each,
-// 36 KiB -- two 1024-thread workgroups per CU): 36 ds_read_b32 + 71 VALU per tuple.
+// 36-byte input: nine big-endian words, 288 bits (w0..w3 src
+// address, w4..w7 dst address, w8 ports).  12-bit tables would need 384 KiB, so the
+// words are cut at word-internal positions into tables that fit the 160 KiB LDS:
+//   w1 w2 w3 w5 w6 w7 w8: [10:0] (2048 entries), [21:11] (2048), [31:22] (1024)
+//   w0 w4 (the network prefixes, which vary least): four byte tables each
+// = 14 x 8 KiB + 7 x 4 KiB + 8 x 1 KiB = 148 KiB, 29 ds_read_b32 per tuple (36 with
+// byte tables only), one 1024-thread workgroup per CU.  Every table index starts at a
+// word-internal bit so the host / port bits that vary between flows select the bank.
 constexpr int kWords6 = RSS_INPUT6_BITS / 32;              // 9
-constexpr int kTables6 = RSS_INPUT6_BITS / 8;              // 36
-constexpr uint32_t kLut6Dwords = kTables6 * 256;           // 9216
-constexpr uint32_t kBinBytesMax6 = 32 * 1024;
-constexpr int kBlocksPerCU6 = 2;
+constexpr uint32_t kLut6Bytes = 14 * 8192 + 7 * 4096 + 8 * 1024;   // 151552
+constexpr uint32_t kLut6Dwords = kLut6Bytes / 4;
+constexpr uint32_t kBinBytesMax6 = kLdsBytes - kLut6Bytes;          // 12 KiB
+constexpr int kBlocksPerCU6 = 1;
+
+__host__ __device__ constexpr bool byte_word6(int k) { return k == 0 || k == 4; }
+// index of word k among the seven 11/11/10-split words (w1 w2 w3 w5 w6 w7 w8 -> 0..6)
+__host__ __device__ constexpr int wide_rank6(int k) { return k < 4 ? k - 1 : k - 2; }
+// slice j of word k: low bit in the word, width, byte offset of its table
+__host__ __device__ constexpr int slice_lo6(int k, int j) {
+    return byte_word6(k) ? 8 * j : (j == 0 ? 0 : (j == 1 ? 11 : 22));
+}
+__host__ __device__ constexpr int slice_width6(int k, int j) {
+    return byte_word6(k) ? 8 : (j == 2 ? 10 : 11);
+}
+__host__ __device__ constexpr uint32_t slice_table6(int k, int j) {
+    return byte_word6(k) ? 14 * 8192 + 7 * 4096 + ((k == 0 ? 0 : 4) + j) * 1024
+         : j < 2         ? (2 * wide_rank6(k) + j) * 8192
+                         : 14 * 8192 + wide_rank6(k) * 4096;
+}
+constexpr int slices6(int k) { return byte_word6(k) ? 4 : 3; }
+static_assert(kLut6Bytes + 32 * 4 * 24 <= kLdsBytes, "IPv6 LUT + private bins for 24 queues fit");
 
 struct LaunchParams6 {
     uint32_t window[RSS_INPUT6_BITS];
@@ -428,42 +451,93 @@ struct LaunchParams6 {
     uint64_t q_m64;
 };
 
-__device__ __forceinline__ void build_lut6(uint32_t* lut, const uint32_t* __restrict__ window,
-                                           uint32_t tid) {
-    for (uint32_t e = tid; e < kLut6Dwords; e += kBlock) {
-        const uint32_t* w = window + 8 * (e >> 8);  // w[j] <-> bit (7 - j) of the byte
-        const uint32_t v = e & 255;
+// entry v of slice (k, j) = XOR of the windows of the set bits of v; word k bit i is
+// input bit 32k + 31 - i (toeplitz.py:65-68 order extended to 36 bytes)
+template <int kK, int kJ>
+__device__ __forceinline__ void build_slice6(uint32_t* lut, const uint32_t* __restrict__ window,
+                                             uint32_t tid) {
+    constexpr int lo = slice_lo6(kK, kJ), width = slice_width6(kK, kJ);
+    constexpr uint32_t entries = 1u << width;
+    uint32_t* dst = lut + slice_table6(kK, kJ) / 4;
+    for (uint32_t v = tid; v < entries; v += kBlock) {
         uint32_t x = 0;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) x ^= ((v >> (7 - j)) & 1u) ? w[j] : 0u;
-        lut[e] = x;
+        for (int b = 0; b < width; ++b) x ^= ((v >> b) & 1u) ? window[32 * kK + 31 - lo - b] : 0u;
+        dst[v] = x;
     }
+}
+
+template <int kK>
+__device__ __forceinline__ void build_word6(uint32_t* lut, const uint32_t* __restrict__ window,
+                                            uint32_t tid) {
+    build_slice6<kK, 0>(lut, window, tid);
+    build_slice6<kK, 1>(lut, window, tid);
+    build_slice6<kK, 2>(lut, window, tid);
+    if constexpr (slices6(kK) == 4) build_slice6<kK, 3>(lut, window, tid);
+}
+
+__device__ __forceinline__ void build_lut6(uint32_t* lut, const uint32_t* __restrict__ window,
+                                           uint32_t tid) {
+    build_word6<0>(lut, window, tid);
+    build_word6<1>(lut, window, tid);
+    build_word6<2>(lut, window, tid);
+    build_word6<3>(lut, window, tid);
+    build_word6<4>(lut, window, tid);
+    build_word6<5>(lut, window, tid);
+    build_word6<6>(lut, window, tid);
+    build_word6<7>(lut, window, tid);
+    build_word6<8>(lut, window, tid);
+}
+
+// One table term: the index moved to bits 2.. and masked (shift + and, or and_or with
+// an opaque 64 KiB / 128 KiB base register -- the ds_read immediate holds 16 bits).
+template <int kK, int kJ>
+__device__ __forceinline__ uint32_t lut6_term(const char* lut, uint32_t w, uint32_t hi1,
+                                              uint32_t hi2) {
+    constexpr int lo = slice_lo6(kK, kJ), width = slice_width6(kK, kJ);
+    constexpr uint32_t mask = ((1u << width) - 1) << 2;
+    constexpr uint32_t table = slice_table6(kK, kJ);
+    constexpr uint32_t imm = table & 0xFFFFu;
+    const uint32_t field = lo >= 2 ? (w >> (lo - 2)) : (w << (2 - lo));
+    uint32_t off;
+    if constexpr ((table >> 16) == 0) {
+        off = field & mask;
+    } else if constexpr ((table >> 16) == 1) {
+        off = (field & mask) | hi1;
+    } else {
+        off = (field & mask) | hi2;
+    }
+    return *reinterpret_cast<const uint32_t*>(lut + imm + off);
+}
+
+template <int kK>
+__device__ __forceinline__ uint32_t word6_terms(const char* lut, uint32_t w, uint32_t hi1,
+                                                uint32_t hi2) {
+    uint32_t x = lut6_term<kK, 0>(lut, w, hi1, hi2) ^ lut6_term<kK, 1>(lut, w, hi1, hi2) ^
+                 lut6_term<kK, 2>(lut, w, hi1, hi2);
+    if constexpr (slices6(kK) == 4) x ^= lut6_term<kK, 3>(lut, w, hi1, hi2);
+    return x;
 }
 
 __device__ __forceinline__ uint32_t toeplitz_hash6(const uint32_t* __restrict__ lut,
-                                                   const uint32_t (&w)[kWords6]) {
+                                                   const uint32_t (&w)[kWords6], uint32_t hi1,
+                                                   uint32_t hi2) {
     const char* base = reinterpret_cast<const char*>(lut);
-    uint32_t h = 0;
-#pragma unroll
-    for (int k = 0; k < kWords6; ++k) {
-        // byte j (MSB first) of word k -> table 4k + j at byte offset (4k + j) * 1024;
-        // folding each word's four terms right away bounds the live registers
-        const uint32_t o0 = (w[k] >> 22) & 0x3FCu, o1 = (w[k] >> 14) & 0x3FCu;
-        const uint32_t o2 = (w[k] >> 6) & 0x3FCu, o3 = (w[k] << 2) & 0x3FCu;
-        h ^= *reinterpret_cast<const uint32_t*>(base + (4 * k + 0) * 1024 + o0) ^
-             *reinterpret_cast<const uint32_t*>(base + (4 * k + 1) * 1024 + o1) ^
-             *reinterpret_cast<const uint32_t*>(base + (4 * k + 2) * 1024 + o2) ^
-             *reinterpret_cast<const uint32_t*>(base + (4 * k + 3) * 1024 + o3);
-    }
-    return h;
+    return (word6_terms<0>(base, w[0], hi1, hi2) ^ word6_terms<1>(base, w[1], hi1, hi2)) ^
+           (word6_terms<2>(base, w[2], hi1, hi2) ^ word6_terms<3>(base, w[3], hi1, hi2)) ^
+           (word6_terms<4>(base, w[4], hi1, hi2) ^ word6_terms<5>(base, w[5], hi1, hi2)) ^
+           (word6_terms<6>(base, w[6], hi1, hi2) ^ word6_terms<7>(base, w[7], hi1, hi2)) ^
+           word6_terms<8>(base, w[8], hi1, hi2);
 }
 
 template <bool kHPow2, int kQMode, int kHist, bool kVec4>
-__global__ __launch_bounds__(kBlock, 8) void rss_toeplitz6_kernel(const LaunchParams6 p6) {
+__global__ __launch_bounds__(kBlock) void rss_toeplitz6_kernel(const LaunchParams6 p6) {
     __shared__ uint32_t lut[kLut6Dwords];
     extern __shared__ uint32_t bins[];
     const uint32_t tid = threadIdx.x;
     build_lut6(lut, p6.window, tid);
+    uint32_t hi1 = 0x10000u, hi2 = 0x20000u;  // opaque table bases (see lut6_term)
+    asm volatile("" : "+v"(hi1), "+v"(hi2));
     // the modulo / histogram helpers read these LaunchParams fields only
     LaunchParams p;
     p.counts = p6.counts;
@@ -502,7 +576,7 @@ __global__ __launch_bounds__(kBlock, 8) void rss_toeplitz6_kernel(const LaunchPa
                 uint32_t w[kWords6];
 #pragma unroll
                 for (int k = 0; k < kWords6; ++k) w[k] = v[kWords6 * t + k];
-                h[t] = toeplitz_hash6(lut, w);
+                h[t] = toeplitz_hash6(lut, w, hi1, hi2);
                 q[t] = queue_of<kQMode>(bucket_of<kHPow2>(h[t], p), p);
             }
             if (p6.hash_out) {
@@ -525,7 +599,7 @@ __global__ __launch_bounds__(kBlock, 8) void rss_toeplitz6_kernel(const LaunchPa
         uint32_t w[kWords6];
 #pragma unroll
         for (int k = 0; k < kWords6; ++k) w[k] = t[k];
-        const uint32_t h = toeplitz_hash6(lut, w);
+        const uint32_t h = toeplitz_hash6(lut, w, hi1, hi2);
         const uint32_t q = queue_of<kQMode>(bucket_of<kHPow2>(h, p), p);
         if (p6.hash_out) stream_store(p6.hash_out + i, h);
         if (p6.queue_out) stream_store(p6.queue_out + i, q);
@@ -851,7 +925,7 @@ int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint
     uint32_t bin_bytes;
     const bool h_pow2 = setup_modes(&tmp, htable, nqueues, d_counts != nullptr, &qmode, &hist,
                                     &bin_bytes);
-    if (bin_bytes > kBinBytesMax6) {  // keep two workgroups per CU: fall back to shared bins
+    if (bin_bytes > kBinBytesMax6) {  // bins share the LDS with the 148 KiB LUT
         hist = (uint64_t)nqueues * 4 <= kBinBytesMax6 ? HIST_SHARED : HIST_GLOBAL;
         bin_bytes = hist == HIST_SHARED ? nqueues * 4 : 0;
     }
