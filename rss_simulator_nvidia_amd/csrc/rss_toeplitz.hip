@@ -83,7 +83,7 @@ struct LaunchParams {
     uint32_t Q;
     uint32_t q_mask;    // Q - 1 (power of two) or ~0u when Q >= H (identity)
     uint32_t q_m32;     // ceil(2^32 / Q): exact b % Q for b, Q < 2^16
-    uint32_t pad_;
+    uint32_t nkeys;     // key search: keys in this launch
     uint64_t q_m64;     // ceil(2^64 / Q): exact b % Q for any 32-bit b, Q
     const uint32_t* key_windows;  // key search: nkeys x 96 windows in device memory
     uint16_t reta[kRetaMax];      // QM_TABLE: queue of bucket b (ethtool -X indirection)
@@ -348,26 +348,141 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
 }
 
 // Key search: per-queue counts of the same tuples under many
-// keys.  blockIdx.y selects the key: each workgroup builds that key's LUT from
-// p.key_windows and histograms its grid-stride share of the tuples into
-// counts[key * Q .. key * Q + Q).  No per-tuple outputs; with the tuples resident
-// in the 256 MiB Infinity Cache the re-reads per key stay on die.
+// keys.  A table index depends only on the tuple, so one table can serve two keys:
+// entry v holds (key A's XOR of windows, key B's) as 8 bytes and ONE ds_read_b64 --
+// 64 banks, 256 B/clk (twice ds_read_b32's rate) -- fetches both keys' terms.  Nine
+// tables of 2048 / 1024 entries (11 / 10 input bits, field LSBs first as in the hash
+// kernel's partition):
+//   t0 w0[10:0]  t1 w0[21:11]  t2 w1[10:0]  t3 w2[15:11] | w2[31:27] << 5  t4 w0[31:22]
+//   t5 w1[21:11] t6 w2[10:0]   t7 w2[26:16] t8 w1[31:22]
+// = 6 x 16 + 3 x 8 KiB = 120 KiB.  Per tuple: 20 VALU of addresses and 9 LDS reads shared
+// by the pair, then XOR / modulo / histogram per key.  blockIdx.y selects the pair; each
+// workgroup histograms its grid-stride share of the tuples into counts rows 2y, 2y+1.
+// With the tuples resident in the 256 MiB Infinity Cache the re-reads stay on die.
+constexpr uint32_t kPairLutBytes = 6 * 16384 + 3 * 8192;   // 122880
+constexpr uint32_t kPairBinBytesMax = kLdsBytes - kPairLutBytes;  // 40 KiB for 2 x Q bins
+
+__host__ __device__ constexpr int pair_width(int t) {
+    return (t == 3 || t == 4 || t == 8) ? 10 : 11;
+}
+__host__ __device__ constexpr uint32_t pair_table(int t) {  // byte offset
+    return t == 0 ? 0u : t == 1 ? 16384u : t == 2 ? 32768u : t == 3 ? 49152u : t == 4 ? 57344u
+         : t == 5 ? 65536u : t == 6 ? 81920u : t == 7 ? 98304u : 114688u;
+}
+// input bit (0 = MSB of the source ip) feeding bit b of table t's index
+__host__ __device__ constexpr int pair_bit(int t, int b) {
+    return t == 0 ? 31 - b : t == 1 ? 20 - b : t == 2 ? 63 - b
+         : t == 3 ? (b < 5 ? 84 - b : 73 - b)
+         : t == 4 ? 9 - b : t == 5 ? 52 - b : t == 6 ? 95 - b : t == 7 ? 79 - b : 41 - b;
+}
+
+template <int kT>
+__device__ __forceinline__ void build_pair_table(uint2* lut, const uint32_t* __restrict__ wa,
+                                                 const uint32_t* __restrict__ wb, uint32_t tid) {
+    uint32_t a = 0, b = 0;
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+        const bool set = (tid >> j) & 1u;
+        a ^= set ? wa[pair_bit(kT, j)] : 0u;
+        b ^= set ? wb[pair_bit(kT, j)] : 0u;
+    }
+    uint2* dst = lut + pair_table(kT) / 8;
+    dst[tid] = make_uint2(a, b);
+    if constexpr (pair_width(kT) == 11)
+        dst[tid + 1024] = make_uint2(a ^ wa[pair_bit(kT, 10)], b ^ wb[pair_bit(kT, 10)]);
+}
+
+// byte address of table t's entry: 2 VALU (4 for the two-field t3); tables 5..8 take
+// their 64 KiB base from the opaque register `hi`
+template <int kT>
+__device__ __forceinline__ uint32_t pair_offset(uint32_t w0, uint32_t w1, uint32_t w2,
+                                                uint32_t hi) {
+    if constexpr (kT == 0) return (w0 << 3) & 0x3FF8u;
+    if constexpr (kT == 1) return (w0 >> 8) & 0x3FF8u;
+    if constexpr (kT == 2) return (w1 << 3) & 0x3FF8u;
+    if constexpr (kT == 3) return ((w2 >> 8) & 0xF8u) | ((w2 >> 19) & 0x1F00u);
+    if constexpr (kT == 4) return (w0 >> 19) & 0x1FF8u;
+    if constexpr (kT == 5) return ((w1 >> 8) & 0x3FF8u) | hi;
+    if constexpr (kT == 6) return ((w2 << 3) & 0x3FF8u) | hi;
+    if constexpr (kT == 7) return ((w2 >> 13) & 0x3FF8u) | hi;
+    return ((w1 >> 19) & 0x1FF8u) | hi;
+}
+
+template <int kT>
+__device__ __forceinline__ uint2 pair_term(const char* lut, uint32_t w0, uint32_t w1, uint32_t w2,
+                                           uint32_t hi) {
+    constexpr uint32_t kImm = pair_table(kT) & 0xFFFFu;
+    return *reinterpret_cast<const uint2*>(lut + kImm + pair_offset<kT>(w0, w1, w2, hi));
+}
+
+// (hash under key A, hash under key B) of one tuple
+__device__ __forceinline__ uint2 toeplitz_hash_pair(const uint2* __restrict__ lut, uint32_t w0,
+                                                    uint32_t w1, uint32_t w2, uint32_t hi) {
+    const char* base = reinterpret_cast<const char*>(lut);
+    const uint2 t0 = pair_term<0>(base, w0, w1, w2, hi), t1 = pair_term<1>(base, w0, w1, w2, hi);
+    const uint2 t2 = pair_term<2>(base, w0, w1, w2, hi), t3 = pair_term<3>(base, w0, w1, w2, hi);
+    const uint2 t4 = pair_term<4>(base, w0, w1, w2, hi), t5 = pair_term<5>(base, w0, w1, w2, hi);
+    const uint2 t6 = pair_term<6>(base, w0, w1, w2, hi), t7 = pair_term<7>(base, w0, w1, w2, hi);
+    const uint2 t8 = pair_term<8>(base, w0, w1, w2, hi);
+    return make_uint2(t0.x ^ t1.x ^ t2.x ^ t3.x ^ t4.x ^ t5.x ^ t6.x ^ t7.x ^ t8.x,
+                      t0.y ^ t1.y ^ t2.y ^ t3.y ^ t4.y ^ t5.y ^ t6.y ^ t7.y ^ t8.y);
+}
+
+template <bool kHPow2, int kQMode, int kHist>
+__device__ __forceinline__ void count_pair(uint32_t* bins_a, uint32_t* bins_b, uint2 h,
+                                           uint32_t col, const LaunchParams& qa,
+                                           const LaunchParams& qb) {
+    count_queue<kHist>(bins_a, queue_of<kQMode>(bucket_of<kHPow2>(h.x, qa), qa), col, qa);
+    count_queue<kHist>(bins_b, queue_of<kQMode>(bucket_of<kHPow2>(h.y, qb), qb), col, qb);
+}
+
+template <int kHist>
+__device__ __forceinline__ void flush_bins(const uint32_t* bins, unsigned long long* counts,
+                                           uint32_t Q, uint32_t tid) {
+    for (uint32_t k = tid; k < Q; k += kBlock) {
+        uint32_t s;
+        if constexpr (kHist == HIST_PRIVATE) {
+            s = 0;
+            for (uint32_t c = 0; c < kBinCols; ++c) s += bins[k * kBinCols + ((c + k) & (kBinCols - 1))];
+        } else {
+            s = bins[k];
+        }
+        if (s) atomicAdd(&counts[k], (unsigned long long)s);
+    }
+}
+
 template <bool kHPow2, int kQMode, int kHist, bool kVec4>
 __global__ __launch_bounds__(kBlock) void rss_key_search_kernel(const LaunchParams p) {
-    __shared__ uint32_t lut[kLutDwords];
+    __shared__ uint2 lut[kPairLutBytes / 8];
     extern __shared__ uint32_t bins[];
     const uint32_t tid = threadIdx.x;
-    const uint32_t key = blockIdx.y;
-    build_lut(lut, p.key_windows + (size_t)RSS_INPUT_BITS * key, tid);
-    const uint32_t nbins =
+    // keys 2y and 2y+1; an odd last key is paired with itself and its copy discarded
+    const uint32_t key_a = 2 * blockIdx.y;
+    const bool has_b = key_a + 1 < p.nkeys;
+    const uint32_t key_b = has_b ? key_a + 1 : key_a;
+    const uint32_t* wa = p.key_windows + (size_t)RSS_INPUT_BITS * key_a;
+    const uint32_t* wb = p.key_windows + (size_t)RSS_INPUT_BITS * key_b;
+    build_pair_table<0>(lut, wa, wb, tid);
+    build_pair_table<1>(lut, wa, wb, tid);
+    build_pair_table<2>(lut, wa, wb, tid);
+    build_pair_table<3>(lut, wa, wb, tid);
+    build_pair_table<4>(lut, wa, wb, tid);
+    build_pair_table<5>(lut, wa, wb, tid);
+    build_pair_table<6>(lut, wa, wb, tid);
+    build_pair_table<7>(lut, wa, wb, tid);
+    build_pair_table<8>(lut, wa, wb, tid);
+    const uint32_t per_key =
         kHist == HIST_PRIVATE ? p.Q * kBinCols : (kHist == HIST_SHARED ? p.Q : 0u);
-    for (uint32_t e = tid; e < nbins; e += kBlock) bins[e] = 0;
+    for (uint32_t e = tid; e < 2 * per_key; e += kBlock) bins[e] = 0;
     __syncthreads();
 
-    LaunchParams q = p;  // per-key counts row
-    q.counts = p.counts + (size_t)key * p.Q;
+    LaunchParams qa = p, qb = p;  // per-key counts rows
+    qa.counts = p.counts + (size_t)key_a * p.Q;
+    qb.counts = p.counts + (size_t)key_b * p.Q;
+    uint32_t* bins_a = bins;
+    uint32_t* bins_b = bins + per_key;
     const uint32_t col = tid & (kBinCols - 1);
-    uint32_t hi = 4 * kTableEntries * 4;
+    uint32_t hi = 65536u;
     asm volatile("" : "+v"(hi));
     const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
     const uint64_t gstride = (uint64_t)gridDim.x * kBlock;
@@ -379,30 +494,21 @@ __global__ __launch_bounds__(kBlock) void rss_key_search_kernel(const LaunchPara
             const uint4 a = src[3 * g + 0];
             const uint4 b = src[3 * g + 1];
             const uint4 c = src[3 * g + 2];
-            count_queue<kHist>(bins, queue_of<kQMode>(bucket_of<kHPow2>(toeplitz_hash(lut, a.x, a.y, a.z, hi), q), q), col, q);
-            count_queue<kHist>(bins, queue_of<kQMode>(bucket_of<kHPow2>(toeplitz_hash(lut, a.w, b.x, b.y, hi), q), q), col, q);
-            count_queue<kHist>(bins, queue_of<kQMode>(bucket_of<kHPow2>(toeplitz_hash(lut, b.z, b.w, c.x, hi), q), q), col, q);
-            count_queue<kHist>(bins, queue_of<kQMode>(bucket_of<kHPow2>(toeplitz_hash(lut, c.y, c.z, c.w, hi), q), q), col, q);
+            count_pair<kHPow2, kQMode, kHist>(bins_a, bins_b, toeplitz_hash_pair(lut, a.x, a.y, a.z, hi), col, qa, qb);
+            count_pair<kHPow2, kQMode, kHist>(bins_a, bins_b, toeplitz_hash_pair(lut, a.w, b.x, b.y, hi), col, qa, qb);
+            count_pair<kHPow2, kQMode, kHist>(bins_a, bins_b, toeplitz_hash_pair(lut, b.z, b.w, c.x, hi), col, qa, qb);
+            count_pair<kHPow2, kQMode, kHist>(bins_a, bins_b, toeplitz_hash_pair(lut, c.y, c.z, c.w, hi), col, qa, qb);
         }
         tail_begin = ngroups << 2;
     }
     for (uint64_t i = tail_begin + gtid; i < p.n; i += gstride) {
         const uint32_t* t = reinterpret_cast<const uint32_t*>(p.tuples) + 3 * i;
-        count_queue<kHist>(bins, queue_of<kQMode>(bucket_of<kHPow2>(toeplitz_hash(lut, t[0], t[1], t[2], hi), q), q), col, q);
+        count_pair<kHPow2, kQMode, kHist>(bins_a, bins_b, toeplitz_hash_pair(lut, t[0], t[1], t[2], hi), col, qa, qb);
     }
     if constexpr (kHist == HIST_PRIVATE || kHist == HIST_SHARED) {
         __syncthreads();
-        for (uint32_t k = tid; k < p.Q; k += kBlock) {
-            uint32_t s;
-            if constexpr (kHist == HIST_PRIVATE) {
-                s = 0;
-                for (uint32_t c = 0; c < kBinCols; ++c)
-                    s += bins[k * kBinCols + ((c + k) & (kBinCols - 1))];
-            } else {
-                s = bins[k];
-            }
-            if (s) atomicAdd(&q.counts[k], (unsigned long long)s);
-        }
+        flush_bins<kHist>(bins_a, qa.counts, p.Q, tid);
+        if (has_b) flush_bins<kHist>(bins_b, qb.counts, p.Q, tid);
     }
 }
 
@@ -785,22 +891,25 @@ int launch_search(const uint32_t* d_windows, size_t nkeys, const rss_tuple4* d_t
     p.tuples = d_tuples;
     p.n = n;
     int qmode, hist;
-    uint32_t bin_bytes;
-    const bool h_pow2 = setup_modes(&p, htable, nqueues, true, &qmode, &hist, &bin_bytes);
+    uint32_t bin_bytes;  // per key; a workgroup holds the bins of its two keys
+    const bool h_pow2 = setup_modes(&p, htable, nqueues, true, &qmode, &hist, &bin_bytes,
+                                    kPairBinBytesMax / 2);
     const bool vec4 = aligned16(d_tuples);
     KernelFn fn = h_pow2 ? pick_search<true>(qmode, hist, vec4) : pick_search<false>(qmode, hist, vec4);
     DeviceInfo info;
     int rc = device_info(&info);
     if (rc) return rc;
-    // ~256K tuples per workgroup amortise its 128 KiB LUT build (~2 us)
+    // ~256K tuples per workgroup amortise its 120 KiB two-key LUT build
     const uint64_t slices = (n + (1u << 18) - 1) >> 18;
     const unsigned gx = (unsigned)(slices < (uint64_t)info.cu_count ? slices : info.cu_count);
-    constexpr size_t kMaxKeysPerLaunch = 65535;  // grid.y limit
+    constexpr size_t kMaxKeysPerLaunch = 2 * 65535;  // grid.y (key pairs) limit
     for (size_t k0 = 0; k0 < nkeys; k0 += kMaxKeysPerLaunch) {
         const size_t kn = nkeys - k0 < kMaxKeysPerLaunch ? nkeys - k0 : kMaxKeysPerLaunch;
         p.key_windows = d_windows + k0 * RSS_INPUT_BITS;
         p.counts = reinterpret_cast<unsigned long long*>(d_counts + k0 * nqueues);
-        hipLaunchKernelGGL(fn, dim3(gx, (unsigned)kn), dim3(kBlock), bin_bytes, stream, p);
+        p.nkeys = (uint32_t)kn;
+        hipLaunchKernelGGL(fn, dim3(gx, (unsigned)((kn + 1) / 2)), dim3(kBlock), 2 * bin_bytes,
+                           stream, p);
         RSS_HIP_CHECK(hipGetLastError());
     }
     return RSS_OK;

@@ -60,3 +60,19 @@ def test_search_end_to_end_improves_on_example_key(native, oracle_lib, example_k
     assert ranked[0]["max_load"] <= base["max_load"][0]
     np.testing.assert_array_equal(ranked[0]["counts"],
                                   oracle_lib.run(ranked[0]["key"], tuples, 128, 24)[2])
+
+
+@pytest.mark.parametrize("nkeys", [1, 3, 7])
+@pytest.mark.parametrize("H,Q", [(128, 24), (512, 2000)])
+def test_key_search_odd_key_counts_flow_input(native, oracle_lib, nkeys, H, Q):
+    """Keys are evaluated in pairs (one 8-byte table entry per pair); an odd last key is
+    paired with itself and its copy discarded.  Flow-like tuples (one IP pair, sequential
+    source ports -- bench.py --distribution flow) exercise broadcast / strided LDS reads."""
+    import bench
+    from rss_simulator_nvidia_amd import keysearch
+    keys = keysearch.random_keys(nkeys, seed=nkeys * 31 + Q)
+    tuples = bench.flow_np(777, 50021)
+    counts = native.HostContext(0).key_search([native.prepare_key(k) for k in keys], tuples, H, Q)
+    assert counts.shape == (nkeys, Q)
+    for k, key in enumerate(keys):
+        np.testing.assert_array_equal(counts[k], oracle_lib.run(key, tuples, H, Q)[2])
