@@ -236,6 +236,24 @@ int rss_csv_format(const rss_tuple4* tuples, const uint32_t* hash, const uint32_
                    const rss_csv_layout* layout, char* out, size_t cap, size_t* out_len,
                    int threads);
 
+/*
+ * ---- CSV on the device ----
+ * The whole `--csv` job for a CANONICAL file image (the rules above): the body goes
+ * to the device once, newlines are indexed, rows parsed, hashed (rss_hash_device or,
+ * with `reta`, rss_hash_device_reta), and the statistics file of write_statistics is
+ * formatted there; the header and per-queue count lines are built on the host.
+ * Replaces pd.read_csv (simulator.py:55), calc_hash / calc_queue_number (:74-98)
+ * and write_statistics (:100-115).  On success *out / *out_len is the file image
+ * in ctx-owned host memory, valid until the next call on ctx; counts (nqueues
+ * uint64) and *n_rows are set.  RSS_CSV_COUNTS_ONLY skips the per-row outputs
+ * and the file (out / out_len may be NULL).  Non-canonical input or a body of 4 GiB
+ * or more -> RSS_ENOTSUP (take the host or pandas path).
+ */
+#define RSS_CSV_COUNTS_ONLY 1u
+int rss_csv_hash_text(rss_ctx* ctx, const rss_key* key, const char* text, size_t len,
+                      uint32_t htable, uint32_t nqueues, const uint32_t* reta, uint32_t flags,
+                      const char** out, size_t* out_len, uint64_t* counts, size_t* n_rows);
+
 /* rss_key_search_device on host buffers (keys: nkeys prepared keys; h_counts:
  * nkeys x nqueues uint64).  Synchronous. */
 int rss_key_search_host(rss_ctx* ctx, const rss_key* keys, size_t nkeys,

@@ -23,6 +23,7 @@ ABI_VERSION = 1
 FLAG_ACCUMULATE = 1
 FLAG_QUEUE_U16 = 2
 FLAG_QUEUE_U8 = 4
+FLAG_CSV_COUNTS_ONLY = 1
 KEY_MIN_BYTES = 4
 
 # Every symbol include/rss_toeplitz.h declares (tests/test_native_abi.py checks them).
@@ -32,7 +33,7 @@ EXPORTED_SYMBOLS = (
     "rss_abi_version", "rss_csv_parse", "rss_csv_format_bound", "rss_csv_format",
     "rss_key_search_device", "rss_key_search_host", "rss_key_select_fields",
     "rss_key6_prepare", "rss_key6_select_fields", "rss_hash6_device", "rss_hash6_host",
-    "rss_pcap_parse", "rss_hash_device_reta", "rss_hash_host_reta",
+    "rss_pcap_parse", "rss_hash_device_reta", "rss_hash_host_reta", "rss_csv_hash_text",
 )
 FIELD_SRC_IP, FIELD_DST_IP, FIELD_SRC_PORT, FIELD_DST_PORT = 1, 2, 4, 8
 FIELDS_IP, FIELDS_ALL = 3, 15
@@ -97,6 +98,9 @@ def _bind(lib):
         "rss_key_select_fields": ([key_p, u32], ctypes.c_int),
         "rss_hash_device_reta": ([key_p, vp, sz, u32, vp, u32, vp, vp, vp, u32, vp], ctypes.c_int),
         "rss_hash_host_reta": ([vp, key_p, vp, sz, u32, vp, u32, vp, vp, vp, u32], ctypes.c_int),
+        "rss_csv_hash_text": ([vp, key_p, vp, sz, u32, u32, vp, u32,
+                               ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t),
+                               vp, ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
         "rss_pcap_parse": ([vp, sz, vp, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)],
                            ctypes.c_int),
         "rss_key6_prepare": ([ctypes.POINTER(ctypes.c_uint8), sz, ctypes.POINTER(RssKey6)],
@@ -258,6 +262,34 @@ class HostContext:
         _check(self._lib.rss_hash6_host(self._ctx, ctypes.byref(key6), ptr(arr), n, htable,
                                         nqueues, ptr(h), ptr(q), ptr(c), 0), "rss_hash6_host")
         return h, q, c
+
+    def csv_hash_text(self, key, data, htable, nqueues, reta=None, counts_only=False):
+        """The whole ``--csv`` job on the device for a canonical file image
+        (``rss_csv_hash_text``): returns ``(file_image, counts, n_rows)`` -- file_image a
+        uint8 view of context-owned memory, valid until the next call on this context
+        (None with ``counts_only``) -- or None when the text is not canonical."""
+        buf = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+        counts = np.zeros(nqueues, dtype=np.uint64)
+        out, out_len, n = ctypes.c_void_p(), ctypes.c_size_t(0), ctypes.c_size_t(0)
+        table = None
+        if reta is not None:
+            table = np.ascontiguousarray(reta, dtype=np.uint32)
+            if len(table) != htable:
+                raise ValueError("indirection table has %d entries, htable is %d"
+                                 % (len(table), htable))
+        rc = self._lib.rss_csv_hash_text(
+            self._ctx, ctypes.byref(key), buf.ctypes.data, len(buf), htable, nqueues,
+            table.ctypes.data if table is not None else None,
+            FLAG_CSV_COUNTS_ONLY if counts_only else 0, ctypes.byref(out), ctypes.byref(out_len),
+            counts.ctypes.data, ctypes.byref(n))
+        if rc == ENOTSUP:
+            return None
+        _check(rc, "rss_csv_hash_text")
+        image = None
+        if not counts_only:
+            image = np.ctypeslib.as_array(ctypes.cast(out, ctypes.POINTER(ctypes.c_uint8)),
+                                          shape=(out_len.value,))
+        return image, counts, n.value
 
     def key_search(self, keys, tuples, htable, nqueues):
         """Per-queue counts (uint64[len(keys), nqueues]) of ``tuples`` under each prepared key."""

@@ -18,6 +18,7 @@
 #include <thread>
 #include <vector>
 
+#include "rss_internal.h"
 #include "rss_toeplitz.h"
 
 namespace {
@@ -189,10 +190,47 @@ constexpr size_t kMaxRowBytes = 15 + 1 + 15 + 1 + 5 + 1 + 5 + 1 + 10 + 1 + 10 + 
 
 }  // namespace
 
+bool rss_csv_header(const char* data, size_t len, rss_csv_layout* layout, size_t* body_offset) {
+    const char* end = data + len;
+    const char* nl = static_cast<const char*>(memchr(data, '\n', len));
+    const char* hend = trim_cr(data, nl ? nl : end);
+    if (!parse_header(data, hend, layout->field_column)) return false;
+    const char* body = nl ? nl + 1 : end;
+    if (body >= end) return false;  // no data rows: the pandas path raises
+    *body_offset = (size_t)(body - data);
+    return true;
+}
+
+size_t rss_csv_prefix_bound(uint32_t nqueues) { return 64 + (size_t)nqueues * 32 + 96; }
+
+size_t rss_csv_format_prefix(const uint64_t* counts, uint32_t nqueues,
+                             const rss_csv_layout* layout, char* out) {
+    char* p = out;
+    // per-queue counts of the non-empty queues, ascending (value_counts().sort_index())
+    memcpy(p, "queue_number,counts\n", 20);
+    p += 20;
+    for (uint32_t q = 0; q < nqueues; ++q)
+        if (counts[q]) {
+            p = put_uint(p, q);
+            *p++ = ',';
+            p = put_uint(p, counts[q]);
+            *p++ = '\n';
+        }
+    for (int f = 0; f < 4; ++f) {
+        const char* name = kColumnNames[layout->field_column[f]];
+        memcpy(p, name, strlen(name));
+        p += strlen(name);
+        *p++ = ',';
+    }
+    memcpy(p, "hash_result,queue_number\n", 25);
+    p += 25;
+    return (size_t)(p - out);
+}
+
 extern "C" {
 
 size_t rss_csv_format_bound(size_t n, uint32_t nqueues) {
-    return 64 + (size_t)nqueues * 32 + 96 + n * kMaxRowBytes;
+    return rss_csv_prefix_bound(nqueues) + n * kMaxRowBytes;
 }
 
 int rss_csv_parse(const char* data, size_t len, rss_tuple4* tuples, size_t cap, size_t* n_rows,
@@ -200,11 +238,9 @@ int rss_csv_parse(const char* data, size_t len, rss_tuple4* tuples, size_t cap, 
     if (!data || !n_rows || !layout) return RSS_EINVAL;
     *n_rows = 0;
     const char* end = data + len;
-    const char* nl = static_cast<const char*>(memchr(data, '\n', len));
-    const char* hend = trim_cr(data, nl ? nl : end);
-    if (!parse_header(data, hend, layout->field_column)) return RSS_ENOTSUP;
-    const char* body = nl ? nl + 1 : end;
-    if (body >= end) return RSS_ENOTSUP;  // no data rows: the pandas path raises
+    size_t body_offset;
+    if (!rss_csv_header(data, len, layout, &body_offset)) return RSS_ENOTSUP;
+    const char* body = data + body_offset;
     // (no separate ASCII check: rows accept only digits . , \r \n, the header only
     // the four column names, so any non-ASCII byte already fails the scan)
 
@@ -257,25 +293,7 @@ int rss_csv_format(const rss_tuple4* tuples, const uint32_t* hash, const uint32_
     if (cap < rss_csv_format_bound(n, nqueues)) return RSS_EINVAL;
     for (int f = 0; f < 4; ++f)
         if (layout->field_column[f] > 3) return RSS_EINVAL;
-    char* p = out;
-    // per-queue counts of the non-empty queues, ascending (value_counts().sort_index())
-    memcpy(p, "queue_number,counts\n", 20);
-    p += 20;
-    for (uint32_t q = 0; q < nqueues; ++q)
-        if (counts[q]) {
-            p = put_uint(p, q);
-            *p++ = ',';
-            p = put_uint(p, counts[q]);
-            *p++ = '\n';
-        }
-    for (int f = 0; f < 4; ++f) {
-        const char* name = kColumnNames[layout->field_column[f]];
-        memcpy(p, name, strlen(name));
-        p += strlen(name);
-        *p++ = ',';
-    }
-    memcpy(p, "hash_result,queue_number\n", 25);
-    p += 25;
+    char* p = out + rss_csv_format_prefix(counts, nqueues, layout, out);
 
     // two passes over row ranges: exact byte count per range, then every thread
     // formats straight into its slice of `out` (no staging copy)

@@ -1,0 +1,47 @@
+// rss_internal.h -- declarations shared by the library's translation units (not ABI).
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+#include "rss_toeplitz.h"
+
+#define RSS_HIDDEN __attribute__((visibility("hidden")))
+
+// HIP's own definition (hip_runtime_api.h); repeated so the g++-built sources need
+// no HIP headers
+typedef struct ihipStream_t* hipStream_t;
+
+// Host-pipeline context (rss_ctx_create): device, streams and staging buffers of
+// rss_hash_host, plus the host output buffer of rss_csv_hash_text.
+struct rss_ctx {
+    int device = 0;
+    size_t chunk = 0;  // tuples per staging buffer
+    hipStream_t stream[2] = {nullptr, nullptr};
+    rss_tuple4* d_in[2] = {nullptr, nullptr};
+    uint32_t* d_hash[2] = {nullptr, nullptr};
+    uint32_t* d_queue[2] = {nullptr, nullptr};
+    uint64_t* d_counts[2] = {nullptr, nullptr};
+    uint32_t counts_cap = 0;
+    rss_tuple4* h_in[2] = {nullptr, nullptr};
+    uint32_t* h_hash[2] = {nullptr, nullptr};
+    uint32_t* h_queue[2] = {nullptr, nullptr};
+    std::vector<char> csv_out;  // rss_csv_hash_text's statistics file image
+};
+
+// Record the thread's rss_last_error() message; returns `code`.
+RSS_HIDDEN int rss_set_error(int code, const char* fmt, ...)
+    __attribute__((format(printf, 2, 3)));
+
+// rss_csv.cpp: canonical header of a file image -> column layout and the byte offset
+// of the first data row; false if the header is not canonical or no row follows.
+RSS_HIDDEN bool rss_csv_header(const char* data, size_t len, rss_csv_layout* layout,
+                               size_t* body_offset);
+
+// rss_csv.cpp: the part of write_statistics' output before the data rows (per-queue
+// counts of the non-empty queues, then the table header); returns its length.  `out`
+// needs rss_csv_prefix_bound(nqueues) bytes.
+RSS_HIDDEN size_t rss_csv_prefix_bound(uint32_t nqueues);
+RSS_HIDDEN size_t rss_csv_format_prefix(const uint64_t* counts, uint32_t nqueues,
+                                        const rss_csv_layout* layout, char* out);

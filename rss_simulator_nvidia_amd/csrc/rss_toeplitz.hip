@@ -25,14 +25,14 @@
 #include <string>
 #include <vector>
 
+#include "rss_internal.h"
 #include "rss_toeplitz.h"
 
 namespace {
-
-// ---------------------------------------------------------------- errors ----
 thread_local std::string g_last_error;
+}  // namespace
 
-int set_error(int code, const char* fmt, ...) {
+int rss_set_error(int code, const char* fmt, ...) {
     char buf[512];
     va_list ap;
     va_start(ap, fmt);
@@ -41,6 +41,11 @@ int set_error(int code, const char* fmt, ...) {
     g_last_error = buf;
     return code;
 }
+
+namespace {
+
+// ---------------------------------------------------------------- errors ----
+#define set_error rss_set_error
 
 #define RSS_HIP_CHECK(expr)                                                        \
     do {                                                                           \
@@ -604,7 +609,12 @@ __device__ __forceinline__ uint32_t lut6_term(const char* lut, uint32_t w, uint3
     constexpr uint32_t mask = ((1u << width) - 1) << 2;
     constexpr uint32_t table = slice_table6(kK, kJ);
     constexpr uint32_t imm = table & 0xFFFFu;
-    const uint32_t field = lo >= 2 ? (w >> (lo - 2)) : (w << (2 - lo));
+    uint32_t field;
+    if constexpr (lo >= 2) {
+        field = w >> (lo - 2);
+    } else {
+        field = w << (2 - lo);
+    }
     uint32_t off;
     if constexpr ((table >> 16) == 0) {
         off = field & mask;
@@ -1098,19 +1108,7 @@ void rotation_windows(const uint8_t* key, size_t len, uint32_t* window, int nbit
 }  // namespace
 
 // ------------------------------------------------------------ C ABI ---------
-struct rss_ctx {
-    int device = 0;
-    size_t chunk = 0;  // tuples per staging buffer
-    hipStream_t stream[2] = {nullptr, nullptr};
-    rss_tuple4* d_in[2] = {nullptr, nullptr};
-    uint32_t* d_hash[2] = {nullptr, nullptr};
-    uint32_t* d_queue[2] = {nullptr, nullptr};
-    uint64_t* d_counts[2] = {nullptr, nullptr};
-    uint32_t counts_cap = 0;
-    rss_tuple4* h_in[2] = {nullptr, nullptr};
-    uint32_t* h_hash[2] = {nullptr, nullptr};
-    uint32_t* h_queue[2] = {nullptr, nullptr};
-};
+// (struct rss_ctx: rss_internal.h)
 
 extern "C" {
 

@@ -20,6 +20,9 @@ class OracleContext:
         self.oracle_lib = oracle_lib
         self.calls = 0
 
+    def csv_hash_text(self, *args, **kwargs):
+        return None  # no device text path on CPU: the host parse/format path runs
+
     def hash(self, key, tuples, htable, nqueues, want_hash=True, want_queue=True,
              want_counts=True, reta=None):
         self.calls += 1

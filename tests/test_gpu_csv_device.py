@@ -1,0 +1,157 @@
+"""GPU parity of the device CSV path (``rss_csv_hash_text``): the statistics file it
+formats on the device must be byte-identical to the reference's golden outputs and to
+the host path (rss_csv_parse + oracle hashes + rss_csv_format, itself pinned to pandas
+and the reference by tests/test_fastcsv.py); it must refuse exactly what the host
+scanner refuses."""
+import os
+import random
+
+import numpy as np
+import pytest
+
+from test_fastcsv import NOT_CANONICAL, HEADER, _random_canonical, parse
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def native():
+    from rss_simulator_nvidia_amd import _native
+    if not torch.cuda.is_available():
+        pytest.fail("gpu tests need a gfx950 device")
+    return _native
+
+
+@pytest.fixture(scope="module")
+def ctx(native):
+    return native.HostContext(0)
+
+
+def _bytes(text):
+    return np.frombuffer(text.encode("latin-1"), dtype=np.uint8)
+
+
+def device_image(native, ctx, text, key, H, Q, reta=None):
+    got = ctx.csv_hash_text(native.prepare_key(key), _bytes(text), H, Q, reta=reta)
+    return None if got is None else (got[0].tobytes(), got[1].copy(), got[2])
+
+
+def host_image(native, oracle_lib, text, key, H, Q, reta=None):
+    tuples, layout = parse(text)
+    arr = np.stack([tuples["sip"], tuples["dip"], tuples["ports"]], axis=1)
+    h, q, c = oracle_lib.run(key, arr, H, Q, threads=8)
+    if reta is not None:
+        q = np.asarray(reta, dtype=np.uint32)[h % H]
+        c = np.bincount(q, minlength=Q).astype(np.uint64)
+    return native.csv_format(tuples, h, q, c, layout).tobytes(), c, len(tuples)
+
+
+def test_example_matches_reference_goldens(native, ctx, golden_dir, example_key):
+    text = open(os.path.join(golden_dir, "example_input", "ips.csv"), "rb").read().decode("latin-1")
+    checked = 0
+    for name in sorted(os.listdir(os.path.join(golden_dir, "example"))):
+        if not name.endswith(".csv"):
+            continue
+        h, q = (int(x[1:]) for x in name[4:-4].split("_"))
+        image, counts, n = device_image(native, ctx, text, example_key, h, q)
+        assert image == open(os.path.join(golden_dir, "example", name), "rb").read(), name
+        assert n == 100 and int(counts.sum()) == 100
+        checked += 1
+    assert checked >= 9
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_random_canonical_equals_host_path(native, ctx, oracle_lib, example_key, seed):
+    rng = random.Random(100 + seed)
+    order = list(range(4))
+    rng.shuffle(order)
+    text = _random_canonical(rng, rng.choice([1, 2, 63, 64, 65, 5000, 40000]), order,
+                             crlf=seed % 2 == 1, blank_lines=seed % 3 == 0,
+                             trailing_nl=seed % 4 != 2)
+    H, Q = rng.choice([(128, 24), (100, 7), (512, 64), (1, 1), (65536, 1000)])
+    got = device_image(native, ctx, text, example_key, H, Q)
+    want = host_image(native, oracle_lib, text, example_key, H, Q)
+    assert got[0] == want[0]
+    np.testing.assert_array_equal(got[1], want[1])
+    assert got[2] == want[2]
+
+
+def test_large_file_multi_tile_scans(native, ctx, oracle_lib, example_key):
+    """~2.5M rows: thousands of scan tiles in both the newline and the row-length scans,
+    CRLF line ends and scattered blank lines (the compaction pass)."""
+    rng = random.Random(7)
+    text = _random_canonical(rng, 2_500_000, [3, 1, 0, 2], crlf=True, blank_lines=True,
+                             trailing_nl=False)
+    got = device_image(native, ctx, text, example_key, 128, 24)
+    want = host_image(native, oracle_lib, text, example_key, 128, 24)
+    assert got[2] == want[2] == 2_500_000
+    assert got[0] == want[0]
+
+
+def test_empty_lines_and_line_end_forms(native, ctx, oracle_lib, example_key):
+    rows = ["1.2.3.4,5.6.7.8,1,2", "9.9.9.9,0.0.0.0,65535,0", "255.255.255.255,1.0.0.1,80,443"]
+    for text in [HEADER + "\n".join(rows),
+                 HEADER + "\n\n" + "\n\n".join(rows) + "\n\n",
+                 HEADER.replace("\n", "\r\n") + "\r\n".join(rows) + "\r\n\r\n",
+                 HEADER + "\n".join(rows) + "\r",
+                 HEADER + "\n".join(rows) + "\n\r"]:
+        got = device_image(native, ctx, text, example_key, 128, 24)
+        want = host_image(native, oracle_lib, text, example_key, 128, 24)
+        assert got[0] == want[0], repr(text)
+
+
+@pytest.mark.parametrize("text", NOT_CANONICAL)
+def test_non_canonical_refused(native, ctx, example_key, text):
+    raw = text.encode("utf-8").decode("latin-1")
+    assert ctx.csv_hash_text(native.prepare_key(example_key), _bytes(raw), 128, 24) is None
+
+
+def test_golden_edge_inputs_refused(native, ctx, golden_dir, example_key):
+    for name in ["octet_overflow.csv", "whitespace.csv", "ports_wide.csv", "extra_reordered.csv",
+                 "missing_col.csv", "header_only.csv", "not_csv.csv"]:
+        data = np.fromfile(os.path.join(golden_dir, "edge", name), dtype=np.uint8)
+        assert ctx.csv_hash_text(native.prepare_key(example_key), data, 128, 24) is None, name
+
+
+def test_mutations_accepted_exactly_when_host_accepts(native, ctx, oracle_lib, example_key):
+    rng = random.Random(11)
+    base = _random_canonical(rng, 60, [1, 0, 3, 2], crlf=False, blank_lines=True,
+                             trailing_nl=True)
+    alphabet = "0123456789.,\n\r -+\"a"
+    agree = accepted = 0
+    for _ in range(300):
+        s = list(base)
+        i = rng.randrange(len(HEADER), len(s))
+        op = rng.random()
+        if op < 0.4:
+            s[i] = rng.choice(alphabet)
+        elif op < 0.7:
+            s.insert(i, rng.choice(alphabet))
+        else:
+            del s[i]
+        text = "".join(s)
+        host = parse(text)
+        got = device_image(native, ctx, text, example_key, 128, 24)
+        assert (host is None) == (got is None), repr(text)
+        if got is not None:
+            accepted += 1
+            assert got[0] == host_image(native, oracle_lib, text, example_key, 128, 24)[0]
+        agree += 1
+    assert agree == 300 and accepted > 20
+
+
+def test_counts_only_and_reta(native, ctx, oracle_lib, example_key):
+    from rss_simulator_nvidia_amd import reta as rt
+    rng = random.Random(3)
+    text = _random_canonical(rng, 30000, [0, 1, 2, 3], crlf=False, blank_lines=False,
+                             trailing_nl=True)
+    key = native.prepare_key(example_key)
+    image, counts, n = ctx.csv_hash_text(key, _bytes(text), 512, 16, counts_only=True)
+    want = host_image(native, oracle_lib, text, example_key, 512, 16)
+    assert image is None and n == 30000
+    np.testing.assert_array_equal(counts, want[1])
+    table = rt.weights(512, [1, 3, 0, 2] * 4)
+    got = device_image(native, ctx, text, example_key, 512, 16, reta=table)
+    assert got[0] == host_image(native, oracle_lib, text, example_key, 512, 16, reta=table)[0]

@@ -1,7 +1,9 @@
 """End-to-end (host memory) rates for DESIGN.md §6 (tool, not product).
 
-1. CSV -> CSV through the CLI fast path (native parse, rss_hash_host = pinned chunked
-   H2D -> kernel -> D2H, native format), per stage;
+1. CSV -> CSV through the CLI fast path, per stage: the device text path
+   (rss_csv_hash_text: parse / hash / format on the GPU) and the host text path
+   (RSS_CSV_DEVICE=0: native parse, rss_hash_host = pinned chunked H2D -> kernel -> D2H,
+   native format); both outputs must be identical;
 2. rss_hash_host alone on host-resident packed tuples (the PCIe-inclusive rate);
 3. the pandas CLI path (RSS_CSV_FASTPATH=0) on a smaller file, for comparison.
 Prints one JSON object.
@@ -35,17 +37,26 @@ key = [int(x, 16) for x in EXAMPLE_KEY.split(":")]
 H, Q = 128, 24
 result = {"rows": rows, "htable": H, "queues": Q}
 
-# warm the device context, then the timed CSV -> CSV run (twice; report the second)
+# warm the device context, then the timed CSV -> CSV runs (twice each; report the second)
 _native.default_context()
-for _ in range(2):
-    t = {}
-    t0 = time.perf_counter()
-    assert fastcsv.run_csv(key, big, H, Q, os.path.join(work, "out_big.csv"), timings=t)
-    wall = time.perf_counter() - t0
-result["csv_fastpath"] = {"wall_s": wall, "rows_per_s": rows / wall,
-                          "stages_s": {k: v for k, v in t.items() if k in
-                                       ("read", "parse", "gpu", "format", "write")},
-                          "bytes_in": t["bytes_in"], "bytes_out": t["bytes_out"]}
+for path in ("device", "host"):
+    os.environ["RSS_CSV_DEVICE"] = "1" if path == "device" else "0"
+    for _ in range(2):
+        t = {}
+        t0 = time.perf_counter()
+        assert fastcsv.run_csv(key, big, H, Q, os.path.join(work, "out_big_%s.csv" % path),
+                               timings=t)
+        wall = time.perf_counter() - t0
+    assert t["path"] == path
+    result["csv_fastpath_" + path] = {
+        "wall_s": wall, "rows_per_s": rows / wall,
+        "stages_s": {k: v for k, v in t.items() if k in
+                     ("read", "parse", "gpu", "format", "write", "device")},
+        "bytes_in": t["bytes_in"], "bytes_out": t["bytes_out"]}
+os.environ["RSS_CSV_DEVICE"] = "1"
+result["device_host_outputs_identical"] = \
+    open(os.path.join(work, "out_big_device.csv"), "rb").read() == \
+    open(os.path.join(work, "out_big_host.csv"), "rb").read()
 
 # rss_hash_host alone (PCIe-inclusive): packed tuples in host memory -> host outputs
 tuples = _native.csv_parse(np.fromfile(big, dtype=np.uint8))[0]
