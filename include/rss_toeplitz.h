@@ -254,6 +254,18 @@ int rss_csv_hash_text(rss_ctx* ctx, const rss_key* key, const char* text, size_t
                       uint32_t htable, uint32_t nqueues, const uint32_t* reta, uint32_t flags,
                       const char** out, size_t* out_len, uint64_t* counts, size_t* n_rows);
 
+/*
+ * rss_csv_hash_text from file to file: the input streams through two pinned staging
+ * buffers of ctx (read of chunk k+1 overlaps the upload of chunk k) and the output
+ * rows stream back the same way (download of chunk k+1 overlaps the write of chunk
+ * k), so no file-sized host buffer exists.  out_path may be NULL with
+ * RSS_CSV_COUNTS_ONLY.  An unreadable input or an output that cannot be created is
+ * RSS_ENOTSUP as well: the pandas path then raises the reference's error.
+ */
+int rss_csv_hash_file(rss_ctx* ctx, const rss_key* key, const char* in_path, const char* out_path,
+                      uint32_t htable, uint32_t nqueues, const uint32_t* reta, uint32_t flags,
+                      uint64_t* counts, size_t* n_rows);
+
 /* rss_key_search_device on host buffers (keys: nkeys prepared keys; h_counts:
  * nkeys x nqueues uint64).  Synchronous. */
 int rss_key_search_host(rss_ctx* ctx, const rss_key* keys, size_t nkeys,

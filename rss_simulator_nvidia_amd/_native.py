@@ -34,6 +34,7 @@ EXPORTED_SYMBOLS = (
     "rss_key_search_device", "rss_key_search_host", "rss_key_select_fields",
     "rss_key6_prepare", "rss_key6_select_fields", "rss_hash6_device", "rss_hash6_host",
     "rss_pcap_parse", "rss_hash_device_reta", "rss_hash_host_reta", "rss_csv_hash_text",
+    "rss_csv_hash_file",
 )
 FIELD_SRC_IP, FIELD_DST_IP, FIELD_SRC_PORT, FIELD_DST_PORT = 1, 2, 4, 8
 FIELDS_IP, FIELDS_ALL = 3, 15
@@ -101,6 +102,8 @@ def _bind(lib):
         "rss_csv_hash_text": ([vp, key_p, vp, sz, u32, u32, vp, u32,
                                ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t),
                                vp, ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+        "rss_csv_hash_file": ([vp, key_p, ctypes.c_char_p, ctypes.c_char_p, u32, u32, vp, u32, vp,
+                               ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
         "rss_pcap_parse": ([vp, sz, vp, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)],
                            ctypes.c_int),
         "rss_key6_prepare": ([ctypes.POINTER(ctypes.c_uint8), sz, ctypes.POINTER(RssKey6)],
@@ -290,6 +293,29 @@ class HostContext:
             image = np.ctypeslib.as_array(ctypes.cast(out, ctypes.POINTER(ctypes.c_uint8)),
                                           shape=(out_len.value,))
         return image, counts, n.value
+
+    def csv_hash_file(self, key, in_path, out_path, htable, nqueues, reta=None):
+        """``rss_csv_hash_file``: the ``--csv`` job from file to file on the device (no
+        file-sized host buffers).  ``out_path`` None = counts only.  Returns
+        ``(counts, n_rows)``, or None when the file is not canonical or a path cannot be
+        opened (the pandas path then raises the reference's error)."""
+        counts = np.zeros(nqueues, dtype=np.uint64)
+        n = ctypes.c_size_t(0)
+        table = None
+        if reta is not None:
+            table = np.ascontiguousarray(reta, dtype=np.uint32)
+            if len(table) != htable:
+                raise ValueError("indirection table has %d entries, htable is %d"
+                                 % (len(table), htable))
+        enc = lambda p: os.fsencode(p) if p is not None else None  # noqa: E731
+        rc = self._lib.rss_csv_hash_file(
+            self._ctx, ctypes.byref(key), enc(in_path), enc(out_path), htable, nqueues,
+            table.ctypes.data if table is not None else None,
+            FLAG_CSV_COUNTS_ONLY if out_path is None else 0, counts.ctypes.data, ctypes.byref(n))
+        if rc == ENOTSUP:
+            return None
+        _check(rc, "rss_csv_hash_file")
+        return counts, n.value
 
     def key_search(self, keys, tuples, htable, nqueues):
         """Per-queue counts (uint64[len(keys), nqueues]) of ``tuples`` under each prepared key."""

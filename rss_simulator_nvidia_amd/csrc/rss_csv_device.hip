@@ -18,6 +18,11 @@
 // The header and the per-queue count lines are built on the host (a few hundred bytes).
 #include <hip/hip_runtime.h>
 
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cerrno>
 #include <cstring>
 
 #include "rss_internal.h"
@@ -362,21 +367,200 @@ int exclusive_scan(const uint32_t* in, uint64_t n, uint64_t* out, uint64_t* h_to
     return RSS_OK;
 }
 
+// One CSV job on the device: the body text (uploaded by the caller into text()) ->
+// rows -> hash / queue / counts -> formatted rows.  Buffers live until destruction.
+class CsvJob {
+  public:
+    CsvJob(hipStream_t s, const rss_csv_layout& layout, uint64_t blen) : s_(s), blen_(blen) {
+        memcpy(lay_.col, layout.field_column, 4);
+    }
+    int alloc_text() { return buf_.alloc(&d_text_, blen_); }
+    uint8_t* text() const { return d_text_; }
+
+    // newline index + parse (+ empty-line drop); RSS_ENOTSUP if not canonical
+    int parse() {
+        int rc;
+        const uint64_t nchunks = (blen_ + kChunk - 1) / kChunk;
+        uint32_t* d_cnt;
+        uint64_t* d_cnt_off;
+        if ((rc = buf_.alloc(&d_cnt, nchunks)) || (rc = buf_.alloc(&d_cnt_off, nchunks))) return rc;
+        hipLaunchKernelGGL(count_newlines, dim3(blocks_for(nchunks, kThreads)), dim3(kThreads), 0,
+                           s_, d_text_, blen_, d_cnt);
+        CSV_HIP_CHECK(hipGetLastError());
+        uint64_t nnl;
+        if ((rc = exclusive_scan(d_cnt, nchunks, d_cnt_off, &nnl, buf_, s_))) return rc;
+        uint32_t* d_pos;
+        if ((rc = buf_.alloc(&d_pos, nnl))) return rc;
+        hipLaunchKernelGGL(emit_newlines, dim3(blocks_for(nchunks, kThreads)), dim3(kThreads), 0,
+                           s_, d_text_, blen_, d_cnt_off, d_pos);
+        CSV_HIP_CHECK(hipGetLastError());
+        uint32_t last_nl = 0;
+        if (nnl)
+            CSV_HIP_CHECK(hipMemcpyAsync(&last_nl, d_pos + nnl - 1, 4, hipMemcpyDeviceToHost, s_));
+        CSV_HIP_CHECK(hipStreamSynchronize(s_));
+        const uint64_t tail_start = nnl ? (uint64_t)last_nl + 1 : 0;
+        const uint64_t nlines = nnl + (tail_start < blen_ ? 1 : 0);
+
+        rss_tuple4* d_lines;
+        uint32_t* d_is_row;
+        unsigned long long* d_stat;  // [0] empty lines, [1] non-canonical lines
+        if ((rc = buf_.alloc(&d_lines, nlines)) || (rc = buf_.alloc(&d_is_row, nlines)) ||
+            (rc = buf_.alloc(&d_stat, 2)))
+            return rc;
+        CSV_HIP_CHECK(hipMemsetAsync(d_stat, 0, 2 * sizeof(unsigned long long), s_));
+        if (nlines)
+            hipLaunchKernelGGL(parse_lines, dim3(blocks_for(nlines, kThreads)), dim3(kThreads), 0,
+                               s_, d_text_, blen_, d_pos, nnl, nlines, lay_, d_lines, d_is_row,
+                               d_stat, d_stat + 1);
+        CSV_HIP_CHECK(hipGetLastError());
+        unsigned long long stat[2];
+        CSV_HIP_CHECK(hipMemcpyAsync(stat, d_stat, sizeof stat, hipMemcpyDeviceToHost, s_));
+        CSV_HIP_CHECK(hipStreamSynchronize(s_));
+        if (stat[1])
+            return rss_set_error(RSS_ENOTSUP, "rss_csv: %llu non-canonical rows", stat[1]);
+        n_ = nlines - stat[0];
+        if (n_ == 0) return rss_set_error(RSS_ENOTSUP, "rss_csv: no data rows");
+        d_tuples_ = d_lines;
+        if (stat[0]) {
+            uint64_t* d_slot;
+            uint64_t kept;
+            if ((rc = buf_.alloc(&d_slot, nlines)) || (rc = buf_.alloc(&d_tuples_, n_))) return rc;
+            if ((rc = exclusive_scan(d_is_row, nlines, d_slot, &kept, buf_, s_))) return rc;
+            hipLaunchKernelGGL(compact_rows, dim3(blocks_for(nlines, kThreads)), dim3(kThreads), 0,
+                               s_, d_lines, d_is_row, d_slot, nlines, d_tuples_);
+            CSV_HIP_CHECK(hipGetLastError());
+        }
+        return RSS_OK;
+    }
+
+    int hash(const rss_key* key, uint32_t htable, uint32_t nqueues, const uint32_t* reta,
+             bool want_rows, uint64_t* h_counts) {
+        int rc;
+        uint64_t* d_counts;
+        if ((rc = buf_.alloc(&d_counts, nqueues))) return rc;
+        if (want_rows && ((rc = buf_.alloc(&d_hash_, n_)) || (rc = buf_.alloc(&d_queue_, n_))))
+            return rc;
+        rc = reta ? rss_hash_device_reta(key, d_tuples_, n_, htable, reta, nqueues, d_hash_,
+                                         d_queue_, d_counts, 0, s_)
+                  : rss_hash_device(key, d_tuples_, n_, htable, nqueues, d_hash_, d_queue_,
+                                    d_counts, 0, s_);
+        if (rc) return rc;
+        CSV_HIP_CHECK(hipMemcpyAsync(h_counts, d_counts, sizeof(uint64_t) * nqueues,
+                                     hipMemcpyDeviceToHost, s_));
+        CSV_HIP_CHECK(hipStreamSynchronize(s_));
+        return RSS_OK;
+    }
+
+    // the data rows of the statistics file -> out() [0, rows_bytes())
+    int format() {
+        int rc;
+        uint32_t* d_len;
+        uint64_t* d_off;
+        if ((rc = buf_.alloc(&d_len, n_)) || (rc = buf_.alloc(&d_off, n_))) return rc;
+        hipLaunchKernelGGL(row_lengths, dim3(blocks_for(n_, kThreads)), dim3(kThreads), 0, s_,
+                           d_tuples_, d_hash_, d_queue_, n_, d_len);
+        CSV_HIP_CHECK(hipGetLastError());
+        if ((rc = exclusive_scan(d_len, n_, d_off, &rows_bytes_, buf_, s_))) return rc;
+        if ((rc = buf_.alloc(&d_out_, rows_bytes_))) return rc;
+        hipLaunchKernelGGL(write_rows, dim3(blocks_for(n_, kThreads)), dim3(kThreads), 0, s_,
+                           d_tuples_, d_hash_, d_queue_, n_, lay_, d_off, d_out_);
+        CSV_HIP_CHECK(hipGetLastError());
+        return RSS_OK;
+    }
+
+    uint64_t rows() const { return n_; }
+    uint64_t rows_bytes() const { return rows_bytes_; }
+    const uint8_t* out() const { return d_out_; }
+
+  private:
+    hipStream_t s_;
+    uint64_t blen_;
+    Layout lay_;
+    DeviceBuffers buf_;
+    uint8_t* d_text_ = nullptr;
+    rss_tuple4* d_tuples_ = nullptr;
+    uint32_t* d_hash_ = nullptr;
+    uint32_t* d_queue_ = nullptr;
+    uint8_t* d_out_ = nullptr;
+    uint64_t n_ = 0, rows_bytes_ = 0;
+};
+
+int check_args(const rss_key* key, uint32_t htable, uint32_t nqueues) {
+    if (!key) return rss_set_error(RSS_EINVAL, "rss_csv: key is NULL");
+    if (htable < 1 || nqueues < 1)
+        return rss_set_error(RSS_EINVAL, "rss_csv: htable (%u) and nqueues (%u) must be >= 1",
+                             htable, nqueues);
+    if (key->len < RSS_KEY_MIN_BYTES) return rss_set_error(RSS_EINVAL, "rss_csv: key not prepared");
+    return RSS_OK;
+}
+
+constexpr size_t kStageBytes = 32u << 20;  // pinned staging per buffer (file I/O)
+
+int reserve_stage(rss_ctx* ctx) {
+    if (ctx->stage_bytes) return RSS_OK;
+    for (int b = 0; b < 2; ++b) {
+        CSV_HIP_CHECK(hipHostMalloc(&ctx->stage[b], kStageBytes, hipHostMallocDefault));
+        CSV_HIP_CHECK(hipEventCreateWithFlags(&ctx->stage_done[b], hipEventDisableTiming));
+    }
+    ctx->stage_bytes = kStageBytes;
+    return RSS_OK;
+}
+
+// full pread / write loops (EINTR-safe)
+bool read_all(int fd, char* dst, size_t len, uint64_t off) {
+    while (len) {
+        const ssize_t r = pread(fd, dst, len, (off_t)off);
+        if (r < 0 && errno == EINTR) continue;
+        if (r <= 0) return false;
+        dst += r;
+        len -= (size_t)r;
+        off += (uint64_t)r;
+    }
+    return true;
+}
+
+bool write_all(int fd, const char* src, size_t len) {
+    while (len) {
+        const ssize_t w = write(fd, src, len);
+        if (w < 0 && errno == EINTR) continue;
+        if (w <= 0) return false;
+        src += w;
+        len -= (size_t)w;
+    }
+    return true;
+}
+
+struct Fd {
+    int fd = -1;
+    ~Fd() {
+        if (fd >= 0) close(fd);
+    }
+};
+
 }  // namespace
+
+void rss_csv_release(rss_ctx* ctx) {
+    for (int b = 0; b < 2; ++b) {
+        if (ctx->stage[b]) (void)hipHostFree(ctx->stage[b]);
+        if (ctx->stage_done[b]) (void)hipEventDestroy(ctx->stage_done[b]);
+        ctx->stage[b] = nullptr;
+        ctx->stage_done[b] = nullptr;
+    }
+    ctx->stage_bytes = 0;
+}
 
 extern "C" {
 
 int rss_csv_hash_text(rss_ctx* ctx, const rss_key* key, const char* text, size_t len,
                       uint32_t htable, uint32_t nqueues, const uint32_t* reta, uint32_t flags,
                       const char** out, size_t* out_len, uint64_t* counts, size_t* n_rows) {
-    if (!ctx || !key || !text || !counts || !n_rows)
+    if (!ctx || !text || !counts || !n_rows)
         return rss_set_error(RSS_EINVAL, "rss_csv_hash_text: NULL argument");
     const bool want_file = !(flags & RSS_CSV_COUNTS_ONLY);
     if (want_file && (!out || !out_len))
         return rss_set_error(RSS_EINVAL, "rss_csv_hash_text: out / out_len NULL");
-    if (htable < 1 || nqueues < 1)
-        return rss_set_error(RSS_EINVAL, "rss_csv_hash_text: htable (%u) and nqueues (%u) must be >= 1",
-                             htable, nqueues);
+    int rc = check_args(key, htable, nqueues);
+    if (rc) return rc;
     *n_rows = 0;
     rss_csv_layout layout;
     size_t body_off;
@@ -388,104 +572,123 @@ int rss_csv_hash_text(rss_ctx* ctx, const rss_key* key, const char* text, size_t
                              (unsigned long long)blen);
     CSV_HIP_CHECK(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream[0];
-    DeviceBuffers buf;
-    int rc;
-    // 1. text up, newline index
-    uint8_t* d_text;
-    const uint64_t nchunks = (blen + kChunk - 1) / kChunk;
-    uint32_t* d_cnt;
-    uint64_t* d_cnt_off;
-    if ((rc = buf.alloc(&d_text, blen)) || (rc = buf.alloc(&d_cnt, nchunks)) ||
-        (rc = buf.alloc(&d_cnt_off, nchunks)))
+    CsvJob job(s, layout, blen);
+    if ((rc = job.alloc_text())) return rc;
+    CSV_HIP_CHECK(hipMemcpyAsync(job.text(), text + body_off, blen, hipMemcpyHostToDevice, s));
+    if ((rc = job.parse()) || (rc = job.hash(key, htable, nqueues, reta, want_file, counts)))
         return rc;
-    CSV_HIP_CHECK(hipMemcpyAsync(d_text, text + body_off, blen, hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(count_newlines, dim3(blocks_for(nchunks, kThreads)), dim3(kThreads), 0, s,
-                       d_text, blen, d_cnt);
-    CSV_HIP_CHECK(hipGetLastError());
-    uint64_t nnl;
-    if ((rc = exclusive_scan(d_cnt, nchunks, d_cnt_off, &nnl, buf, s))) return rc;
-    uint32_t* d_pos;
-    if ((rc = buf.alloc(&d_pos, nnl))) return rc;
-    hipLaunchKernelGGL(emit_newlines, dim3(blocks_for(nchunks, kThreads)), dim3(kThreads), 0, s,
-                       d_text, blen, d_cnt_off, d_pos);
-    CSV_HIP_CHECK(hipGetLastError());
-    uint32_t last_nl = 0;
-    if (nnl)
-        CSV_HIP_CHECK(hipMemcpyAsync(&last_nl, d_pos + nnl - 1, 4, hipMemcpyDeviceToHost, s));
-    CSV_HIP_CHECK(hipStreamSynchronize(s));
-    const uint64_t tail_start = nnl ? (uint64_t)last_nl + 1 : 0;
-    const uint64_t nlines = nnl + (tail_start < blen ? 1 : 0);
-
-    // 2. parse every line
-    rss_tuple4* d_lines;
-    uint32_t* d_is_row;
-    unsigned long long* d_stat;  // [0] empty lines, [1] non-canonical lines
-    if ((rc = buf.alloc(&d_lines, nlines)) || (rc = buf.alloc(&d_is_row, nlines)) ||
-        (rc = buf.alloc(&d_stat, 2)))
-        return rc;
-    CSV_HIP_CHECK(hipMemsetAsync(d_stat, 0, 2 * sizeof(unsigned long long), s));
-    Layout lay;
-    memcpy(lay.col, layout.field_column, 4);
-    if (nlines)
-        hipLaunchKernelGGL(parse_lines, dim3(blocks_for(nlines, kThreads)), dim3(kThreads), 0, s,
-                           d_text, blen, d_pos, nnl, nlines, lay, d_lines, d_is_row, d_stat,
-                           d_stat + 1);
-    CSV_HIP_CHECK(hipGetLastError());
-    unsigned long long stat[2];
-    CSV_HIP_CHECK(hipMemcpyAsync(stat, d_stat, sizeof stat, hipMemcpyDeviceToHost, s));
-    CSV_HIP_CHECK(hipStreamSynchronize(s));
-    if (stat[1]) return rss_set_error(RSS_ENOTSUP, "rss_csv_hash_text: %llu non-canonical rows", stat[1]);
-    const uint64_t n = nlines - stat[0];
-    if (n == 0) return rss_set_error(RSS_ENOTSUP, "rss_csv_hash_text: no data rows");
-
-    // 3. drop empty lines (only if there are any)
-    rss_tuple4* d_tuples = d_lines;
-    if (stat[0]) {
-        uint64_t* d_slot;
-        uint64_t kept;
-        if ((rc = buf.alloc(&d_slot, nlines)) || (rc = buf.alloc(&d_tuples, n))) return rc;
-        if ((rc = exclusive_scan(d_is_row, nlines, d_slot, &kept, buf, s))) return rc;
-        hipLaunchKernelGGL(compact_rows, dim3(blocks_for(nlines, kThreads)), dim3(kThreads), 0, s,
-                           d_lines, d_is_row, d_slot, nlines, d_tuples);
-        CSV_HIP_CHECK(hipGetLastError());
-    }
-
-    // 4. hash + queue + counts
-    uint64_t* d_counts;
-    uint32_t *d_hash = nullptr, *d_queue = nullptr;
-    if ((rc = buf.alloc(&d_counts, nqueues))) return rc;
-    if (want_file && ((rc = buf.alloc(&d_hash, n)) || (rc = buf.alloc(&d_queue, n)))) return rc;
-    rc = reta ? rss_hash_device_reta(key, d_tuples, n, htable, reta, nqueues, d_hash, d_queue,
-                                     d_counts, 0, s)
-              : rss_hash_device(key, d_tuples, n, htable, nqueues, d_hash, d_queue, d_counts, 0, s);
-    if (rc) return rc;
-    CSV_HIP_CHECK(hipMemcpyAsync(counts, d_counts, sizeof(uint64_t) * nqueues,
-                                 hipMemcpyDeviceToHost, s));
-    CSV_HIP_CHECK(hipStreamSynchronize(s));
-    *n_rows = n;
+    *n_rows = job.rows();
     if (!want_file) return RSS_OK;
-
-    // 5. format the rows on the device, the prefix on the host, one copy down
-    uint32_t* d_len;
-    uint64_t* d_off;
-    if ((rc = buf.alloc(&d_len, n)) || (rc = buf.alloc(&d_off, n))) return rc;
-    hipLaunchKernelGGL(row_lengths, dim3(blocks_for(n, kThreads)), dim3(kThreads), 0, s, d_tuples,
-                       d_hash, d_queue, n, d_len);
-    CSV_HIP_CHECK(hipGetLastError());
-    uint64_t rows_bytes;
-    if ((rc = exclusive_scan(d_len, n, d_off, &rows_bytes, buf, s))) return rc;
-    uint8_t* d_out;
-    if ((rc = buf.alloc(&d_out, rows_bytes))) return rc;
-    hipLaunchKernelGGL(write_rows, dim3(blocks_for(n, kThreads)), dim3(kThreads), 0, s, d_tuples,
-                       d_hash, d_queue, n, lay, d_off, d_out);
-    CSV_HIP_CHECK(hipGetLastError());
-    ctx->csv_out.resize(rss_csv_prefix_bound(nqueues) + rows_bytes);
+    if ((rc = job.format())) return rc;
+    ctx->csv_out.resize(rss_csv_prefix_bound(nqueues) + job.rows_bytes());
     const size_t prefix = rss_csv_format_prefix(counts, nqueues, &layout, ctx->csv_out.data());
-    CSV_HIP_CHECK(hipMemcpyAsync(ctx->csv_out.data() + prefix, d_out, rows_bytes,
+    CSV_HIP_CHECK(hipMemcpyAsync(ctx->csv_out.data() + prefix, job.out(), job.rows_bytes(),
                                  hipMemcpyDeviceToHost, s));
     CSV_HIP_CHECK(hipStreamSynchronize(s));
     *out = ctx->csv_out.data();
-    *out_len = prefix + rows_bytes;
+    *out_len = prefix + job.rows_bytes();
+    return RSS_OK;
+}
+
+int rss_csv_hash_file(rss_ctx* ctx, const rss_key* key, const char* in_path, const char* out_path,
+                      uint32_t htable, uint32_t nqueues, const uint32_t* reta, uint32_t flags,
+                      uint64_t* counts, size_t* n_rows) {
+    if (!ctx || !in_path || !counts || !n_rows)
+        return rss_set_error(RSS_EINVAL, "rss_csv_hash_file: NULL argument");
+    const bool want_file = !(flags & RSS_CSV_COUNTS_ONLY);
+    if (want_file && !out_path)
+        return rss_set_error(RSS_EINVAL, "rss_csv_hash_file: out_path NULL");
+    int rc = check_args(key, htable, nqueues);
+    if (rc) return rc;
+    *n_rows = 0;
+    CSV_HIP_CHECK(hipSetDevice(ctx->device));
+    if ((rc = reserve_stage(ctx))) return rc;
+    hipStream_t s = ctx->stream[0];
+    Fd in;
+    in.fd = open(in_path, O_RDONLY);
+    struct stat st;
+    if (in.fd < 0 || fstat(in.fd, &st) != 0 || !S_ISREG(st.st_mode))
+        return rss_set_error(RSS_ENOTSUP, "rss_csv_hash_file: cannot read %s", in_path);
+    const uint64_t len = (uint64_t)st.st_size;
+    // the header must sit in the first staging buffer (a canonical one is < 64 B)
+    const size_t first = (size_t)(len < kStageBytes ? len : kStageBytes);
+    if (!read_all(in.fd, ctx->stage[0], first, 0))
+        return rss_set_error(RSS_ENOTSUP, "rss_csv_hash_file: cannot read %s", in_path);
+    rss_csv_layout layout;
+    size_t body_off;
+    if (!rss_csv_header(ctx->stage[0], first, &layout, &body_off))
+        return rss_set_error(RSS_ENOTSUP, "rss_csv_hash_file: header is not canonical");
+    const uint64_t blen = len - body_off;
+    if (blen >= 0xFFFFFFFFull)
+        return rss_set_error(RSS_ENOTSUP, "rss_csv_hash_file: body of %llu B exceeds 4 GiB",
+                             (unsigned long long)blen);
+    CsvJob job(s, layout, blen);
+    if ((rc = job.alloc_text())) return rc;
+    // stream the body up: read chunk k+1 into one pinned buffer while chunk k copies
+    // from the other
+    uint64_t file_pos = 0, dev_pos = 0;
+    for (int k = 0; file_pos < len; ++k) {
+        const int b = k & 1;
+        size_t got;
+        if (k == 0) {
+            got = first;
+        } else {
+            CSV_HIP_CHECK(hipEventSynchronize(ctx->stage_done[b]));  // buffer b is free again
+            got = (size_t)(len - file_pos < kStageBytes ? len - file_pos : kStageBytes);
+            if (!read_all(in.fd, ctx->stage[b], got, file_pos))
+                return rss_set_error(RSS_EIO, "rss_csv_hash_file: read of %s failed", in_path);
+        }
+        const size_t skip = k == 0 ? body_off : 0;
+        const size_t body_bytes = got - skip;
+        if (body_bytes) {
+            CSV_HIP_CHECK(hipMemcpyAsync(job.text() + dev_pos, ctx->stage[b] + skip, body_bytes,
+                                         hipMemcpyHostToDevice, s));
+            dev_pos += body_bytes;
+        }
+        CSV_HIP_CHECK(hipEventRecord(ctx->stage_done[b], s));
+        file_pos += got;
+    }
+    if ((rc = job.parse()) || (rc = job.hash(key, htable, nqueues, reta, want_file, counts)))
+        return rc;
+    *n_rows = job.rows();
+    if (!want_file) return RSS_OK;
+    if ((rc = job.format())) return rc;
+    Fd outf;
+    outf.fd = open(out_path, O_WRONLY | O_CREAT | O_TRUNC, 0666);
+    if (outf.fd < 0)  // the pandas path raises the reference's error for this path
+        return rss_set_error(RSS_ENOTSUP, "rss_csv_hash_file: cannot create %s", out_path);
+    {
+        std::vector<char> prefix(rss_csv_prefix_bound(nqueues));
+        const size_t plen = rss_csv_format_prefix(counts, nqueues, &layout, prefix.data());
+        if (!write_all(outf.fd, prefix.data(), plen))
+            return rss_set_error(RSS_EIO, "rss_csv_hash_file: write to %s failed", out_path);
+    }
+    // stream the rows down: chunk k+1 copies into one pinned buffer while chunk k is
+    // written from the other
+    const uint64_t total = job.rows_bytes();
+    const uint64_t nchunks = (total + kStageBytes - 1) / kStageBytes;
+    auto issue = [&](uint64_t k) -> int {
+        const uint64_t a = k * kStageBytes;
+        const size_t bytes = (size_t)(total - a < kStageBytes ? total - a : kStageBytes);
+        CSV_HIP_CHECK(hipMemcpyAsync(ctx->stage[k & 1], job.out() + a, bytes,
+                                     hipMemcpyDeviceToHost, s));
+        CSV_HIP_CHECK(hipEventRecord(ctx->stage_done[k & 1], s));
+        return RSS_OK;
+    };
+    if (nchunks && (rc = issue(0))) return rc;
+    for (uint64_t k = 0; k < nchunks; ++k) {
+        CSV_HIP_CHECK(hipEventSynchronize(ctx->stage_done[k & 1]));
+        if (k + 1 < nchunks && (rc = issue(k + 1))) return rc;
+        const uint64_t a = k * kStageBytes;
+        const size_t bytes = (size_t)(total - a < kStageBytes ? total - a : kStageBytes);
+        if (!write_all(outf.fd, ctx->stage[k & 1], bytes))
+            return rss_set_error(RSS_EIO, "rss_csv_hash_file: write to %s failed", out_path);
+    }
+    if (close(outf.fd) != 0) {
+        outf.fd = -1;
+        return rss_set_error(RSS_EIO, "rss_csv_hash_file: close of %s failed", out_path);
+    }
+    outf.fd = -1;
     return RSS_OK;
 }
 

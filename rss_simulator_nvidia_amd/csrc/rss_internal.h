@@ -12,6 +12,7 @@
 // HIP's own definition (hip_runtime_api.h); repeated so the g++-built sources need
 // no HIP headers
 typedef struct ihipStream_t* hipStream_t;
+typedef struct ihipEvent_t* hipEvent_t;
 
 // Host-pipeline context (rss_ctx_create): device, streams and staging buffers of
 // rss_hash_host, plus the host output buffer of rss_csv_hash_text.
@@ -28,7 +29,14 @@ struct rss_ctx {
     uint32_t* h_hash[2] = {nullptr, nullptr};
     uint32_t* h_queue[2] = {nullptr, nullptr};
     std::vector<char> csv_out;  // rss_csv_hash_text's statistics file image
+    // rss_csv_hash_file: two pinned staging buffers for the streamed file I/O
+    char* stage[2] = {nullptr, nullptr};
+    hipEvent_t stage_done[2] = {nullptr, nullptr};
+    size_t stage_bytes = 0;
 };
+
+// rss_csv_device.hip: release the rss_csv_hash_file staging of a context
+RSS_HIDDEN void rss_csv_release(rss_ctx* ctx);
 
 // Record the thread's rss_last_error() message; returns `code`.
 RSS_HIDDEN int rss_set_error(int code, const char* fmt, ...)

@@ -1276,6 +1276,7 @@ int rss_generate_tuples(uint64_t seed, uint64_t first_index, size_t n, rss_tuple
 void rss_ctx_destroy(rss_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
+    rss_csv_release(ctx);
     for (int b = 0; b < 2; ++b) {
         if (ctx->stream[b]) (void)hipStreamSynchronize(ctx->stream[b]);
         (void)hipFree(ctx->d_in[b]);

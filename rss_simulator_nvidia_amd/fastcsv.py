@@ -1,7 +1,8 @@
 """CLI fast path for ``--csv`` runs.
 
-canonical CSV file --rss_csv_hash_text (text up, newline index, parse, hash, format
-on the device, file image down)--> statistics file, byte-identical to the reference's
+canonical CSV file --rss_csv_hash_file (text streamed up through pinned staging,
+newline index, parse, hash, format on the device, rows streamed down into the output
+file)--> statistics file, byte-identical to the reference's
 ``write_statistics`` output (``rss_simulator/simulator.py:100-116``).  When the device
 text path declines (body of 4 GiB or more) the host path runs: native parse
 (rss_csv_parse) --> rss_hash_host (pinned, chunked H2D -> kernel -> D2H) --> native
@@ -33,26 +34,23 @@ def run_csv(hash_key, ips_file, htable, nqueues, output, threads=0, timings=None
             fields=_native.FIELDS_ALL, reta=None):
     """Process ``ips_file`` into ``output``; False if the file needs the pandas path."""
     t = [time.perf_counter()]
+    key = _native.prepare_key(hash_key, fields)
+    ctx = _native.default_context()
+    if device_text_enabled():
+        done = ctx.csv_hash_file(key, ips_file, output, htable, nqueues, reta=reta)
+        if done is not None:
+            if timings is not None:
+                timings.update(device_file=time.perf_counter() - t[0], rows=done[1],
+                               bytes_in=os.path.getsize(ips_file),
+                               bytes_out=os.path.getsize(output), path="device")
+            print("Wrote statistics to {csv}.".format(csv=output))
+            return True
+    t = [time.perf_counter()]
     try:
         data = np.fromfile(ips_file, dtype=np.uint8)
     except (OSError, ValueError):
         return False
     t.append(time.perf_counter())
-    key = _native.prepare_key(hash_key, fields)
-    ctx = _native.default_context()
-    done = ctx.csv_hash_text(key, data, htable, nqueues, reta=reta) \
-        if device_text_enabled() else None
-    if done is not None:
-        image, _, n = done
-        t.append(time.perf_counter())
-        image.tofile(output)
-        t.append(time.perf_counter())
-        if timings is not None:
-            for name, a, b in zip(("read", "device", "write"), t, t[1:]):
-                timings[name] = b - a
-            timings.update(rows=n, bytes_in=len(data), bytes_out=len(image), path="device")
-        print("Wrote statistics to {csv}.".format(csv=output))
-        return True
     parsed = _native.csv_parse(data, threads)
     if parsed is None:
         return False
@@ -62,7 +60,10 @@ def run_csv(hash_key, ips_file, htable, nqueues, output, threads=0, timings=None
     t.append(time.perf_counter())
     out = _native.csv_format(tuples, h, q, c, layout, threads)
     t.append(time.perf_counter())
-    out.tofile(output)
+    try:
+        out.tofile(output)
+    except OSError:
+        return False  # the pandas path raises the reference's error for this path
     t.append(time.perf_counter())
     if timings is not None:
         for name, a, b in zip(("read", "parse", "gpu", "format", "write"), t, t[1:]):
@@ -76,16 +77,16 @@ def run_counts(hash_key, ips_file, htable, nqueues, threads=0, fields=_native.FI
                reta=None):
     """Per-queue counts of a canonical file via the counts-only kernel (12 B/tuple);
     None if the file needs the pandas path."""
+    key = _native.prepare_key(hash_key, fields)
+    ctx = _native.default_context()
+    if device_text_enabled():
+        done = ctx.csv_hash_file(key, ips_file, None, htable, nqueues, reta=reta)
+        if done is not None:
+            return done[0]
     try:
         data = np.fromfile(ips_file, dtype=np.uint8)
     except (OSError, ValueError):
         return None
-    key = _native.prepare_key(hash_key, fields)
-    ctx = _native.default_context()
-    if device_text_enabled():
-        done = ctx.csv_hash_text(key, data, htable, nqueues, reta=reta, counts_only=True)
-        if done is not None:
-            return done[1]
     parsed = _native.csv_parse(data, threads)
     if parsed is None:
         return None

@@ -23,6 +23,9 @@ class OracleContext:
     def csv_hash_text(self, *args, **kwargs):
         return None  # no device text path on CPU: the host parse/format path runs
 
+    def csv_hash_file(self, *args, **kwargs):
+        return None
+
     def hash(self, key, tuples, htable, nqueues, want_hash=True, want_queue=True,
              want_counts=True, reta=None):
         self.calls += 1

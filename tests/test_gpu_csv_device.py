@@ -155,3 +155,39 @@ def test_counts_only_and_reta(native, ctx, oracle_lib, example_key):
     table = rt.weights(512, [1, 3, 0, 2] * 4)
     got = device_image(native, ctx, text, example_key, 512, 16, reta=table)
     assert got[0] == host_image(native, oracle_lib, text, example_key, 512, 16, reta=table)[0]
+
+
+def test_file_to_file_streams_through_staging(native, ctx, oracle_lib, example_key, tmp_path):
+    """rss_csv_hash_file: > 2 pinned staging buffers (32 MiB) of input and of output; the
+    file it writes equals the in-memory image and the host path."""
+    rng = random.Random(21)
+    text = _random_canonical(rng, 1_800_000, [0, 2, 1, 3], crlf=False, blank_lines=True,
+                             trailing_nl=True)
+    src, dst = tmp_path / "in.csv", tmp_path / "out.csv"
+    src.write_bytes(text.encode())
+    assert src.stat().st_size > 2 * (32 << 20)
+    key = native.prepare_key(example_key)
+    counts, n = ctx.csv_hash_file(key, str(src), str(dst), 128, 24)
+    want = host_image(native, oracle_lib, text, example_key, 128, 24)
+    assert dst.read_bytes() == want[0]
+    assert n == want[2]
+    np.testing.assert_array_equal(counts, want[1])
+    c2, n2 = ctx.csv_hash_file(key, str(src), None, 128, 24)  # counts only
+    np.testing.assert_array_equal(c2, want[1])
+    assert n2 == n
+
+
+def test_file_api_refusals_leave_no_output(native, ctx, example_key, golden_dir, tmp_path):
+    key = native.prepare_key(example_key)
+    dst = tmp_path / "out.csv"
+    bad = tmp_path / "bad.csv"
+    bad.write_bytes((HEADER + "3.3.3.300,1.1.1.1,1,1\n").encode())
+    assert ctx.csv_hash_file(key, str(bad), str(dst), 128, 24) is None
+    assert not dst.exists()
+    assert ctx.csv_hash_file(key, str(tmp_path / "missing.csv"), str(dst), 128, 24) is None
+    good = os.path.join(golden_dir, "example_input", "ips.csv")
+    assert ctx.csv_hash_file(key, good, str(tmp_path / "no_dir" / "o.csv"), 128, 24) is None
+    assert ctx.csv_hash_file(key, str(tmp_path), str(dst), 128, 24) is None  # a directory
+    counts, n = ctx.csv_hash_file(key, good, str(dst), 128, 24)
+    assert n == 100 and dst.read_bytes() == open(
+        os.path.join(golden_dir, "example", "out_h128_q24.csv"), "rb").read()
