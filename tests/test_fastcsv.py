@@ -161,3 +161,46 @@ def test_accepted_mutations_agree_with_pandas(tmp_path):
         path.write_bytes(text.encode())
         np.testing.assert_array_equal(got[0], pack_frame(pd.read_csv(path)))
     assert accepted > 20
+
+
+class _RoutingCtx:
+    """Stands in for the device context: records which fast-path entry points ran."""
+
+    def __init__(self, accept):
+        self.accept, self.calls = accept, []
+
+    def csv_hash_file(self, key, in_path, out_path, htable, nqueues, reta=None):
+        self.calls.append(("file", out_path))
+        if not self.accept:
+            return None
+        if out_path is not None:
+            open(out_path, "wb").write(b"device\n")
+        return np.arange(nqueues, dtype=np.uint64), 3
+
+    def hash(self, key, tuples, htable, nqueues, **kwargs):
+        self.calls.append(("hash", len(tuples)))
+        n = len(tuples)
+        return (np.zeros(n, np.uint32), np.zeros(n, np.uint32),
+                np.bincount(np.zeros(n, np.int64), minlength=nqueues).astype(np.uint64))
+
+
+def test_fast_path_routing(monkeypatch, tmp_path, golden_dir, example_key):
+    from rss_simulator_nvidia_amd import fastcsv
+    src = os.path.join(golden_dir, "example_input", "ips.csv")
+    out = str(tmp_path / "o.csv")
+    ctx = _RoutingCtx(accept=True)
+    monkeypatch.setattr(_native, "default_context", lambda: ctx)
+    assert fastcsv.run_csv(example_key, src, 128, 24, out)
+    assert ctx.calls == [("file", out)] and open(out, "rb").read() == b"device\n"
+    assert fastcsv.run_counts(example_key, src, 128, 24).tolist() == list(range(24))
+    ctx = _RoutingCtx(accept=False)  # device declines -> host parse + rss_hash_host
+    monkeypatch.setattr(_native, "default_context", lambda: ctx)
+    assert fastcsv.run_csv(example_key, src, 128, 24, out)
+    assert ctx.calls == [("file", out), ("hash", 100)]
+    assert open(out, "rb").read().startswith(b"queue_number,counts\n0,100\n")
+    monkeypatch.setenv("RSS_CSV_DEVICE", "0")  # host text path only
+    ctx = _RoutingCtx(accept=True)
+    monkeypatch.setattr(_native, "default_context", lambda: ctx)
+    assert fastcsv.run_csv(example_key, src, 128, 24, out)
+    assert ctx.calls == [("hash", 100)]
+    assert not fastcsv.run_csv(example_key, str(tmp_path / "missing.csv"), 128, 24, out)
