@@ -15,8 +15,14 @@ from rss_simulator_nvidia_amd.arg_parse_types import PositiveInt
 from rss_simulator_nvidia_amd.arg_parse_types import arg_parse_type_decorator as apt_decorator
 from rss_simulator_nvidia_amd.exceptions import ParseException
 from rss_simulator_nvidia_amd.hash_key import HashKey
-from rss_simulator_nvidia_amd.simulator import Simulator
-from rss_simulator_nvidia_amd.toeplitz import Toeplitz
+
+# simulator.py (pandas, ~0.4 s to import) is imported only when the pandas path runs:
+# canonical files never need it
+
+
+def _key_str(key):
+    """``Toeplitz.hash_key_str()`` (toeplitz.py:37-44) without importing the pandas path."""
+    return ":".join("{:02x}".format(b) for b in key)
 
 
 def _fields_arg(text):
@@ -52,7 +58,7 @@ def run_pcap(args, table):
     key = _native.prepare_key(args.key, args.hash_fields)
     h, q, c = _native.default_context().hash(key, tuples, args.htable_size, args.num_queues,
                                              reta=table)
-    key_str = Toeplitz(args.key).hash_key_str()
+    key_str = _key_str(args.key)
     if args.csv:
         out = _native.csv_format(tuples, h, q, c, _native.RssCsvLayout((0, 1, 2, 3)))
         out.tofile(args.csv)
@@ -122,9 +128,10 @@ def main(argv=None):
         counts = fastcsv.run_counts(args.key, args.ips_file, args.htable_size, args.num_queues,
                                     fields=args.hash_fields, reta=table)
         if counts is not None:  # histogram mode needs the per-queue counts only
-            histogram.show(counts, Toeplitz(args.key).hash_key_str(), args.htable_size,
+            histogram.show(counts, _key_str(args.key), args.htable_size,
                            args.num_queues, args.histogram_png)
             return
+    from rss_simulator_nvidia_amd.simulator import Simulator
     rss_sim = Simulator(args.key, args.htable_size, args.num_queues, args.hash_fields, args.ipv6,
                         table)
     rss_sim.load_ips_from_csv(args.ips_file)

@@ -75,6 +75,22 @@ result["csv_hash_text_in_memory"] = {"wall_s": time.perf_counter() - t0,
                                              "host memory (PCIe-inclusive, no file I/O)"}
 del img, data
 
+# the CLI as a user runs it: a fresh process (interpreter start, imports, GPU init)
+cli = [sys.executable, "-m", "rss_simulator_nvidia_amd", "--key-file",
+       os.path.join(ROOT, "tests", "golden", "example_input", "hash_key.txt"), "--ips-file", big,
+       "--htable-size", str(H), "--num-queues", str(Q), "--csv", os.path.join(work, "out_cli.csv")]
+walls = []
+for _ in range(2):
+    if os.path.exists(os.path.join(work, "out_cli.csv")):
+        os.unlink(os.path.join(work, "out_cli.csv"))
+    t0 = time.perf_counter()
+    subprocess.run(cli, check=True, cwd=ROOT, stdout=subprocess.DEVNULL)
+    walls.append(time.perf_counter() - t0)
+result["cli_process"] = {"wall_s": min(walls), "rows_per_s": rows / min(walls), "walls_s": walls,
+                         "note": "python -m rss_simulator_nvidia_amd --csv, whole process"}
+result["cli_output_identical"] = open(os.path.join(work, "out_cli.csv"), "rb").read() == \
+    open(os.path.join(work, "out_big_device.csv"), "rb").read()
+
 # rss_hash_host alone (PCIe-inclusive): packed tuples in host memory -> host outputs
 tuples = _native.csv_parse(np.fromfile(big, dtype=np.uint8))[0]
 ctx = _native.default_context()
