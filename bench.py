@@ -280,11 +280,14 @@ def main():
 
     # secondary lines (rank 0, after the timed region): counts-only mode (12 B/tuple,
     # the HBM-read roofline) and u32 queue outputs (20 B/tuple)
-    co_ms = u32_ms = None
+    co_ms = u32_ms = flow_ms = None
     if rank == 0:
         reps = max(5, args.steps // 2)
         co_ms = kernel_ms_of(None, None, 0, reps)
         u32_ms = kernel_ms_of(hashes.data_ptr(), queues.data_ptr(), 0, reps)
+        if args.distribution == "uniform":  # same kernel on SURVEY.md 8(d)'s flow-like input
+            flow_device(torch, tuples, 0, n, dev)
+            flow_ms = kernel_ms_of(hashes.data_ptr(), queues.data_ptr(), qflag, reps)
 
     if rank == 0:
         value = n * world * args.steps / elapsed
@@ -350,6 +353,11 @@ def main():
             },
             "cpu_baseline": baseline,
         }
+        if flow_ms is not None:
+            line["flow_like"] = {
+                "kernel_ms": flow_ms, "tuples_per_s_per_gpu": n / (flow_ms / 1e3),
+                "note": "same outputs on flow-like input (one IP pair, sequential source ports; "
+                        "--distribution flow), timed after the uniform run"}
         print(json.dumps(line), flush=True)
     if world > 1:
         barrier()  # ranks leave together (rank 0 ran the secondary timings alone)
