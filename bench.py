@@ -142,9 +142,28 @@ def load_traffic(profile_dir, n, htable, queues, queue_width):
 
 
 # ------------------------------------------------------------------- main -----
+def relaunch_distributed(n):
+    """``--gpus N`` (N > 1) outside a launcher: run this script under torch.distributed.run
+    as a child process (nothing has touched the GPU yet) and return its exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(n), "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
 def main():
     args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch_distributed(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world:
+        print("bench: --gpus %d but WORLD_SIZE=%d; reporting %d" % (args.gpus, world, world),
+              file=sys.stderr)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     key_bytes = [int(x, 16) for x in EXAMPLE_KEY.split(":")]
