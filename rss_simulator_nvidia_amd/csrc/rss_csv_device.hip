@@ -215,23 +215,9 @@ struct Layout {
     uint8_t col[4];
 };
 
-__global__ __launch_bounds__(kThreads) void parse_lines(
-    const uint8_t* __restrict__ text, uint64_t len, const uint32_t* __restrict__ pos,
-    uint64_t nnl, uint64_t nlines, Layout layout, rss_tuple4* tuples, uint32_t* is_row,
-    unsigned long long* n_empty, unsigned long long* n_bad) {
-    const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-    if (i >= nlines) return;
-    const uint64_t s = i ? (uint64_t)pos[i - 1] + 1 : 0;
-    uint64_t e = i < nnl ? pos[i] : len;
-    if (e > s && text[e - 1] == '\r') --e;
-    if (e == s) {  // "\n", "\r\n" or a final "\r": skipped like skip_empty_line
-        is_row[i] = 0;
-        atomicAdd(n_empty, 1ull);
-        return;
-    }
-    const uint8_t* p = text + s;
-    const uint8_t* end = text + e;
-    uint32_t v[4];
+// one canonical row in [p, end) (line end and one '\r' already cut off)
+__device__ __forceinline__ bool parse_row(const uint8_t* p, const uint8_t* end, const Layout& layout,
+                                          uint32_t (&v)[4]) {
     bool ok = true;
     for (int f = 0; f < 4 && ok; ++f) {
         const int c = layout.col[f];
@@ -241,7 +227,61 @@ __global__ __launch_bounds__(kThreads) void parse_lines(
             ++p;
         }
     }
-    if (!ok || p != end) {
+    return ok && p == end;
+}
+
+// line [p, e) without its '\n': 0 = empty ("", "\r"), 1 = canonical row (-> v), 2 = not
+__device__ __forceinline__ int classify_line(const uint8_t* p, const uint8_t* e, const Layout& layout,
+                                             uint32_t (&v)[4]) {
+    if (e > p && e[-1] == '\r') --e;
+    if (e == p) return 0;
+    return parse_row(p, e, layout, v) ? 1 : 2;
+}
+
+// One workgroup parses 256 consecutive lines.  Their text is one contiguous span: it is
+// staged into LDS with coalesced 16-byte loads and parsed from there (a canonical line is
+// <= 45 bytes, 256 of them < 12 KiB); a span over kParseSpan (only possible for
+// non-canonical text) is parsed straight from global memory.
+constexpr uint32_t kParseSpan = 16384;
+
+__global__ __launch_bounds__(kThreads) void parse_lines(
+    const uint8_t* __restrict__ text, uint64_t len, const uint32_t* __restrict__ pos,
+    uint64_t nnl, uint64_t nlines, Layout layout, rss_tuple4* tuples, uint32_t* is_row,
+    unsigned long long* n_empty, unsigned long long* n_bad) {
+    __shared__ __attribute__((aligned(16))) uint8_t span[kParseSpan + 32];
+    const uint64_t i0 = (uint64_t)blockIdx.x * kThreads;
+    const uint64_t i = i0 + threadIdx.x;
+    const uint64_t last = (i0 + kThreads < nlines ? i0 + kThreads : nlines) - 1;
+    const uint64_t span_s = i0 ? (uint64_t)pos[i0 - 1] + 1 : 0;
+    const uint64_t span_e = last < nnl ? (uint64_t)pos[last] : len;
+    const uint64_t base = span_s & ~15ull;  // 16-B aligned copy window [base, span_e)
+    const bool staged = span_e - base <= kParseSpan;
+    if (staged) {
+        const uint64_t chunks = (span_e - base + 15) / 16;
+        for (uint64_t c = threadIdx.x; c < chunks; c += kThreads) {
+            const uint64_t g = base + 16 * c;
+            if (g + 16 <= len) {
+                *reinterpret_cast<uint4*>(span + 16 * c) = *reinterpret_cast<const uint4*>(text + g);
+            } else {
+                for (uint64_t k = g; k < len; ++k) span[16 * c + (k - g)] = text[k];
+            }
+        }
+    }
+    __syncthreads();
+    if (i >= nlines) return;
+    const uint64_t s = i ? (uint64_t)pos[i - 1] + 1 : 0;
+    const uint64_t e = i < nnl ? pos[i] : len;
+    uint32_t v[4];
+    // 0 = empty line, 1 = row, 2 = not canonical; the two branches keep LDS and global
+    // addressing apart (ds_read vs global_load, no flat loads)
+    const int kind = staged ? classify_line(span + (s - base), span + (e - base), layout, v)
+                            : classify_line(text + s, text + e, layout, v);
+    if (kind == 0) {  // "\n", "\r\n" or a final "\r": skipped like skip_empty_line
+        is_row[i] = 0;
+        atomicAdd(n_empty, 1ull);
+        return;
+    }
+    if (kind == 2) {
         atomicAdd(n_bad, 1ull);
         is_row[i] = 0;
         return;
@@ -299,27 +339,51 @@ __global__ __launch_bounds__(kThreads) void row_lengths(const rss_tuple4* __rest
              d_uint_len(r.ports & 0xFFFFu) + d_uint_len(hash[i]) + d_uint_len(queue[i]) + 6;
 }
 
+// One workgroup formats 256 consecutive rows.  Their output is one contiguous span
+// [g0, g1): each thread writes its row into an LDS image of the span laid out on the
+// global 16-byte grid, then the workgroup stores the whole 16-byte chunks with coalesced
+// 16-byte stores and the (at most two) partial chunks at the span's ends byte by byte,
+// so neighbouring workgroups never write the same bytes.
+constexpr uint32_t kMaxRowBytes = 15 + 1 + 15 + 1 + 5 + 1 + 5 + 1 + 10 + 1 + 10 + 1;  // 66
+
 __global__ __launch_bounds__(kThreads) void write_rows(const rss_tuple4* __restrict__ t,
                                                        const uint32_t* __restrict__ hash,
                                                        const uint32_t* __restrict__ queue,
                                                        uint64_t n, Layout layout,
                                                        const uint64_t* __restrict__ off,
-                                                       uint8_t* out) {
-    const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-    if (i >= n) return;
-    const rss_tuple4 r = t[i];
-    const uint32_t col[4] = {r.sip, r.dip, r.ports >> 16, r.ports & 0xFFFFu};
-    uint8_t* w = out + off[i];
+                                                       uint64_t total, uint8_t* out) {
+    __shared__ __attribute__((aligned(16))) uint8_t img[kThreads * kMaxRowBytes + 32];
+    const uint64_t r0 = (uint64_t)blockIdx.x * kThreads;
+    const uint64_t i = r0 + threadIdx.x;
+    const uint64_t g0 = off[r0];
+    const uint64_t g1 = r0 + kThreads < n ? off[r0 + kThreads] : total;
+    const uint64_t base = g0 & ~15ull;
+    if (i < n) {
+        const rss_tuple4 r = t[i];
+        const uint32_t col[4] = {r.sip, r.dip, r.ports >> 16, r.ports & 0xFFFFu};
+        uint8_t* w = img + (off[i] - base);
 #pragma unroll
-    for (int f = 0; f < 4; ++f) {
-        const int c = layout.col[f];
-        w = c < 2 ? d_put_ip(w, col[c]) : d_put_uint(w, col[c]);
+        for (int f = 0; f < 4; ++f) {
+            const int c = layout.col[f];
+            w = c < 2 ? d_put_ip(w, col[c]) : d_put_uint(w, col[c]);
+            *w++ = ',';
+        }
+        w = d_put_uint(w, hash[i]);
         *w++ = ',';
+        w = d_put_uint(w, queue[i]);
+        *w = '\n';
     }
-    w = d_put_uint(w, hash[i]);
-    *w++ = ',';
-    w = d_put_uint(w, queue[i]);
-    *w = '\n';
+    __syncthreads();
+    const uint64_t a16 = (g0 + 15) & ~15ull, b16 = g1 & ~15ull;
+    if (a16 >= b16) {  // the span lies inside one or two 16-B chunks
+        for (uint64_t p = g0 + threadIdx.x; p < g1; p += kThreads) out[p] = img[p - base];
+        return;
+    }
+    if (threadIdx.x < a16 - g0) out[g0 + threadIdx.x] = img[g0 + threadIdx.x - base];
+    if (threadIdx.x < g1 - b16) out[b16 + threadIdx.x] = img[b16 + threadIdx.x - base];
+    const uint4* src = reinterpret_cast<const uint4*>(img + (a16 - base));
+    uint4* dst = reinterpret_cast<uint4*>(out + a16);
+    for (uint64_t c = threadIdx.x; c < (b16 - a16) / 16; c += kThreads) dst[c] = src[c];
 }
 
 // ---------------------------------------------------------------- host -------
@@ -463,7 +527,7 @@ class CsvJob {
         if ((rc = exclusive_scan(d_len, n_, d_off, &rows_bytes_, buf_, s_))) return rc;
         if ((rc = buf_.alloc(&d_out_, rows_bytes_))) return rc;
         hipLaunchKernelGGL(write_rows, dim3(blocks_for(n_, kThreads)), dim3(kThreads), 0, s_,
-                           d_tuples_, d_hash_, d_queue_, n_, lay_, d_off, d_out_);
+                           d_tuples_, d_hash_, d_queue_, n_, lay_, d_off, rows_bytes_, d_out_);
         CSV_HIP_CHECK(hipGetLastError());
         return RSS_OK;
     }
