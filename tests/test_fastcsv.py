@@ -7,7 +7,6 @@ import numpy as np
 import pandas as pd
 import pytest
 
-from oracle import oracle as o
 from rss_simulator_nvidia_amd import _native
 from rss_simulator_nvidia_amd.ingest import pack_frame
 

@@ -5,7 +5,6 @@ reference only plans it), so parsing parity is against the constructed expectati
 the hashes of the extracted tuples are pinned like every other input."""
 import os
 
-import numpy as np
 import pytest
 
 from oracle import oracle as o
