@@ -23,8 +23,10 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "rss_internal.h"
@@ -1378,6 +1380,25 @@ int rss_hash_host_reta(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tup
                           reta);
 }
 
+// memcpy split over up to 8 threads: the pinned staging copies, not PCIe or the kernel,
+// bound rss_hash_host (one thread moves ~10 GB/s; a 4M-tuple slot is 80 MB each way)
+static void par_memcpy(void* dst, const void* src, size_t bytes) {
+    constexpr size_t kPerThread = (size_t)4 << 20;
+    const size_t nt = std::min<size_t>(8, bytes / kPerThread);
+    if (nt <= 1) {
+        memcpy(dst, src, bytes);
+        return;
+    }
+    std::vector<std::thread> pool;
+    for (size_t k = 1; k < nt; ++k)
+        pool.emplace_back([=] {
+            const size_t a = bytes * k / nt, b = bytes * (k + 1) / nt;
+            memcpy(static_cast<char*>(dst) + a, static_cast<const char*>(src) + a, b - a);
+        });
+    memcpy(dst, src, bytes / nt);
+    for (auto& t : pool) t.join();
+}
+
 static int hash_host_impl(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples, size_t n,
                           uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
                           uint64_t* h_counts, uint32_t flags, const uint32_t* reta) {
@@ -1401,8 +1422,8 @@ static int hash_host_impl(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_
     auto drain = [&](int b) -> int {
         RSS_HIP_CHECK(hipStreamSynchronize(ctx->stream[b]));
         if (pending_len[b]) {
-            if (h_hash) memcpy(h_hash + pending_off[b], ctx->h_hash[b], pending_len[b] * 4);
-            if (h_queue) memcpy(h_queue + pending_off[b], ctx->h_queue[b], pending_len[b] * 4);
+            if (h_hash) par_memcpy(h_hash + pending_off[b], ctx->h_hash[b], pending_len[b] * 4);
+            if (h_queue) par_memcpy(h_queue + pending_off[b], ctx->h_queue[b], pending_len[b] * 4);
             pending_len[b] = 0;
         }
         return RSS_OK;
@@ -1413,7 +1434,7 @@ static int hash_host_impl(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_
         if (rc) return rc;
         const size_t off = c * chunk;
         const size_t len = (n - off) < chunk ? (n - off) : chunk;
-        memcpy(ctx->h_in[b], h_tuples + off, len * sizeof(rss_tuple4));
+        par_memcpy(ctx->h_in[b], h_tuples + off, len * sizeof(rss_tuple4));
         hipStream_t s = ctx->stream[b];
         RSS_HIP_CHECK(hipMemcpyAsync(ctx->d_in[b], ctx->h_in[b], len * sizeof(rss_tuple4),
                                      hipMemcpyHostToDevice, s));
