@@ -166,8 +166,9 @@ int rss_key_search_device(const uint32_t* d_windows, size_t nkeys,
  * host-order words whose big-endian bytes are that input (w[0..3] src, w[4..7]
  * dst, w[8] = sport << 16 | dport).  288 input bits use key bits up to 319, which
  * a 40-byte key covers without wrapping.  Fields for rss_key6_select_fields use
- * the same RSS_FIELD_* bits (RSS_FIELDS_IP = the "IPv6 only" hash).  Queue outputs
- * are uint32 (RSS_FLAG_QUEUE_U8/U16 are rejected).
+ * the same RSS_FIELD_* bits (RSS_FIELDS_IP = the "IPv6 only" hash).  Flags as for
+ * rss_hash_device (d_queue holds uint32, or uint16 / uint8 with RSS_FLAG_QUEUE_U16 /
+ * RSS_FLAG_QUEUE_U8); rss_hash6_host writes uint32 queues.
  */
 #define RSS_INPUT6_BITS 288
 typedef struct rss_tuple6 {
@@ -182,7 +183,7 @@ typedef struct rss_key6 {
 int rss_key6_prepare(const uint8_t* key, size_t len, rss_key6* out);
 int rss_key6_select_fields(rss_key6* key, uint32_t fields);
 int rss_hash6_device(const rss_key6* key, const rss_tuple6* d_tuples, size_t n,
-                     uint32_t htable, uint32_t nqueues, uint32_t* d_hash, uint32_t* d_queue,
+                     uint32_t htable, uint32_t nqueues, uint32_t* d_hash, void* d_queue,
                      uint64_t* d_counts, uint32_t flags, void* stream);
 
 /* Host-memory convenience path (CSV in -> CSV out): owns device buffers. */

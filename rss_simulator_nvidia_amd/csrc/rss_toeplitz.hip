@@ -558,11 +558,12 @@ struct LaunchParams6 {
     uint32_t window[RSS_INPUT6_BITS];
     const rss_tuple6* tuples;
     uint32_t* hash_out;
-    uint32_t* queue_out;
+    void* queue_out;
     unsigned long long* counts;
     uint64_t n;
     uint64_t h_m64;
-    uint32_t h_mask, H, Q, q_mask, q_m32, pad_;
+    uint32_t h_mask, H, Q, q_mask, q_m32;
+    uint32_t qwidth;  // QueueWidth of queue_out (grid-uniform runtime switch)
     uint64_t q_m64;
 };
 
@@ -705,9 +706,13 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz6_kernel(const LaunchParam
                 for (int t = 0; t < 4; ++t) stream_store(o + t, h[t]);
             }
             if (p6.queue_out) {
-                uint32_t* o = p6.queue_out + 4 * g;
-#pragma unroll
-                for (int t = 0; t < 4; ++t) stream_store(o + t, q[t]);
+                if (p6.qwidth == QW_U8) {
+                    store_queue4<QW_U8>(p6.queue_out, g, q[0], q[1], q[2], q[3]);
+                } else if (p6.qwidth == QW_U16) {
+                    store_queue4<QW_U16>(p6.queue_out, g, q[0], q[1], q[2], q[3]);
+                } else {
+                    store_queue4<QW_U32>(p6.queue_out, g, q[0], q[1], q[2], q[3]);
+                }
             }
 #pragma unroll
             for (int t = 0; t < 4; ++t) count_queue<kHist>(bins, q[t], col, p);
@@ -722,7 +727,15 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz6_kernel(const LaunchParam
         const uint32_t h = toeplitz_hash6(lut, w, hi1, hi2);
         const uint32_t q = queue_of<kQMode>(bucket_of<kHPow2>(h, p), p);
         if (p6.hash_out) stream_store(p6.hash_out + i, h);
-        if (p6.queue_out) stream_store(p6.queue_out + i, q);
+        if (p6.queue_out) {
+            if (p6.qwidth == QW_U8) {
+                store_queue1<QW_U8>(p6.queue_out, i, q);
+            } else if (p6.qwidth == QW_U16) {
+                store_queue1<QW_U16>(p6.queue_out, i, q);
+            } else {
+                store_queue1<QW_U32>(p6.queue_out, i, q);
+            }
+        }
         count_queue<kHist>(bins, q, col, p);
     }
     if constexpr (kHist == HIST_PRIVATE || kHist == HIST_SHARED) {
@@ -1029,7 +1042,7 @@ KernelFn6 pick6(int qmode, int hist, bool vec4) {
 }
 
 int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint32_t htable,
-                 uint32_t nqueues, uint32_t* d_hash, uint32_t* d_queue, uint64_t* d_counts,
+                 uint32_t nqueues, uint32_t* d_hash, void* d_queue, uint64_t* d_counts,
                  uint32_t flags, hipStream_t stream) {
     if (!key || key->len < RSS_KEY_MIN_BYTES)
         return set_error(RSS_EINVAL, "rss_hash6_device: key NULL or not prepared");
@@ -1037,8 +1050,16 @@ int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint
         return set_error(RSS_EINVAL, "rss_hash6_device: htable (%u) and nqueues (%u) must be >= 1",
                          htable, nqueues);
     if (n && !d_tuples) return set_error(RSS_EINVAL, "rss_hash6_device: tuples is NULL");
-    if (flags & (RSS_FLAG_QUEUE_U8 | RSS_FLAG_QUEUE_U16))
-        return set_error(RSS_EINVAL, "rss_hash6_device: IPv6 queues are uint32 only");
+    uint32_t qwidth = QW_U32;
+    if (flags & RSS_FLAG_QUEUE_U8) {
+        if (nqueues > 256)
+            return set_error(RSS_EINVAL, "rss_hash6_device: RSS_FLAG_QUEUE_U8 needs nqueues <= 256");
+        qwidth = QW_U8;
+    } else if (flags & RSS_FLAG_QUEUE_U16) {
+        if (nqueues > 65536)
+            return set_error(RSS_EINVAL, "rss_hash6_device: RSS_FLAG_QUEUE_U16 needs nqueues <= 65536");
+        qwidth = QW_U16;
+    }
     if (d_counts && !(flags & RSS_FLAG_ACCUMULATE))
         RSS_HIP_CHECK(hipMemsetAsync(d_counts, 0, sizeof(uint64_t) * nqueues, stream));
     if (n == 0) return RSS_OK;
@@ -1067,8 +1088,10 @@ int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint
     p.q_mask = tmp.q_mask;
     p.q_m32 = tmp.q_m32;
     p.q_m64 = tmp.q_m64;
+    p.qwidth = qwidth;
+    const uintptr_t qalign = qwidth == QW_U8 ? 4 : (qwidth == QW_U16 ? 8 : 16);
     const bool vec4 = aligned16(d_tuples) && (!d_hash || aligned16(d_hash)) &&
-                      (!d_queue || aligned16(d_queue));
+                      (!d_queue || ((uintptr_t)d_queue % qalign) == 0);
     KernelFn6 fn = h_pow2 ? pick6<true>(qmode, hist, vec4) : pick6<false>(qmode, hist, vec4);
     DeviceInfo info;
     int rc = device_info(&info);
@@ -1166,7 +1189,7 @@ int rss_key6_select_fields(rss_key6* key, uint32_t fields) {
 }
 
 int rss_hash6_device(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint32_t htable,
-                     uint32_t nqueues, uint32_t* d_hash, uint32_t* d_queue, uint64_t* d_counts,
+                     uint32_t nqueues, uint32_t* d_hash, void* d_queue, uint64_t* d_counts,
                      uint32_t flags, void* stream) {
     return launch_hash6(key, d_tuples, n, htable, nqueues, d_hash, d_queue, d_counts, flags,
                         static_cast<hipStream_t>(stream));

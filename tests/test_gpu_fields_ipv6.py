@@ -93,6 +93,41 @@ def test_ipv6_device_api_misaligned(native, oracle_lib):
         assert int(counts.sum()) == n
 
 
+@pytest.mark.parametrize("flag_name,dtype,H,Q", [("FLAG_QUEUE_U8", np.uint8, 128, 24),
+                                                 ("FLAG_QUEUE_U8", np.uint8, 100, 256),
+                                                 ("FLAG_QUEUE_U16", np.uint16, 65536, 1000),
+                                                 (None, np.uint32, 512, 64)])
+def test_ipv6_narrow_queue_outputs(native, oracle_lib, flag_name, dtype, H, Q):
+    """RSS_FLAG_QUEUE_U8 / U16 on the IPv6 kernel: aligned (4 queues per store) and
+    misaligned (scalar stores) queue buffers, no bytes written outside the output."""
+    dev = torch.device("cuda:0")
+    s = torch.cuda.current_stream(dev).cuda_stream
+    rng = np.random.default_rng(H + Q)
+    key = [int(x) for x in rng.integers(0, 256, 40)]
+    n = 40003
+    words = rng.integers(0, 2**32, (n, 9), dtype=np.uint64).astype(np.uint32)
+    h = o.hash_words_np(oracle_lib.windows_n(key, 288), words)
+    qo = (h % H) % Q
+    raw = torch.from_numpy(words.view(np.int32).reshape(-1)).to(dev)
+    k6 = native.prepare_key6(key)
+    item = np.dtype(dtype).itemsize
+    flags = getattr(native, flag_name) if flag_name else 0
+    for offset in (0, item):
+        buf = torch.full((n * item + 64,), 0xAB, dtype=torch.uint8, device=dev)
+        counts = torch.empty(Q, dtype=torch.int64, device=dev)
+        native.hash6_device(k6, raw.data_ptr(), n, H, Q, None, buf.data_ptr() + offset,
+                            counts.data_ptr(), flags, s)
+        torch.cuda.synchronize()
+        got = buf.cpu().numpy()
+        np.testing.assert_array_equal(got[offset:offset + n * item].view(dtype), qo.astype(dtype))
+        assert (got[:offset] == 0xAB).all() and (got[offset + n * item:] == 0xAB).all()
+        np.testing.assert_array_equal(counts.cpu().numpy().view(np.uint64),
+                                      np.bincount(qo.astype(np.int64), minlength=Q))
+    from rss_simulator_nvidia_amd.exceptions import DeviceError
+    with pytest.raises(DeviceError, match="QUEUE_U8"):
+        native.hash6_device(k6, 0, 0, 1024, 257, None, None, None, native.FLAG_QUEUE_U8)
+
+
 def test_cli_ipv6_and_fields(tmp_path, golden_dir, oracle_lib, capsys):
     from cli_cases import run_main
     rng = np.random.default_rng(3)

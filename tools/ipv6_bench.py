@@ -19,9 +19,12 @@ hashes = torch.empty(n, dtype=torch.int32, device=dev)
 queues = torch.empty(n, dtype=torch.int32, device=dev)
 counts = torch.empty(24, dtype=torch.int64, device=dev)
 res = {"tuples": n}
-for name, hp, qp in (("full", hashes.data_ptr(), queues.data_ptr()), ("counts_only", None, None)):
+for name, hp, qp, fl, qbytes in (
+        ("full", hashes.data_ptr(), queues.data_ptr(), 0, 4),
+        ("full_u8", hashes.data_ptr(), queues.data_ptr(), _native.FLAG_QUEUE_U8, 1),
+        ("counts_only", None, None, 0, 0)):
     run = lambda: _native.hash6_device(key, tuples.data_ptr(), n, 128, 24, hp, qp,  # noqa: E731
-                                       counts.data_ptr(), 0, s)
+                                       counts.data_ptr(), fl, s)
     run()
     torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -31,6 +34,6 @@ for name, hp, qp in (("full", hashes.data_ptr(), queues.data_ptr()), ("counts_on
     b.record()
     torch.cuda.synchronize()
     ms = a.elapsed_time(b) / 10
-    nbytes = 36 + (8 if hp else 0)
+    nbytes = 36 + (4 + qbytes if hp else 0)
     res[name] = {"ms": ms, "tuples_per_s": n / ms * 1e3, "GB_per_s": n * nbytes / ms / 1e6}
 print(json.dumps(res))
