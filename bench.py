@@ -44,8 +44,9 @@ def parse_args():
     p.add_argument("--queues", type=int, default=24)
     p.add_argument("--queue-width", choices=["auto", "u8", "u16", "u32"], default="auto",
                    help="queue_number output dtype; auto = narrowest that holds every queue")
-    p.add_argument("--cpu-sample", type=int, default=12000,
-                   help="tuples for the CPU baseline (about 20 CPU-seconds)")
+    p.add_argument("--cpu-sample", type=int, default=20000,
+                   help="tuples for the CPU baseline (the 20k-tuple subsample of BASELINE.md; "
+                        "about 17 CPU-seconds)")
     p.add_argument("--cpu-procs", type=int, default=16,
                    help="worker processes for the CPU baseline (the box's CPU share)")
     p.add_argument("--no-cpu-baseline", action="store_true")

@@ -151,6 +151,55 @@ __global__ __launch_bounds__(1024) void mem_stream(Params p) {
     if (!kWrite && acc == 0x12345678u) p.counts[0] = acc;
 }
 
+// work-distribution probe for the 12R+5W mix: instead of a static grid-stride share,
+// every wave claims chunks of kIters x 64 lane-groups (4 tuples each) from eight
+// per-XCD heads (own XCD first, then the others), so a CU / XCD that streams slower
+// is helped by the rest at the end of the launch.  heads[8] must be zero at launch.
+template <int kIters, bool kWrite>
+__global__ __launch_bounds__(1024) void mem_dyn(Params p, unsigned* heads) {
+    const u32x4* src = reinterpret_cast<const u32x4*>(p.tuples);
+    const uint64_t ng = p.n >> 2;
+    constexpr uint64_t kChunk = (uint64_t)kIters * 64;
+    const uint64_t nchunks = (ng + kChunk - 1) / kChunk;
+    const uint32_t per_head = (uint32_t)((nchunks + 7) / 8);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t xcd = blockIdx.x & 7;
+    uint32_t k = 0;  // heads found empty so far (wave-uniform)
+    auto claim = [&]() -> uint64_t {
+        while (k < 8) {
+            const uint32_t h = (xcd + k) & 7;
+            uint32_t v = 0;
+            if (lane == 0) v = atomicAdd(&heads[h], 1u);
+            v = __builtin_amdgcn_readfirstlane(v);
+            const uint64_t c = (uint64_t)h * per_head + v;
+            if (v < per_head && c < nchunks) return c;
+            ++k;
+        }
+        return ~0ull;
+    };
+    uint32_t acc = 0;
+    uint64_t c = claim();
+    while (c != ~0ull) {
+        const uint64_t next = claim();  // in flight while this chunk streams
+        const uint64_t g1 = min(ng, (c + 1) * kChunk);
+        for (uint64_t g = c * kChunk + lane; g < g1; g += 64) {
+            const u32x4 a = src[3 * g], b = src[3 * g + 1], cc = src[3 * g + 2];
+            const uint32_t h0 = a.x ^ a.y ^ a.z, h1 = a.w ^ b.x ^ b.y, h2 = b.z ^ b.w ^ cc.x,
+                           h3 = cc.y ^ cc.z ^ cc.w;
+            if (kWrite) {
+                uint32_t* o = p.hash_out + 4 * g;
+                __builtin_nontemporal_store(h0, o); __builtin_nontemporal_store(h1, o + 1);
+                __builtin_nontemporal_store(h2, o + 2); __builtin_nontemporal_store(h3, o + 3);
+                __builtin_nontemporal_store((a.x ^ cc.w) & 0x17171717u, p.queue_out + g);
+            } else {
+                acc ^= h0 ^ h1 ^ h2 ^ h3;
+            }
+        }
+        c = next;
+    }
+    if (!kWrite && acc == 0x12345678u) p.counts[0] = acc;
+}
+
 // ------------------------------------------------------------ LUT variants
 // chunk t covers input bits [t*B, t*B + B) of the 96-bit MSB-first string.
 template <int B>
@@ -441,6 +490,47 @@ int main(int argc, char** argv) {
                        n * v.bytes / t * 1e3);
             }
         }
+    }
+    if (strstr("dyn", filter)) {  // static grid-stride vs per-wave dynamic chunks
+        p.hash_out = h1;
+        p.queue_out = q1;
+        unsigned* heads;
+        CK(hipMalloc(&heads, 8 * sizeof(unsigned)));
+        struct SV { const char* name; void (*k)(Params); double bytes; };
+        const SV ref[2] = {{"dyn-ref 12R+5W static grid-stride", mem_stream<false, false, true>, 17e-9},
+                           {"dyn-ref 12R static grid-stride", mem_stream<false, false, false>, 12e-9}};
+        struct DV { const char* name; void (*k)(Params, unsigned*); double bytes; };
+        const DV dv[6] = {{"dyn 12R+5W chunk 16 iters", mem_dyn<16, true>, 17e-9},
+                          {"dyn 12R+5W chunk 64 iters", mem_dyn<64, true>, 17e-9},
+                          {"dyn 12R+5W chunk 256 iters", mem_dyn<256, true>, 17e-9},
+                          {"dyn 12R chunk 16 iters", mem_dyn<16, false>, 12e-9},
+                          {"dyn 12R chunk 64 iters", mem_dyn<64, false>, 12e-9},
+                          {"dyn 12R chunk 256 iters", mem_dyn<256, false>, 12e-9}};
+        for (int rep = 0; rep < 2; ++rep) {
+            for (const SV& v : ref) {
+                t = time_ms([&] { hipLaunchKernelGGL(v.k, dim3(g_cus), dim3(1024), 0, 0, p); }, reps);
+                printf("%-40s %8.3f ms  %7.1f Gt/s  %6.0f GB/s\n", v.name, t, n / t / 1e6, n * v.bytes / t * 1e3);
+            }
+            for (const DV& v : dv) {
+                t = time_ms([&] {
+                    CK(hipMemsetAsync(heads, 0, 8 * sizeof(unsigned), 0));
+                    hipLaunchKernelGGL(v.k, dim3(g_cus), dim3(1024), 0, 0, p, heads);
+                }, reps);
+                printf("%-40s %8.3f ms  %7.1f Gt/s  %6.0f GB/s\n", v.name, t, n / t / 1e6, n * v.bytes / t * 1e3);
+            }
+        }
+        // the dynamic stream must cover every group exactly once: check its hash output
+        CK(hipMemset(h1, 0xFF, n * 4));
+        CK(hipMemsetAsync(heads, 0, 8 * sizeof(unsigned), 0));
+        hipLaunchKernelGGL((mem_dyn<64, true>), dim3(g_cus), dim3(1024), 0, 0, p, heads);
+        CK(hipDeviceSynchronize());
+        std::vector<uint32_t> th(n), tt(3 * n);
+        CK(hipMemcpy(th.data(), h1, n * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(tt.data(), tup, n * 12, hipMemcpyDeviceToHost));
+        uint64_t bad = 0;
+        for (uint64_t i = 0; i < n; ++i) bad += th[i] != (tt[3 * i] ^ tt[3 * i + 1] ^ tt[3 * i + 2]);
+        printf("dyn coverage check: %llu mismatches\n", (unsigned long long)bad);
+        CK(hipFree(heads));
     }
     auto run_variant = [&](const char* name, void (*k)(Params), int block, int wgs_per_cu, bool write,
                            bool q8 = false) {
