@@ -196,11 +196,21 @@ void rss_ctx_destroy(rss_ctx* ctx);
  * Same contract as rss_hash_device but on host buffers: chunked
  * H2D -> kernel -> D2H through pinned staging, synchronous on return.
  * h_hash / h_queue (uint32) / h_counts may be NULL; only RSS_FLAG_ACCUMULATE
- * is honoured.
+ * is honoured.  Buffers that are already page-locked (rss_host_alloc,
+ * hipHostMalloc, hipHostRegister) are copied by DMA directly, without the
+ * staging copy; pageable buffers go through the context's pinned staging.
  */
 int rss_hash_host(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples,
                   size_t n, uint32_t htable, uint32_t nqueues, uint32_t* h_hash,
                   uint32_t* h_queue, uint64_t* h_counts, uint32_t flags);
+
+/*
+ * Page-locked host memory for rss_hash_host's direct-DMA path (hipHostMalloc).
+ * Pinning costs far more than a copy, so allocate once and reuse across batches.
+ * rss_host_free(NULL) is a no-op.
+ */
+int rss_host_alloc(size_t bytes, void** out);
+void rss_host_free(void* p);
 
 /*
  * ---- CSV fast path (host, multi-threaded) ----

@@ -34,7 +34,7 @@ EXPORTED_SYMBOLS = (
     "rss_key_search_device", "rss_key_search_host", "rss_key_select_fields",
     "rss_key6_prepare", "rss_key6_select_fields", "rss_hash6_device", "rss_hash6_host",
     "rss_pcap_parse", "rss_hash_device_reta", "rss_hash_host_reta", "rss_csv_hash_text",
-    "rss_csv_hash_file",
+    "rss_csv_hash_file", "rss_host_alloc", "rss_host_free",
 )
 FIELD_SRC_IP, FIELD_DST_IP, FIELD_SRC_PORT, FIELD_DST_PORT = 1, 2, 4, 8
 FIELDS_IP, FIELDS_ALL = 3, 15
@@ -116,6 +116,8 @@ def _bind(lib):
         "rss_key_search_host": ([vp, vp, sz, vp, sz, u32, u32, vp], ctypes.c_int),
         "rss_csv_format": ([vp, vp, vp, sz, vp, u32, ctypes.POINTER(RssCsvLayout), vp, sz,
                             ctypes.POINTER(sz), ctypes.c_int], ctypes.c_int),
+        "rss_host_alloc": ([sz, ctypes.POINTER(vp)], ctypes.c_int),
+        "rss_host_free": ([vp], None),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(lib, name)
@@ -201,6 +203,34 @@ def prepare_key6(key_bytes, fields=FIELDS_ALL):
     return key
 
 
+class PinnedBuffer:
+    """Page-locked host memory from ``rss_host_alloc``, freed when the last numpy view
+    of it is gone (views keep this object alive through their ``base`` chain)."""
+
+    def __init__(self, nbytes):
+        self._lib = load()
+        ptr = ctypes.c_void_p()
+        _check(self._lib.rss_host_alloc(nbytes, ctypes.byref(ptr)), "rss_host_alloc")
+        self.ptr, self.nbytes = ptr.value, nbytes
+        self.__array_interface__ = {"shape": (nbytes,), "typestr": "|u1",
+                                    "data": (ptr.value, False), "version": 3}
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            self._lib.rss_host_free(self.ptr)
+            self.ptr = None
+
+
+def pinned_empty(shape, dtype):
+    """Uninitialised numpy array in page-locked memory: ``HostContext.hash`` moves such
+    arrays by DMA without a staging copy.  Pinning is expensive -- allocate once, reuse."""
+    dtype = np.dtype(dtype)
+    shape = (shape,) if np.isscalar(shape) else tuple(shape)
+    nbytes = int(np.prod(shape, dtype=np.int64)) * dtype.itemsize
+    raw = np.asarray(PinnedBuffer(max(nbytes, 1)))
+    return raw[:nbytes].view(dtype).reshape(shape)
+
+
 class HostContext:
     """Owns an ``rss_ctx`` (device buffers + streams) for host-memory batches."""
 
@@ -222,19 +252,28 @@ class HostContext:
             pass
 
     def hash(self, key, tuples, htable, nqueues, want_hash=True, want_queue=True, want_counts=True,
-             reta=None):
+             reta=None, out=None):
         """Hash packed tuples (structured ``TUPLE_DTYPE`` or uint32 (n, 3)) on the GPU.
 
         ``reta`` (optional, ``htable`` queue ids) maps buckets to queues instead of
-        ``bucket % nqueues``.  Returns ``(hash_u32, queue_u32, counts_u64)``; disabled
-        outputs are None.
+        ``bucket % nqueues``.  ``out`` (optional) = caller-owned ``(hash_u32[n],
+        queue_u32[n])`` to fill, e.g. :func:`pinned_empty` arrays reused across batches
+        (page-locked tuples and outputs skip the staging copies).  Returns
+        ``(hash_u32, queue_u32, counts_u64)``; disabled outputs are None.
         """
         arr = np.ascontiguousarray(tuples)
         if arr.dtype != TUPLE_DTYPE:
             arr = np.ascontiguousarray(arr, dtype=np.uint32).reshape(-1, 3)
         n = len(arr)
-        h = np.empty(n, dtype=np.uint32) if want_hash else None
-        q = np.empty(n, dtype=np.uint32) if want_queue else None
+        if out is not None:
+            h, q = out
+            for a in (h, q):
+                if a is not None and (a.dtype != np.uint32 or a.shape != (n,)
+                                      or not a.flags.c_contiguous):
+                    raise ValueError("out arrays must be contiguous uint32[%d]" % n)
+        else:
+            h = np.empty(n, dtype=np.uint32) if want_hash else None
+            q = np.empty(n, dtype=np.uint32) if want_queue else None
         c = np.zeros(nqueues, dtype=np.uint64) if want_counts else None
         ptr = lambda a: a.ctypes.data if a is not None else None  # noqa: E731
         if reta is None:

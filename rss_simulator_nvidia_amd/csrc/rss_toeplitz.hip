@@ -1422,6 +1422,22 @@ static void par_memcpy(void* dst, const void* src, size_t bytes) {
     for (auto& t : pool) t.join();
 }
 
+// Whether [p, p + bytes) is page-locked host memory (rss_host_alloc, hipHostMalloc,
+// hipHostRegister) that the copy engines can read / write directly.
+static bool host_pinned(const void* p, size_t bytes) {
+    if (!p || !bytes) return true;
+    const char* ends[2] = {static_cast<const char*>(p), static_cast<const char*>(p) + bytes - 1};
+    for (const char* q : ends) {
+        hipPointerAttribute_t a;
+        if (hipPointerGetAttributes(&a, q) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        if (a.type != hipMemoryTypeHost) return false;
+    }
+    return true;
+}
+
 static int hash_host_impl(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples, size_t n,
                           uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
                           uint64_t* h_counts, uint32_t flags, const uint32_t* reta) {
@@ -1440,37 +1456,52 @@ static int hash_host_impl(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_
 
     // Double-buffered pipeline: while slot b runs H2D -> kernel -> D2H on its
     // stream, the host fills the other slot's pinned input and drains its output.
+    // Caller buffers that are already page-locked skip the staging copy: the copy
+    // engines move them directly, so only PCIe bounds the pipeline.
+    const bool in_direct = host_pinned(h_tuples, n * sizeof(rss_tuple4));
+    const bool hash_direct = host_pinned(h_hash, h_hash ? n * 4 : 0);
+    const bool queue_direct = host_pinned(h_queue, h_queue ? n * 4 : 0);
     const size_t nchunks = (n + chunk - 1) / chunk;
     size_t pending_off[2] = {0, 0}, pending_len[2] = {0, 0};
     auto drain = [&](int b) -> int {
         RSS_HIP_CHECK(hipStreamSynchronize(ctx->stream[b]));
         if (pending_len[b]) {
-            if (h_hash) par_memcpy(h_hash + pending_off[b], ctx->h_hash[b], pending_len[b] * 4);
-            if (h_queue) par_memcpy(h_queue + pending_off[b], ctx->h_queue[b], pending_len[b] * 4);
+            if (h_hash && !hash_direct)
+                par_memcpy(h_hash + pending_off[b], ctx->h_hash[b], pending_len[b] * 4);
+            if (h_queue && !queue_direct)
+                par_memcpy(h_queue + pending_off[b], ctx->h_queue[b], pending_len[b] * 4);
             pending_len[b] = 0;
         }
         return RSS_OK;
     };
     for (size_t c = 0; c < nchunks; ++c) {
         const int b = (int)(c & 1);
-        rc = drain(b);
-        if (rc) return rc;
         const size_t off = c * chunk;
         const size_t len = (n - off) < chunk ? (n - off) : chunk;
-        par_memcpy(ctx->h_in[b], h_tuples + off, len * sizeof(rss_tuple4));
         hipStream_t s = ctx->stream[b];
-        RSS_HIP_CHECK(hipMemcpyAsync(ctx->d_in[b], ctx->h_in[b], len * sizeof(rss_tuple4),
+        // staged slots are reused only after the host has drained them; direct copies
+        // are ordered behind the slot's previous chunk by the stream itself
+        if (!(in_direct && hash_direct && queue_direct)) {
+            rc = drain(b);
+            if (rc) return rc;
+        }
+        const rss_tuple4* up = h_tuples + off;
+        if (!in_direct) {
+            par_memcpy(ctx->h_in[b], up, len * sizeof(rss_tuple4));
+            up = ctx->h_in[b];
+        }
+        RSS_HIP_CHECK(hipMemcpyAsync(ctx->d_in[b], up, len * sizeof(rss_tuple4),
                                      hipMemcpyHostToDevice, s));
         rc = launch_hash(key, ctx->d_in[b], len, htable, nqueues, h_hash ? ctx->d_hash[b] : nullptr,
                          h_queue ? ctx->d_queue[b] : nullptr, ctx->d_counts[b],
                          RSS_FLAG_ACCUMULATE, s, reta);  // u32 queues on the host path
         if (rc) return rc;
         if (h_hash)
-            RSS_HIP_CHECK(hipMemcpyAsync(ctx->h_hash[b], ctx->d_hash[b], len * 4,
-                                         hipMemcpyDeviceToHost, s));
+            RSS_HIP_CHECK(hipMemcpyAsync(hash_direct ? h_hash + off : ctx->h_hash[b],
+                                         ctx->d_hash[b], len * 4, hipMemcpyDeviceToHost, s));
         if (h_queue)
-            RSS_HIP_CHECK(hipMemcpyAsync(ctx->h_queue[b], ctx->d_queue[b], len * 4,
-                                         hipMemcpyDeviceToHost, s));
+            RSS_HIP_CHECK(hipMemcpyAsync(queue_direct ? h_queue + off : ctx->h_queue[b],
+                                         ctx->d_queue[b], len * 4, hipMemcpyDeviceToHost, s));
         pending_off[b] = off;
         pending_len[b] = len;
     }
@@ -1488,6 +1519,17 @@ static int hash_host_impl(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_
         }
     }
     return RSS_OK;
+}
+
+int rss_host_alloc(size_t bytes, void** out) {
+    if (!out) return set_error(RSS_EINVAL, "rss_host_alloc: NULL argument");
+    *out = nullptr;
+    RSS_HIP_CHECK(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
+    return RSS_OK;
+}
+
+void rss_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
 }
 
 int rss_key_search_host(rss_ctx* ctx, const rss_key* keys, size_t nkeys,

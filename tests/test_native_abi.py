@@ -101,6 +101,9 @@ def test_no_gpu_is_reported_not_faked(lib):
     assert _native.device_count() == 0
     with pytest.raises(DeviceError, match="no HIP device"):
         _native.HostContext(0)
+    with pytest.raises(DeviceError, match="rss_host_alloc"):
+        _native.pinned_empty(16, np.uint32)
+    lib.rss_host_free(None)  # documented no-op
 
 
 def test_missing_library_fails_loudly(monkeypatch, tmp_path):
