@@ -94,6 +94,7 @@ struct LaunchParams {
     uint32_t q_m32;     // ceil(2^32 / Q): exact b % Q for b, Q < 2^16
     uint32_t nkeys;     // key search: keys in this launch
     uint64_t q_m64;     // ceil(2^64 / Q): exact b % Q for any 32-bit b, Q
+    uint32_t q_m16;     // ceil(2^16 / Q): packed key search, b < 256 (queue_of_byte)
     const uint32_t* key_windows;  // key search: nkeys x 96 windows in device memory
     uint16_t reta[kRetaMax];      // QM_TABLE: queue of bucket b (ethtool -X indirection)
 };
@@ -175,14 +176,20 @@ __device__ __forceinline__ uint32_t lut_term(const char* lut, uint32_t w0, uint3
     return *reinterpret_cast<const uint32_t*>(lut + kImm + chunk_offset<kT>(w0, w1, w2, hi));
 }
 
+// a ^ b ^ c in one VALU op (v_bitop3_b32, truth table 0x96)
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
 // Toeplitz hash of one 96-bit input (toeplitz.py:46-69 over the bytes of :113-142).
 __device__ __forceinline__ uint32_t toeplitz_hash(const uint32_t* __restrict__ lut, uint32_t w0,
                                                   uint32_t w1, uint32_t w2, uint32_t hi) {
     const char* base = reinterpret_cast<const char*>(lut);
-    return (lut_term<0>(base, w0, w1, w2, hi) ^ lut_term<1>(base, w0, w1, w2, hi)) ^
-           (lut_term<2>(base, w0, w1, w2, hi) ^ lut_term<3>(base, w0, w1, w2, hi)) ^
-           (lut_term<4>(base, w0, w1, w2, hi) ^ lut_term<5>(base, w0, w1, w2, hi)) ^
-           (lut_term<6>(base, w0, w1, w2, hi) ^ lut_term<7>(base, w0, w1, w2, hi));
+    return xor3(xor3(lut_term<0>(base, w0, w1, w2, hi), lut_term<1>(base, w0, w1, w2, hi),
+                     lut_term<2>(base, w0, w1, w2, hi)),
+                xor3(lut_term<3>(base, w0, w1, w2, hi), lut_term<4>(base, w0, w1, w2, hi),
+                     lut_term<5>(base, w0, w1, w2, hi)),
+                lut_term<6>(base, w0, w1, w2, hi) ^ lut_term<7>(base, w0, w1, w2, hi));
 }
 
 // hash % htable  (simulator.py:97, first modulo)
@@ -433,8 +440,8 @@ __device__ __forceinline__ uint2 toeplitz_hash_pair(const uint2* __restrict__ lu
     const uint2 t4 = pair_term<4>(base, w0, w1, w2, hi), t5 = pair_term<5>(base, w0, w1, w2, hi);
     const uint2 t6 = pair_term<6>(base, w0, w1, w2, hi), t7 = pair_term<7>(base, w0, w1, w2, hi);
     const uint2 t8 = pair_term<8>(base, w0, w1, w2, hi);
-    return make_uint2(t0.x ^ t1.x ^ t2.x ^ t3.x ^ t4.x ^ t5.x ^ t6.x ^ t7.x ^ t8.x,
-                      t0.y ^ t1.y ^ t2.y ^ t3.y ^ t4.y ^ t5.y ^ t6.y ^ t7.y ^ t8.y);
+    return make_uint2(xor3(xor3(t0.x, t1.x, t2.x), xor3(t3.x, t4.x, t5.x), xor3(t6.x, t7.x, t8.x)),
+                      xor3(xor3(t0.y, t1.y, t2.y), xor3(t3.y, t4.y, t5.y), xor3(t6.y, t7.y, t8.y)));
 }
 
 template <bool kHPow2, int kQMode, int kHist>
@@ -518,6 +525,143 @@ __global__ __launch_bounds__(kBlock) void rss_key_search_kernel(const LaunchPara
         __syncthreads();
         flush_bins<kHist>(bins_a, qa.counts, p.Q, tid);
         if (has_b) flush_bins<kHist>(bins_b, qb.counts, p.Q, tid);
+    }
+}
+
+// Packed-bucket key search.  For a power-of-two H the bucket (simulator.py:97,
+// `hash % htable`) is the low log2(H) bits of the hash, and the low bits of a XOR are
+// the XOR of the low bits: a table term needs only those bits of each key.  With
+// H <= 256 an 8-byte entry holds the low BYTE of 8 keys' terms (H <= 65536: the low
+// half-word of 4 keys'), so the same nine ds_read_b64 of the pair kernel serve 8 (4)
+// keys and the per-key work is a bit-field extract, the queue step and one LDS add.
+// Bins are [q][key][lane column]: the key's offset is a ds_add immediate and every
+// half-wave's adds stay conflict-free.
+constexpr uint32_t kPackedPrepBytes = RSS_INPUT_BITS * 8;  // packed windows, before the bins
+
+// H <= 256, Q < H: b % Q = b - Q * ((b * ceil(2^16 / Q)) >> 16), exact for all b < 256,
+// Q < 256 (checked exhaustively) with 24-bit multiplies only (full-rate v_mul_u32_u24);
+// the packed kernel folds it into the bin address.
+
+// table t entry v (and v + 1024) of the packed kernel: XOR of the packed windows
+template <int kT>
+__device__ __forceinline__ void build_packed_table(uint2* lut, const uint2* packed, uint32_t tid) {
+    uint32_t a = 0, b = 0;
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+        const bool set = (tid >> j) & 1u;
+        const uint2 w = packed[pair_bit(kT, j)];
+        a ^= set ? w.x : 0u;
+        b ^= set ? w.y : 0u;
+    }
+    uint2* dst = lut + pair_table(kT) / 8;
+    dst[tid] = make_uint2(a, b);
+    if constexpr (pair_width(kT) == 11) {
+        const uint2 w = packed[pair_bit(kT, 10)];
+        dst[tid + 1024] = make_uint2(a ^ w.x, b ^ w.y);
+    }
+}
+
+template <int kLaneBits, int kQMode, bool kVec4>
+__global__ __launch_bounds__(kBlock) void rss_key_search_packed_kernel(const LaunchParams p) {
+    constexpr uint32_t kKeys = 64 / kLaneBits;
+    __shared__ uint2 lut[kPairLutBytes / 8];
+    extern __shared__ uint32_t bins[];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t key0 = kKeys * blockIdx.y;
+
+    // 1. pack: lane k of packed[i] = low kLaneBits of key (key0 + k)'s window i (a key
+    //    past the end repeats the last key; its counts are discarded)
+    uint2* packed = reinterpret_cast<uint2*>(bins);
+    if (tid < RSS_INPUT_BITS) {
+        uint32_t lo = 0, hi = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kKeys; ++k) {
+            const uint32_t key = min(key0 + k, p.nkeys - 1);
+            const uint32_t w = p.key_windows[(size_t)RSS_INPUT_BITS * key + tid] &
+                               ((1u << kLaneBits) - 1);
+            const uint32_t shift = k * kLaneBits;
+            if (shift < 32) lo |= w << shift;
+            else hi |= w << (shift - 32);
+        }
+        packed[tid] = make_uint2(lo, hi);
+    }
+    __syncthreads();
+    build_packed_table<0>(lut, packed, tid);
+    build_packed_table<1>(lut, packed, tid);
+    build_packed_table<2>(lut, packed, tid);
+    build_packed_table<3>(lut, packed, tid);
+    build_packed_table<4>(lut, packed, tid);
+    build_packed_table<5>(lut, packed, tid);
+    build_packed_table<6>(lut, packed, tid);
+    build_packed_table<7>(lut, packed, tid);
+    build_packed_table<8>(lut, packed, tid);
+    __syncthreads();  // packed windows are dead: the region becomes bins
+    const uint32_t nbins = p.Q * kKeys * kBinCols;
+    for (uint32_t e = tid; e < nbins; e += kBlock) bins[e] = 0;
+    __syncthreads();
+
+    uint32_t* bins_col = bins + (tid & (kBinCols - 1));
+    char* bins_colb = reinterpret_cast<char*>(bins_col);
+    const uint32_t hbits = 31 - __clz(p.H);  // log2(H)
+    constexpr uint32_t kRowShift = kLaneBits == 8 ? 10 : 9;  // log2(kKeys * kBinCols * 4)
+    // byte-lane queue step folded into the bin address: q * 2^kRowShift =
+    // (b << kRowShift) - d * (Q << kRowShift), d = floor(b / Q) (queue_of_byte): two
+    // full-rate 24-bit multiplies, the second a v_mad_i32_i24
+    const int neg_q_row = -(int)(p.Q << kRowShift);
+    uint32_t hi = 65536u;
+    asm volatile("" : "+v"(hi));
+    // byte lanes: mask every lane to the bucket bits at once, then each key's bucket is
+    // a plain byte select (which the multiplies and shifts take as an SDWA operand)
+    const uint32_t lane_mask4 = (p.H - 1) * 0x01010101u;
+    auto count = [&](uint2 x) {
+        if constexpr (kLaneBits == 8) {
+            x.x &= lane_mask4;
+            x.y &= lane_mask4;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kKeys; ++k) {
+            const uint32_t word = (k * kLaneBits) < 32 ? x.x : x.y;
+            const uint32_t b = kLaneBits == 8 ? (word >> ((k * 8) & 31)) & 0xFFu
+                                              : __builtin_amdgcn_ubfe(word, (k * kLaneBits) & 31, hbits);
+            uint32_t row;
+            if constexpr (kLaneBits == 8 && kQMode == QM_FAST16) {
+                const uint32_t d = __umul24(b, p.q_m16) >> 16;
+                row = (uint32_t)__mul24((int)d, neg_q_row) + (b << kRowShift);
+            } else {
+                row = queue_of<kQMode>(b, p) << kRowShift;
+            }
+            __hip_atomic_fetch_add(reinterpret_cast<uint32_t*>(bins_colb + row) + k * kBinCols, 1u,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    };
+    const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
+    const uint64_t gstride = (uint64_t)gridDim.x * kBlock;
+    uint64_t tail_begin = 0;
+    if constexpr (kVec4) {
+        const uint4* __restrict__ src = reinterpret_cast<const uint4*>(p.tuples);
+        const uint64_t ngroups = p.n >> 2;
+        for (uint64_t g = gtid; g < ngroups; g += gstride) {
+            const uint4 a = src[3 * g + 0];
+            const uint4 b = src[3 * g + 1];
+            const uint4 c = src[3 * g + 2];
+            count(toeplitz_hash_pair(lut, a.x, a.y, a.z, hi));
+            count(toeplitz_hash_pair(lut, a.w, b.x, b.y, hi));
+            count(toeplitz_hash_pair(lut, b.z, b.w, c.x, hi));
+            count(toeplitz_hash_pair(lut, c.y, c.z, c.w, hi));
+        }
+        tail_begin = ngroups << 2;
+    }
+    for (uint64_t i = tail_begin + gtid; i < p.n; i += gstride) {
+        const uint32_t* t = reinterpret_cast<const uint32_t*>(p.tuples) + 3 * i;
+        count(toeplitz_hash_pair(lut, t[0], t[1], t[2], hi));
+    }
+    __syncthreads();
+    for (uint32_t e = tid; e < p.Q * kKeys; e += kBlock) {
+        const uint32_t q = e / kKeys, k = e % kKeys;
+        if (key0 + k >= p.nkeys) continue;
+        uint32_t s = 0;
+        for (uint32_t c = 0; c < kBinCols; ++c) s += bins[e * kBinCols + ((c + e) & (kBinCols - 1))];
+        if (s) atomicAdd(&p.counts[(size_t)(key0 + k) * p.Q + q], (unsigned long long)s);
     }
 }
 
@@ -902,6 +1046,24 @@ KernelFn pick_search(int qmode, int hist, bool vec4) {
     }
 }
 
+// ~256K tuples per workgroup amortise its 120 KiB table build
+unsigned search_grid_x(size_t n, int cu_count) {
+    const uint64_t slices = (n + (1u << 18) - 1) >> 18;
+    return (unsigned)(slices < (uint64_t)cu_count ? slices : cu_count);
+}
+
+template <int kLaneBits, int kQMode>
+KernelFn pick_packed_vec(bool vec4) {
+    return vec4 ? rss_key_search_packed_kernel<kLaneBits, kQMode, true>
+                : rss_key_search_packed_kernel<kLaneBits, kQMode, false>;
+}
+
+KernelFn pick_packed(int lane_bits, int qmode, bool vec4) {
+    if (lane_bits == 8)
+        return qmode == QM_MASK ? pick_packed_vec<8, QM_MASK>(vec4) : pick_packed_vec<8, QM_FAST16>(vec4);
+    return qmode == QM_MASK ? pick_packed_vec<16, QM_MASK>(vec4) : pick_packed_vec<16, QM_FAST16>(vec4);
+}
+
 int launch_search(const uint32_t* d_windows, size_t nkeys, const rss_tuple4* d_tuples, size_t n,
                   uint32_t htable, uint32_t nqueues, uint64_t* d_counts, hipStream_t stream) {
     if (!d_windows || !d_counts || nkeys == 0)
@@ -922,13 +1084,34 @@ int launch_search(const uint32_t* d_windows, size_t nkeys, const rss_tuple4* d_t
     const bool h_pow2 = setup_modes(&p, htable, nqueues, true, &qmode, &hist, &bin_bytes,
                                     kPairBinBytesMax / 2);
     const bool vec4 = aligned16(d_tuples);
-    KernelFn fn = h_pow2 ? pick_search<true>(qmode, hist, vec4) : pick_search<false>(qmode, hist, vec4);
     DeviceInfo info;
     int rc = device_info(&info);
     if (rc) return rc;
-    // ~256K tuples per workgroup amortise its 120 KiB two-key LUT build
-    const uint64_t slices = (n + (1u << 18) - 1) >> 18;
-    const unsigned gx = (unsigned)(slices < (uint64_t)info.cu_count ? slices : info.cu_count);
+    // packed buckets (8 keys per table entry for H <= 256, 4 for H <= 65536) whenever
+    // their private bins fit (8 keys: Q <= 40, 4 keys: Q <= 80); else pairs of full hashes
+    const bool bytes_fit = (uint64_t)nqueues * 8 * kBinCols * 4 <= kPairBinBytesMax;
+    const int lane_bits = htable <= 256u && bytes_fit ? 8 : 16;
+    const uint32_t keys_per_wg = 64 / lane_bits;
+    const uint64_t packed_bins = (uint64_t)nqueues * keys_per_wg * kBinCols * 4;
+    if (h_pow2 && htable <= 65536u && packed_bins <= kPairBinBytesMax) {
+        p.q_m16 = 65536u / nqueues + (65536u % nqueues != 0);
+        KernelFn fn = pick_packed(lane_bits, qmode, vec4);
+        const unsigned gx = search_grid_x(n, info.cu_count);
+        const uint32_t shmem = (uint32_t)std::max<uint64_t>(packed_bins, kPackedPrepBytes);
+        const size_t max_keys = (size_t)keys_per_wg * 65535;  // grid.y limit
+        for (size_t k0 = 0; k0 < nkeys; k0 += max_keys) {
+            const size_t kn = nkeys - k0 < max_keys ? nkeys - k0 : max_keys;
+            p.key_windows = d_windows + k0 * RSS_INPUT_BITS;
+            p.counts = reinterpret_cast<unsigned long long*>(d_counts + k0 * nqueues);
+            p.nkeys = (uint32_t)kn;
+            hipLaunchKernelGGL(fn, dim3(gx, (unsigned)((kn + keys_per_wg - 1) / keys_per_wg)),
+                               dim3(kBlock), shmem, stream, p);
+            RSS_HIP_CHECK(hipGetLastError());
+        }
+        return RSS_OK;
+    }
+    KernelFn fn = h_pow2 ? pick_search<true>(qmode, hist, vec4) : pick_search<false>(qmode, hist, vec4);
+    const unsigned gx = search_grid_x(n, info.cu_count);
     constexpr size_t kMaxKeysPerLaunch = 2 * 65535;  // grid.y (key pairs) limit
     for (size_t k0 = 0; k0 < nkeys; k0 += kMaxKeysPerLaunch) {
         const size_t kn = nkeys - k0 < kMaxKeysPerLaunch ? nkeys - k0 : kMaxKeysPerLaunch;

@@ -17,7 +17,13 @@ def native():
 
 @pytest.mark.parametrize("H,Q,n", [(128, 24, 100003), (512, 64, 65536), (100, 7, 4097),
                                    (65536, 1000, 30001), (100000, 7, 20000), (50000, 10000, 9999),
-                                   (1, 1, 5), (128, 24, 0)])
+                                   (1, 1, 5), (128, 24, 0),
+                                   # packed-bucket kernel: 8 keys / entry (H <= 256), 4 keys
+                                   # (H <= 65536), its bin-budget edges and the fallbacks past them
+                                   (256, 40, 70001), (256, 41, 7001), (16, 24, 33333), (2, 3, 999),
+                                   (256, 255, 5000), (65536, 80, 40003), (1024, 81, 4001),
+                                   (4096, 64, 12345), (128, 1, 777), (128, 64, 5555), (256, 80, 6000),
+                                   (256, 81, 3000)])
 def test_key_search_matches_oracle(native, oracle_lib, H, Q, n):
     from rss_simulator_nvidia_amd import keysearch
     keys = keysearch.random_keys(19, seed=H + Q) + [[int(x) for x in range(52)]]
@@ -62,11 +68,11 @@ def test_search_end_to_end_improves_on_example_key(native, oracle_lib, example_k
                                   oracle_lib.run(ranked[0]["key"], tuples, 128, 24)[2])
 
 
-@pytest.mark.parametrize("nkeys", [1, 3, 7])
-@pytest.mark.parametrize("H,Q", [(128, 24), (512, 2000)])
+@pytest.mark.parametrize("nkeys", [1, 3, 7, 9, 17])
+@pytest.mark.parametrize("H,Q", [(128, 24), (512, 2000), (512, 24)])
 def test_key_search_odd_key_counts_flow_input(native, oracle_lib, nkeys, H, Q):
-    """Keys are evaluated in pairs (one 8-byte table entry per pair); an odd last key is
-    paired with itself and its copy discarded.  Flow-like tuples (one IP pair, sequential
+    """Keys share 8-byte table entries (8 / 4 keys by packed buckets, else pairs); a
+    partial last group repeats its last key and the copies are discarded.  Flow-like tuples (one IP pair, sequential
     source ports -- bench.py --distribution flow) exercise broadcast / strided LDS reads."""
     import bench
     from rss_simulator_nvidia_amd import keysearch

@@ -1,6 +1,6 @@
 """Key-search throughput (tool, not product): K random keys x n resident flows, one launch.
 Prints key-tuple evaluations per second.
-usage: python tools/keysearch_bench.py [K] [n] [uniform|flow]"""
+usage: python tools/keysearch_bench.py [K] [n] [uniform|flow] [H] [Q]"""
 import json
 import os
 import sys
@@ -16,7 +16,8 @@ from rss_simulator_nvidia_amd import _native, keysearch  # noqa: E402
 K = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 20
 dist = sys.argv[3] if len(sys.argv) > 3 else "uniform"
-H, Q = 128, 24
+H = int(sys.argv[4]) if len(sys.argv) > 4 else 128
+Q = int(sys.argv[5]) if len(sys.argv) > 5 else 24
 dev = torch.device("cuda:0")
 s = torch.cuda.current_stream(dev).cuda_stream
 keys = keysearch.random_keys(K, seed=0)
