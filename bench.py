@@ -159,6 +159,8 @@ def relaunch_distributed(n):
 
 def main():
     args = parse_args()
+    if args.steps < 1 or args.warmup < 0:
+        raise SystemExit("bench: --steps must be >= 1 and --warmup >= 0")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(relaunch_distributed(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -219,11 +221,15 @@ def main():
     # step i-1's buffer (async, on the collective stream) overlaps it.
     counts2 = [counts, torch.zeros(Q, dtype=torch.int64, device=dev)]
 
-    def body(c):
+    def body(c, ev=None):
         c.zero_()
+        if ev is not None:
+            ev[0].record(stream)
         _native.hash_device(key, tuples.data_ptr(), n, H, Q, hashes.data_ptr(), queues.data_ptr(),
                             c.data_ptr(), _native.FLAG_ACCUMULATE | qflag,
                             torch.cuda.current_stream(dev).cuda_stream)
+        if ev is not None:
+            ev[1].record(stream)
 
     graphs = None
     if args.graph:
@@ -245,14 +251,18 @@ def main():
 
     pending = [None, None]
 
-    def step(i):
+    def step(i, ev=None):
         b = i & 1
         if pending[b] is not None:
             pending[b].wait()  # buffer b's previous all-reduce must finish before reuse
         if graphs is not None:
+            if ev is not None:
+                ev[0].record(stream)
             graphs[b].replay()
+            if ev is not None:
+                ev[1].record(stream)
         else:
-            body(counts2[b])
+            body(counts2[b], ev)
         if world > 1:
             pending[b] = dist.all_reduce(counts2[b], async_op=True)  # RCCL over xGMI
 
@@ -267,9 +277,13 @@ def main():
     drain()
     barrier()
     torch.cuda.synchronize()
+    # HIP events on the launch stream bracket every timed hash launch: roofline.achieved
+    # is the algorithmic bytes over the mean launch time inside the timed region
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps)]
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(i)
+        step(i, events[i])
     drain()
     torch.cuda.synchronize()
     barrier()
@@ -292,7 +306,8 @@ def main():
     total = int(last.sum().item())
     if total != n * world:
         raise SystemExit("bench: per-queue counts sum to %d, expected %d" % (total, n * world))
-    kernel_ms = kernel_ms_of(hashes.data_ptr(), queues.data_ptr(), qflag, args.steps)
+    launch_ms = [a.elapsed_time(b) for a, b in events]
+    kernel_ms = sum(launch_ms) / len(launch_ms)
     stats = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(stats, op=dist.ReduceOp.MAX)
@@ -358,6 +373,9 @@ def main():
                 "bytes_per_tuple": READ_BYTES + write_bytes,
                 "kernel_ms": kernel_ms,
                 "kernel_ms_max_rank": kernel_ms_max,
+                "kernel_ms_min_max": [min(launch_ms), max(launch_ms)],
+                "timing": "HIP events around each of the %d timed launches (launch stream)"
+                          % args.steps,
             },
             "hbm_read_roofline_frac": value / (world * HBM_PEAK_GBS * 1e9 / READ_BYTES),
             "counts_only": {
