@@ -1139,10 +1139,14 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
         if (htable > kRetaMax)
             return set_error(RSS_EINVAL, "rss_hash_device_reta: htable %u exceeds %u entries",
                              htable, kRetaMax);
-        for (uint32_t b = 0; b < htable; ++b)
+        for (uint32_t b = 0; b < htable; ++b) {
             if (reta[b] >= nqueues)
                 return set_error(RSS_EINVAL, "rss_hash_device_reta: reta[%u] = %u >= nqueues %u",
                                  b, reta[b], nqueues);
+            if (reta[b] > 0xFFFFu)  // the table travels in the kernel arguments as u16
+                return set_error(RSS_EINVAL, "rss_hash_device_reta: reta[%u] = %u exceeds 65535",
+                                 b, reta[b]);
+        }
     }
     int qwidth = QW_U32;
     if (flags & RSS_FLAG_QUEUE_U8) {

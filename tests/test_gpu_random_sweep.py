@@ -1,0 +1,121 @@
+"""Seeded randomised parity sweep of the device API (rss_hash_device / _reta) against the
+C oracle: random sizes (incl. 0 and ragged tails), power-of-two and arbitrary htable /
+nqueues (every modulo and histogram mode), key lengths 16..52, queue widths u8 / u16 /
+u32, NULL outputs, accumulation into non-zero counts and 4-byte-misaligned tuples.
+Bar: bit-exact (integer work)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+CASES = 48
+
+
+@pytest.fixture(scope="module")
+def native():
+    from rss_simulator_nvidia_amd import _native
+    if not torch.cuda.is_available():
+        pytest.fail("gpu tests need a gfx950 device")
+    return _native
+
+
+def _config(seed):
+    rng = np.random.default_rng(1000 + seed)
+    n = int(rng.choice([0, 1, 3, 4, 5, 63, 64, 65, 1023, 4097, int(rng.integers(1, 300000))]))
+    if rng.random() < 0.5:
+        H = 1 << int(rng.integers(0, 21))
+    else:
+        H = int(rng.integers(1, 1 << 20))
+    Q = int(rng.choice([1, 2, 3, 24, 64, 255, 256, 257, 1000, 9000, 70000, int(rng.integers(1, 2 * H + 2))]))
+    key_len = int(rng.choice([16, 40, 52, int(rng.integers(16, 53))]))
+    key = [int(x) for x in rng.integers(0, 256, key_len)]
+    width = "u8" if Q <= 256 and rng.random() < 0.4 else ("u16" if Q <= 65536 and rng.random() < 0.5 else "u32")
+    return dict(rng=rng, n=n, H=H, Q=Q, key=key, width=width,
+                want_hash=bool(rng.random() < 0.8), want_queue=bool(rng.random() < 0.8),
+                accumulate=bool(rng.random() < 0.3), misaligned=bool(rng.random() < 0.3),
+                reta=bool(H <= 1024 and Q <= 65536 and rng.random() < 0.25))
+
+
+@pytest.mark.parametrize("seed", range(CASES))
+def test_random_config_matches_oracle(native, oracle_lib, seed):
+    c = _config(seed)
+    rng, n, H, Q = c["rng"], c["n"], c["H"], c["Q"]
+    dev = torch.device("cuda:0")
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    host = oracle_lib.generate(seed * 7919 + 1, seed, n)
+    # tuples at a 16-byte-aligned or a 4-byte-misaligned device address
+    off = 1 if c["misaligned"] else 0
+    raw = torch.zeros(3 * n + off + 1, dtype=torch.int32, device=dev)
+    if n:
+        raw[off:off + 3 * n] = torch.from_numpy(host.view(np.int32).reshape(-1)).to(dev)
+    tup_ptr = raw.data_ptr() + 4 * off
+    qbytes = {"u8": 1, "u16": 2, "u32": 4}[c["width"]]
+    qflag = {"u8": native.FLAG_QUEUE_U8, "u16": native.FLAG_QUEUE_U16, "u32": 0}[c["width"]]
+    guard = 64
+    hbuf = torch.full((n + guard,), -1, dtype=torch.int32, device=dev)
+    qbuf = torch.full((n * qbytes + guard,), 0x5A, dtype=torch.uint8, device=dev)
+    base = rng.integers(0, 1000, Q).astype(np.int64)
+    counts = torch.from_numpy(base if c["accumulate"] else np.full(Q, 77, np.int64)).to(dev)
+    flags = qflag | (native.FLAG_ACCUMULATE if c["accumulate"] else 0)
+    key = native.prepare_key(c["key"])
+    h_ptr = hbuf.data_ptr() if c["want_hash"] else None
+    q_ptr = qbuf.data_ptr() if c["want_queue"] else None
+    if c["reta"]:
+        reta = rng.integers(0, Q, H).astype(np.uint32)
+        native.hash_device_reta(key, tup_ptr, n, H, reta, Q, h_ptr, q_ptr, counts.data_ptr(),
+                                flags, stream)
+    else:
+        reta = None
+        native.hash_device(key, tup_ptr, n, H, Q, h_ptr, q_ptr, counts.data_ptr(), flags, stream)
+    torch.cuda.synchronize()
+
+    eh, eq, ec = oracle_lib.run(c["key"], host, H, Q, threads=8)
+    if reta is not None:
+        eq = reta[eh % H].astype(np.uint32)
+        ec = np.bincount(eq, minlength=Q).astype(np.uint64)
+    got_h = hbuf.cpu().numpy().view(np.uint32)
+    got_q = qbuf.cpu().numpy()
+    if c["want_hash"]:
+        np.testing.assert_array_equal(got_h[:n], eh)
+    assert (got_h[n:] == 0xFFFFFFFF).all(), "hash store past n"
+    if c["want_queue"]:
+        qdt = {"u8": np.uint8, "u16": np.uint16, "u32": np.uint32}[c["width"]]
+        np.testing.assert_array_equal(got_q[:n * qbytes].view(qdt), eq.astype(qdt))
+        assert (got_q[n * qbytes:] == 0x5A).all(), "queue store past n"
+    else:
+        assert (got_q == 0x5A).all()
+    want = ec.astype(np.uint64) + (base.astype(np.uint64) if c["accumulate"] else 0)
+    np.testing.assert_array_equal(counts.cpu().numpy().view(np.uint64), want)
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_random_key_search_matches_oracle(native, oracle_lib, seed):
+    """Key search under random (H, Q, n, key count): packed 8 / 4 keys per entry, pairs,
+    partial last groups; every key's counts equal the oracle's."""
+    from rss_simulator_nvidia_amd import keysearch
+    rng = np.random.default_rng(5000 + seed)
+    H = 1 << int(rng.integers(0, 17)) if rng.random() < 0.7 else int(rng.integers(1, 70000))
+    Q = int(rng.choice([1, 7, 24, 40, 41, 64, 80, 81, 300, int(rng.integers(1, 2 * H + 2))]))
+    n = int(rng.choice([0, 5, 4096, int(rng.integers(1, 200000))]))
+    nkeys = int(rng.integers(1, 20))
+    keys = keysearch.random_keys(nkeys, seed=seed)
+    tuples = oracle_lib.generate(seed + 17, 0, n)
+    counts = native.HostContext(0).key_search([native.prepare_key(k) for k in keys], tuples, H, Q)
+    assert counts.shape == (nkeys, Q)
+    for k, key in enumerate(keys):
+        np.testing.assert_array_equal(counts[k], oracle_lib.run(key, tuples, H, Q)[2])
+
+
+def test_reta_entries_above_u16_are_refused(native):
+    """Indirection-table entries travel as u16: a queue id >= 65536 is an error, not a
+    silent truncation."""
+    from rss_simulator_nvidia_amd.exceptions import DeviceError
+    dev = torch.device("cuda:0")
+    tup = torch.zeros(3 * 8, dtype=torch.int32, device=dev)
+    counts = torch.zeros(70000, dtype=torch.int64, device=dev)
+    reta = np.array([1, 65536, 2, 69999], dtype=np.uint32)
+    with pytest.raises(DeviceError, match="exceeds 65535"):
+        native.hash_device_reta(native.prepare_key(list(range(40))), tup.data_ptr(), 8, 4, reta,
+                                70000, None, None, counts.data_ptr(), 0, None)

@@ -94,6 +94,10 @@ def test_argument_validation_before_any_device_work(lib, example_key):
     empty = _native.RssKey()
     with pytest.raises(DeviceError, match="key not prepared"):
         _native.hash_device(empty, 0, 16, 128, 24)
+    with pytest.raises(DeviceError, match="exceeds 65535"):  # RETA travels as u16
+        _native.hash_device_reta(key, 16, 1, 2, [3, 65536], 70000)
+    with pytest.raises(DeviceError, match=">= nqueues"):
+        _native.hash_device_reta(key, 16, 1, 2, [0, 24], 24)
 
 
 @pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="only meaningful without a GPU")
