@@ -119,3 +119,53 @@ def test_reta_entries_above_u16_are_refused(native):
     with pytest.raises(DeviceError, match="exceeds 65535"):
         native.hash_device_reta(native.prepare_key(list(range(40))), tup.data_ptr(), 8, 4, reta,
                                 70000, None, None, counts.data_ptr(), 0, None)
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_random_ipv6_config_matches_oracle(native, oracle_lib, seed):
+    """IPv6 kernel (36-byte input) under random n / H / Q / field masks / queue widths /
+    alignment; the numpy closed form over the oracle's 288 windows is the reference."""
+    from oracle import oracle as o
+    rng = np.random.default_rng(9000 + seed)
+    n = int(rng.choice([0, 1, 5, 4097, int(rng.integers(1, 150000))]))
+    H = 1 << int(rng.integers(0, 21)) if rng.random() < 0.5 else int(rng.integers(1, 1 << 20))
+    Q = int(rng.choice([1, 3, 24, 256, 257, 5000, int(rng.integers(1, 2 * H + 2))]))
+    width = "u8" if Q <= 256 and rng.random() < 0.5 else ("u16" if Q <= 65536 and rng.random() < 0.5 else "u32")
+    key = [int(x) for x in rng.integers(0, 256, 40)]
+    fields = str(rng.choice(["sdfn", "sd", "fn", "s", "sdn"]))
+    words = rng.integers(0, 2**32, (n, 9), dtype=np.uint64).astype(np.uint32)
+    k6 = native.prepare_key6(key, fields)
+    full = oracle_lib.windows_n(key, 288)
+    dev = torch.device("cuda:0")
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    off = int(rng.integers(0, 2))
+    raw = torch.zeros(9 * n + off + 1, dtype=torch.int32, device=dev)
+    if n:
+        raw[off:off + 9 * n] = torch.from_numpy(words.view(np.int32).reshape(-1)).to(dev)
+    qbytes = {"u8": 1, "u16": 2, "u32": 4}[width]
+    qflag = {"u8": native.FLAG_QUEUE_U8, "u16": native.FLAG_QUEUE_U16, "u32": 0}[width]
+    hbuf = torch.full((n + 16,), -1, dtype=torch.int32, device=dev)
+    qbuf = torch.full((n * qbytes + 16,), 0x5A, dtype=torch.uint8, device=dev)
+    counts = torch.full((Q,), 3, dtype=torch.int64, device=dev)
+    native.hash6_device(k6, raw.data_ptr() + 4 * off, n, H, Q, hbuf.data_ptr(), qbuf.data_ptr(),
+                        counts.data_ptr(), qflag, stream)
+    torch.cuda.synchronize()
+    if fields == "sdfn":
+        want = o.hash_words_np(full, words)
+    else:
+        # field selection = the concatenated selected fields hashed from key bit 0
+        sel = []
+        for f, (a, b) in zip("sdfn", [(0, 128), (128, 256), (256, 272), (272, 288)]):
+            if f in fields:
+                sel.extend(range(a, b))
+        w = np.zeros(288, dtype=np.uint32)
+        w[sel] = oracle_lib.windows_n(key, len(sel))
+        want = o.hash_words_np(w, words)
+    np.testing.assert_array_equal(hbuf.cpu().numpy().view(np.uint32)[:n], want)
+    assert (hbuf.cpu().numpy()[n:] == -1).all()
+    qo, co = o.queue_and_counts(want, H, Q)
+    qdt = {"u8": np.uint8, "u16": np.uint16, "u32": np.uint32}[width]
+    got_q = qbuf.cpu().numpy()
+    np.testing.assert_array_equal(got_q[:n * qbytes].view(qdt), qo.astype(qdt))
+    assert (got_q[n * qbytes:] == 0x5A).all()
+    np.testing.assert_array_equal(counts.cpu().numpy().view(np.uint64), co)
