@@ -377,7 +377,15 @@ def main():
                 "timing": "HIP events around each of the %d timed launches (launch stream)"
                           % args.steps,
             },
-            "hbm_read_roofline_frac": value / (world * HBM_PEAK_GBS * 1e9 / READ_BYTES),
+            # the HBM-read roofline is the counts-only mode's bound (12 B read
+            # per tuple, 666.7 G tuples/s per GPU); the full-output `value` also writes
+            # write_bytes per tuple, so its share of that read-only bound understates its
+            # HBM use (roofline.frac is its own algorithmic-byte fraction)
+            "hbm_read_roofline": {
+                "bound_tuples_per_s_per_gpu": HBM_PEAK_GBS * 1e9 / READ_BYTES,
+                "counts_only_frac": n / (co_ms / 1e3) / (HBM_PEAK_GBS * 1e9 / READ_BYTES),
+                "full_value_frac": value / (world * HBM_PEAK_GBS * 1e9 / READ_BYTES),
+            },
             "counts_only": {
                 "kernel_ms": co_ms,
                 "tuples_per_s_per_gpu": n / (co_ms / 1e3),
