@@ -292,16 +292,26 @@ def main():
 
     # kernel-only timing (HIP events on the launch stream), for roofline.achieved
     def kernel_ms_of(hash_ptr, queue_ptr, flags, reps):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        _native.hash_device(key, tuples.data_ptr(), n, H, Q, hash_ptr, queue_ptr,
-                            counts.data_ptr(), flags | _native.FLAG_ACCUMULATE, sp)
-        a.record(stream)
-        for _ in range(reps):
+        """Mean launch time of `reps` launches of one output mode (HIP events on the
+        launch stream around each launch), after 30 untimed launches of that mode: right
+        after the memory-bound full-output steps, the LDS/VALU-heavier counts-only launches
+        run 10-35 % slow for ~20 launches while the clocks settle
+        (profiles/r01_runs/mode_switch_probe.json, bench_secondary_warmup.json)."""
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(reps)]
+        for i in range(-30, reps):
+            if i >= 0:
+                ev[i][0].record(stream)
             _native.hash_device(key, tuples.data_ptr(), n, H, Q, hash_ptr, queue_ptr,
                                 counts.data_ptr(), flags | _native.FLAG_ACCUMULATE, sp)
-        b.record(stream)
+            if i >= 0:
+                ev[i][1].record(stream)
         torch.cuda.synchronize()
-        return a.elapsed_time(b) / reps
+        t = sorted(a.elapsed_time(b) for a, b in ev)
+        secondary_spread.append([t[0], t[len(t) // 2], t[-1]])
+        return sum(t) / len(t)
+
+    secondary_spread = []  # [min, median, max] ms of each secondary line, in order
 
     total = int(last.sum().item())
     if total != n * world:
@@ -399,6 +409,7 @@ def main():
             },
             "cpu_baseline": baseline,
         }
+        line["secondary_min_median_max_ms"] = secondary_spread
         if flow_ms is not None:
             line["flow_like"] = {
                 "kernel_ms": flow_ms, "tuples_per_s_per_gpu": n / (flow_ms / 1e3),

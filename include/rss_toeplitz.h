@@ -305,6 +305,22 @@ int rss_hash_host_reta(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tup
                        uint32_t htable, const uint32_t* reta, uint32_t nqueues, uint32_t* h_hash,
                        uint32_t* h_queue, uint64_t* h_counts, uint32_t flags);
 
+/*
+ * Multi-GPU host batch (replaces the same rows of Simulator.calc_hash /
+ * calc_queue_number / write_statistics as rss_hash_host, simulator.py:74-113).  The n
+ * tuples are split into nctx contiguous ranges of ceil(n / nctx) (the last shorter);
+ * context i hashes range i on its own device from its own host thread and copies the
+ * hash / queue slice straight into the caller's output range (no collective), and the
+ * per-queue counts of all ranges are summed on the host -- exact integers, so identical
+ * to one device.  Contexts must be distinct (several may share a device).  reta is
+ * NULL for the reference's `% nqueues` mapping, else htable queue ids (as
+ * rss_hash_host_reta).  Only RSS_FLAG_ACCUMULATE is honoured.  Synchronous.
+ */
+int rss_hash_host_multi(rss_ctx* const* ctxs, int nctx, const rss_key* key,
+                        const rss_tuple4* h_tuples, size_t n, uint32_t htable,
+                        const uint32_t* reta, uint32_t nqueues, uint32_t* h_hash,
+                        uint32_t* h_queue, uint64_t* h_counts, uint32_t flags);
+
 /* Number of visible gfx950 devices (0 when there is no GPU). */
 int rss_device_count(int* out);
 

@@ -34,7 +34,7 @@ EXPORTED_SYMBOLS = (
     "rss_key_search_device", "rss_key_search_host", "rss_key_select_fields",
     "rss_key6_prepare", "rss_key6_select_fields", "rss_hash6_device", "rss_hash6_host",
     "rss_pcap_parse", "rss_hash_device_reta", "rss_hash_host_reta", "rss_csv_hash_text",
-    "rss_csv_hash_file", "rss_host_alloc", "rss_host_free",
+    "rss_csv_hash_file", "rss_host_alloc", "rss_host_free", "rss_hash_host_multi",
 )
 FIELD_SRC_IP, FIELD_DST_IP, FIELD_SRC_PORT, FIELD_DST_PORT = 1, 2, 4, 8
 FIELDS_IP, FIELDS_ALL = 3, 15
@@ -118,6 +118,8 @@ def _bind(lib):
                             ctypes.POINTER(sz), ctypes.c_int], ctypes.c_int),
         "rss_host_alloc": ([sz, ctypes.POINTER(vp)], ctypes.c_int),
         "rss_host_free": ([vp], None),
+        "rss_hash_host_multi": ([ctypes.POINTER(vp), ctypes.c_int, key_p, vp, sz, u32, vp, u32,
+                                 vp, vp, vp, u32], ctypes.c_int),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(lib, name)
@@ -231,6 +233,37 @@ def pinned_empty(shape, dtype):
     return raw[:nbytes].view(dtype).reshape(shape)
 
 
+def ptr(a):
+    """Data pointer of a numpy array, or None (NULL) for a disabled output."""
+    return a.ctypes.data if a is not None else None
+
+
+def _host_batch(tuples, nqueues, want_hash, want_queue, want_counts, out):
+    """Packed tuples as a contiguous array + the (hash, queue, counts) outputs to fill."""
+    arr = np.ascontiguousarray(tuples)
+    if arr.dtype != TUPLE_DTYPE:
+        arr = np.ascontiguousarray(arr, dtype=np.uint32).reshape(-1, 3)
+    n = len(arr)
+    if out is not None:
+        h, q = out
+        for a in (h, q):
+            if a is not None and (a.dtype != np.uint32 or a.shape != (n,)
+                                  or not a.flags.c_contiguous):
+                raise ValueError("out arrays must be contiguous uint32[%d]" % n)
+    else:
+        h = np.empty(n, dtype=np.uint32) if want_hash else None
+        q = np.empty(n, dtype=np.uint32) if want_queue else None
+    c = np.zeros(nqueues, dtype=np.uint64) if want_counts else None
+    return arr, n, h, q, c
+
+
+def _reta_table(reta, htable):
+    table = np.ascontiguousarray(reta, dtype=np.uint32)
+    if len(table) != htable:
+        raise ValueError("indirection table has %d entries, htable is %d" % (len(table), htable))
+    return table
+
+
 class HostContext:
     """Owns an ``rss_ctx`` (device buffers + streams) for host-memory batches."""
 
@@ -261,29 +294,12 @@ class HostContext:
         (page-locked tuples and outputs skip the staging copies).  Returns
         ``(hash_u32, queue_u32, counts_u64)``; disabled outputs are None.
         """
-        arr = np.ascontiguousarray(tuples)
-        if arr.dtype != TUPLE_DTYPE:
-            arr = np.ascontiguousarray(arr, dtype=np.uint32).reshape(-1, 3)
-        n = len(arr)
-        if out is not None:
-            h, q = out
-            for a in (h, q):
-                if a is not None and (a.dtype != np.uint32 or a.shape != (n,)
-                                      or not a.flags.c_contiguous):
-                    raise ValueError("out arrays must be contiguous uint32[%d]" % n)
-        else:
-            h = np.empty(n, dtype=np.uint32) if want_hash else None
-            q = np.empty(n, dtype=np.uint32) if want_queue else None
-        c = np.zeros(nqueues, dtype=np.uint64) if want_counts else None
-        ptr = lambda a: a.ctypes.data if a is not None else None  # noqa: E731
+        arr, n, h, q, c = _host_batch(tuples, nqueues, want_hash, want_queue, want_counts, out)
         if reta is None:
             _check(self._lib.rss_hash_host(self._ctx, ctypes.byref(key), ptr(arr), n, htable,
                                            nqueues, ptr(h), ptr(q), ptr(c), 0), "rss_hash_host")
         else:
-            table = np.ascontiguousarray(reta, dtype=np.uint32)
-            if len(table) != htable:
-                raise ValueError("indirection table has %d entries, htable is %d"
-                                 % (len(table), htable))
+            table = _reta_table(reta, htable)
             _check(self._lib.rss_hash_host_reta(self._ctx, ctypes.byref(key), ptr(arr), n, htable,
                                                 table.ctypes.data, nqueues, ptr(h), ptr(q), ptr(c),
                                                 0), "rss_hash_host_reta")
@@ -300,7 +316,6 @@ class HostContext:
         h = np.empty(n, dtype=np.uint32) if want_hash else None
         q = np.empty(n, dtype=np.uint32) if want_queue else None
         c = np.zeros(nqueues, dtype=np.uint64) if want_counts else None
-        ptr = lambda a: a.ctypes.data if a is not None else None  # noqa: E731
         _check(self._lib.rss_hash6_host(self._ctx, ctypes.byref(key6), ptr(arr), n, htable,
                                         nqueues, ptr(h), ptr(q), ptr(c), 0), "rss_hash6_host")
         return h, q, c
@@ -371,6 +386,33 @@ class HostContext:
 
 _default_ctx = None
 _ctx_lock = threading.Lock()
+
+
+class MultiHostContext:
+    """One ``rss_ctx`` per entry of ``devices`` for host batches split over several GPUs
+    (``rss_hash_host_multi``: contiguous ranges, one host thread per context, counts summed
+    on the host).  A device may appear more than once (several contexts on one GPU)."""
+
+    def __init__(self, devices):
+        self.contexts = [HostContext(d) for d in devices]
+        if not self.contexts:
+            raise ValueError("MultiHostContext needs at least one device")
+        self._lib = load()
+
+    def close(self):
+        for c in self.contexts:
+            c.close()
+
+    def hash(self, key, tuples, htable, nqueues, want_hash=True, want_queue=True, want_counts=True,
+             reta=None, out=None):
+        """Same contract as :meth:`HostContext.hash`, over every context's device."""
+        arr, n, h, q, c = _host_batch(tuples, nqueues, want_hash, want_queue, want_counts, out)
+        handles = (ctypes.c_void_p * len(self.contexts))(*[x._ctx.value for x in self.contexts])
+        table = _reta_table(reta, htable) if reta is not None else None
+        _check(self._lib.rss_hash_host_multi(handles, len(self.contexts), ctypes.byref(key),
+                                             ptr(arr), n, htable, ptr(table), nqueues, ptr(h),
+                                             ptr(q), ptr(c), 0), "rss_hash_host_multi")
+        return h, q, c
 
 
 def default_context():

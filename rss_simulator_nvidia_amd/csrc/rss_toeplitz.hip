@@ -1590,6 +1590,53 @@ int rss_hash_host_reta(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tup
                           reta);
 }
 
+int rss_hash_host_multi(rss_ctx* const* ctxs, int nctx, const rss_key* key,
+                        const rss_tuple4* h_tuples, size_t n, uint32_t htable,
+                        const uint32_t* reta, uint32_t nqueues, uint32_t* h_hash,
+                        uint32_t* h_queue, uint64_t* h_counts, uint32_t flags) {
+    if (!ctxs || nctx < 1 || !key)
+        return set_error(RSS_EINVAL, "rss_hash_host_multi: NULL argument or no contexts");
+    for (int i = 0; i < nctx; ++i) {
+        if (!ctxs[i]) return set_error(RSS_EINVAL, "rss_hash_host_multi: context %d is NULL", i);
+        for (int j = 0; j < i; ++j)
+            if (ctxs[j] == ctxs[i])
+                return set_error(RSS_EINVAL, "rss_hash_host_multi: contexts %d and %d are the same",
+                                 j, i);
+    }
+    if (n && !h_tuples) return set_error(RSS_EINVAL, "rss_hash_host_multi: tuples is NULL");
+    if (htable < 1 || nqueues < 1)
+        return set_error(RSS_EINVAL, "rss_hash_host_multi: htable (%u) and nqueues (%u) must be >= 1",
+                         htable, nqueues);
+    // contiguous ranges, as sharding.shard_range: ceil(n / nctx) each, the last shorter
+    const size_t per = (n + (size_t)nctx - 1) / (size_t)nctx;
+    std::vector<std::vector<uint64_t>> part(nctx, std::vector<uint64_t>(h_counts ? nqueues : 0));
+    std::vector<int> rcs(nctx, RSS_OK);
+    std::vector<std::string> errs(nctx);
+    auto work = [&](int i) {
+        const size_t a = std::min(n, per * (size_t)i), b = std::min(n, a + per);
+        const int rc = hash_host_impl(ctxs[i], key, h_tuples ? h_tuples + a : nullptr, b - a, htable,
+                                      nqueues, h_hash ? h_hash + a : nullptr,
+                                      h_queue ? h_queue + a : nullptr,
+                                      h_counts ? part[i].data() : nullptr, 0, reta);
+        if (rc) {
+            rcs[i] = rc;
+            errs[i] = g_last_error;  // thread-local: carried back to the calling thread
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int i = 1; i < nctx; ++i) pool.emplace_back(work, i);
+    work(0);
+    for (auto& t : pool) t.join();
+    for (int i = 0; i < nctx; ++i)
+        if (rcs[i]) return set_error(rcs[i], "rss_hash_host_multi: context %d: %s", i, errs[i].c_str());
+    if (h_counts) {
+        if (!(flags & RSS_FLAG_ACCUMULATE)) memset(h_counts, 0, sizeof(uint64_t) * nqueues);
+        for (int i = 0; i < nctx; ++i)
+            for (uint32_t q = 0; q < nqueues; ++q) h_counts[q] += part[i][q];
+    }
+    return RSS_OK;
+}
+
 // memcpy split over up to 8 threads: the pinned staging copies, not PCIe or the kernel,
 // bound rss_hash_host (one thread moves ~10 GB/s; a 4M-tuple slot is 80 MB each way)
 static void par_memcpy(void* dst, const void* src, size_t bytes) {

@@ -79,3 +79,41 @@ def test_pinned_empty_shapes(native):
     assert int(a.sum()) == 84
     z = native.pinned_empty(0, np.uint32)
     assert z.shape == (0,)
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])
+def test_multi_context_host_batch_matches_oracle(native, example_key, expected, devices):
+    """rss_hash_host_multi: contiguous ranges over several contexts (here all on cuda:0,
+    each with its own streams and host thread) give exactly the single-device result."""
+    tup, ho, qo, co = expected
+    multi = native.MultiHostContext(devices)
+    key = native.prepare_key(example_key)
+    h, q, c = multi.hash(key, tup, 128, 24)
+    np.testing.assert_array_equal(h, ho)
+    np.testing.assert_array_equal(q, qo)
+    np.testing.assert_array_equal(c, co)
+    # page-locked outputs (direct DMA per range) and hash-only
+    out = (native.pinned_empty(N, np.uint32), None)
+    h2, q2, c2 = multi.hash(key, tup, 128, 24, want_queue=False, want_counts=False, out=out)
+    assert q2 is None and c2 is None
+    np.testing.assert_array_equal(h2, ho)
+    multi.close()
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 5, 4099])
+def test_multi_context_small_and_ragged(native, oracle_lib, example_key, n):
+    """Fewer tuples than contexts (empty ranges), ragged splits and an indirection table."""
+    tup = oracle_lib.generate(99, 0, n)
+    multi = native.MultiHostContext([0, 0, 0])
+    key = native.prepare_key(example_key)
+    h, q, c = multi.hash(key, tup, 100, 7)
+    eh, eq, ec = oracle_lib.run(example_key, tup, 100, 7)
+    np.testing.assert_array_equal(h, eh)
+    np.testing.assert_array_equal(q, eq)
+    np.testing.assert_array_equal(c, ec)
+    reta = np.arange(64, dtype=np.uint32)[::-1] % 5
+    h, q, c = multi.hash(key, tup, 64, 5, reta=reta)
+    eh = oracle_lib.run(example_key, tup, 64, 5)[0]
+    np.testing.assert_array_equal(q, reta[eh % 64])
+    np.testing.assert_array_equal(c, np.bincount(reta[eh % 64], minlength=5).astype(np.uint64))
+    multi.close()

@@ -98,6 +98,18 @@ def test_argument_validation_before_any_device_work(lib, example_key):
         _native.hash_device_reta(key, 16, 1, 2, [3, 65536], 70000)
     with pytest.raises(DeviceError, match=">= nqueues"):
         _native.hash_device_reta(key, 16, 1, 2, [0, 24], 24)
+    fn = lib.rss_hash_host_multi
+    with pytest.raises(DeviceError, match="no contexts"):
+        _native._check(fn(None, 0, ctypes.byref(key), None, 0, 128, None, 24, None, None, None, 0),
+                       "rss_hash_host_multi")
+    two = (ctypes.c_void_p * 2)(0x1000, 0x1000)  # never dereferenced: validation comes first
+    with pytest.raises(DeviceError, match="contexts 0 and 1 are the same"):
+        _native._check(fn(two, 2, ctypes.byref(key), None, 0, 128, None, 24, None, None, None, 0),
+                       "rss_hash_host_multi")
+    two[1] = None
+    with pytest.raises(DeviceError, match="context 1 is NULL"):
+        _native._check(fn(two, 2, ctypes.byref(key), None, 0, 128, None, 24, None, None, None, 0),
+                       "rss_hash_host_multi")
 
 
 @pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="only meaningful without a GPU")
