@@ -384,6 +384,7 @@ def main():
                 "kernel_ms": kernel_ms,
                 "kernel_ms_max_rank": kernel_ms_max,
                 "kernel_ms_min_max": [min(launch_ms), max(launch_ms)],
+                "kernel_ms_median": sorted(launch_ms)[len(launch_ms) // 2],
                 "timing": "HIP events around each of the %d timed launches (launch stream)"
                           % args.steps,
             },
