@@ -291,12 +291,15 @@ int rss_hash6_host(rss_ctx* ctx, const rss_key6* key, const rss_tuple6* h_tuples
 /*
  * ---- pcap input (host) ----
  * One packed 4-tuple per IPv4 packet of a classic libpcap image (either byte
- * order, us/ns timestamps; Ethernet incl. 802.1Q/802.1ad tags, Linux cooked v1,
- * raw IPv4).  TCP/UDP/SCTP packets carry their ports; other protocols and every
+ * order, us/ns timestamps) or a pcapng image (sections of either byte order,
+ * per-interface link types, enhanced / simple / obsolete packet blocks; other
+ * blocks skipped).  Link types: Ethernet incl. 802.1Q/802.1ad tags, Linux cooked
+ * v1, raw IPv4.  TCP/UDP/SCTP packets carry their ports; other protocols and every
  * fragment carry ports 0 (the 2-tuple hash, as NICs do).  protocols (nullable)
- * gets the IP protocol byte per tuple.  Non-IPv4 / malformed packets are skipped
- * and counted in *skipped.  Returns RSS_ENOTSUP for non-pcap images (incl.
- * pcapng); RSS_EINVAL with *n_out = the needed size when cap is too small.
+ * gets the IP protocol byte per tuple.  Non-IPv4 / malformed packets, and packets
+ * of interfaces with other link types, are skipped and counted in *skipped.
+ * Returns RSS_ENOTSUP for other images; RSS_EINVAL with *n_out = the needed size
+ * when cap is too small.
  */
 int rss_pcap_parse(const uint8_t* data, size_t len, rss_tuple4* tuples, uint8_t* protocols,
                    size_t cap, size_t* n_out, size_t* skipped);

@@ -2,12 +2,16 @@
 // "Use pcap as input", docs/rss_general_explaination.md:19).
 //
 // Reads a classic libpcap file image (either byte order, microsecond or nanosecond
-// timestamps) and emits one packed IPv4 4-tuple per IPv4 packet, as a NIC's RSS unit
-// would see it: TCP / UDP / SCTP packets contribute their ports, everything else
-// (other protocols, and every fragment of a fragmented datagram) contributes ports 0,
-// i.e. the 2-tuple hash.  Link types: Ethernet (with 802.1Q / 802.1ad tags), Linux
-// cooked capture v1, raw IPv4.  Non-IPv4 and truncated packets are skipped and counted.
+// timestamps) or a pcapng image (Wireshark's default format: any number of sections of
+// either byte order, per-interface link types, enhanced / simple / obsolete packet
+// blocks, every other block skipped) and emits one packed IPv4 4-tuple per IPv4 packet,
+// as a NIC's RSS unit would see it: TCP / UDP / SCTP packets contribute their ports,
+// everything else (other protocols, and every fragment of a fragmented datagram)
+// contributes ports 0, i.e. the 2-tuple hash.  Link types: Ethernet (with 802.1Q /
+// 802.1ad tags), Linux cooked capture v1, raw IPv4.  Non-IPv4 and truncated packets,
+// and packets of interfaces with other link types, are skipped and counted.
 #include <cstring>
+#include <vector>
 
 #include "rss_toeplitz.h"
 
@@ -63,49 +67,36 @@ bool link_payload(const uint8_t* pkt, uint32_t caplen, uint32_t linktype, uint32
     }
 }
 
-}  // namespace
+inline uint16_t rd16(const uint8_t* p, bool swap) {
+    uint16_t v;
+    memcpy(&v, p, 2);
+    return swap ? __builtin_bswap16(v) : v;
+}
 
-extern "C" {
+bool supported_linktype(uint32_t lt) {
+    return lt == DLT_EN10MB || lt == DLT_RAW || lt == DLT_LINUX_SLL || lt == DLT_IPV4;
+}
 
-int rss_pcap_parse(const uint8_t* data, size_t len, rss_tuple4* tuples, uint8_t* protocols,
-                   size_t cap, size_t* n_out, size_t* skipped) {
-    if (!data || !n_out) return RSS_EINVAL;
-    *n_out = 0;
-    if (skipped) *skipped = 0;
-    if (len < 24) return RSS_ENOTSUP;
-    FileHeader fh;
-    uint32_t magic;
-    memcpy(&magic, data, 4);
-    if (magic == 0xA1B2C3D4u || magic == 0xA1B23C4Du) {
-        fh.swap = false;
-    } else if (magic == 0xD4C3B2A1u || magic == 0x4D3CB2A1u) {
-        fh.swap = true;
-    } else {
-        return RSS_ENOTSUP;  // not a classic pcap file (pcapng is not supported)
-    }
-    fh.linktype = rd32(data + 20, fh.swap) & 0x0FFFFFFF;
-    if (fh.linktype != DLT_EN10MB && fh.linktype != DLT_RAW && fh.linktype != DLT_LINUX_SLL &&
-        fh.linktype != DLT_IPV4)
-        return RSS_ENOTSUP;
-    size_t pos = 24, n = 0, skip = 0;
-    while (pos + 16 <= len) {
-        const uint32_t caplen = rd32(data + pos + 8, fh.swap);
-        pos += 16;
-        if (caplen > len - pos) break;  // truncated file: stop at the last whole record
-        const uint8_t* pkt = data + pos;
-        pos += caplen;
+// Collects the tuples of a capture: one per IPv4 packet, `skip` counts the rest.
+struct TupleSink {
+    rss_tuple4* tuples;
+    uint8_t* protocols;
+    size_t cap;
+    size_t n = 0, skip = 0;
+
+    void packet(const uint8_t* pkt, uint32_t caplen, uint32_t linktype) {
         uint32_t off;
         uint16_t et;
-        if (!link_payload(pkt, caplen, fh.linktype, &off, &et) || et != 0x0800 ||
-            off + 20 > caplen || (pkt[off] >> 4) != 4) {
+        if (!supported_linktype(linktype) || !link_payload(pkt, caplen, linktype, &off, &et) ||
+            et != 0x0800 || off + 20 > caplen || (pkt[off] >> 4) != 4) {
             ++skip;
-            continue;
+            return;
         }
         const uint8_t* ip = pkt + off;
         const uint32_t ihl = (uint32_t)(ip[0] & 15) * 4;
         if (ihl < 20 || off + ihl > caplen) {
             ++skip;
-            continue;
+            return;
         }
         const uint8_t proto = ip[9];
         const uint16_t frag = be16(ip + 6);
@@ -114,7 +105,7 @@ int rss_pcap_parse(const uint8_t* data, size_t len, rss_tuple4* tuples, uint8_t*
         if (!fragment && (proto == 6 || proto == 17 || proto == 132)) {
             if (off + ihl + 4 > caplen) {
                 ++skip;
-                continue;
+                return;
             }
             ports = be32(ip + ihl);  // src port << 16 | dst port
         }
@@ -126,9 +117,117 @@ int rss_pcap_parse(const uint8_t* data, size_t len, rss_tuple4* tuples, uint8_t*
         }
         ++n;
     }
-    *n_out = n;
-    if (skipped) *skipped = skip;
-    return (tuples && n > cap) ? RSS_EINVAL : RSS_OK;
+};
+
+int parse_classic(const uint8_t* data, size_t len, TupleSink* sink) {
+    FileHeader fh;
+    uint32_t magic;
+    memcpy(&magic, data, 4);
+    if (magic == 0xA1B2C3D4u || magic == 0xA1B23C4Du) {
+        fh.swap = false;
+    } else if (magic == 0xD4C3B2A1u || magic == 0x4D3CB2A1u) {
+        fh.swap = true;
+    } else {
+        return RSS_ENOTSUP;
+    }
+    fh.linktype = rd32(data + 20, fh.swap) & 0x0FFFFFFF;
+    if (!supported_linktype(fh.linktype)) return RSS_ENOTSUP;
+    size_t pos = 24;
+    while (pos + 16 <= len) {
+        const uint32_t caplen = rd32(data + pos + 8, fh.swap);
+        pos += 16;
+        if (caplen > len - pos) break;  // truncated file: stop at the last whole record
+        sink->packet(data + pos, caplen, fh.linktype);
+        pos += caplen;
+    }
+    return RSS_OK;
+}
+
+// pcapng (IETF draft-ietf-opsawg-pcapng): blocks of [type u32][total length u32][body]
+// [total length u32], byte order fixed per section by the Section Header Block's magic.
+enum : uint32_t {
+    PCAPNG_SHB = 0x0A0D0D0Au, PCAPNG_IDB = 1, PCAPNG_OPB = 2, PCAPNG_SPB = 3, PCAPNG_EPB = 6
+};
+
+int parse_pcapng(const uint8_t* data, size_t len, TupleSink* sink) {
+    bool swap = false;
+    std::vector<uint32_t> linktype, snaplen;  // per interface of the current section
+    size_t pos = 0;
+    bool first = true;
+    while (pos + 12 <= len) {
+        uint32_t type;
+        memcpy(&type, data + pos, 4);  // the SHB type reads the same in both byte orders
+        if (type == PCAPNG_SHB) {
+            if (pos + 28 > len) break;
+            uint32_t bom;
+            memcpy(&bom, data + pos + 8, 4);
+            if (bom == 0x1A2B3C4Du) swap = false;
+            else if (bom == 0x4D3C2B1Au) swap = true;
+            else return first ? RSS_ENOTSUP : RSS_OK;  // corrupt section: keep what we have
+            linktype.clear();
+            snaplen.clear();
+        } else if (first) {
+            return RSS_ENOTSUP;  // a pcapng image starts with a section header
+        } else {
+            type = rd32(data + pos, swap);
+        }
+        first = false;
+        const uint32_t blen = rd32(data + pos + 4, swap);
+        if (blen < 12 || (blen & 3) || blen > len - pos) break;  // truncated / corrupt: stop
+        const uint8_t* body = data + pos + 8;
+        const uint32_t body_len = blen - 12;
+        if (type == PCAPNG_IDB) {
+            if (body_len >= 8) {
+                linktype.push_back(rd16(body, swap));
+                snaplen.push_back(rd32(body + 4, swap));
+            }
+        } else if (type == PCAPNG_EPB || type == PCAPNG_OPB) {
+            // EPB: if_id u32, ts u32 x2, caplen, origlen; OPB: if_id u16, drops u16, ...
+            if (body_len >= 20) {
+                const uint32_t ifc = type == PCAPNG_EPB ? rd32(body, swap) : rd16(body, swap);
+                const uint32_t caplen = rd32(body + 12, swap);
+                if (caplen > body_len - 20 || ifc >= linktype.size())
+                    ++sink->skip;
+                else
+                    sink->packet(body + 20, caplen, linktype[ifc]);
+            } else {
+                ++sink->skip;
+            }
+        } else if (type == PCAPNG_SPB) {
+            // original length u32, then the packet cut to interface 0's snap length
+            if (body_len >= 4 && !linktype.empty()) {
+                uint32_t caplen = rd32(body, swap);
+                if (snaplen[0] && caplen > snaplen[0]) caplen = snaplen[0];
+                if (caplen > body_len - 4) caplen = body_len - 4;
+                sink->packet(body + 4, caplen, linktype[0]);
+            } else {
+                ++sink->skip;
+            }
+        }  // every other block (name resolution, statistics, custom, ...) is skipped
+        pos += blen;
+    }
+    return RSS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rss_pcap_parse(const uint8_t* data, size_t len, rss_tuple4* tuples, uint8_t* protocols,
+                   size_t cap, size_t* n_out, size_t* skipped) {
+    if (!data || !n_out) return RSS_EINVAL;
+    *n_out = 0;
+    if (skipped) *skipped = 0;
+    if (len < 24) return RSS_ENOTSUP;
+    TupleSink sink{tuples, protocols, cap};
+    uint32_t magic;
+    memcpy(&magic, data, 4);
+    const int rc = magic == PCAPNG_SHB ? parse_pcapng(data, len, &sink)
+                                       : parse_classic(data, len, &sink);
+    if (rc) return rc;
+    *n_out = sink.n;
+    if (skipped) *skipped = sink.skip;
+    return (tuples && sink.n > cap) ? RSS_EINVAL : RSS_OK;
 }
 
 }  // extern "C"

@@ -94,7 +94,7 @@ def build_parser():
     parser.add_argument("--hash-fields", metavar="FIELDS", default="sdfn",
                         type=apt_decorator(_fields_arg), help=argparse.SUPPRESS)
     parser.add_argument("--ipv6", action="store_true", help=argparse.SUPPRESS)
-    #   --pcap                --ips-file is a classic pcap capture (unique IPv4 flows)
+    #   --pcap                --ips-file is a pcap / pcapng capture (unique IPv4 flows)
     #   --pcap-l4 LIST        protocols whose ports are hashed (tcp,udp,sctp | none)
     parser.add_argument("--pcap", action="store_true", help=argparse.SUPPRESS)
     parser.add_argument("--pcap-l4", metavar="LIST", default="all",

@@ -36,7 +36,7 @@ def read_flows(path, l4=None, unique=True):
         raise ParseException("Couldn't read pcap file %s: %s" % (path, err))
     parsed = _native.pcap_parse(data)
     if parsed is None:
-        raise ParseException("%s is not a classic pcap file" % path)
+        raise ParseException("%s is not a pcap or pcapng file" % path)
     tuples, protos, skipped = parsed
     keep = parse_l4(l4)
     if keep != set(PROTOCOLS.values()):

@@ -1,5 +1,5 @@
-"""Synthetic classic-pcap captures for the pcap tests (test infrastructure), plus the
-expected tuples computed independently of the native parser."""
+"""Synthetic classic-pcap and pcapng captures for the pcap tests (test infrastructure),
+plus the expected tuples computed independently of the native parser."""
 import struct
 
 ETH_SRC, ETH_DST = b"\x02\x00\x00\x00\x00\x01", b"\x02\x00\x00\x00\x00\x02"
@@ -33,3 +33,35 @@ def pcap_file(packets, linktype=1, big_endian=False, nanos=False, truncate_last=
     for i, p in enumerate(packets):
         out += struct.pack(e + "IIII", i, 0, len(p), len(p)) + p
     return out[:len(out) - truncate_last] if truncate_last else out
+
+
+def _block(e, btype, body):
+    body += b"\x00" * (-len(body) % 4)
+    total = 12 + len(body)
+    return struct.pack(e + "II", btype, total) + body + struct.pack(e + "I", total)
+
+
+def pcapng_section(packets, interfaces=((1, 65535),), big_endian=False, kinds=None,
+                   extra_blocks=True):
+    """One pcapng section: SHB, an IDB per (linktype, snaplen), then one packet block per
+    entry of ``packets`` -- (interface, bytes) pairs or plain bytes for interface 0.
+    ``kinds`` picks the block per packet: "epb" (default), "spb" or "opb"."""
+    e = ">" if big_endian else "<"
+    out = _block(e, 0x0A0D0D0A, struct.pack(e + "IHHq", 0x1A2B3C4D, 1, 0, -1))
+    for lt, snap in interfaces:
+        out += _block(e, 1, struct.pack(e + "HHI", lt, 0, snap))
+    if extra_blocks:  # name resolution block + a custom block: both skipped
+        out += _block(e, 4, struct.pack(e + "HH", 0, 0))
+        out += _block(e, 0x00000BAD, b"\x01\x02\x03\x04\x05")
+    for i, p in enumerate(packets):
+        ifc, data = p if isinstance(p, tuple) else (0, p)
+        kind = kinds[i] if kinds else "epb"
+        if kind == "epb":
+            out += _block(e, 6, struct.pack(e + "IIIII", ifc, 0, i, len(data), len(data)) + data)
+        elif kind == "opb":
+            out += _block(e, 2, struct.pack(e + "HHIIII", ifc, 0, 0, i, len(data), len(data)) + data)
+        else:
+            out += _block(e, 3, struct.pack(e + "I", len(data)) + data)
+    if extra_blocks:  # interface statistics block after the packets
+        out += _block(e, 5, struct.pack(e + "III", 0, 0, 0))
+    return out

@@ -160,10 +160,12 @@ def test_cli_ipv6_and_fields(tmp_path, golden_dir, oracle_lib, capsys):
         assert table.queue_number.tolist() == [h % 128 % 24 for h in want]
 
 
-def test_cli_pcap_gpu(tmp_path, golden_dir, oracle_lib, capsys):
-    """20K-packet synthetic capture (Ethernet/VLAN, TCP/UDP/ICMP, repeats) through --pcap."""
+@pytest.mark.parametrize("fmt", ["pcap", "pcapng"])
+def test_cli_pcap_gpu(tmp_path, golden_dir, oracle_lib, capsys, fmt):
+    """20K-packet synthetic capture (Ethernet/VLAN, TCP/UDP/ICMP, repeats) through --pcap,
+    as a classic pcap and as a pcapng image."""
     from cli_cases import run_main
-    from pcap_builder import ether, ipv4, l4, pcap_file
+    from pcap_builder import ether, ipv4, l4, pcap_file, pcapng_section
     from rss_simulator_nvidia_amd import pcap
     rng = np.random.default_rng(9)
     pk = []
@@ -174,8 +176,8 @@ def test_cli_pcap_gpu(tmp_path, golden_dir, oracle_lib, capsys):
         pk.append(ether(ipv4(a, b, proto, body), vlans=[(0x8100, 5)] if i % 5 == 0 else ()))
         if i % 7 == 0:
             pk.append(pk[-1])  # repeated packet of the same flow
-    path = tmp_path / "cap.pcap"
-    path.write_bytes(pcap_file(pk))
+    path = tmp_path / ("cap." + fmt)
+    path.write_bytes(pcap_file(pk) if fmt == "pcap" else pcapng_section(pk))
     out = tmp_path / "out.csv"
     key_file = os.path.join(golden_dir, "example_input", "hash_key.txt")
     status, so, _, exc = run_main(["--key-file", key_file, "--ips-file", str(path), "--pcap",

@@ -8,7 +8,7 @@ import os
 import pytest
 
 from oracle import oracle as o
-from pcap_builder import ether, ipv4, l4, pcap_file, sll
+from pcap_builder import ether, ipv4, l4, pcap_file, pcapng_section, sll
 from rss_simulator_nvidia_amd import _native, pcap
 from rss_simulator_nvidia_amd.main import main
 from test_cli_host import OracleContext
@@ -70,7 +70,7 @@ def test_truncated_file_and_non_pcap():
     t, p, _ = _native.pcap_parse(pcap_file(pk, truncate_last=5))
     assert as_rows(t, p) == want[:-1]
     assert _native.pcap_parse(b"src_ip,dst_ip,src_port,dst_port\n" * 3) is None
-    assert _native.pcap_parse(b"\x0a\x0d\x0d\x0a" + b"\x00" * 40) is None  # pcapng
+    assert _native.pcap_parse(b"\x0a\x0d\x0d\x0a" + b"\x00" * 40) is None  # bad pcapng magic
     assert _native.pcap_parse(pcap_file(pk, linktype=147)) is None
 
 
@@ -113,3 +113,46 @@ def test_cli_pcap_csv(fields, tmp_path, monkeypatch, oracle_lib, golden_dir, cap
     assert [int(x.split(",")[4]) for x in body] == want_h
     assert [int(x.split(",")[5]) for x in body] == [h % 128 % 24 for h in want_h]
     assert body[0].startswith("10.0.0.1,192.168.1.20,1234,80,")
+
+
+@pytest.mark.parametrize("big_endian", [False, True])
+def test_pcapng_matches_classic(big_endian):
+    """The same packets as enhanced packet blocks of a pcapng section (with name-resolution,
+    custom and statistics blocks to skip) parse exactly as the classic capture does."""
+    pk, want, skipped = packets_and_expected()
+    got = _native.pcap_parse(pcapng_section(pk, big_endian=big_endian))
+    assert got is not None
+    assert as_rows(got[0], got[1]) == want and got[2] == skipped
+
+
+def test_pcapng_interfaces_blocks_and_sections():
+    """Per-interface link types (Ethernet, cooked, raw, and an unsupported one whose
+    packets are skipped), simple / obsolete packet blocks, SPB cut to the snap length,
+    a second section of the other byte order, and a truncated last block."""
+    p_eth = ether(ipv4(A, B, 6, l4(1, 2)))
+    p_sll = sll(ipv4(B, C, 17, l4(3, 4)))
+    p_raw = ipv4(C, A, 6, l4(5, 6))
+    ifaces = ((1, 65535), (113, 65535), (101, 65535), (147, 65535))
+    sec1 = pcapng_section([(0, p_eth), (1, p_sll), (2, p_raw), (3, p_eth), (9, p_eth)],
+                          interfaces=ifaces)
+    want1 = [(u32(A), u32(B), 1 << 16 | 2, 6), (u32(B), u32(C), 3 << 16 | 4, 17),
+             (u32(C), u32(A), 5 << 16 | 6, 6)]
+    # section 2 (big endian): SPB + OPB on one Ethernet interface; snap length 34 cuts
+    # the SPB packet inside its TCP header (ports unreadable -> skipped)
+    sec2 = pcapng_section([p_eth, p_eth, p_eth], interfaces=((1, 34),), big_endian=True,
+                          kinds=["spb", "opb", "epb"])
+    got = _native.pcap_parse(sec1 + sec2)
+    assert as_rows(got[0], got[1]) == want1 + [(u32(A), u32(B), 1 << 16 | 2, 6)] * 2
+    assert got[2] == 3  # unsupported link type, unknown interface 9, cut SPB packet
+    sec2_bare = pcapng_section([p_eth, p_eth, p_eth], interfaces=((1, 34),), big_endian=True,
+                               kinds=["spb", "opb", "epb"], extra_blocks=False)
+    cut = _native.pcap_parse(sec1 + sec2_bare[:-7])  # last packet block truncated: dropped
+    assert as_rows(cut[0], cut[1]) == want1 + [(u32(A), u32(B), 1 << 16 | 2, 6)]
+
+
+def test_read_flows_pcapng(tmp_path):
+    pk, want, _ = packets_and_expected()
+    path = tmp_path / "c.pcapng"
+    path.write_bytes(pcapng_section(pk))
+    tuples, protos, skipped = pcap.read_flows(str(path))
+    assert len(tuples) == len(set(want)) and skipped == 3
