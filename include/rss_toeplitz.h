@@ -304,6 +304,16 @@ int rss_hash6_host(rss_ctx* ctx, const rss_key6* key, const rss_tuple6* h_tuples
 int rss_pcap_parse(const uint8_t* data, size_t len, rss_tuple4* tuples, uint8_t* protocols,
                    size_t cap, size_t* n_out, size_t* skipped);
 
+/*
+ * The same captures, one rss_tuple6 per IPv6 packet (link types as above plus raw
+ * IPv6): the fixed header's addresses; the extension-header chain (hop-by-hop,
+ * routing, destination options, AH, fragment) is walked to the upper layer, whose
+ * ports count for TCP/UDP/SCTP; fragments, ESP and other upper layers carry ports 0.
+ * protocols gets the upper-layer protocol.  IPv4 and malformed packets are skipped.
+ */
+int rss_pcap_parse6(const uint8_t* data, size_t len, rss_tuple6* tuples, uint8_t* protocols,
+                    size_t cap, size_t* n_out, size_t* skipped);
+
 int rss_hash_host_reta(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples, size_t n,
                        uint32_t htable, const uint32_t* reta, uint32_t nqueues, uint32_t* h_hash,
                        uint32_t* h_queue, uint64_t* h_counts, uint32_t flags);

@@ -35,6 +35,7 @@ EXPORTED_SYMBOLS = (
     "rss_key6_prepare", "rss_key6_select_fields", "rss_hash6_device", "rss_hash6_host",
     "rss_pcap_parse", "rss_hash_device_reta", "rss_hash_host_reta", "rss_csv_hash_text",
     "rss_csv_hash_file", "rss_host_alloc", "rss_host_free", "rss_hash_host_multi",
+    "rss_pcap_parse6",
 )
 FIELD_SRC_IP, FIELD_DST_IP, FIELD_SRC_PORT, FIELD_DST_PORT = 1, 2, 4, 8
 FIELDS_IP, FIELDS_ALL = 3, 15
@@ -106,6 +107,8 @@ def _bind(lib):
                                ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
         "rss_pcap_parse": ([vp, sz, vp, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)],
                            ctypes.c_int),
+        "rss_pcap_parse6": ([vp, sz, vp, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)],
+                            ctypes.c_int),
         "rss_key6_prepare": ([ctypes.POINTER(ctypes.c_uint8), sz, ctypes.POINTER(RssKey6)],
                              ctypes.c_int),
         "rss_key6_select_fields": ([ctypes.POINTER(RssKey6), u32], ctypes.c_int),
@@ -502,17 +505,20 @@ def csv_format(tuples, hashes, queues, counts, layout, threads=0):
 
 
 # ------------------------------------------------------------------ pcap ----
-def pcap_parse(data):
-    """Classic pcap image -> ``(tuples, protocols, skipped)`` or None if not pcap."""
+def pcap_parse(data, ipv6=False):
+    """pcap / pcapng image -> ``(tuples, protocols, skipped)`` or None if neither.
+    ``ipv6``: one ``TUPLE6_DTYPE`` per IPv6 packet instead of one 4-tuple per IPv4 one."""
     buf = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data
     lib = load()
-    cap = len(buf) // 36 + 1  # a record holds >= 16 B header + 20 B IPv4 header
-    tuples = np.empty(cap, dtype=TUPLE_DTYPE)
+    cap = len(buf) // 36 + 1  # a packet record holds >= 16 B of header + a 20 B IP header
+    tuples = np.empty(cap, dtype=TUPLE6_DTYPE if ipv6 else TUPLE_DTYPE)
     protos = np.empty(cap, dtype=np.uint8)
     n, skipped = ctypes.c_size_t(0), ctypes.c_size_t(0)
-    rc = lib.rss_pcap_parse(buf.ctypes.data, len(buf), tuples.ctypes.data, protos.ctypes.data, cap,
-                            ctypes.byref(n), ctypes.byref(skipped))
+    fn, name = (lib.rss_pcap_parse6, "rss_pcap_parse6") if ipv6 else (lib.rss_pcap_parse,
+                                                                       "rss_pcap_parse")
+    rc = fn(buf.ctypes.data, len(buf), tuples.ctypes.data, protos.ctypes.data, cap,
+            ctypes.byref(n), ctypes.byref(skipped))
     if rc == ENOTSUP:
         return None
-    _check(rc, "rss_pcap_parse")
+    _check(rc, name)
     return tuples[:n.value], protos[:n.value], skipped.value

@@ -33,7 +33,7 @@ inline uint32_t rd32(const uint8_t* p, bool swap) {
     return swap ? __builtin_bswap32(v) : v;
 }
 
-enum { DLT_EN10MB = 1, DLT_RAW = 101, DLT_LINUX_SLL = 113, DLT_IPV4 = 228 };
+enum { DLT_EN10MB = 1, DLT_RAW = 101, DLT_LINUX_SLL = 113, DLT_IPV4 = 228, DLT_IPV6 = 229 };
 
 // Offset of the network-layer header and its ethertype; false if not parseable.
 bool link_payload(const uint8_t* pkt, uint32_t caplen, uint32_t linktype, uint32_t* off,
@@ -58,6 +58,7 @@ bool link_payload(const uint8_t* pkt, uint32_t caplen, uint32_t linktype, uint32
             return true;
         case DLT_RAW:
         case DLT_IPV4:
+        case DLT_IPV6:
             if (caplen < 1) return false;
             *off = 0;
             *ethertype = (pkt[0] >> 4) == 4 ? 0x0800 : 0x86DD;
@@ -74,21 +75,34 @@ inline uint16_t rd16(const uint8_t* p, bool swap) {
 }
 
 bool supported_linktype(uint32_t lt) {
-    return lt == DLT_EN10MB || lt == DLT_RAW || lt == DLT_LINUX_SLL || lt == DLT_IPV4;
+    return lt == DLT_EN10MB || lt == DLT_RAW || lt == DLT_LINUX_SLL || lt == DLT_IPV4 ||
+           lt == DLT_IPV6;
 }
 
-// Collects the tuples of a capture: one per IPv4 packet, `skip` counts the rest.
+bool l4_has_ports(uint8_t proto) { return proto == 6 || proto == 17 || proto == 132; }
+
+// Collects the tuples of a capture: one per IPv4 packet (tuples) or per IPv6 packet
+// (tuples6); `skip` counts the rest.
 struct TupleSink {
     rss_tuple4* tuples;
     uint8_t* protocols;
     size_t cap;
+    rss_tuple6* tuples6 = nullptr;
+    bool v6 = false;
     size_t n = 0, skip = 0;
 
     void packet(const uint8_t* pkt, uint32_t caplen, uint32_t linktype) {
         uint32_t off;
         uint16_t et;
-        if (!supported_linktype(linktype) || !link_payload(pkt, caplen, linktype, &off, &et) ||
-            et != 0x0800 || off + 20 > caplen || (pkt[off] >> 4) != 4) {
+        if (!supported_linktype(linktype) || !link_payload(pkt, caplen, linktype, &off, &et)) {
+            ++skip;
+            return;
+        }
+        if (v6) {
+            packet6(pkt, caplen, off, et);
+            return;
+        }
+        if (et != 0x0800 || off + 20 > caplen || (pkt[off] >> 4) != 4) {
             ++skip;
             return;
         }
@@ -102,7 +116,7 @@ struct TupleSink {
         const uint16_t frag = be16(ip + 6);
         const bool fragment = (frag & 0x2000) || (frag & 0x1FFF);  // MF or offset
         uint32_t ports = 0;
-        if (!fragment && (proto == 6 || proto == 17 || proto == 132)) {
+        if (!fragment && l4_has_ports(proto)) {
             if (off + ihl + 4 > caplen) {
                 ++skip;
                 return;
@@ -114,6 +128,58 @@ struct TupleSink {
             tuples[n].dip = be32(ip + 16);
             tuples[n].ports = ports;
             if (protocols) protocols[n] = proto;
+        }
+        ++n;
+    }
+
+    // IPv6: the fixed header's addresses; the extension-header chain (hop-by-hop,
+    // routing, destination options, AH, fragment) is walked to the upper layer, whose
+    // ports count for TCP / UDP / SCTP.  Fragments (offset or M flag set), ESP and
+    // no-next-header packets hash with ports 0, as IPv4 fragments do.
+    void packet6(const uint8_t* pkt, uint32_t caplen, uint32_t off, uint16_t et) {
+        if (et != 0x86DD || off + 40 > caplen || (pkt[off] >> 4) != 6) {
+            ++skip;
+            return;
+        }
+        const uint8_t* ip = pkt + off;
+        uint8_t next = ip[6];
+        uint32_t pos = off + 40;
+        bool fragment = false, truncated = false;
+        for (int hops = 0; hops < 16; ++hops) {
+            if (next != 0 && next != 43 && next != 60 && next != 51 && next != 44) break;
+            if (pos + 8 > caplen) {
+                truncated = true;
+                break;
+            }
+            uint32_t hlen;
+            if (next == 51) {  // authentication header: length in 4-octet units, minus 2
+                hlen = (pkt[pos + 1] + 2u) * 4;
+            } else if (next == 44) {  // fragment header: offset or M flag -> a fragment
+                const uint16_t fo = be16(pkt + pos + 2);
+                fragment = fragment || (fo & 0xFFF8) || (fo & 1);
+                hlen = 8;
+            } else {  // hop-by-hop, routing, destination options: 8-octet units, minus 1
+                hlen = (pkt[pos + 1] + 1u) * 8;
+            }
+            next = pkt[pos];
+            pos += hlen;
+        }
+        uint32_t ports = 0;
+        if (!truncated && !fragment && l4_has_ports(next)) {
+            if (pos + 4 > caplen) truncated = true;
+            else ports = be32(pkt + pos);
+        }
+        if (truncated) {
+            ++skip;
+            return;
+        }
+        if (tuples6 && n < cap) {
+            for (int k = 0; k < 4; ++k) {
+                tuples6[n].w[k] = be32(ip + 8 + 4 * k);
+                tuples6[n].w[4 + k] = be32(ip + 24 + 4 * k);
+            }
+            tuples6[n].w[8] = ports;
+            if (protocols) protocols[n] = next;
         }
         ++n;
     }
@@ -220,6 +286,25 @@ int rss_pcap_parse(const uint8_t* data, size_t len, rss_tuple4* tuples, uint8_t*
     if (skipped) *skipped = 0;
     if (len < 24) return RSS_ENOTSUP;
     TupleSink sink{tuples, protocols, cap};
+    uint32_t magic;
+    memcpy(&magic, data, 4);
+    const int rc = magic == PCAPNG_SHB ? parse_pcapng(data, len, &sink)
+                                       : parse_classic(data, len, &sink);
+    if (rc) return rc;
+    *n_out = sink.n;
+    if (skipped) *skipped = sink.skip;
+    return (tuples && sink.n > cap) ? RSS_EINVAL : RSS_OK;
+}
+
+int rss_pcap_parse6(const uint8_t* data, size_t len, rss_tuple6* tuples, uint8_t* protocols,
+                    size_t cap, size_t* n_out, size_t* skipped) {
+    if (!data || !n_out) return RSS_EINVAL;
+    *n_out = 0;
+    if (skipped) *skipped = 0;
+    if (len < 24) return RSS_ENOTSUP;
+    TupleSink sink{nullptr, protocols, cap};
+    sink.tuples6 = tuples;
+    sink.v6 = true;
     uint32_t magic;
     memcpy(&magic, data, 4);
     const int rc = magic == PCAPNG_SHB ? parse_pcapng(data, len, &sink)

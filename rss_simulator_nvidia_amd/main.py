@@ -51,17 +51,29 @@ def indirection_table(args):
 
 
 def run_pcap(args, table):
-    """--pcap: unique IPv4 flows of a capture -> the same kernel -> CSV or histogram."""
-    tuples, _, _ = pcap.read_flows(args.ips_file, args.pcap_l4)
+    """--pcap: unique IPv4 (or, with --ipv6, IPv6) flows of a capture -> the same kernels
+    -> CSV or histogram."""
+    tuples, _, _ = pcap.read_flows(args.ips_file, args.pcap_l4, ipv6=args.ipv6)
     if len(tuples) == 0:
-        raise ParseException("%s holds no IPv4 packets" % args.ips_file)
-    key = _native.prepare_key(args.key, args.hash_fields)
-    h, q, c = _native.default_context().hash(key, tuples, args.htable_size, args.num_queues,
-                                             reta=table)
+        raise ParseException("%s holds no %s packets" % (args.ips_file,
+                                                          "IPv6" if args.ipv6 else "IPv4"))
+    ctx = _native.default_context()
+    if args.ipv6:
+        if table is not None:
+            raise ValueError("indirection tables are supported for IPv4 input only")
+        key6 = _native.prepare_key6(args.key, args.hash_fields)
+        h, q, c = ctx.hash6(key6, tuples, args.htable_size, args.num_queues)
+    else:
+        key = _native.prepare_key(args.key, args.hash_fields)
+        h, q, c = ctx.hash(key, tuples, args.htable_size, args.num_queues, reta=table)
     key_str = _key_str(args.key)
     if args.csv:
-        out = _native.csv_format(tuples, h, q, c, _native.RssCsvLayout((0, 1, 2, 3)))
-        out.tofile(args.csv)
+        if args.ipv6:
+            with open(args.csv, "w") as f:
+                f.write(pcap.format_statistics6(tuples, h, q, c))
+        else:
+            out = _native.csv_format(tuples, h, q, c, _native.RssCsvLayout((0, 1, 2, 3)))
+            out.tofile(args.csv)
         print("Wrote statistics to {csv}.".format(csv=args.csv))
     else:
         histogram.show(c, key_str, args.htable_size, args.num_queues, args.histogram_png)
@@ -94,7 +106,8 @@ def build_parser():
     parser.add_argument("--hash-fields", metavar="FIELDS", default="sdfn",
                         type=apt_decorator(_fields_arg), help=argparse.SUPPRESS)
     parser.add_argument("--ipv6", action="store_true", help=argparse.SUPPRESS)
-    #   --pcap                --ips-file is a pcap / pcapng capture (unique IPv4 flows)
+    #   --pcap                --ips-file is a pcap / pcapng capture (unique IPv4 flows;
+    #                         with --ipv6 its unique IPv6 flows)
     #   --pcap-l4 LIST        protocols whose ports are hashed (tcp,udp,sctp | none)
     parser.add_argument("--pcap", action="store_true", help=argparse.SUPPRESS)
     parser.add_argument("--pcap-l4", metavar="LIST", default="all",

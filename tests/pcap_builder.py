@@ -13,6 +13,26 @@ def ipv4(src, dst, proto, payload, frag=0, ihl_words=5):
     return hdr + opts + payload
 
 
+def ipv6(src, dst, next_header, payload, ext=()):
+    """IPv6 packet: 16-byte addresses, optional extension headers ``ext`` = [(type, body)]
+    (each body padded to the header's length unit), then ``payload``."""
+    chain = [t for t, _ in ext] + [next_header]
+    hdrs = b""
+    for i, (t, body) in enumerate(ext):
+        nxt = chain[i + 1]
+        if t == 44:  # fragment header: fixed 8 bytes, body = (offset << 3 | M) as u16
+            hdrs += struct.pack("!BBH4s", nxt, 0, body, b"\x00\x00\x00\x01")
+        elif t == 51:  # AH: length in 4-octet units minus 2
+            body += b"\x00" * (-(len(body) + 2) % 4)
+            hdrs += struct.pack("!BB", nxt, (len(body) + 2) // 4 - 2) + body
+        else:  # hop-by-hop / routing / destination options: 8-octet units minus 1
+            body += b"\x00" * (-(len(body) + 2) % 8)
+            hdrs += struct.pack("!BB", nxt, (len(body) + 2) // 8 - 1) + body
+    first = chain[0]
+    return struct.pack("!IHBB16s16s", 0x60000000, len(hdrs) + len(payload), first, 64,
+                       bytes(src), bytes(dst)) + hdrs + payload
+
+
 def l4(sport, dport, extra=16):
     return struct.pack("!HH", sport, dport) + b"\x00" * extra
 

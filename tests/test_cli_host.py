@@ -45,6 +45,14 @@ class OracleContext:
     def key_search(self, keys, tuples, htable, nqueues):
         return np.stack([self.hash(k, tuples, htable, nqueues)[2] for k in keys])
 
+    def hash6(self, key6, tuples6, htable, nqueues, want_hash=True, want_queue=True,
+              want_counts=True):
+        self.calls += 1
+        words = np.ascontiguousarray(tuples6).view(np.uint32).reshape(-1, 9)
+        h = o.hash_words_np(np.ctypeslib.as_array(key6.window), words)
+        q, c = o.queue_and_counts(h, htable, nqueues)
+        return h, q, c
+
 
 @pytest.fixture(params=["fast", "pandas"])
 def oracle_device(request, monkeypatch, oracle_lib):

@@ -192,3 +192,28 @@ def test_cli_pcap_gpu(tmp_path, golden_dir, oracle_lib, capsys, fmt):
     body = lines[lines.index("src_ip,dst_ip,src_port,dst_port,hash_result,queue_number") + 1:]
     assert [int(x.split(",")[4]) for x in body] == h.tolist()
     assert lines[1:17] == ["%d,%d" % (i, c[i]) for i in range(16) if c[i]]
+
+
+def test_cli_pcap_ipv6_gpu(tmp_path, golden_dir, oracle_lib, capsys):
+    """--pcap --ipv6 on the GPU: IPv6 flows (extension headers, fragments, VLAN) of a pcapng
+    capture through the IPv6 kernel; hashes equal the oracle's literal 36-byte loop."""
+    from cli_cases import run_main
+    from pcap_builder import pcapng_section
+    from test_pcap import packets6_and_expected
+    pk, want, _ = packets6_and_expected()
+    path = tmp_path / "c6.pcapng"
+    path.write_bytes(pcapng_section(pk * 50))
+    out = tmp_path / "out6.csv"
+    key_file = os.path.join(golden_dir, "example_input", "hash_key.txt")
+    status, so, _, exc = run_main(["--key-file", key_file, "--ips-file", str(path), "--pcap",
+                                   "--ipv6", "--htable-size", "64", "--num-queues", "6",
+                                   "--csv", str(out)], capsys)
+    assert status == 0, exc
+    key = [int(x, 16) for x in open(key_file).read().split(":")]
+    uniq = list(dict.fromkeys(r[:9] for r in want))
+    want_h = [oracle_lib.hash_bytes(key, b"".join(int(w).to_bytes(4, "big") for w in r))
+              for r in uniq]
+    lines = out.read_text().splitlines()
+    body = lines[lines.index("src_ip,dst_ip,src_port,dst_port,hash_result,queue_number") + 1:]
+    assert [int(x.split(",")[4]) for x in body] == want_h
+    assert [int(x.split(",")[5]) for x in body] == [h % 64 % 6 for h in want_h]

@@ -156,3 +156,100 @@ def test_read_flows_pcapng(tmp_path):
     path.write_bytes(pcapng_section(pk))
     tuples, protos, skipped = pcap.read_flows(str(path))
     assert len(tuples) == len(set(want)) and skipped == 3
+
+
+S6 = bytes.fromhex("20010db8000000000000000000000001")
+D6 = bytes.fromhex("20010db8000000000000000000000002")
+E6 = bytes.fromhex("fe800000000000000211223344556677")
+
+
+def w6(addr):
+    return tuple(int.from_bytes(addr[i:i + 4], "big") for i in range(0, 16, 4))
+
+
+def packets6_and_expected():
+    """IPv6 packets with extension-header chains and the tuples a NIC's RSS unit hashes."""
+    from pcap_builder import ipv6
+    pk, want = [], []
+
+    def add(pkt, src, dst, ports, proto):
+        pk.append(pkt)
+        if src is not None:
+            want.append(w6(src) + w6(dst) + (ports, proto))
+
+    add(ether(ipv6(S6, D6, 6, l4(1000, 443)), ethertype=0x86DD), S6, D6, 1000 << 16 | 443, 6)
+    add(ether(ipv6(D6, S6, 17, l4(53, 5353), ext=[(0, b"\x01\x00" * 2), (60, b"\x00" * 10)]),
+              ethertype=0x86DD), D6, S6, 53 << 16 | 5353, 17)                    # HBH + dst opts
+    add(ether(ipv6(S6, E6, 6, l4(7, 8), ext=[(43, b"\x00" * 22)]), ethertype=0x86DD),
+        S6, E6, 7 << 16 | 8, 6)                                                  # routing header
+    add(ether(ipv6(S6, D6, 17, l4(1, 2), ext=[(44, 0x0001)]), ethertype=0x86DD),
+        S6, D6, 0, 17)                                                           # first fragment
+    add(ether(ipv6(S6, D6, 17, b"\x00" * 16, ext=[(44, 185 << 3)]), ethertype=0x86DD),
+        S6, D6, 0, 17)                                                           # later fragment
+    add(ether(ipv6(E6, D6, 6, l4(9, 10), ext=[(44, 0)]), ethertype=0x86DD),
+        E6, D6, 9 << 16 | 10, 6)                                                 # atomic fragment
+    add(ether(ipv6(S6, D6, 132, l4(11, 12), ext=[(51, b"\x00" * 10)]), ethertype=0x86DD),
+        S6, D6, 11 << 16 | 12, 132)                                              # AH + SCTP
+    add(ether(ipv6(S6, D6, 50, b"\x00" * 24), ethertype=0x86DD), S6, D6, 0, 50)  # ESP
+    add(ether(ipv6(D6, E6, 58, b"\x80\x00" + b"\x00" * 10), ethertype=0x86DD),
+        D6, E6, 0, 58)                                                           # ICMPv6
+    add(ether(ipv6(S6, D6, 17, l4(3, 4)), ethertype=0x86DD, vlans=[(0x8100, 9)]),
+        S6, D6, 3 << 16 | 4, 17)                                                 # VLAN
+    add(ether(ipv4(A, B, 6, l4(1234, 80))), None, None, 0, 0)                    # IPv4: skipped
+    add(ether(ipv6(S6, D6, 6, b"\x00\x01"), ethertype=0x86DD), None, None, 0, 0)  # cut TCP: skip
+    add(ether(ipv6(S6, D6, 6, l4(1, 2), ext=[(0, b"\x00" * 40)])[:60], ethertype=0x86DD),
+        None, None, 0, 0)                                                        # cut ext hdr
+    add(ether(ipv6(S6, D6, 6, l4(1000, 443)), ethertype=0x86DD), S6, D6, 1000 << 16 | 443, 6)
+    return pk, want, 3
+
+
+def as_rows6(tuples, protos):
+    return [tuple(int(x) for x in t["sip"]) + tuple(int(x) for x in t["dip"]) +
+            (int(t["ports"]), int(p)) for t, p in zip(tuples, protos)]
+
+
+@pytest.mark.parametrize("fmt", ["pcap", "pcapng", "pcapng_be"])
+def test_parse_ipv6(fmt):
+    pk, want, skipped = packets6_and_expected()
+    img = pcap_file(pk) if fmt == "pcap" else pcapng_section(pk, big_endian=fmt == "pcapng_be")
+    t, p, s = _native.pcap_parse(img, ipv6=True)
+    assert as_rows6(t, p) == want and s == skipped
+    # the IPv4 view of the same capture sees only the one IPv4 packet
+    t4, _, s4 = _native.pcap_parse(img)
+    assert len(t4) == 1 and s4 == len(pk) - 1
+
+
+def test_parse_ipv6_raw_link_types():
+    from pcap_builder import ipv6
+    pkt = ipv6(S6, D6, 17, l4(5, 6))
+    for lt in (101, 229):
+        t, p, s = _native.pcap_parse(pcap_file([pkt, ipv4(A, B, 6, l4(1, 2))], linktype=lt),
+                                     ipv6=True)
+        assert as_rows6(t, p) == [w6(S6) + w6(D6) + (5 << 16 | 6, 17)] and s == 1
+
+
+def test_cli_pcap_ipv6_csv(tmp_path, monkeypatch, oracle_lib, golden_dir, capsys):
+    """--pcap --ipv6: unique IPv6 flows hashed with the 36-byte input; the CSV carries
+    RFC 5952 addresses; hashes follow the oracle's literal loop over the 36 bytes."""
+    monkeypatch.setattr(_native, "default_context", lambda: OracleContext(oracle_lib))
+    pk, want, _ = packets6_and_expected()
+    path = tmp_path / "c6.pcapng"
+    path.write_bytes(pcapng_section(pk))
+    out = tmp_path / "out6.csv"
+    key_file = os.path.join(golden_dir, "example_input", "hash_key.txt")
+    main(["--key-file", key_file, "--ips-file", str(path), "--pcap", "--ipv6",
+          "--htable-size", "128", "--num-queues", "24", "--csv", str(out)])
+    assert capsys.readouterr().out == "Wrote statistics to %s.\n" % out
+    key = [int(x, 16) for x in open(key_file).read().split(":")]
+    uniq = list(dict.fromkeys(r[:9] for r in want))
+    want_h = [oracle_lib.hash_bytes(key, b"".join(int(w).to_bytes(4, "big") for w in r))
+              for r in uniq]
+    lines = out.read_text().splitlines()
+    body = lines[lines.index("src_ip,dst_ip,src_port,dst_port,hash_result,queue_number") + 1:]
+    assert [int(x.split(",")[4]) for x in body] == want_h
+    assert [int(x.split(",")[5]) for x in body] == [h % 128 % 24 for h in want_h]
+    assert body[0] == "2001:db8::1,2001:db8::2,1000,443,%d,%d" % (want_h[0], want_h[0] % 128 % 24)
+    counts = {}
+    for h in want_h:
+        counts[h % 128 % 24] = counts.get(h % 128 % 24, 0) + 1
+    assert lines[1:1 + len(counts)] == ["%d,%d" % (q, counts[q]) for q in sorted(counts)]
