@@ -318,6 +318,16 @@ int rss_hash_host_reta(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tup
                        uint32_t htable, const uint32_t* reta, uint32_t nqueues, uint32_t* h_hash,
                        uint32_t* h_queue, uint64_t* h_counts, uint32_t flags);
 
+/* The IPv6 counterparts: rss_hash6_device / rss_hash6_host with the bucket -> queue
+ * step through reta[htable] (same limits as rss_hash_device_reta). */
+int rss_hash6_device_reta(const rss_key6* key, const rss_tuple6* d_tuples, size_t n,
+                          uint32_t htable, const uint32_t* reta, uint32_t nqueues,
+                          uint32_t* d_hash, void* d_queue, uint64_t* d_counts, uint32_t flags,
+                          void* stream);
+int rss_hash6_host_reta(rss_ctx* ctx, const rss_key6* key, const rss_tuple6* h_tuples, size_t n,
+                        uint32_t htable, const uint32_t* reta, uint32_t nqueues, uint32_t* h_hash,
+                        uint32_t* h_queue, uint64_t* h_counts, uint32_t flags);
+
 /*
  * Multi-GPU host batch (replaces the same rows of Simulator.calc_hash /
  * calc_queue_number / write_statistics as rss_hash_host, simulator.py:74-113).  The n

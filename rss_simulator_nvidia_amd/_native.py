@@ -35,7 +35,7 @@ EXPORTED_SYMBOLS = (
     "rss_key6_prepare", "rss_key6_select_fields", "rss_hash6_device", "rss_hash6_host",
     "rss_pcap_parse", "rss_hash_device_reta", "rss_hash_host_reta", "rss_csv_hash_text",
     "rss_csv_hash_file", "rss_host_alloc", "rss_host_free", "rss_hash_host_multi",
-    "rss_pcap_parse6",
+    "rss_pcap_parse6", "rss_hash6_device_reta", "rss_hash6_host_reta",
 )
 FIELD_SRC_IP, FIELD_DST_IP, FIELD_SRC_PORT, FIELD_DST_PORT = 1, 2, 4, 8
 FIELDS_IP, FIELDS_ALL = 3, 15
@@ -116,6 +116,10 @@ def _bind(lib):
                              ctypes.c_int),
         "rss_hash6_host": ([vp, ctypes.POINTER(RssKey6), vp, sz, u32, u32, vp, vp, vp, u32],
                            ctypes.c_int),
+        "rss_hash6_device_reta": ([ctypes.POINTER(RssKey6), vp, sz, u32, vp, u32, vp, vp, vp, u32,
+                                   vp], ctypes.c_int),
+        "rss_hash6_host_reta": ([vp, ctypes.POINTER(RssKey6), vp, sz, u32, vp, u32, vp, vp, vp,
+                                 u32], ctypes.c_int),
         "rss_key_search_host": ([vp, vp, sz, vp, sz, u32, u32, vp], ctypes.c_int),
         "rss_csv_format": ([vp, vp, vp, sz, vp, u32, ctypes.POINTER(RssCsvLayout), vp, sz,
                             ctypes.POINTER(sz), ctypes.c_int], ctypes.c_int),
@@ -310,8 +314,9 @@ class HostContext:
 
 
     def hash6(self, key6, tuples6, htable, nqueues, want_hash=True, want_queue=True,
-              want_counts=True):
-        """IPv6 batch (``TUPLE6_DTYPE`` or uint32 (n, 9)) -> (hash, queue, counts)."""
+              want_counts=True, reta=None):
+        """IPv6 batch (``TUPLE6_DTYPE`` or uint32 (n, 9)) -> (hash, queue, counts);
+        ``reta`` as for :meth:`hash`."""
         arr = np.ascontiguousarray(tuples6)
         if arr.dtype != TUPLE6_DTYPE:
             arr = np.ascontiguousarray(arr, dtype=np.uint32).reshape(-1, 9)
@@ -319,8 +324,14 @@ class HostContext:
         h = np.empty(n, dtype=np.uint32) if want_hash else None
         q = np.empty(n, dtype=np.uint32) if want_queue else None
         c = np.zeros(nqueues, dtype=np.uint64) if want_counts else None
-        _check(self._lib.rss_hash6_host(self._ctx, ctypes.byref(key6), ptr(arr), n, htable,
-                                        nqueues, ptr(h), ptr(q), ptr(c), 0), "rss_hash6_host")
+        if reta is None:
+            _check(self._lib.rss_hash6_host(self._ctx, ctypes.byref(key6), ptr(arr), n, htable,
+                                            nqueues, ptr(h), ptr(q), ptr(c), 0), "rss_hash6_host")
+        else:
+            table = _reta_table(reta, htable)
+            _check(self._lib.rss_hash6_host_reta(self._ctx, ctypes.byref(key6), ptr(arr), n,
+                                                 htable, ptr(table), nqueues, ptr(h), ptr(q),
+                                                 ptr(c), 0), "rss_hash6_host_reta")
         return h, q, c
 
     def csv_hash_text(self, key, data, htable, nqueues, reta=None, counts_only=False):
@@ -451,6 +462,15 @@ def hash6_device(key6, tuples_ptr, n, htable, nqueues, hash_ptr=None, queue_ptr=
     """Stream-ordered ``rss_hash6_device`` on raw device pointers (ints)."""
     _check(load().rss_hash6_device(ctypes.byref(key6), tuples_ptr, n, htable, nqueues, hash_ptr,
                                    queue_ptr, counts_ptr, flags, stream), "rss_hash6_device")
+
+
+def hash6_device_reta(key6, tuples_ptr, n, htable, reta, nqueues, hash_ptr=None, queue_ptr=None,
+                      counts_ptr=None, flags=0, stream=None):
+    """Stream-ordered ``rss_hash6_device_reta`` (``reta``: host sequence of htable queue ids)."""
+    table = _reta_table(reta, htable)
+    _check(load().rss_hash6_device_reta(ctypes.byref(key6), tuples_ptr, n, htable,
+                                        table.ctypes.data, nqueues, hash_ptr, queue_ptr,
+                                        counts_ptr, flags, stream), "rss_hash6_device_reta")
 
 
 def key_search_device(windows_ptr, nkeys, tuples_ptr, n, htable, nqueues, counts_ptr,

@@ -697,6 +697,7 @@ __host__ __device__ constexpr uint32_t slice_table6(int k, int j) {
 }
 constexpr int slices6(int k) { return byte_word6(k) ? 4 : 3; }
 static_assert(kLut6Bytes + 32 * 4 * 24 <= kLdsBytes, "IPv6 LUT + private bins for 24 queues fit");
+static_assert(kBinBytesMax6 >= 4 * kRetaMax + 4096, "IPv6 bins keep >= 4 KiB beside a full RETA");
 
 struct LaunchParams6 {
     uint32_t window[RSS_INPUT6_BITS];
@@ -709,6 +710,7 @@ struct LaunchParams6 {
     uint32_t h_mask, H, Q, q_mask, q_m32;
     uint32_t qwidth;  // QueueWidth of queue_out (grid-uniform runtime switch)
     uint64_t q_m64;
+    uint16_t reta[kRetaMax];  // QM_TABLE: queue of bucket b, as LaunchParams::reta
 };
 
 // entry v of slice (k, j) = XOR of the windows of the set bits of v; word k bit i is
@@ -816,6 +818,9 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz6_kernel(const LaunchParam
     const uint32_t nbins =
         kHist == HIST_PRIVATE ? p.Q * kBinCols : (kHist == HIST_SHARED ? p.Q : 0u);
     for (uint32_t e = tid; e < nbins; e += kBlock) bins[e] = 0;
+    uint32_t* reta_lds = bins + nbins;  // QM_TABLE: H entries after the bins
+    if constexpr (kQMode == QM_TABLE)
+        for (uint32_t e = tid; e < p6.H; e += kBlock) reta_lds[e] = p6.reta[e];
     __syncthreads();
     const uint32_t col = tid & (kBinCols - 1);
     const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
@@ -842,7 +847,7 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz6_kernel(const LaunchParam
 #pragma unroll
                 for (int k = 0; k < kWords6; ++k) w[k] = v[kWords6 * t + k];
                 h[t] = toeplitz_hash6(lut, w, hi1, hi2);
-                q[t] = queue_of<kQMode>(bucket_of<kHPow2>(h[t], p), p);
+                q[t] = queue_lookup<kQMode>(bucket_of<kHPow2>(h[t], p), p, reta_lds);
             }
             if (p6.hash_out) {
                 uint32_t* o = p6.hash_out + 4 * g;
@@ -869,7 +874,7 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz6_kernel(const LaunchParam
 #pragma unroll
         for (int k = 0; k < kWords6; ++k) w[k] = t[k];
         const uint32_t h = toeplitz_hash6(lut, w, hi1, hi2);
-        const uint32_t q = queue_of<kQMode>(bucket_of<kHPow2>(h, p), p);
+        const uint32_t q = queue_lookup<kQMode>(bucket_of<kHPow2>(h, p), p, reta_lds);
         if (p6.hash_out) stream_store(p6.hash_out + i, h);
         if (p6.queue_out) {
             if (p6.qwidth == QW_U8) {
@@ -1125,6 +1130,20 @@ int launch_search(const uint32_t* d_windows, size_t nkeys, const rss_tuple4* d_t
     return RSS_OK;
 }
 
+// An indirection table travels in the kernel arguments as u16[htable <= kRetaMax].
+int check_reta(const uint32_t* reta, uint32_t htable, uint32_t nqueues, const char* who) {
+    if (htable > kRetaMax)
+        return set_error(RSS_EINVAL, "%s: htable %u exceeds %u entries", who, htable, kRetaMax);
+    for (uint32_t b = 0; b < htable; ++b) {
+        if (reta[b] >= nqueues)
+            return set_error(RSS_EINVAL, "%s: reta[%u] = %u >= nqueues %u", who, b, reta[b],
+                             nqueues);
+        if (reta[b] > 0xFFFFu)
+            return set_error(RSS_EINVAL, "%s: reta[%u] = %u exceeds 65535", who, b, reta[b]);
+    }
+    return RSS_OK;
+}
+
 int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32_t htable,
                 uint32_t nqueues, uint32_t* d_hash, void* d_queue, uint64_t* d_counts,
                 uint32_t flags, hipStream_t stream, const uint32_t* reta = nullptr) {
@@ -1136,17 +1155,8 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
                          htable, nqueues);
     if (n && !d_tuples) return set_error(RSS_EINVAL, "rss_hash_device: tuples is NULL");
     if (reta) {
-        if (htable > kRetaMax)
-            return set_error(RSS_EINVAL, "rss_hash_device_reta: htable %u exceeds %u entries",
-                             htable, kRetaMax);
-        for (uint32_t b = 0; b < htable; ++b) {
-            if (reta[b] >= nqueues)
-                return set_error(RSS_EINVAL, "rss_hash_device_reta: reta[%u] = %u >= nqueues %u",
-                                 b, reta[b], nqueues);
-            if (reta[b] > 0xFFFFu)  // the table travels in the kernel arguments as u16
-                return set_error(RSS_EINVAL, "rss_hash_device_reta: reta[%u] = %u exceeds 65535",
-                                 b, reta[b]);
-        }
+        const int rc = check_reta(reta, htable, nqueues, "rss_hash_device_reta");
+        if (rc) return rc;
     }
     int qwidth = QW_U32;
     if (flags & RSS_FLAG_QUEUE_U8) {
@@ -1224,19 +1234,24 @@ KernelFn6 pick6(int qmode, int hist, bool vec4) {
     switch (qmode) {
         case QM_MASK: return pick6_hist<kHPow2, QM_MASK>(hist, vec4);
         case QM_FAST16: return pick6_hist<kHPow2, QM_FAST16>(hist, vec4);
+        case QM_TABLE: return pick6_hist<kHPow2, QM_TABLE>(hist, vec4);
         default: return pick6_hist<kHPow2, QM_FAST32>(hist, vec4);
     }
 }
 
 int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint32_t htable,
                  uint32_t nqueues, uint32_t* d_hash, void* d_queue, uint64_t* d_counts,
-                 uint32_t flags, hipStream_t stream) {
+                 uint32_t flags, hipStream_t stream, const uint32_t* reta = nullptr) {
     if (!key || key->len < RSS_KEY_MIN_BYTES)
         return set_error(RSS_EINVAL, "rss_hash6_device: key NULL or not prepared");
     if (htable < 1 || nqueues < 1)
         return set_error(RSS_EINVAL, "rss_hash6_device: htable (%u) and nqueues (%u) must be >= 1",
                          htable, nqueues);
     if (n && !d_tuples) return set_error(RSS_EINVAL, "rss_hash6_device: tuples is NULL");
+    if (reta) {
+        const int rc = check_reta(reta, htable, nqueues, "rss_hash6_device_reta");
+        if (rc) return rc;
+    }
     uint32_t qwidth = QW_U32;
     if (flags & RSS_FLAG_QUEUE_U8) {
         if (nqueues > 256)
@@ -1254,12 +1269,11 @@ int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint
     memset(&tmp, 0, sizeof tmp);
     int qmode, hist;
     uint32_t bin_bytes;
+    const uint32_t reta_bytes = reta ? htable * 4 : 0;  // the table in LDS after the bins
+    const uint32_t budget = kBinBytesMax6 - reta_bytes;   // bins share the LDS with the LUT
     const bool h_pow2 = setup_modes(&tmp, htable, nqueues, d_counts != nullptr, &qmode, &hist,
-                                    &bin_bytes);
-    if (bin_bytes > kBinBytesMax6) {  // bins share the LDS with the 148 KiB LUT
-        hist = (uint64_t)nqueues * 4 <= kBinBytesMax6 ? HIST_SHARED : HIST_GLOBAL;
-        bin_bytes = hist == HIST_SHARED ? nqueues * 4 : 0;
-    }
+                                    &bin_bytes, budget);
+    if (reta) qmode = QM_TABLE;
     LaunchParams6 p;
     memset(&p, 0, sizeof p);
     memcpy(p.window, key->window, sizeof p.window);
@@ -1276,6 +1290,8 @@ int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint
     p.q_m32 = tmp.q_m32;
     p.q_m64 = tmp.q_m64;
     p.qwidth = qwidth;
+    if (reta)
+        for (uint32_t b = 0; b < htable; ++b) p.reta[b] = (uint16_t)reta[b];
     const uintptr_t qalign = qwidth == QW_U8 ? 4 : (qwidth == QW_U16 ? 8 : 16);
     const bool vec4 = aligned16(d_tuples) && (!d_hash || aligned16(d_hash)) &&
                       (!d_queue || ((uintptr_t)d_queue % qalign) == 0);
@@ -1287,7 +1303,7 @@ int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint
     const uint64_t want = (n + per_lane * kBlock - 1) / (per_lane * kBlock);
     const uint64_t cap = (uint64_t)info.cu_count * kBlocksPerCU6;
     const unsigned grid = (unsigned)(want < cap ? want : cap);
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), bin_bytes, stream, p);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), bin_bytes + reta_bytes, stream, p);
     RSS_HIP_CHECK(hipGetLastError());
     return RSS_OK;
 }
@@ -1382,9 +1398,37 @@ int rss_hash6_device(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, 
                         static_cast<hipStream_t>(stream));
 }
 
+int rss_hash6_device_reta(const rss_key6* key, const rss_tuple6* d_tuples, size_t n,
+                          uint32_t htable, const uint32_t* reta, uint32_t nqueues,
+                          uint32_t* d_hash, void* d_queue, uint64_t* d_counts, uint32_t flags,
+                          void* stream) {
+    if (!reta) return set_error(RSS_EINVAL, "rss_hash6_device_reta: reta is NULL");
+    return launch_hash6(key, d_tuples, n, htable, nqueues, d_hash, d_queue, d_counts, flags,
+                        static_cast<hipStream_t>(stream), reta);
+}
+
+static int hash6_host_impl(rss_ctx* ctx, const rss_key6* key, const rss_tuple6* h_tuples, size_t n,
+                           uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
+                           uint64_t* h_counts, uint32_t flags, const uint32_t* reta);
+
 int rss_hash6_host(rss_ctx* ctx, const rss_key6* key, const rss_tuple6* h_tuples, size_t n,
                    uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
                    uint64_t* h_counts, uint32_t flags) {
+    return hash6_host_impl(ctx, key, h_tuples, n, htable, nqueues, h_hash, h_queue, h_counts,
+                           flags, nullptr);
+}
+
+int rss_hash6_host_reta(rss_ctx* ctx, const rss_key6* key, const rss_tuple6* h_tuples, size_t n,
+                        uint32_t htable, const uint32_t* reta, uint32_t nqueues, uint32_t* h_hash,
+                        uint32_t* h_queue, uint64_t* h_counts, uint32_t flags) {
+    if (!reta) return set_error(RSS_EINVAL, "rss_hash6_host_reta: reta is NULL");
+    return hash6_host_impl(ctx, key, h_tuples, n, htable, nqueues, h_hash, h_queue, h_counts,
+                           flags, reta);
+}
+
+static int hash6_host_impl(rss_ctx* ctx, const rss_key6* key, const rss_tuple6* h_tuples, size_t n,
+                           uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
+                           uint64_t* h_counts, uint32_t flags, const uint32_t* reta) {
     if (!ctx) return set_error(RSS_EINVAL, "rss_hash6_host: ctx is NULL");
     if (n && !h_tuples) return set_error(RSS_EINVAL, "rss_hash6_host: tuples is NULL");
     RSS_HIP_CHECK(hipSetDevice(ctx->device));
@@ -1411,7 +1455,7 @@ int rss_hash6_host(rss_ctx* ctx, const rss_key6* key, const rss_tuple6* h_tuples
                          hipGetErrorString(e));
     }
     int rc = launch_hash6(key, d_t, n, htable, nqueues, d_h, d_q, d_c,
-                          0u, s);  // device counts start at 0; accumulation happens on the host
+                          0u, s, reta);  // device counts start at 0; accumulation on the host
     if (rc == RSS_OK) {
         if (d_h) e = hipMemcpyAsync(h_hash, d_h, n * 4, hipMemcpyDeviceToHost, s);
         if (e == hipSuccess && d_q) e = hipMemcpyAsync(h_queue, d_q, n * 4, hipMemcpyDeviceToHost, s);

@@ -59,10 +59,8 @@ def run_pcap(args, table):
                                                           "IPv6" if args.ipv6 else "IPv4"))
     ctx = _native.default_context()
     if args.ipv6:
-        if table is not None:
-            raise ValueError("indirection tables are supported for IPv4 input only")
         key6 = _native.prepare_key6(args.key, args.hash_fields)
-        h, q, c = ctx.hash6(key6, tuples, args.htable_size, args.num_queues)
+        h, q, c = ctx.hash6(key6, tuples, args.htable_size, args.num_queues, reta=table)
     else:
         key = _native.prepare_key(args.key, args.hash_fields)
         h, q, c = ctx.hash(key, tuples, args.htable_size, args.num_queues, reta=table)

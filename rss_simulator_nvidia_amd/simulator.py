@@ -46,8 +46,6 @@ class Simulator(object):
         self.__toeplitz = Toeplitz(hash_key, hash_fields or "sdfn")
         self.__ipv6 = ipv6
         self.__reta = reta
-        if reta is not None and ipv6:
-            raise ValueError("indirection tables are supported for IPv4 input only")
         self.__hash_table_size = hash_table_size
         self.__queue_num = queue_number
         self.__queues = None
@@ -92,7 +90,7 @@ class Simulator(object):
                              "hash_result")
         if self.__ipv6:
             h, q, c = self.__toeplitz.compute_queues6(pack_frame6(df), self.__hash_table_size,
-                                                      self.__queue_num)
+                                                      self.__queue_num, self.__reta)
         else:
             h, q, c = self.__toeplitz.compute_queues(pack_frame(df), self.__hash_table_size,
                                                      self.__queue_num, self.__reta)

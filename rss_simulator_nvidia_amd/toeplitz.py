@@ -76,7 +76,7 @@ class Toeplitz(object):
         return _native.default_context().hash(self.prepared_key, np.asarray(tuples),
                                               hash_table_size, queue_number, reta=reta)
 
-    def compute_queues6(self, tuples6, hash_table_size, queue_number):
+    def compute_queues6(self, tuples6, hash_table_size, queue_number, reta=None):
         """IPv6 counterpart of :meth:`compute_queues` (``rss_tuple6`` rows)."""
         return _native.default_context().hash6(self.prepared_key6, np.asarray(tuples6),
-                                               hash_table_size, queue_number)
+                                               hash_table_size, queue_number, reta=reta)

@@ -46,11 +46,15 @@ class OracleContext:
         return np.stack([self.hash(k, tuples, htable, nqueues)[2] for k in keys])
 
     def hash6(self, key6, tuples6, htable, nqueues, want_hash=True, want_queue=True,
-              want_counts=True):
+              want_counts=True, reta=None):
         self.calls += 1
         words = np.ascontiguousarray(tuples6).view(np.uint32).reshape(-1, 9)
         h = o.hash_words_np(np.ctypeslib.as_array(key6.window), words)
-        q, c = o.queue_and_counts(h, htable, nqueues)
+        if reta is None:
+            q, c = o.queue_and_counts(h, htable, nqueues)
+        else:
+            q = np.asarray(reta, dtype=np.uint32)[h % htable]
+            c = np.bincount(q, minlength=nqueues).astype(np.uint64)
         return h, q, c
 
 

@@ -121,10 +121,11 @@ def test_reta_entries_above_u16_are_refused(native):
                                 70000, None, None, counts.data_ptr(), 0, None)
 
 
-@pytest.mark.parametrize("seed", range(16))
+@pytest.mark.parametrize("seed", range(24))
 def test_random_ipv6_config_matches_oracle(native, oracle_lib, seed):
     """IPv6 kernel (36-byte input) under random n / H / Q / field masks / queue widths /
-    alignment; the numpy closed form over the oracle's 288 windows is the reference."""
+    alignment / indirection tables; the numpy closed form over the oracle's 288 windows
+    is the reference."""
     from oracle import oracle as o
     rng = np.random.default_rng(9000 + seed)
     n = int(rng.choice([0, 1, 5, 4097, int(rng.integers(1, 150000))]))
@@ -147,8 +148,14 @@ def test_random_ipv6_config_matches_oracle(native, oracle_lib, seed):
     hbuf = torch.full((n + 16,), -1, dtype=torch.int32, device=dev)
     qbuf = torch.full((n * qbytes + 16,), 0x5A, dtype=torch.uint8, device=dev)
     counts = torch.full((Q,), 3, dtype=torch.int64, device=dev)
-    native.hash6_device(k6, raw.data_ptr() + 4 * off, n, H, Q, hbuf.data_ptr(), qbuf.data_ptr(),
-                        counts.data_ptr(), qflag, stream)
+    use_reta = H <= 1024 and Q <= 65536 and rng.random() < 0.4
+    reta = rng.integers(0, Q, H).astype(np.uint32) if use_reta else None
+    if use_reta:
+        native.hash6_device_reta(k6, raw.data_ptr() + 4 * off, n, H, reta, Q, hbuf.data_ptr(),
+                                 qbuf.data_ptr(), counts.data_ptr(), qflag, stream)
+    else:
+        native.hash6_device(k6, raw.data_ptr() + 4 * off, n, H, Q, hbuf.data_ptr(),
+                            qbuf.data_ptr(), counts.data_ptr(), qflag, stream)
     torch.cuda.synchronize()
     if fields == "sdfn":
         want = o.hash_words_np(full, words)
@@ -164,6 +171,9 @@ def test_random_ipv6_config_matches_oracle(native, oracle_lib, seed):
     np.testing.assert_array_equal(hbuf.cpu().numpy().view(np.uint32)[:n], want)
     assert (hbuf.cpu().numpy()[n:] == -1).all()
     qo, co = o.queue_and_counts(want, H, Q)
+    if use_reta:
+        qo = reta[want % H]
+        co = np.bincount(qo, minlength=Q).astype(np.uint64)
     qdt = {"u8": np.uint8, "u16": np.uint16, "u32": np.uint32}[width]
     got_q = qbuf.cpu().numpy()
     np.testing.assert_array_equal(got_q[:n * qbytes].view(qdt), qo.astype(qdt))

@@ -89,3 +89,75 @@ def test_table_validation(native, example_key):
         native.hash_device_reta(key, 0, 0, 4, [0, 1, 4, 2], 4)
     with pytest.raises(DeviceError, match="exceeds"):
         native.hash_device_reta(key, 0, 0, 2048, [0] * 2048, 1)
+
+
+@pytest.mark.parametrize("H,Q,flag_name", [(128, 24, "FLAG_QUEUE_U8"), (1024, 5000, None),
+                                           (100, 7, "FLAG_QUEUE_U16"), (1024, 300, None)])
+def test_ipv6_tables_vs_oracle(native, ctx, oracle_lib, H, Q, flag_name):
+    """IPv6 kernel with an indirection table (rss_hash6_device_reta / _host_reta): queue =
+    reta[hash % H] on the 36-byte hashes, all histogram modes the bin budget reaches
+    (the table takes 4 * H bytes of the IPv6 kernel's 12 KiB bin region)."""
+    from oracle import oracle as o
+    rng = np.random.default_rng(H * 3 + Q)
+    key = [int(x) for x in rng.integers(0, 256, 40)]
+    n = 100003
+    words = rng.integers(0, 2**32, (n, 9), dtype=np.uint64).astype(np.uint32)
+    want = o.hash_words_np(oracle_lib.windows_n(key, 288), words)
+    table = rng.integers(0, Q, H).astype(np.uint32)
+    wq = table[want % H]
+    wc = np.bincount(wq, minlength=Q).astype(np.uint64)
+    k6 = native.prepare_key6(key)
+    h, q, c = ctx.hash6(k6, words, H, Q, reta=table)  # host path
+    np.testing.assert_array_equal(h, want)
+    np.testing.assert_array_equal(q, wq)
+    np.testing.assert_array_equal(c, wc)
+    dev = torch.device("cuda:0")
+    s = torch.cuda.current_stream(dev).cuda_stream
+    raw = torch.from_numpy(words.view(np.int32).reshape(-1)).to(dev)
+    dtype = {"FLAG_QUEUE_U8": np.uint8, "FLAG_QUEUE_U16": np.uint16, None: np.uint32}[flag_name]
+    item = np.dtype(dtype).itemsize
+    buf = torch.full((n * item + 16,), 0xAB, dtype=torch.uint8, device=dev)
+    counts = torch.empty(Q, dtype=torch.int64, device=dev)
+    flags = getattr(native, flag_name) if flag_name else 0
+    native.hash6_device_reta(k6, raw.data_ptr(), n, H, table, Q, None, buf.data_ptr(),
+                             counts.data_ptr(), flags, s)
+    torch.cuda.synchronize()
+    got = buf.cpu().numpy()
+    np.testing.assert_array_equal(got[:n * item].view(dtype), wq.astype(dtype))
+    assert (got[n * item:] == 0xAB).all()
+    np.testing.assert_array_equal(counts.cpu().numpy().view(np.uint64), wc)
+
+
+def test_ipv6_cli_reta_weights(tmp_path, golden_dir, oracle_lib, capsys):
+    """--ipv6 --reta-weights through the pandas path of Simulator on the GPU."""
+    from cli_cases import run_main
+    from oracle import oracle as o
+    rng = np.random.default_rng(4)
+    n = 300
+    addrs = ["2001:db8::%x" % int(x) for x in rng.integers(1, 1 << 16, 2 * n)]
+    ports = rng.integers(0, 65536, (n, 2))
+    path = tmp_path / "ips6.csv"
+    path.write_text("src_ip,dst_ip,src_port,dst_port\n" + "".join(
+        "%s,%s,%d,%d\n" % (addrs[2 * i], addrs[2 * i + 1], ports[i, 0], ports[i, 1])
+        for i in range(n)))
+    out = tmp_path / "out.csv"
+    key_file = str(tmp_path / "k.txt")
+    key = [int(x) for x in rng.integers(0, 256, 40)]
+    open(key_file, "w").write(":".join("%02x" % b for b in key))
+    status, _, _, exc = run_main(["--key-file", key_file, "--ips-file", str(path), "--ipv6",
+                                  "--htable-size", "16", "--num-queues", "4", "--csv", str(out),
+                                  "--reta-weights", "1,0,2,1"], capsys)
+    assert status == 0, exc
+    import ipaddress
+    words = np.array([[int.from_bytes(ipaddress.IPv6Address(addrs[2 * i]).packed[j:j + 4], "big")
+                       for j in range(0, 16, 4)] +
+                      [int.from_bytes(ipaddress.IPv6Address(addrs[2 * i + 1]).packed[j:j + 4], "big")
+                       for j in range(0, 16, 4)] +
+                      [int(ports[i, 0]) << 16 | int(ports[i, 1])] for i in range(n)], dtype=np.uint32)
+    want = o.hash_words_np(oracle_lib.windows_n(key, 288), words)
+    table = np.array(rt.weights(16, [1, 0, 2, 1]), dtype=np.uint32)
+    lines = out.read_text().splitlines()
+    body = lines[lines.index("src_ip,dst_ip,src_port,dst_port,hash_result,queue_number") + 1:]
+    assert [int(x.split(",")[4]) for x in body] == want.tolist()
+    assert [int(x.split(",")[5]) for x in body] == table[want % 16].tolist()
+    assert 1 not in {int(x.split(",")[5]) for x in body}  # weight 0: never selected
