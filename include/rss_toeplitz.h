@@ -248,6 +248,23 @@ int rss_csv_format(const rss_tuple4* tuples, const uint32_t* hash, const uint32_
                    int threads);
 
 /*
+ * IPv6 rows through the same fast path (the --ipv6 input of SURVEY.md §8f row 4;
+ * pandas path: Simulator with ipv6, ingest.pack_frame6).  Canonical IPv6 fields are
+ * RFC 4291 text without an embedded IPv4 part or zone id (1-4 hex digits per group,
+ * at most one "::"); ports and the header as above.  rss_csv_parse6 fills tuples[n]
+ * and spans[2n] (byte offsets of each row's text, line end excluded); pandas keeps
+ * the address strings verbatim, so rss_csv_format6 writes each row as its input text
+ * + ",hash,queue" after the same counts prefix.  Same return codes as the IPv4 pair.
+ */
+int rss_csv_parse6(const char* data, size_t len, rss_tuple6* tuples, uint64_t* spans, size_t cap,
+                   size_t* n_rows, rss_csv_layout* layout, int threads);
+size_t rss_csv_format6_bound(const uint64_t* spans, size_t n, uint32_t nqueues);
+int rss_csv_format6(const char* data, const uint64_t* spans, const uint32_t* hash,
+                    const uint32_t* queue, size_t n, const uint64_t* counts, uint32_t nqueues,
+                    const rss_csv_layout* layout, char* out, size_t cap, size_t* out_len,
+                    int threads);
+
+/*
  * ---- CSV on the device ----
  * The whole `--csv` job for a CANONICAL file image (the rules above): the body goes
  * to the device once, newlines are indexed, rows parsed, hashed (rss_hash_device or,

@@ -35,7 +35,8 @@ EXPORTED_SYMBOLS = (
     "rss_key6_prepare", "rss_key6_select_fields", "rss_hash6_device", "rss_hash6_host",
     "rss_pcap_parse", "rss_hash_device_reta", "rss_hash_host_reta", "rss_csv_hash_text",
     "rss_csv_hash_file", "rss_host_alloc", "rss_host_free", "rss_hash_host_multi",
-    "rss_pcap_parse6", "rss_hash6_device_reta", "rss_hash6_host_reta",
+    "rss_pcap_parse6", "rss_hash6_device_reta", "rss_hash6_host_reta", "rss_csv_parse6",
+    "rss_csv_format6_bound", "rss_csv_format6",
 )
 FIELD_SRC_IP, FIELD_DST_IP, FIELD_SRC_PORT, FIELD_DST_PORT = 1, 2, 4, 8
 FIELDS_IP, FIELDS_ALL = 3, 15
@@ -123,6 +124,11 @@ def _bind(lib):
         "rss_key_search_host": ([vp, vp, sz, vp, sz, u32, u32, vp], ctypes.c_int),
         "rss_csv_format": ([vp, vp, vp, sz, vp, u32, ctypes.POINTER(RssCsvLayout), vp, sz,
                             ctypes.POINTER(sz), ctypes.c_int], ctypes.c_int),
+        "rss_csv_parse6": ([vp, sz, vp, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(RssCsvLayout),
+                            ctypes.c_int], ctypes.c_int),
+        "rss_csv_format6_bound": ([vp, sz, u32], sz),
+        "rss_csv_format6": ([vp, vp, vp, vp, sz, vp, u32, ctypes.POINTER(RssCsvLayout), vp, sz,
+                             ctypes.POINTER(sz), ctypes.c_int], ctypes.c_int),
         "rss_host_alloc": ([sz, ctypes.POINTER(vp)], ctypes.c_int),
         "rss_host_free": ([vp], None),
         "rss_hash_host_multi": ([ctypes.POINTER(vp), ctypes.c_int, key_p, vp, sz, u32, vp, u32,
@@ -521,6 +527,44 @@ def csv_format(tuples, hashes, queues, counts, layout, threads=0):
     _check(lib.rss_csv_format(tuples.ctypes.data, hashes.ctypes.data, queues.ctypes.data, n,
                               counts.ctypes.data, nq, ctypes.byref(layout), out.ctypes.data, cap,
                               ctypes.byref(out_len), threads), "rss_csv_format")
+    return out[:out_len.value]
+
+
+def csv_parse6(data, threads=0):
+    """Parse a canonical IPv6 4-tuple CSV image: ``(tuples6, spans, layout)`` with
+    ``spans`` uint64 (n, 2) = byte range of each row's text, or ``None`` when the file
+    is not canonical (the pandas path then runs)."""
+    buf = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+    lib = load()
+    cap = len(buf) // 9 + 1  # a canonical row takes >= 9 bytes ("::,::,0,0\n")
+    tuples = np.empty(cap, dtype=TUPLE6_DTYPE)
+    spans = np.empty((cap, 2), dtype=np.uint64)
+    n = ctypes.c_size_t(0)
+    layout = RssCsvLayout()
+    rc = lib.rss_csv_parse6(buf.ctypes.data, len(buf), tuples.ctypes.data, spans.ctypes.data, cap,
+                            ctypes.byref(n), ctypes.byref(layout), threads)
+    if rc == ENOTSUP:
+        return None
+    _check(rc, "rss_csv_parse6")
+    return tuples[:n.value], spans[:n.value], layout
+
+
+def csv_format6(data, spans, hashes, queues, counts, layout, threads=0):
+    """Statistics CSV bytes for IPv6 rows: each row's input text + hash + queue."""
+    lib = load()
+    buf = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+    spans = np.ascontiguousarray(spans, dtype=np.uint64)
+    n, nq = len(spans), len(counts)
+    hashes = np.ascontiguousarray(hashes, dtype=np.uint32)
+    queues = np.ascontiguousarray(queues, dtype=np.uint32)
+    counts = np.ascontiguousarray(counts, dtype=np.uint64)
+    cap = lib.rss_csv_format6_bound(spans.ctypes.data, n, nq)
+    out = np.empty(cap, dtype=np.uint8)
+    out_len = ctypes.c_size_t(0)
+    _check(lib.rss_csv_format6(buf.ctypes.data, spans.ctypes.data, hashes.ctypes.data,
+                               queues.ctypes.data, n, counts.ctypes.data, nq, ctypes.byref(layout),
+                               out.ctypes.data, cap, ctypes.byref(out_len), threads),
+           "rss_csv_format6")
     return out[:out_len.value]
 
 

@@ -188,6 +188,83 @@ inline char* put_ip(char* p, uint32_t ip) {
 
 constexpr size_t kMaxRowBytes = 15 + 1 + 15 + 1 + 5 + 1 + 5 + 1 + 10 + 1 + 10 + 1;
 
+// ---- IPv6 rows (SURVEY.md §8f row 4 input through the row-1 fast path) ----
+// A canonical IPv6 address is RFC 4291 text without an embedded IPv4 part or zone:
+// 1-4 hex digits per group, ':' between groups, at most one '::' standing for one or
+// more zero groups, 8 groups without it and at most 7 with it.  ipaddress.IPv6Address
+// (the pandas path's parser, ingest.py) reads every such text to the same 128 bits;
+// pandas keeps it as a str and writes it back verbatim, so the output row is the
+// input line's text plus the two new columns.
+inline int hex_value(char c) {
+    if ((unsigned)(c - '0') <= 9) return c - '0';
+    const unsigned l = (unsigned)((c | 0x20) - 'a');
+    return l <= 5 ? (int)l + 10 : -1;
+}
+
+inline bool field_end(const char* p, const char* e) {
+    return p >= e || *p == ',' || *p == '\r' || *p == '\n';
+}
+
+inline bool scan_ip6(const char*& p, const char* e, uint32_t out[4]) {
+    uint32_t g[8];
+    int ng = 0, gap = -1;
+    if (p + 1 < e && p[0] == ':' && p[1] == ':') {
+        gap = 0;
+        p += 2;
+    }
+    while (!(gap >= 0 && field_end(p, e))) {
+        uint32_t v = 0;
+        int digits = 0;
+        for (int h; digits < 4 && p < e && (h = hex_value(*p)) >= 0; ++digits, ++p) v = v << 4 | (uint32_t)h;
+        if (digits == 0 || (p < e && hex_value(*p) >= 0) || ng == 8) return false;
+        g[ng++] = v;
+        if (field_end(p, e)) break;
+        if (*p != ':') return false;
+        if (p + 1 < e && p[1] == ':') {
+            if (gap >= 0) return false;
+            gap = ng;
+            p += 2;
+        } else {
+            ++p;  // a single ':' must be followed by another group
+        }
+    }
+    if (gap < 0 ? ng != 8 : ng > 7) return false;
+    uint32_t full[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int tail = gap < 0 ? 0 : ng - gap;
+    for (int k = 0; k < ng; ++k) full[(gap < 0 || k < gap) ? k : 8 - tail + (k - gap)] = g[k];
+    for (int k = 0; k < 4; ++k) out[k] = full[2 * k] << 16 | full[2 * k + 1];
+    return true;
+}
+
+// One IPv6 data row at p: tuple + the byte span of its text (without the line end).
+inline bool scan_row6(const char*& p, const char* e, const uint8_t field_column[4], rss_tuple6& t,
+                      const char*& text_end) {
+    uint32_t addr[2][4], port[2];
+    for (int f = 0; f < 4; ++f) {
+        const int col = field_column[f];
+        if (!(col < 2 ? scan_ip6(p, e, addr[col]) : scan_uint<5, 65535>(p, e, port[col - 2])))
+            return false;
+        if (f < 3) {
+            if (p >= e || *p != ',') return false;
+            ++p;
+        }
+    }
+    text_end = p;
+    if (p < e && *p == '\r') ++p;
+    if (p < e) {
+        if (*p != '\n') return false;
+        ++p;
+    }
+    for (int k = 0; k < 4; ++k) {
+        t.w[k] = addr[0][k];
+        t.w[4 + k] = addr[1][k];
+    }
+    t.w[8] = port[0] << 16 | port[1];
+    return true;
+}
+
+constexpr size_t kMaxRow6Extra = 1 + 10 + 1 + 10 + 1;  // ",hash,queue\n"
+
 }  // namespace
 
 bool rss_csv_header(const char* data, size_t len, rss_csv_layout* layout, size_t* body_offset) {
@@ -282,6 +359,118 @@ int rss_csv_parse(const char* data, size_t len, rss_tuple4* tuples, size_t cap, 
                 memcpy(tuples + off[k], local[k].data(), local[k].size() * sizeof(rss_tuple4));
         });
     for (auto& t : pool) t.join();
+    return RSS_OK;
+}
+
+int rss_csv_parse6(const char* data, size_t len, rss_tuple6* tuples, uint64_t* spans, size_t cap,
+                   size_t* n_rows, rss_csv_layout* layout, int threads) {
+    if (!data || !n_rows || !layout) return RSS_EINVAL;
+    *n_rows = 0;
+    const char* end = data + len;
+    size_t body_offset;
+    if (!rss_csv_header(data, len, layout, &body_offset)) return RSS_ENOTSUP;
+    const char* body = data + body_offset;
+    const int nt = pick_threads(threads, (end - body) / 64);
+    const std::vector<const char*> cuts = split_lines(body, end, nt);
+    const int parts = (int)cuts.size() - 1;
+    struct Row {
+        rss_tuple6 t;
+        uint64_t b, e;
+    };
+    std::vector<std::vector<Row>> local(parts);
+    std::atomic<bool> ok{true};
+    std::vector<std::thread> pool;
+    for (int k = 0; k < parts; ++k)
+        pool.emplace_back([&, k] {
+            const char* p = cuts[k];
+            const char* e = cuts[k + 1];
+            std::vector<Row>& out = local[k];
+            out.reserve((size_t)std::count(p, e, '\n') + 1);
+            Row r;
+            while (p < e) {
+                if (skip_empty_line(p, e)) continue;
+                const char* b = p;
+                const char* te;
+                if (!scan_row6(p, e, layout->field_column, r.t, te)) {
+                    ok = false;
+                    return;
+                }
+                r.b = (uint64_t)(b - data);
+                r.e = (uint64_t)(te - data);
+                out.push_back(r);
+                if ((out.size() & 4095) == 0 && !ok.load(std::memory_order_relaxed)) return;
+            }
+        });
+    for (auto& t : pool) t.join();
+    pool.clear();
+    if (!ok) return RSS_ENOTSUP;
+    std::vector<size_t> off(parts + 1, 0);
+    for (int k = 0; k < parts; ++k) off[k + 1] = off[k] + local[k].size();
+    *n_rows = off[parts];
+    if (off[parts] == 0) return RSS_ENOTSUP;
+    if (off[parts] > cap || !tuples || !spans) return RSS_EINVAL;
+    for (int k = 0; k < parts; ++k)
+        pool.emplace_back([&, k] {
+            for (size_t i = 0; i < local[k].size(); ++i) {
+                const Row& r = local[k][i];
+                tuples[off[k] + i] = r.t;
+                spans[2 * (off[k] + i)] = r.b;
+                spans[2 * (off[k] + i) + 1] = r.e;
+            }
+        });
+    for (auto& t : pool) t.join();
+    return RSS_OK;
+}
+
+size_t rss_csv_format6_bound(const uint64_t* spans, size_t n, uint32_t nqueues) {
+    size_t text = 0;
+    for (size_t i = 0; i < n; ++i) text += (size_t)(spans[2 * i + 1] - spans[2 * i]);
+    return rss_csv_prefix_bound(nqueues) + text + n * kMaxRow6Extra;
+}
+
+int rss_csv_format6(const char* data, const uint64_t* spans, const uint32_t* hash,
+                    const uint32_t* queue, size_t n, const uint64_t* counts, uint32_t nqueues,
+                    const rss_csv_layout* layout, char* out, size_t cap, size_t* out_len,
+                    int threads) {
+    if ((n && (!data || !spans || !hash || !queue)) || !counts || !layout || !out || !out_len)
+        return RSS_EINVAL;
+    if (cap < rss_csv_format6_bound(spans, n, nqueues)) return RSS_EINVAL;
+    for (int f = 0; f < 4; ++f)
+        if (layout->field_column[f] > 3) return RSS_EINVAL;
+    char* p = out + rss_csv_format_prefix(counts, nqueues, layout, out);
+    const int nt = pick_threads(threads, n);
+    std::vector<size_t> off(nt + 1, 0);
+    std::vector<std::thread> pool;
+    for (int k = 0; k < nt; ++k)
+        pool.emplace_back([&, k] {
+            const size_t a = n * k / nt, b = n * (k + 1) / nt;
+            size_t bytes = 0;
+            for (size_t i = a; i < b; ++i)
+                bytes += (size_t)(spans[2 * i + 1] - spans[2 * i]) + uint_len(hash[i]) +
+                         uint_len(queue[i]) + 3;
+            off[k + 1] = bytes;
+        });
+    for (auto& t : pool) t.join();
+    pool.clear();
+    off[0] = (size_t)(p - out);
+    for (int k = 0; k < nt; ++k) off[k + 1] += off[k];
+    for (int k = 0; k < nt; ++k)
+        pool.emplace_back([&, k] {
+            const size_t a = n * k / nt, b = n * (k + 1) / nt;
+            char* w = out + off[k];
+            for (size_t i = a; i < b; ++i) {
+                const size_t len = (size_t)(spans[2 * i + 1] - spans[2 * i]);
+                memcpy(w, data + spans[2 * i], len);
+                w += len;
+                *w++ = ',';
+                w = put_uint(w, hash[i]);
+                *w++ = ',';
+                w = put_uint(w, queue[i]);
+                *w++ = '\n';
+            }
+        });
+    for (auto& t : pool) t.join();
+    *out_len = off[nt];
     return RSS_OK;
 }
 

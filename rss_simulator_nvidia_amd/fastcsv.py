@@ -93,3 +93,53 @@ def run_counts(hash_key, ips_file, htable, nqueues, threads=0, fields=_native.FI
     _, _, counts = ctx.hash(key, parsed[0], htable, nqueues, want_hash=False, want_queue=False,
                             reta=reta)
     return counts
+
+
+def run_csv6(hash_key, ips_file, htable, nqueues, output, threads=0, timings=None,
+             fields=_native.FIELDS_ALL, reta=None):
+    """``--ipv6 --csv`` for a canonical IPv6 file: native parse (rss_csv_parse6) -> the
+    IPv6 kernel (rss_hash6_host) -> native format (rss_csv_format6, rows copied from the
+    input text).  False if the file needs the pandas path."""
+    t = [time.perf_counter()]
+    try:
+        data = np.fromfile(ips_file, dtype=np.uint8)
+    except (OSError, ValueError):
+        return False
+    t.append(time.perf_counter())
+    parsed = _native.csv_parse6(data, threads)
+    if parsed is None:
+        return False
+    tuples, spans, layout = parsed
+    t.append(time.perf_counter())
+    key6 = _native.prepare_key6(hash_key, fields)
+    h, q, c = _native.default_context().hash6(key6, tuples, htable, nqueues, reta=reta)
+    t.append(time.perf_counter())
+    out = _native.csv_format6(data, spans, h, q, c, layout, threads)
+    t.append(time.perf_counter())
+    try:
+        out.tofile(output)
+    except OSError:
+        return False  # the pandas path raises the reference's error for this path
+    t.append(time.perf_counter())
+    if timings is not None:
+        for name, a, b in zip(("read", "parse", "gpu", "format", "write"), t, t[1:]):
+            timings[name] = b - a
+        timings.update(rows=len(tuples), bytes_in=len(data), bytes_out=len(out), path="host6")
+    print("Wrote statistics to {csv}.".format(csv=output))
+    return True
+
+
+def run_counts6(hash_key, ips_file, htable, nqueues, threads=0, fields=_native.FIELDS_ALL,
+                reta=None):
+    """Per-queue counts of a canonical IPv6 file; None if it needs the pandas path."""
+    try:
+        data = np.fromfile(ips_file, dtype=np.uint8)
+    except (OSError, ValueError):
+        return None
+    parsed = _native.csv_parse6(data, threads)
+    if parsed is None:
+        return None
+    key6 = _native.prepare_key6(hash_key, fields)
+    _, _, counts = _native.default_context().hash6(key6, parsed[0], htable, nqueues,
+                                                   want_hash=False, want_queue=False, reta=reta)
+    return counts

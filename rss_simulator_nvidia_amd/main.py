@@ -130,14 +130,15 @@ def main(argv=None):
     table = indirection_table(args)
     if args.pcap:
         return run_pcap(args, table)
-    fast = fastcsv.enabled() and not args.ipv6
-    if args.csv and fast and fastcsv.run_csv(args.key, args.ips_file, args.htable_size,
-                                             args.num_queues, args.csv, fields=args.hash_fields,
-                                             reta=table):
+    fast = fastcsv.enabled()
+    run_csv = fastcsv.run_csv6 if args.ipv6 else fastcsv.run_csv
+    run_counts = fastcsv.run_counts6 if args.ipv6 else fastcsv.run_counts
+    if args.csv and fast and run_csv(args.key, args.ips_file, args.htable_size, args.num_queues,
+                                     args.csv, fields=args.hash_fields, reta=table):
         return  # canonical input: native CSV parse/format around the same GPU kernel
     if not args.csv and fast:
-        counts = fastcsv.run_counts(args.key, args.ips_file, args.htable_size, args.num_queues,
-                                    fields=args.hash_fields, reta=table)
+        counts = run_counts(args.key, args.ips_file, args.htable_size, args.num_queues,
+                            fields=args.hash_fields, reta=table)
         if counts is not None:  # histogram mode needs the per-queue counts only
             histogram.show(counts, _key_str(args.key), args.htable_size,
                            args.num_queues, args.histogram_png)

@@ -217,3 +217,27 @@ def test_cli_pcap_ipv6_gpu(tmp_path, golden_dir, oracle_lib, capsys):
     body = lines[lines.index("src_ip,dst_ip,src_port,dst_port,hash_result,queue_number") + 1:]
     assert [int(x.split(",")[4]) for x in body] == want_h
     assert [int(x.split(",")[5]) for x in body] == [h % 64 % 6 for h in want_h]
+
+
+def test_cli_ipv6_csv_fast_path_equals_pandas_path(tmp_path, golden_dir, monkeypatch, capsys):
+    """--ipv6 --csv: the native IPv6 CSV path (rss_csv_parse6 / rss_csv_format6 around the
+    IPv6 kernel) writes the same file as the pandas path on the GPU, byte for byte."""
+    from cli_cases import run_main
+    from test_fastcsv6 import random_ipv6_text
+    rng = np.random.default_rng(12)
+    rows = ["%s,%d,%s,%d" % (random_ipv6_text(rng), int(rng.integers(0, 65536)),
+                             random_ipv6_text(rng), int(rng.integers(0, 65536)))
+            for _ in range(20000)]
+    path = tmp_path / "ips6.csv"
+    path.write_text("dst_ip,src_port,src_ip,dst_port\r\n" + "\r\n".join(rows) + "\r\n")
+    key_file = os.path.join(golden_dir, "example_input", "hash_key.txt")
+    outs = []
+    for fast in ("1", "0"):
+        monkeypatch.setenv("RSS_CSV_FASTPATH", fast)
+        out = tmp_path / ("out%s.csv" % fast)
+        status, so, _, exc = run_main(["--key-file", key_file, "--ips-file", str(path), "--ipv6",
+                                       "--htable-size", "128", "--num-queues", "24",
+                                       "--csv", str(out)], capsys)
+        assert status == 0, exc
+        outs.append(out.read_bytes())
+    assert outs[0] == outs[1]
