@@ -27,9 +27,16 @@ def per_dispatch(path):
     return list(agg.values())
 
 
-fetch = per_dispatch("%s/fetch_counter_collection.csv" % src)
-write = per_dispatch("%s/write_counter_collection.csv" % src)
-req = per_dispatch("%s/req_counter_collection.csv" % src)
+def pass_csv(name):
+    """A pass's counter CSV: flattened (profiles/) or as rocprofv3 wrote it (gpurun_out/)."""
+    import os
+    flat = "%s/%s_counter_collection.csv" % (src, name)
+    return flat if os.path.exists(flat) else "%s/%s/run_counter_collection.csv" % (src, name)
+
+
+fetch = per_dispatch(pass_csv("fetch"))
+write = per_dispatch(pass_csv("write"))
+req = per_dispatch(pass_csv("req"))
 modes = {}
 for i, m in enumerate(MODES):
     rd = 2 * fetch[i]["FETCH_SIZE"] * 1024
