@@ -13,9 +13,11 @@
 // 12-bit slice of the input selects, 128 KiB, built per workgroup from the 96
 // windows; slices cut field-LSB first so structured flows spread over the LDS
 // banks): 8 ds_read_b32 + ~31 VALU per tuple instead of the reference's 96-step
-// bit-serial loop.  Key search evaluates two keys per 8-byte table entry
-// (ds_read_b64); IPv6 uses 29 word-aligned 11/11/10-bit and byte tables.  The per-queue histogram is privatised per lane
-// column in LDS and folded into global uint64 counts once per workgroup.
+// bit-serial loop (XOR trees as three-input v_bitop3).  Key search packs the low
+// bucket bits of 8 (H <= 256) or 4 (H <= 65536) keys, else the full hashes of 2 keys,
+// into each 8-byte table entry (ds_read_b64); IPv6 uses 29 word-aligned 11/11/10-bit
+// and byte tables.  The per-queue histogram is privatised per lane column in LDS and
+// folded into global uint64 counts once per workgroup.
 // tools/kbench.hip holds the measured design space (4/6/8/12-bit tables).
 #include <hip/hip_runtime.h>
 
