@@ -151,6 +151,81 @@ __global__ __launch_bounds__(1024) void mem_stream(Params p) {
     if (!kWrite && acc == 0x12345678u) p.counts[0] = acc;
 }
 
+// store-policy / mapping probes for the 12R+5W mix (the bench's byte mix):
+//   kPol 0 = nt stores (as product), 1 = sc1 stores, 2 = sc0 sc1 stores, 3 = sc0 sc1 nt,
+//   4 = plain stores; kXcd = workgroup w streams tiles of XCD (w % 8)'s contiguous eighth;
+//   kUnroll = 2 iterations' loads issued before either is consumed
+template <int kPol>
+__device__ __forceinline__ void store4(uint32_t* dst, u32x4 v) {
+    if constexpr (kPol == 0) {
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst));
+    } else if constexpr (kPol == 1) {
+        asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst), "v"(v) : "memory");
+    } else if constexpr (kPol == 2) {
+        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(dst), "v"(v) : "memory");
+    } else if constexpr (kPol == 3) {
+        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(dst), "v"(v) : "memory");
+    } else {
+        *reinterpret_cast<u32x4*>(dst) = v;
+    }
+}
+template <int kPol>
+__device__ __forceinline__ void store1(uint32_t* dst, uint32_t v) {
+    if constexpr (kPol == 0) {
+        __builtin_nontemporal_store(v, dst);
+    } else if constexpr (kPol == 1) {
+        asm volatile("global_store_dword %0, %1, off sc1" ::"v"(dst), "v"(v) : "memory");
+    } else if constexpr (kPol == 2) {
+        asm volatile("global_store_dword %0, %1, off sc0 sc1" ::"v"(dst), "v"(v) : "memory");
+    } else if constexpr (kPol == 3) {
+        asm volatile("global_store_dword %0, %1, off sc0 sc1 nt" ::"v"(dst), "v"(v) : "memory");
+    } else {
+        *dst = v;
+    }
+}
+
+template <int kPol, bool kXcd, bool kUnroll>
+__global__ __launch_bounds__(1024) void mem_policy(Params p) {
+    const u32x4* src = reinterpret_cast<const u32x4*>(p.tuples);
+    const uint64_t ng = p.n >> 2;
+    uint64_t g0, step;
+    if (kXcd) {  // grid = 8 * m workgroups; XCD x = w % 8 owns groups [x*ng/8, (x+1)*ng/8)
+        const uint32_t x = blockIdx.x & 7, l = blockIdx.x >> 3, m = gridDim.x >> 3;
+        g0 = x * (ng / 8) + (uint64_t)l * 1024 + threadIdx.x;
+        step = (uint64_t)m * 1024;
+        const uint64_t g1 = (x + 1) * (ng / 8);
+        for (uint64_t g = g0; g < g1; g += step) {
+            u32x4 a = src[3 * g], b = src[3 * g + 1], c = src[3 * g + 2];
+            u32x4 h = {a.x ^ a.y ^ a.z, a.w ^ b.x ^ b.y, b.z ^ b.w ^ c.x, c.y ^ c.z ^ c.w};
+            store4<kPol>(p.hash_out + 4 * g, h);
+            store1<kPol>(p.queue_out + g, (a.x ^ c.w) & 0x17171717u);
+        }
+        return;
+    }
+    g0 = (uint64_t)blockIdx.x * 1024 + threadIdx.x;
+    step = (uint64_t)gridDim.x * 1024;
+    uint64_t g = g0;
+    if (kUnroll) {
+        for (; g + step < ng; g += 2 * step) {
+            const uint64_t g2 = g + step;
+            u32x4 a = src[3 * g], b = src[3 * g + 1], c = src[3 * g + 2];
+            u32x4 a2 = src[3 * g2], b2 = src[3 * g2 + 1], c2 = src[3 * g2 + 2];
+            u32x4 h = {a.x ^ a.y ^ a.z, a.w ^ b.x ^ b.y, b.z ^ b.w ^ c.x, c.y ^ c.z ^ c.w};
+            u32x4 h2 = {a2.x ^ a2.y ^ a2.z, a2.w ^ b2.x ^ b2.y, b2.z ^ b2.w ^ c2.x, c2.y ^ c2.z ^ c2.w};
+            store4<kPol>(p.hash_out + 4 * g, h);
+            store1<kPol>(p.queue_out + g, (a.x ^ c.w) & 0x17171717u);
+            store4<kPol>(p.hash_out + 4 * g2, h2);
+            store1<kPol>(p.queue_out + g2, (a2.x ^ c2.w) & 0x17171717u);
+        }
+    }
+    for (; g < ng; g += step) {
+        u32x4 a = src[3 * g], b = src[3 * g + 1], c = src[3 * g + 2];
+        u32x4 h = {a.x ^ a.y ^ a.z, a.w ^ b.x ^ b.y, b.z ^ b.w ^ c.x, c.y ^ c.z ^ c.w};
+        store4<kPol>(p.hash_out + 4 * g, h);
+        store1<kPol>(p.queue_out + g, (a.x ^ c.w) & 0x17171717u);
+    }
+}
+
 // work-distribution probe for the 12R+5W mix: instead of a static grid-stride share,
 // every wave claims chunks of kIters x 64 lane-groups (4 tuples each) from eight
 // per-XCD heads (own XCD first, then the others), so a CU / XCD that streams slower
@@ -489,6 +564,24 @@ int main(int argc, char** argv) {
                 printf("%-36s x%d %8.3f ms  %7.1f Gt/s  %6.0f GB/s\n", v.name, wpc, t, n / t / 1e6,
                        n * v.bytes / t * 1e3);
             }
+        }
+    }
+    if (strstr("policy", filter)) {  // store cache policy / XCD mapping / unroll, 12R+5W
+        p.hash_out = h1;
+        p.queue_out = q1;
+        struct PV { const char* name; void (*k)(Params); int wpc; };
+        const PV pv[9] = {{"policy nt stores (as product)", mem_policy<0, false, false>, 1},
+                          {"policy sc1 stores", mem_policy<1, false, false>, 1},
+                          {"policy sc0 sc1 stores", mem_policy<2, false, false>, 1},
+                          {"policy sc0 sc1 nt stores", mem_policy<3, false, false>, 1},
+                          {"policy plain stores", mem_policy<4, false, false>, 1},
+                          {"policy nt, XCD-contiguous eighths", mem_policy<0, true, false>, 1},
+                          {"policy nt, 2 iterations of loads first", mem_policy<0, false, true>, 1},
+                          {"policy nt, XCD-contiguous, grid 2x", mem_policy<0, true, false>, 2},
+                          {"policy nt (as product) again", mem_policy<0, false, false>, 1}};
+        for (const PV& v : pv) {
+            t = time_ms([&] { hipLaunchKernelGGL(v.k, dim3(g_cus * v.wpc), dim3(1024), 0, 0, p); }, reps);
+            printf("%-40s %8.3f ms  %7.1f Gt/s  %6.0f GB/s\n", v.name, t, n / t / 1e6, n * 17e-9 / t * 1e3);
         }
     }
     if (strstr("dyn", filter)) {  // static grid-stride vs per-wave dynamic chunks
