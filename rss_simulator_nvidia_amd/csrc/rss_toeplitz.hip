@@ -75,7 +75,7 @@ constexpr int kBinCols = 32;            // private histogram columns (one per ba
 static_assert(kLutBytes == 128 * 1024, "LUT layout: 8 tables x 4096 x u32");
 static_assert(kBlock * 4 == (int)kTableEntries, "LUT build maps 4 entries per thread per table");
 
-enum QueueMode { QM_MASK = 0, QM_FAST16 = 1, QM_FAST32 = 2, QM_TABLE = 3 };
+enum QueueMode { QM_MASK = 0, QM_FAST16 = 1, QM_FAST32 = 2, QM_TABLE = 3, QM_FAST8 = 4 };
 constexpr uint32_t kRetaMax = 1024;  // indirection-table entries carried in the kernarg
 enum HistMode { HIST_PRIVATE = 0, HIST_SHARED = 1, HIST_GLOBAL = 2, HIST_NONE = 3 };
 enum QueueWidth { QW_U32 = 0, QW_U16 = 1, QW_U8 = 2 };
@@ -96,7 +96,7 @@ struct LaunchParams {
     uint32_t q_m32;     // ceil(2^32 / Q): exact b % Q for b, Q < 2^16
     uint32_t nkeys;     // key search: keys in this launch
     uint64_t q_m64;     // ceil(2^64 / Q): exact b % Q for any 32-bit b, Q
-    uint32_t q_m16;     // ceil(2^16 / Q): packed key search, b < 256 (queue_of_byte)
+    uint32_t q_m16;     // ceil(2^16 / Q): exact b % Q for b < 256 (QM_FAST8, packed search)
     const uint32_t* key_windows;  // key search: nkeys x 96 windows in device memory
     uint16_t reta[kRetaMax];      // QM_TABLE: queue of bucket b (ethtool -X indirection)
 };
@@ -211,6 +211,11 @@ template <int kQMode>
 __device__ __forceinline__ uint32_t queue_of(uint32_t b, const LaunchParams& p) {
     if constexpr (kQMode == QM_MASK) {
         return b & p.q_mask;
+    } else if constexpr (kQMode == QM_FAST8) {
+        // b < 256, Q < 256: b - Q * ((b * ceil(2^16 / Q)) >> 16), exact (checked for every
+        // b, Q), with full-rate 24-bit multiplies instead of FAST16's two quarter-rate ones
+        const uint32_t d = __umul24(b, p.q_m16) >> 16;
+        return b - __umul24(d, p.Q);
     } else if constexpr (kQMode == QM_FAST16) {
         return __umulhi(p.q_m32 * b, p.Q);  // b < 2^16, Q < 2^16
     } else {
@@ -711,6 +716,7 @@ struct LaunchParams6 {
     uint64_t h_m64;
     uint32_t h_mask, H, Q, q_mask, q_m32;
     uint32_t qwidth;  // QueueWidth of queue_out (grid-uniform runtime switch)
+    uint32_t q_m16;
     uint64_t q_m64;
     uint16_t reta[kRetaMax];  // QM_TABLE: queue of bucket b, as LaunchParams::reta
 };
@@ -816,6 +822,7 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz6_kernel(const LaunchParam
     p.Q = p6.Q;
     p.q_mask = p6.q_mask;
     p.q_m32 = p6.q_m32;
+    p.q_m16 = p6.q_m16;
     p.q_m64 = p6.q_m64;
     const uint32_t nbins =
         kHist == HIST_PRIVATE ? p.Q * kBinCols : (kHist == HIST_SHARED ? p.Q : 0u);
@@ -979,6 +986,7 @@ KernelFn pick_queue(int qmode, int hist, int qwidth, bool vec4) {
     switch (qmode) {
         case QM_MASK: return pick_hist<kHPow2, QM_MASK>(hist, qwidth, vec4);
         case QM_FAST16: return pick_hist<kHPow2, QM_FAST16>(hist, qwidth, vec4);
+        case QM_FAST8: return pick_hist<kHPow2, QM_FAST8>(hist, qwidth, vec4);
         case QM_TABLE: return pick_hist<kHPow2, QM_TABLE>(hist, qwidth, vec4);
         default: return pick_hist<kHPow2, QM_FAST32>(hist, qwidth, vec4);
     }
@@ -996,7 +1004,8 @@ uint32_t magic32(uint32_t d) { return UINT32_MAX / d + 1; }
 // placement (private LDS columns / shared LDS bins / global atomics) for H and Q.
 // Returns whether H is a power of two.
 bool setup_modes(LaunchParams* p, uint32_t htable, uint32_t nqueues, bool want_counts, int* qmode,
-                 int* hist, uint32_t* bin_bytes, uint32_t bin_budget = kBinBytesMax) {
+                 int* hist, uint32_t* bin_bytes, uint32_t bin_budget = kBinBytesMax,
+                 bool allow_fast8 = true) {
     p->H = htable;
     p->Q = nqueues;
     p->h_mask = htable - 1;
@@ -1008,8 +1017,9 @@ bool setup_modes(LaunchParams* p, uint32_t htable, uint32_t nqueues, bool want_c
         *qmode = QM_MASK;
         p->q_mask = nqueues - 1;
     } else if (htable <= 65536u) {  // bucket < 2^16 and nqueues < htable <= 2^16
-        *qmode = QM_FAST16;
+        *qmode = htable <= 256u && allow_fast8 ? QM_FAST8 : QM_FAST16;
         p->q_m32 = magic32(nqueues);
+        p->q_m16 = 65536u / nqueues + (65536u % nqueues != 0);
     } else {
         *qmode = QM_FAST32;
         p->q_m64 = magic64(nqueues);
@@ -1089,7 +1099,7 @@ int launch_search(const uint32_t* d_windows, size_t nkeys, const rss_tuple4* d_t
     int qmode, hist;
     uint32_t bin_bytes;  // per key; a workgroup holds the bins of its two keys
     const bool h_pow2 = setup_modes(&p, htable, nqueues, true, &qmode, &hist, &bin_bytes,
-                                    kPairBinBytesMax / 2);
+                                    kPairBinBytesMax / 2, false);
     const bool vec4 = aligned16(d_tuples);
     DeviceInfo info;
     int rc = device_info(&info);
@@ -1236,6 +1246,7 @@ KernelFn6 pick6(int qmode, int hist, bool vec4) {
     switch (qmode) {
         case QM_MASK: return pick6_hist<kHPow2, QM_MASK>(hist, vec4);
         case QM_FAST16: return pick6_hist<kHPow2, QM_FAST16>(hist, vec4);
+        case QM_FAST8: return pick6_hist<kHPow2, QM_FAST8>(hist, vec4);
         case QM_TABLE: return pick6_hist<kHPow2, QM_TABLE>(hist, vec4);
         default: return pick6_hist<kHPow2, QM_FAST32>(hist, vec4);
     }
@@ -1290,6 +1301,7 @@ int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint
     p.Q = tmp.Q;
     p.q_mask = tmp.q_mask;
     p.q_m32 = tmp.q_m32;
+    p.q_m16 = tmp.q_m16;
     p.q_m64 = tmp.q_m64;
     p.qwidth = qwidth;
     if (reta)

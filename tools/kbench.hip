@@ -307,6 +307,94 @@ __device__ __forceinline__ uint32_t hash_lut(const char* lds, const uint32_t (&w
     return h;
 }
 
+// Nine 11/10-bit tables (the key-search partition with 4-byte entries): 60 KiB, so two
+// 1024-thread workgroups fit a CU (32 waves instead of 16), at 9 lookups per tuple
+// instead of 8.  Every table base is below 64 KiB: it folds into the ds_read offset.
+__host__ __device__ constexpr int t9_bit(int t, int b) {  // input bit of index bit b
+    return t == 0 ? 31 - b : t == 1 ? 20 - b : t == 2 ? 63 - b
+         : t == 3 ? (b < 5 ? 84 - b : 73 - b)
+         : t == 4 ? 9 - b : t == 5 ? 52 - b : t == 6 ? 95 - b : t == 7 ? 79 - b : 41 - b;
+}
+__host__ __device__ constexpr uint32_t t9_base(int t) {
+    return t == 0 ? 0u : t == 1 ? 8192u : t == 2 ? 16384u : t == 3 ? 24576u : t == 4 ? 28672u
+         : t == 5 ? 32768u : t == 6 ? 40960u : t == 7 ? 49152u : 57344u;
+}
+__host__ __device__ constexpr int t9_width(int t) { return (t == 3 || t == 4 || t == 8) ? 10 : 11; }
+
+template <int kT>
+__device__ __forceinline__ uint32_t t9_off(uint32_t w0, uint32_t w1, uint32_t w2) {
+    if constexpr (kT == 0) return (w0 << 2) & 0x1FFCu;
+    if constexpr (kT == 1) return (w0 >> 9) & 0x1FFCu;
+    if constexpr (kT == 2) return (w1 << 2) & 0x1FFCu;
+    if constexpr (kT == 3) return ((w2 >> 9) & 0x7Cu) | ((w2 >> 20) & 0xF80u);
+    if constexpr (kT == 4) return (w0 >> 20) & 0xFFCu;
+    if constexpr (kT == 5) return (w1 >> 9) & 0x1FFCu;
+    if constexpr (kT == 6) return (w2 << 2) & 0x1FFCu;
+    if constexpr (kT == 7) return (w2 >> 14) & 0x1FFCu;
+    return (w1 >> 20) & 0xFFCu;
+}
+template <int kT>
+__device__ __forceinline__ uint32_t t9_term(const char* lds, uint32_t w0, uint32_t w1, uint32_t w2) {
+    return *reinterpret_cast<const uint32_t*>(lds + t9_base(kT) + t9_off<kT>(w0, w1, w2));
+}
+__device__ __forceinline__ uint32_t x3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint32_t hash9(const char* l, uint32_t w0, uint32_t w1, uint32_t w2) {
+    return x3(x3(t9_term<0>(l, w0, w1, w2), t9_term<1>(l, w0, w1, w2), t9_term<2>(l, w0, w1, w2)),
+              x3(t9_term<3>(l, w0, w1, w2), t9_term<4>(l, w0, w1, w2), t9_term<5>(l, w0, w1, w2)),
+              x3(t9_term<6>(l, w0, w1, w2), t9_term<7>(l, w0, w1, w2), t9_term<8>(l, w0, w1, w2)));
+}
+template <int kT>
+__device__ __forceinline__ void t9_build(uint32_t* lut, const uint32_t* window, uint32_t tid) {
+    uint32_t x = 0;
+#pragma unroll
+    for (int j = 0; j < 10; ++j) x ^= ((tid >> j) & 1u) ? window[t9_bit(kT, j)] : 0u;
+    uint32_t* dst = lut + t9_base(kT) / 4;
+    dst[tid] = x;
+    if constexpr (t9_width(kT) == 11) dst[tid + 1024] = x ^ window[t9_bit(kT, 10)];
+}
+
+template <bool kWrite>
+__global__ __launch_bounds__(1024, 2) void lut9_kernel(Params p) {
+    __shared__ uint32_t lut[61440 / 4];
+    __shared__ uint32_t bins[24 * 32];
+    const uint32_t tid = threadIdx.x;
+    t9_build<0>(lut, p.window, tid); t9_build<1>(lut, p.window, tid); t9_build<2>(lut, p.window, tid);
+    t9_build<3>(lut, p.window, tid); t9_build<4>(lut, p.window, tid); t9_build<5>(lut, p.window, tid);
+    t9_build<6>(lut, p.window, tid); t9_build<7>(lut, p.window, tid); t9_build<8>(lut, p.window, tid);
+    for (uint32_t e = tid; e < p.Q * 32; e += 1024) bins[e] = 0;
+    __syncthreads();
+    const char* lds = reinterpret_cast<const char*>(lut);
+    const uint32_t col = tid & 31;
+    const uint4* src = reinterpret_cast<const uint4*>(p.tuples);
+    const uint64_t ng = p.n >> 2;
+    const uint64_t stride = (uint64_t)gridDim.x * 1024;
+    for (uint64_t g = (uint64_t)blockIdx.x * 1024 + tid; g < ng; g += stride) {
+        const uint4 a = src[3 * g], b = src[3 * g + 1], c = src[3 * g + 2];
+        uint32_t h[4] = {hash9(lds, a.x, a.y, a.z), hash9(lds, a.w, b.x, b.y),
+                         hash9(lds, b.z, b.w, c.x), hash9(lds, c.y, c.z, c.w)};
+        uint32_t q[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) q[t] = __umulhi(p.q_m32 * (h[t] & p.h_mask), p.Q);
+        if (kWrite) {
+            uint32_t* o = p.hash_out + 4 * g;
+            __builtin_nontemporal_store(h[0], o); __builtin_nontemporal_store(h[1], o + 1);
+            __builtin_nontemporal_store(h[2], o + 2); __builtin_nontemporal_store(h[3], o + 3);
+            __builtin_nontemporal_store(q[0] | q[1] << 8 | q[2] << 16 | q[3] << 24, p.queue_out + g);
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+            __hip_atomic_fetch_add(&bins[q[t] * 32 + col], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __syncthreads();
+    for (uint32_t k = tid; k < p.Q; k += 1024) {
+        uint32_t s = 0;
+        for (uint32_t c2 = 0; c2 < 32; ++c2) s += bins[k * 32 + ((c2 + k) & 31)];
+        if (s) atomicAdd(&p.counts[k], (unsigned long long)s);
+    }
+}
+
 template <int B, int R, int BLOCK, bool kWrite, bool kPrefetch, bool kQ8 = false, bool kNT = false>
 __global__ __launch_bounds__(BLOCK) void lut_kernel(Params p) {
     constexpr int C = 96 / B, E = 1 << B;
@@ -674,5 +762,9 @@ int main(int argc, char** argv) {
     run_variant("B8 R1 blk1024 x2 q8 full", lut_kernel<8, 1, 1024, true, false, true>, 1024, 2, true, true);
     run_variant("B8 R1 blk1024 x2 nt full", lut_kernel<8, 1, 1024, true, false, false, true>, 1024, 2, true);
     run_variant("B8 R1 blk1024 x2 q8nt full", lut_kernel<8, 1, 1024, true, false, true, true>, 1024, 2, true, true);
+    run_variant("T9 x2 q8nt full", lut9_kernel<true>, 1024, 2, true, true);
+    run_variant("T9 x2 counts", lut9_kernel<false>, 1024, 2, false);
+    run_variant("T9 x1 q8nt full", lut9_kernel<true>, 1024, 1, true, true);
+    run_variant("T9ref B12 R1 blk1024 x1 q8nt full", lut_kernel<12, 1, 1024, true, false, true, true>, 1024, 1, true, true);
     return 0;
 }
