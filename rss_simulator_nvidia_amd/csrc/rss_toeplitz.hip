@@ -545,10 +545,6 @@ __global__ __launch_bounds__(kBlock) void rss_key_search_kernel(const LaunchPara
 // half-wave's adds stay conflict-free.
 constexpr uint32_t kPackedPrepBytes = RSS_INPUT_BITS * 8;  // packed windows, before the bins
 
-// H <= 256, Q < H: b % Q = b - Q * ((b * ceil(2^16 / Q)) >> 16), exact for all b < 256,
-// Q < 256 (checked exhaustively) with 24-bit multiplies only (full-rate v_mul_u32_u24);
-// the packed kernel folds it into the bin address.
-
 // table t entry v (and v + 1024) of the packed kernel: XOR of the packed windows
 template <int kT>
 __device__ __forceinline__ void build_packed_table(uint2* lut, const uint2* packed, uint32_t tid) {
@@ -612,7 +608,7 @@ __global__ __launch_bounds__(kBlock) void rss_key_search_packed_kernel(const Lau
     const uint32_t hbits = 31 - __clz(p.H);  // log2(H)
     constexpr uint32_t kRowShift = kLaneBits == 8 ? 10 : 9;  // log2(kKeys * kBinCols * 4)
     // byte-lane queue step folded into the bin address: q * 2^kRowShift =
-    // (b << kRowShift) - d * (Q << kRowShift), d = floor(b / Q) (queue_of_byte): two
+    // (b << kRowShift) - d * (Q << kRowShift), d = floor(b / Q) (as QM_FAST8): two
     // full-rate 24-bit multiplies, the second a v_mad_i32_i24
     const int neg_q_row = -(int)(p.Q << kRowShift);
     uint32_t hi = 65536u;
