@@ -50,6 +50,9 @@ def parse_args():
     p.add_argument("--cpu-procs", type=int, default=16,
                    help="worker processes for the CPU baseline (the box's CPU share)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-extras", action="store_true",
+                   help="skip the rank-0 secondary lines of the row-f kernels (IPv6 hash, key "
+                        "search), timed after the main measurement")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl = RCCL over xGMI; gloo only to rehearse N>1 on one GPU")
     p.add_argument("--graph", action="store_true",
@@ -155,6 +158,55 @@ def relaunch_distributed(n):
            "--nproc-per-node", str(n), "--master-addr", "127.0.0.1", "--master-port", str(port),
            os.path.abspath(__file__)] + sys.argv[1:]
     return subprocess.run(cmd).returncode
+
+
+def extra_lines(torch, _native, dev, stream, key_bytes):
+    """Secondary timings of the row-f kernels on this GPU, after the main measurement
+    (DESIGN.md §7-§8): the IPv6 kernel (2^26 uniform 36-byte tuples, u32 hash + u8 queue +
+    counts: 36 B read + 5 B written per tuple) and key search (1024 random keys x 2^20 resident
+    tuples, H=128, Q=24, counts only).  Mean of per-launch HIP events after warm launches."""
+    from rss_simulator_nvidia_amd import keysearch
+    sp = stream.cuda_stream
+
+    def timed(fn, warm=10, reps=20):
+        for _ in range(warm):
+            fn()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(reps)]
+        for a, b in ev:
+            a.record(stream)
+            fn()
+            b.record(stream)
+        torch.cuda.synchronize()
+        return sum(a.elapsed_time(b) for a, b in ev) / reps
+
+    out = {}
+    n6 = 1 << 26
+    words = torch.randint(-2**31, 2**31 - 1, (9 * n6,), dtype=torch.int32, device=dev)
+    h6 = torch.empty(n6, dtype=torch.int32, device=dev)
+    q6 = torch.empty(n6, dtype=torch.uint8, device=dev)
+    c6 = torch.zeros(24, dtype=torch.int64, device=dev)
+    k6 = _native.prepare_key6(key_bytes)
+    ms = timed(lambda: _native.hash6_device(k6, words.data_ptr(), n6, 128, 24, h6.data_ptr(),
+                                            q6.data_ptr(), c6.data_ptr(),
+                                            _native.FLAG_QUEUE_U8 | _native.FLAG_ACCUMULATE, sp))
+    out["ipv6_hash"] = {"tuples": n6, "kernel_ms": ms, "tuples_per_s": n6 / (ms / 1e3),
+                        "achieved_GBs": n6 * 41 / (ms / 1e3) / 1e9,
+                        "bytes_per_tuple": 41, "outputs": "hash u32 + queue u8 + counts"}
+    del words, h6, q6
+    nk, nt = 1024, 1 << 20
+    keys = keysearch.random_keys(nk, seed=0)
+    import numpy as np
+    win = np.stack([np.ctypeslib.as_array(_native.prepare_key(k).window) for k in keys])
+    windows = torch.from_numpy(win.astype(np.uint32).view(np.int32)).to(dev)
+    tup = torch.empty(3 * nt, dtype=torch.int32, device=dev)
+    _native.generate_device(1, 0, nt, tup.data_ptr(), sp)
+    kc = torch.empty((nk, 24), dtype=torch.int64, device=dev)
+    ms = timed(lambda: _native.key_search_device(windows.data_ptr(), nk, tup.data_ptr(), nt, 128,
+                                                 24, kc.data_ptr(), sp), warm=3, reps=10)
+    out["key_search"] = {"keys": nk, "tuples": nt, "kernel_ms": ms,
+                         "key_tuple_evals_per_s": nk * nt / (ms / 1e3), "htable": 128, "queues": 24}
+    return out
 
 
 def main():
@@ -334,6 +386,10 @@ def main():
             flow_device(torch, tuples, 0, n, dev)
             flow_ms = kernel_ms_of(hashes.data_ptr(), queues.data_ptr(), qflag, reps)
 
+    extras = None
+    if rank == 0 and not args.no_extras:
+        extras = extra_lines(torch, _native, dev, stream, key_bytes)
+
     if rank == 0:
         value = n * world * args.steps / elapsed
         kernel_s = kernel_ms / 1e3
@@ -416,6 +472,8 @@ def main():
                 "kernel_ms": flow_ms, "tuples_per_s_per_gpu": n / (flow_ms / 1e3),
                 "note": "same outputs on flow-like input (one IP pair, sequential source ports; "
                         "--distribution flow), timed after the uniform run"}
+        if extras is not None:
+            line["row_f_kernels"] = extras
         print(json.dumps(line), flush=True)
     if world > 1:
         barrier()  # ranks leave together (rank 0 ran the secondary timings alone)
