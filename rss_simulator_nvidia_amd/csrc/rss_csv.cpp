@@ -195,15 +195,33 @@ constexpr size_t kMaxRowBytes = 15 + 1 + 15 + 1 + 5 + 1 + 5 + 1 + 10 + 1 + 10 + 
 // (the pandas path's parser, ingest.py) reads every such text to the same 128 bits;
 // pandas keeps it as a str and writes it back verbatim, so the output row is the
 // input line's text plus the two new columns.
-inline int hex_value(char c) {
-    if ((unsigned)(c - '0') <= 9) return c - '0';
-    const unsigned l = (unsigned)((c | 0x20) - 'a');
-    return l <= 5 ? (int)l + 10 : -1;
+// character classes of the IPv6 scanner: 0..15 hex digit, kColon, kEnd (',' '\r' '\n'),
+// kBad (anything else)
+enum : int8_t { kColon = 16, kEnd = 17, kBad = -1 };
+struct Hex6Table {
+    int8_t v[256];
+    constexpr Hex6Table() : v() {
+        for (int c = 0; c < 256; ++c)
+            v[c] = (c >= '0' && c <= '9') ? (int8_t)(c - '0')
+                 : (c >= 'a' && c <= 'f') ? (int8_t)(c - 'a' + 10)
+                 : (c >= 'A' && c <= 'F') ? (int8_t)(c - 'A' + 10)
+                 : c == ':'                ? (int8_t)kColon
+                 : (c == ',' || c == '\r' || c == '\n') ? (int8_t)kEnd
+                                                         : (int8_t)kBad;
+    }
+};
+constexpr Hex6Table kHex6{};
+
+inline int char_class(const char* p, const char* e) {
+    return p < e ? kHex6.v[(unsigned char)*p] : kEnd;
 }
 
-inline bool field_end(const char* p, const char* e) {
-    return p >= e || *p == ',' || *p == '\r' || *p == '\n';
+inline int hex_value(char c) {
+    const int v = kHex6.v[(unsigned char)c];
+    return v < 16 ? v : -1;
 }
+
+inline bool field_end(const char* p, const char* e) { return char_class(p, e) == kEnd; }
 
 inline bool scan_ip6(const char*& p, const char* e, uint32_t out[4]) {
     uint32_t g[8];
@@ -214,12 +232,16 @@ inline bool scan_ip6(const char*& p, const char* e, uint32_t out[4]) {
     }
     while (!(gap >= 0 && field_end(p, e))) {
         uint32_t v = 0;
-        int digits = 0;
-        for (int h; digits < 4 && p < e && (h = hex_value(*p)) >= 0; ++digits, ++p) v = v << 4 | (uint32_t)h;
-        if (digits == 0 || (p < e && hex_value(*p) >= 0) || ng == 8) return false;
+        int digits = 0, h;
+        while ((h = char_class(p, e)) >= 0 && h < 16 && digits < 4) {
+            v = v << 4 | (uint32_t)h;
+            ++digits;
+            ++p;
+        }
+        if (digits == 0 || (h >= 0 && h < 16) || ng == 8) return false;
         g[ng++] = v;
-        if (field_end(p, e)) break;
-        if (*p != ':') return false;
+        if (h == kEnd) break;
+        if (h != kColon) return false;
         if (p + 1 < e && p[1] == ':') {
             if (gap >= 0) return false;
             gap = ng;
