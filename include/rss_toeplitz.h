@@ -286,7 +286,9 @@ int rss_csv_hash_text(rss_ctx* ctx, const rss_key* key, const char* text, size_t
  * rss_csv_hash_text from file to file: the input streams through two pinned staging
  * buffers of ctx (read of chunk k+1 overlaps the upload of chunk k) and the output
  * rows stream back the same way (download of chunk k+1 overlaps the write of chunk
- * k), so no file-sized host buffer exists.  out_path may be NULL with
+ * k), so no file-sized host buffer exists.  Bodies of any size are processed in
+ * line-aligned segments below 4 GiB (3 GiB; RSS_CSV_SEGMENT_BYTES lowers it), counts
+ * summed over the segments and rows written after the last one.  out_path may be NULL with
  * RSS_CSV_COUNTS_ONLY.  An unreadable input or an output that cannot be created is
  * RSS_ENOTSUP as well: the pandas path then raises the reference's error.
  */

@@ -23,7 +23,10 @@
 #include <unistd.h>
 
 #include <cerrno>
+#include <cstdlib>
 #include <cstring>
+#include <memory>
+#include <vector>
 
 #include "rss_internal.h"
 #include "rss_toeplitz.h"
@@ -440,6 +443,8 @@ class CsvJob {
     }
     int alloc_text() { return buf_.alloc(&d_text_, blen_); }
     uint8_t* text() const { return d_text_; }
+    // a segment's text may end before the allocated capacity (rss_csv_hash_file)
+    void set_text_len(uint64_t len) { blen_ = len; }
 
     // newline index + parse (+ empty-line drop); RSS_ENOTSUP if not canonical
     int parse() {
@@ -559,6 +564,19 @@ int check_args(const rss_key* key, uint32_t htable, uint32_t nqueues) {
 }
 
 constexpr size_t kStageBytes = 32u << 20;  // pinned staging per buffer (file I/O)
+
+// rss_csv_hash_file splits bodies into line-aligned segments below the 32-bit newline
+// positions' 4 GiB: 3 GiB by default; RSS_CSV_SEGMENT_BYTES (>= 2 staging buffers + 4 KiB)
+// lowers it, which the tests use to exercise the segmented path on small files.
+uint64_t segment_bytes() {
+    uint64_t seg = 3ull << 30;
+    if (const char* env = getenv("RSS_CSV_SEGMENT_BYTES")) {
+        const unsigned long long v = strtoull(env, nullptr, 10);
+        if (v) seg = v;
+    }
+    const uint64_t lo = 2 * (uint64_t)kStageBytes + 4096, hi = 0xFFFFFFFFull - 1;
+    return seg < lo ? lo : (seg > hi ? hi : seg);
+}
 
 int reserve_stage(rss_ctx* ctx) {
     if (ctx->stage_bytes) return RSS_OK;
@@ -683,14 +701,44 @@ int rss_csv_hash_file(rss_ctx* ctx, const rss_key* key, const char* in_path, con
     if (!rss_csv_header(ctx->stage[0], first, &layout, &body_off))
         return rss_set_error(RSS_ENOTSUP, "rss_csv_hash_file: header is not canonical");
     const uint64_t blen = len - body_off;
-    if (blen >= 0xFFFFFFFFull)
-        return rss_set_error(RSS_ENOTSUP, "rss_csv_hash_file: body of %llu B exceeds 4 GiB",
-                             (unsigned long long)blen);
-    CsvJob job(s, layout, blen);
-    if ((rc = job.alloc_text())) return rc;
-    // stream the body up: read chunk k+1 into one pinned buffer while chunk k copies
-    // from the other
-    uint64_t file_pos = 0, dev_pos = 0;
+
+    // Stream the body up in line-aligned segments (each below 4 GiB: newline positions
+    // are 32-bit): the pread of chunk k+1 into one pinned buffer overlaps the upload of
+    // chunk k from the other.  When the next chunk might not fit the current segment,
+    // this chunk is cut after its last newline and the rest opens the next segment.
+    // Every segment is parsed, hashed (counts summed here) and formatted in HBM; the rows
+    // are written only after the last one, since the file starts with the counts.
+    const uint64_t seg_cap = segment_bytes();
+    std::vector<std::unique_ptr<CsvJob>> jobs;
+    std::vector<uint64_t> seg_counts(nqueues);
+    memset(counts, 0, sizeof(uint64_t) * nqueues);
+    uint64_t body_left = blen, dev_pos = 0;
+    auto open_segment = [&]() -> int {
+        jobs.emplace_back(new CsvJob(s, layout, body_left < seg_cap ? body_left : seg_cap));
+        dev_pos = 0;
+        return jobs.back()->alloc_text();
+    };
+    auto close_segment = [&]() -> int {
+        CsvJob& job = *jobs.back();
+        job.set_text_len(dev_pos);
+        int r;
+        if ((r = job.parse()) ||
+            (r = job.hash(key, htable, nqueues, reta, want_file, seg_counts.data())))
+            return r;
+        for (uint32_t q = 0; q < nqueues; ++q) counts[q] += seg_counts[q];
+        *n_rows += job.rows();
+        return want_file ? job.format() : RSS_OK;
+    };
+    auto upload = [&](const char* src, size_t bytes) -> int {
+        if (!bytes) return RSS_OK;
+        CSV_HIP_CHECK(hipMemcpyAsync(jobs.back()->text() + dev_pos, src, bytes,
+                                     hipMemcpyHostToDevice, s));
+        dev_pos += bytes;
+        body_left -= bytes;
+        return RSS_OK;
+    };
+    if (blen && (rc = open_segment())) return rc;
+    uint64_t file_pos = 0;
     for (int k = 0; file_pos < len; ++k) {
         const int b = k & 1;
         size_t got;
@@ -702,21 +750,27 @@ int rss_csv_hash_file(rss_ctx* ctx, const rss_key* key, const char* in_path, con
             if (!read_all(in.fd, ctx->stage[b], got, file_pos))
                 return rss_set_error(RSS_EIO, "rss_csv_hash_file: read of %s failed", in_path);
         }
-        const size_t skip = k == 0 ? body_off : 0;
-        const size_t body_bytes = got - skip;
-        if (body_bytes) {
-            CSV_HIP_CHECK(hipMemcpyAsync(job.text() + dev_pos, ctx->stage[b] + skip, body_bytes,
-                                         hipMemcpyHostToDevice, s));
-            dev_pos += body_bytes;
-        }
-        CSV_HIP_CHECK(hipEventRecord(ctx->stage_done[b], s));
+        const char* chunk = ctx->stage[b] + (k == 0 ? body_off : 0);
+        size_t bytes = got - (k == 0 ? body_off : 0);
         file_pos += got;
+        if (bytes && file_pos < len && dev_pos + bytes + kStageBytes > seg_cap) {
+            // cut after this chunk's last newline; the remainder opens the next segment
+            const char* nl = static_cast<const char*>(memrchr(chunk, '\n', bytes));
+            if (!nl)
+                return rss_set_error(RSS_ENOTSUP, "rss_csv_hash_file: a line spans %zu B",
+                                     bytes);
+            const size_t head = (size_t)(nl - chunk) + 1;
+            if ((rc = upload(chunk, head)) || (rc = close_segment()) || (rc = open_segment()))
+                return rc;
+            chunk += head;
+            bytes -= head;
+        }
+        if ((rc = upload(chunk, bytes))) return rc;
+        CSV_HIP_CHECK(hipEventRecord(ctx->stage_done[b], s));
     }
-    if ((rc = job.parse()) || (rc = job.hash(key, htable, nqueues, reta, want_file, counts)))
-        return rc;
-    *n_rows = job.rows();
+    if (jobs.empty()) return rss_set_error(RSS_ENOTSUP, "rss_csv: no data rows");
+    if ((rc = close_segment())) return rc;
     if (!want_file) return RSS_OK;
-    if ((rc = job.format())) return rc;
     Fd outf;
     outf.fd = open(out_path, O_WRONLY | O_CREAT | O_TRUNC, 0666);
     if (outf.fd < 0)  // the pandas path raises the reference's error for this path
@@ -727,26 +781,28 @@ int rss_csv_hash_file(rss_ctx* ctx, const rss_key* key, const char* in_path, con
         if (!write_all(outf.fd, prefix.data(), plen))
             return rss_set_error(RSS_EIO, "rss_csv_hash_file: write to %s failed", out_path);
     }
-    // stream the rows down: chunk k+1 copies into one pinned buffer while chunk k is
-    // written from the other
-    const uint64_t total = job.rows_bytes();
-    const uint64_t nchunks = (total + kStageBytes - 1) / kStageBytes;
-    auto issue = [&](uint64_t k) -> int {
-        const uint64_t a = k * kStageBytes;
-        const size_t bytes = (size_t)(total - a < kStageBytes ? total - a : kStageBytes);
-        CSV_HIP_CHECK(hipMemcpyAsync(ctx->stage[k & 1], job.out() + a, bytes,
-                                     hipMemcpyDeviceToHost, s));
-        CSV_HIP_CHECK(hipEventRecord(ctx->stage_done[k & 1], s));
-        return RSS_OK;
-    };
-    if (nchunks && (rc = issue(0))) return rc;
-    for (uint64_t k = 0; k < nchunks; ++k) {
-        CSV_HIP_CHECK(hipEventSynchronize(ctx->stage_done[k & 1]));
-        if (k + 1 < nchunks && (rc = issue(k + 1))) return rc;
-        const uint64_t a = k * kStageBytes;
-        const size_t bytes = (size_t)(total - a < kStageBytes ? total - a : kStageBytes);
-        if (!write_all(outf.fd, ctx->stage[k & 1], bytes))
-            return rss_set_error(RSS_EIO, "rss_csv_hash_file: write to %s failed", out_path);
+    // stream every segment's rows down: chunk k+1 copies into one pinned buffer while
+    // chunk k is written from the other
+    for (const auto& job : jobs) {
+        const uint64_t total = job->rows_bytes();
+        const uint64_t nchunks = (total + kStageBytes - 1) / kStageBytes;
+        auto issue = [&](uint64_t k) -> int {
+            const uint64_t a = k * kStageBytes;
+            const size_t bytes = (size_t)(total - a < kStageBytes ? total - a : kStageBytes);
+            CSV_HIP_CHECK(hipMemcpyAsync(ctx->stage[k & 1], job->out() + a, bytes,
+                                         hipMemcpyDeviceToHost, s));
+            CSV_HIP_CHECK(hipEventRecord(ctx->stage_done[k & 1], s));
+            return RSS_OK;
+        };
+        if (nchunks && (rc = issue(0))) return rc;
+        for (uint64_t k = 0; k < nchunks; ++k) {
+            CSV_HIP_CHECK(hipEventSynchronize(ctx->stage_done[k & 1]));
+            if (k + 1 < nchunks && (rc = issue(k + 1))) return rc;
+            const uint64_t a = k * kStageBytes;
+            const size_t bytes = (size_t)(total - a < kStageBytes ? total - a : kStageBytes);
+            if (!write_all(outf.fd, ctx->stage[k & 1], bytes))
+                return rss_set_error(RSS_EIO, "rss_csv_hash_file: write to %s failed", out_path);
+        }
     }
     if (close(outf.fd) != 0) {
         outf.fd = -1;

@@ -4,7 +4,7 @@ canonical CSV file --rss_csv_hash_file (text streamed up through pinned staging,
 newline index, parse, hash, format on the device, rows streamed down into the output
 file)--> statistics file, byte-identical to the reference's
 ``write_statistics`` output (``rss_simulator/simulator.py:100-116``).  When the device
-text path declines (body of 4 GiB or more) the host path runs: native parse
+text path declines (RSS_CSV_DEVICE=0) the host path runs: native parse
 (rss_csv_parse) --> rss_hash_host (pinned, chunked H2D -> kernel -> D2H) --> native
 format (rss_csv_format).
 

@@ -191,3 +191,27 @@ def test_file_api_refusals_leave_no_output(native, ctx, example_key, golden_dir,
     counts, n = ctx.csv_hash_file(key, good, str(dst), 128, 24)
     assert n == 100 and dst.read_bytes() == open(
         os.path.join(golden_dir, "example", "out_h128_q24.csv"), "rb").read()
+
+
+@pytest.mark.parametrize("rows,crlf,trailing_nl", [(3_400_000, False, True), (2_000_000, True, False)])
+def test_file_to_file_in_segments(native, ctx, oracle_lib, example_key, tmp_path, monkeypatch,
+                                  rows, crlf, trailing_nl):
+    """Bodies are processed in line-aligned segments below the 4 GiB of 32-bit newline
+    positions (3 GiB by default); RSS_CSV_SEGMENT_BYTES at its 64 MiB + 4 KiB floor cuts
+    these files into 2-3 segments, counts summed across them, rows written in order."""
+    monkeypatch.setenv("RSS_CSV_SEGMENT_BYTES", str((64 << 20) + 4096))
+    rng = random.Random(rows)
+    text = _random_canonical(rng, rows, [3, 1, 0, 2], crlf=crlf, blank_lines=True,
+                             trailing_nl=trailing_nl)
+    src, dst = tmp_path / "in.csv", tmp_path / "out.csv"
+    src.write_bytes(text.encode())
+    assert src.stat().st_size > (64 << 20) + 4096
+    key = native.prepare_key(example_key)
+    counts, n = ctx.csv_hash_file(key, str(src), str(dst), 128, 24)
+    want = host_image(native, oracle_lib, text, example_key, 128, 24)
+    assert n == want[2]
+    np.testing.assert_array_equal(counts, want[1])
+    assert dst.read_bytes() == want[0]
+    c2, n2 = ctx.csv_hash_file(key, str(src), None, 128, 24)  # counts only, segmented too
+    np.testing.assert_array_equal(c2, want[1])
+    assert n2 == n
