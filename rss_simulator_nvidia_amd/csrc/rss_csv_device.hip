@@ -16,6 +16,8 @@
 //   4. hash            -- rss_hash_device / rss_hash_device_reta (rss_toeplitz.hip)
 //   5. format          -- row lengths, exclusive scan, every thread writes its row
 // The header and the per-queue count lines are built on the host (a few hundred bytes).
+// rss_csv_hash_file streams a file through pinned staging and runs the same steps per
+// line-aligned segment below 4 GiB (newline positions are 32-bit), so any file size works.
 #include <hip/hip_runtime.h>
 
 #include <fcntl.h>
