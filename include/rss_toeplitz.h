@@ -296,6 +296,20 @@ int rss_csv_hash_file(rss_ctx* ctx, const rss_key* key, const char* in_path, con
                       uint32_t htable, uint32_t nqueues, const uint32_t* reta, uint32_t flags,
                       uint64_t* counts, size_t* n_rows);
 
+/*
+ * The IPv6 `--ipv6 --csv` job on the device, same contracts as rss_csv_hash_text /
+ * rss_csv_hash_file: rows are the canonical IPv6 form of rss_csv_parse6 (RFC 4291 text,
+ * no embedded IPv4 or zone), hashed with rss_hash6_device (or rss_hash6_device_reta),
+ * and each output row is the input row's own text plus ",hash,queue" -- the bytes
+ * rss_csv_format6 writes, which are the pandas path's (ingest.py / simulator.py:100-115).
+ */
+int rss_csv6_hash_text(rss_ctx* ctx, const rss_key6* key, const char* text, size_t len,
+                       uint32_t htable, uint32_t nqueues, const uint32_t* reta, uint32_t flags,
+                       const char** out, size_t* out_len, uint64_t* counts, size_t* n_rows);
+int rss_csv6_hash_file(rss_ctx* ctx, const rss_key6* key, const char* in_path,
+                       const char* out_path, uint32_t htable, uint32_t nqueues,
+                       const uint32_t* reta, uint32_t flags, uint64_t* counts, size_t* n_rows);
+
 /* rss_key_search_device on host buffers (keys: nkeys prepared keys; h_counts:
  * nkeys x nqueues uint64).  Synchronous. */
 int rss_key_search_host(rss_ctx* ctx, const rss_key* keys, size_t nkeys,

@@ -36,7 +36,7 @@ EXPORTED_SYMBOLS = (
     "rss_pcap_parse", "rss_hash_device_reta", "rss_hash_host_reta", "rss_csv_hash_text",
     "rss_csv_hash_file", "rss_host_alloc", "rss_host_free", "rss_hash_host_multi",
     "rss_pcap_parse6", "rss_hash6_device_reta", "rss_hash6_host_reta", "rss_csv_parse6",
-    "rss_csv_format6_bound", "rss_csv_format6",
+    "rss_csv_format6_bound", "rss_csv_format6", "rss_csv6_hash_text", "rss_csv6_hash_file",
 )
 FIELD_SRC_IP, FIELD_DST_IP, FIELD_SRC_PORT, FIELD_DST_PORT = 1, 2, 4, 8
 FIELDS_IP, FIELDS_ALL = 3, 15
@@ -106,6 +106,12 @@ def _bind(lib):
                                vp, ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
         "rss_csv_hash_file": ([vp, key_p, ctypes.c_char_p, ctypes.c_char_p, u32, u32, vp, u32, vp,
                                ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+        "rss_csv6_hash_text": ([vp, ctypes.POINTER(RssKey6), vp, sz, u32, u32, vp, u32,
+                                ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t),
+                                vp, ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+        "rss_csv6_hash_file": ([vp, ctypes.POINTER(RssKey6), ctypes.c_char_p, ctypes.c_char_p,
+                                u32, u32, vp, u32, vp, ctypes.POINTER(ctypes.c_size_t)],
+                               ctypes.c_int),
         "rss_pcap_parse": ([vp, sz, vp, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)],
                            ctypes.c_int),
         "rss_pcap_parse6": ([vp, sz, vp, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)],
@@ -216,6 +222,16 @@ def prepare_key6(key_bytes, fields=FIELDS_ALL):
     if fields != FIELDS_ALL:
         _check(load().rss_key6_select_fields(ctypes.byref(key), fields), "rss_key6_select_fields")
     return key
+
+
+def _csv_reta(reta, htable):
+    """The CSV device path's indirection table: None, or htable uint32 queue ids."""
+    if reta is None:
+        return None
+    table = np.ascontiguousarray(reta, dtype=np.uint32)
+    if len(table) != htable:
+        raise ValueError("indirection table has %d entries, htable is %d" % (len(table), htable))
+    return table
 
 
 class PinnedBuffer:
@@ -342,26 +358,23 @@ class HostContext:
 
     def csv_hash_text(self, key, data, htable, nqueues, reta=None, counts_only=False):
         """The whole ``--csv`` job on the device for a canonical file image
-        (``rss_csv_hash_text``): returns ``(file_image, counts, n_rows)`` -- file_image a
-        uint8 view of context-owned memory, valid until the next call on this context
-        (None with ``counts_only``) -- or None when the text is not canonical."""
+        (``rss_csv_hash_text``; ``rss_csv6_hash_text`` when ``key`` is an :class:`RssKey6`):
+        returns ``(file_image, counts, n_rows)`` -- file_image a uint8 view of
+        context-owned memory, valid until the next call on this context (None with
+        ``counts_only``) -- or None when the text is not canonical."""
         buf = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data
         counts = np.zeros(nqueues, dtype=np.uint64)
         out, out_len, n = ctypes.c_void_p(), ctypes.c_size_t(0), ctypes.c_size_t(0)
-        table = None
-        if reta is not None:
-            table = np.ascontiguousarray(reta, dtype=np.uint32)
-            if len(table) != htable:
-                raise ValueError("indirection table has %d entries, htable is %d"
-                                 % (len(table), htable))
-        rc = self._lib.rss_csv_hash_text(
+        table = _csv_reta(reta, htable)
+        name = "rss_csv6_hash_text" if isinstance(key, RssKey6) else "rss_csv_hash_text"
+        rc = getattr(self._lib, name)(
             self._ctx, ctypes.byref(key), buf.ctypes.data, len(buf), htable, nqueues,
             table.ctypes.data if table is not None else None,
             FLAG_CSV_COUNTS_ONLY if counts_only else 0, ctypes.byref(out), ctypes.byref(out_len),
             counts.ctypes.data, ctypes.byref(n))
         if rc == ENOTSUP:
             return None
-        _check(rc, "rss_csv_hash_text")
+        _check(rc, name)
         image = None
         if not counts_only:
             image = np.ctypeslib.as_array(ctypes.cast(out, ctypes.POINTER(ctypes.c_uint8)),
@@ -369,26 +382,23 @@ class HostContext:
         return image, counts, n.value
 
     def csv_hash_file(self, key, in_path, out_path, htable, nqueues, reta=None):
-        """``rss_csv_hash_file``: the ``--csv`` job from file to file on the device (no
-        file-sized host buffers).  ``out_path`` None = counts only.  Returns
-        ``(counts, n_rows)``, or None when the file is not canonical or a path cannot be
-        opened (the pandas path then raises the reference's error)."""
+        """``rss_csv_hash_file`` (``rss_csv6_hash_file`` for an :class:`RssKey6`): the
+        ``--csv`` job from file to file on the device (no file-sized host buffers).
+        ``out_path`` None = counts only.  Returns ``(counts, n_rows)``, or None when the
+        file is not canonical or a path cannot be opened (the pandas path then raises the
+        reference's error)."""
         counts = np.zeros(nqueues, dtype=np.uint64)
         n = ctypes.c_size_t(0)
-        table = None
-        if reta is not None:
-            table = np.ascontiguousarray(reta, dtype=np.uint32)
-            if len(table) != htable:
-                raise ValueError("indirection table has %d entries, htable is %d"
-                                 % (len(table), htable))
+        table = _csv_reta(reta, htable)
         enc = lambda p: os.fsencode(p) if p is not None else None  # noqa: E731
-        rc = self._lib.rss_csv_hash_file(
+        name = "rss_csv6_hash_file" if isinstance(key, RssKey6) else "rss_csv_hash_file"
+        rc = getattr(self._lib, name)(
             self._ctx, ctypes.byref(key), enc(in_path), enc(out_path), htable, nqueues,
             table.ctypes.data if table is not None else None,
             FLAG_CSV_COUNTS_ONLY if out_path is None else 0, counts.ctypes.data, ctypes.byref(n))
         if rc == ENOTSUP:
             return None
-        _check(rc, "rss_csv_hash_file")
+        _check(rc, name)
         return counts, n.value
 
     def key_search(self, keys, tuples, htable, nqueues):

@@ -213,7 +213,7 @@ struct Hex6Table {
 constexpr Hex6Table kHex6{};
 
 inline int char_class(const char* p, const char* e) {
-    return p < e ? kHex6.v[(unsigned char)*p] : kEnd;
+    return p < e ? (int)kHex6.v[(unsigned char)*p] : (int)kEnd;
 }
 
 inline int hex_value(char c) {

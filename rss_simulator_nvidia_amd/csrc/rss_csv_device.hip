@@ -28,6 +28,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <type_traits>
 #include <vector>
 
 #include "rss_internal.h"
@@ -235,24 +236,141 @@ __device__ __forceinline__ bool parse_row(const uint8_t* p, const uint8_t* end, 
     return ok && p == end;
 }
 
-// line [p, e) without its '\n': 0 = empty ("", "\r"), 1 = canonical row (-> v), 2 = not
-__device__ __forceinline__ int classify_line(const uint8_t* p, const uint8_t* e, const Layout& layout,
-                                             uint32_t (&v)[4]) {
-    if (e > p && e[-1] == '\r') --e;
-    if (e == p) return 0;
-    return parse_row(p, e, layout, v) ? 1 : 2;
+// ---- IPv6 rows: the scanner of rss_csv.cpp (scan_ip6 / scan_row6) on one line ----
+// character classes of rss_csv.cpp's Hex6Table: 0..15 hex digit, kColon6, kEnd6 (',' '\r'
+// '\n' or the line end), -1 anything else
+constexpr int kColon6 = 16, kEnd6 = 17;
+
+__device__ __forceinline__ int d_class6(const uint8_t* p, const uint8_t* e) {
+    if (p >= e) return kEnd6;
+    const uint32_t c = *p, l = c | 0x20u;
+    if (c - '0' <= 9u) return (int)(c - '0');
+    if (l - 'a' <= 5u) return (int)(l - 'a' + 10);
+    if (c == ':') return kColon6;
+    return (c == ',' || c == '\r' || c == '\n') ? kEnd6 : -1;
 }
 
-// One workgroup parses 256 consecutive lines.  Their text is one contiguous span: it is
-// staged into LDS with coalesced 16-byte loads and parsed from there (a canonical line is
-// <= 45 bytes, 256 of them < 12 KiB); a span over kParseSpan (only possible for
-// non-canonical text) is parsed straight from global memory.
-constexpr uint32_t kParseSpan = 16384;
+// Groups are shifted into a 128-bit accumulator; at '::' the head moves aside and the
+// tail starts from zero, so the address is head << 16 * (8 - gap) | tail (no group array).
+__device__ __forceinline__ bool d_scan_ip6(const uint8_t*& p, const uint8_t* e, uint32_t (&out)[4]) {
+    unsigned __int128 acc = 0, head = 0;
+    int ng = 0, gap = -1;
+    if (p + 1 < e && p[0] == ':' && p[1] == ':') {
+        gap = 0;
+        p += 2;
+    }
+    while (!(gap >= 0 && d_class6(p, e) == kEnd6)) {
+        uint32_t v = 0;
+        int digits = 0, h;
+        while ((h = d_class6(p, e)) >= 0 && h < 16 && digits < 4) {
+            v = v << 4 | (uint32_t)h;
+            ++digits;
+            ++p;
+        }
+        if (digits == 0 || (h >= 0 && h < 16) || ng == 8) return false;
+        acc = acc << 16 | v;
+        ++ng;
+        if (h == kEnd6) break;
+        if (h != kColon6) return false;
+        if (p + 1 < e && p[1] == ':') {
+            if (gap >= 0) return false;
+            gap = ng;
+            head = acc;
+            acc = 0;
+            p += 2;
+        } else {
+            ++p;  // a single ':' must be followed by another group
+        }
+    }
+    if (gap < 0 ? ng != 8 : ng > 7) return false;
+    if (gap > 0) acc |= head << (16 * (8 - gap));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) out[k] = (uint32_t)(acc >> (96 - 32 * k));
+    return true;
+}
 
+// one canonical IPv6 row in [p, end) (line end and one '\r' already cut off)
+__device__ __forceinline__ bool parse_row6(const uint8_t* p, const uint8_t* end, const Layout& layout,
+                                           rss_tuple6& t) {
+    uint32_t a0[4] = {0, 0, 0, 0}, a1[4] = {0, 0, 0, 0}, port0 = 0, port1 = 0;
+    for (int f = 0; f < 4; ++f) {
+        const int c = layout.col[f];
+        if (c < 2) {
+            uint32_t a[4];
+            if (!d_scan_ip6(p, end, a)) return false;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {  // selects, not a dynamically indexed array
+                a0[k] = c == 0 ? a[k] : a0[k];
+                a1[k] = c == 1 ? a[k] : a1[k];
+            }
+        } else {
+            uint32_t v;
+            if (!d_scan_uint<5, 65535>(p, end, v)) return false;
+            port0 = c == 2 ? v : port0;
+            port1 = c == 3 ? v : port1;
+        }
+        if (f < 3) {
+            if (p >= end || *p != ',') return false;
+            ++p;
+        }
+    }
+    if (p != end) return false;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        t.w[k] = a0[k];
+        t.w[4 + k] = a1[k];
+    }
+    t.w[8] = port0 << 16 | port1;
+    return true;
+}
+
+// The two row families of the device path: IPv4 rows are parsed into packed 4-tuples
+// and formatted from them; IPv6 rows keep the byte span of their text, which pandas
+// writes back verbatim (rss_csv.cpp), plus the 36-byte tuple of rss_hash6_device.
+struct Span {
+    uint32_t start, len;  // line text in the segment, without its line end
+};
+
+struct RowsV4 {
+    using Tuple = rss_tuple4;
+    static constexpr uint32_t kParseSpan = 16384;  // 256 canonical lines <= 11.5 KiB
+    __device__ static int classify(const uint8_t* p, const uint8_t* e, const Layout& layout,
+                                   Tuple& t, uint32_t& len) {
+        if (e > p && e[-1] == '\r') --e;
+        if (e == p) return 0;
+        uint32_t v[4];
+        if (!parse_row(p, e, layout, v)) return 2;
+        t.sip = v[0];
+        t.dip = v[1];
+        t.ports = v[2] << 16 | v[3];
+        len = (uint32_t)(e - p);
+        return 1;
+    }
+};
+
+struct RowsV6 {
+    using Tuple = rss_tuple6;
+    static constexpr uint32_t kParseSpan = 24576;  // 256 canonical lines <= 23.3 KiB
+    __device__ static int classify(const uint8_t* p, const uint8_t* e, const Layout& layout,
+                                   Tuple& t, uint32_t& len) {
+        if (e > p && e[-1] == '\r') --e;
+        if (e == p) return 0;
+        if (!parse_row6(p, e, layout, t)) return 2;
+        len = (uint32_t)(e - p);
+        return 1;
+    }
+};
+
+// One workgroup parses 256 consecutive lines.  Their text is one contiguous span: it is
+// staged into LDS with coalesced 16-byte loads and parsed from there (canonical lines fit
+// Rows::kParseSpan); a longer span (only possible for non-canonical text) is parsed
+// straight from global memory.  spans (IPv6 only) gets each row's text span.
+template <class Rows>
 __global__ __launch_bounds__(kThreads) void parse_lines(
     const uint8_t* __restrict__ text, uint64_t len, const uint32_t* __restrict__ pos,
-    uint64_t nnl, uint64_t nlines, Layout layout, rss_tuple4* tuples, uint32_t* is_row,
-    unsigned long long* n_empty, unsigned long long* n_bad) {
+    uint64_t nnl, uint64_t nlines, Layout layout, typename Rows::Tuple* tuples, Span* spans,
+    uint32_t* is_row, unsigned long long* n_empty, unsigned long long* n_bad) {
+    constexpr uint32_t kParseSpan = Rows::kParseSpan;
     __shared__ __attribute__((aligned(16))) uint8_t span[kParseSpan + 32];
     const uint64_t i0 = (uint64_t)blockIdx.x * kThreads;
     const uint64_t i = i0 + threadIdx.x;
@@ -276,11 +394,12 @@ __global__ __launch_bounds__(kThreads) void parse_lines(
     if (i >= nlines) return;
     const uint64_t s = i ? (uint64_t)pos[i - 1] + 1 : 0;
     const uint64_t e = i < nnl ? pos[i] : len;
-    uint32_t v[4];
+    typename Rows::Tuple t;
+    uint32_t row_len = 0;
     // 0 = empty line, 1 = row, 2 = not canonical; the two branches keep LDS and global
     // addressing apart (ds_read vs global_load, no flat loads)
-    const int kind = staged ? classify_line(span + (s - base), span + (e - base), layout, v)
-                            : classify_line(text + s, text + e, layout, v);
+    const int kind = staged ? Rows::classify(span + (s - base), span + (e - base), layout, t, row_len)
+                            : Rows::classify(text + s, text + e, layout, t, row_len);
     if (kind == 0) {  // "\n", "\r\n" or a final "\r": skipped like skip_empty_line
         is_row[i] = 0;
         atomicAdd(n_empty, 1ull);
@@ -292,17 +411,21 @@ __global__ __launch_bounds__(kThreads) void parse_lines(
         return;
     }
     is_row[i] = 1;
-    tuples[i].sip = v[0];
-    tuples[i].dip = v[1];
-    tuples[i].ports = v[2] << 16 | v[3];
+    tuples[i] = t;
+    if (spans) spans[i] = Span{(uint32_t)s, row_len};
 }
 
-__global__ __launch_bounds__(kThreads) void compact_rows(const rss_tuple4* __restrict__ in,
+template <class Tuple>
+__global__ __launch_bounds__(kThreads) void compact_rows(const Tuple* __restrict__ in,
+                                                         const Span* __restrict__ in_spans,
                                                          const uint32_t* __restrict__ is_row,
                                                          const uint64_t* __restrict__ slot,
-                                                         uint64_t nlines, rss_tuple4* out) {
+                                                         uint64_t nlines, Tuple* out,
+                                                         Span* out_spans) {
     const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-    if (i < nlines && is_row[i]) out[slot[i]] = in[i];
+    if (i >= nlines || !is_row[i]) return;
+    out[slot[i]] = in[i];
+    if (in_spans) out_spans[slot[i]] = in_spans[i];
 }
 
 // --------------------------------------------------------------- format ------
@@ -391,6 +514,56 @@ __global__ __launch_bounds__(kThreads) void write_rows(const rss_tuple4* __restr
     for (uint64_t c = threadIdx.x; c < (b16 - a16) / 16; c += kThreads) dst[c] = src[c];
 }
 
+// IPv6 rows: the row's own text (pandas writes the address strings back verbatim),
+// then ",hash,queue\n".  Same LDS-image scheme as write_rows.
+constexpr uint32_t kMaxRow6Bytes = 39 + 1 + 39 + 1 + 5 + 1 + 5 + 1 + 10 + 1 + 10 + 1;  // 114
+
+__global__ __launch_bounds__(kThreads) void row_lengths6(const Span* __restrict__ spans,
+                                                         const uint32_t* __restrict__ hash,
+                                                         const uint32_t* __restrict__ queue,
+                                                         uint64_t n, uint32_t* len) {
+    const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (i >= n) return;
+    len[i] = spans[i].len + d_uint_len(hash[i]) + d_uint_len(queue[i]) + 3;
+}
+
+__global__ __launch_bounds__(kThreads) void write_rows6(const uint8_t* __restrict__ text,
+                                                        const Span* __restrict__ spans,
+                                                        const uint32_t* __restrict__ hash,
+                                                        const uint32_t* __restrict__ queue,
+                                                        uint64_t n, const uint64_t* __restrict__ off,
+                                                        uint64_t total, uint8_t* out) {
+    __shared__ __attribute__((aligned(16))) uint8_t img[kThreads * kMaxRow6Bytes + 32];
+    const uint64_t r0 = (uint64_t)blockIdx.x * kThreads;
+    const uint64_t i = r0 + threadIdx.x;
+    const uint64_t g0 = off[r0];
+    const uint64_t g1 = r0 + kThreads < n ? off[r0 + kThreads] : total;
+    const uint64_t base = g0 & ~15ull;
+    if (i < n) {
+        const Span sp = spans[i];
+        uint8_t* w = img + (off[i] - base);
+        const uint8_t* src = text + sp.start;
+        for (uint32_t k = 0; k < sp.len; ++k) w[k] = src[k];
+        w += sp.len;
+        *w++ = ',';
+        w = d_put_uint(w, hash[i]);
+        *w++ = ',';
+        w = d_put_uint(w, queue[i]);
+        *w = '\n';
+    }
+    __syncthreads();
+    const uint64_t a16 = (g0 + 15) & ~15ull, b16 = g1 & ~15ull;
+    if (a16 >= b16) {
+        for (uint64_t p = g0 + threadIdx.x; p < g1; p += kThreads) out[p] = img[p - base];
+        return;
+    }
+    if (threadIdx.x < a16 - g0) out[g0 + threadIdx.x] = img[g0 + threadIdx.x - base];
+    if (threadIdx.x < g1 - b16) out[b16 + threadIdx.x] = img[b16 + threadIdx.x - base];
+    const uint4* src = reinterpret_cast<const uint4*>(img + (a16 - base));
+    uint4* dst = reinterpret_cast<uint4*>(out + a16);
+    for (uint64_t c = threadIdx.x; c < (b16 - a16) / 16; c += kThreads) dst[c] = src[c];
+}
+
 // ---------------------------------------------------------------- host -------
 inline unsigned blocks_for(uint64_t n, uint64_t per_block) {
     return (unsigned)((n + per_block - 1) / per_block);
@@ -408,7 +581,7 @@ struct DeviceBuffers {
         const hipError_t e = hipMalloc(&p, count ? count * sizeof(T) : 1);
         if (e != hipSuccess)
             return rss_set_error(e == hipErrorOutOfMemory ? RSS_ENOMEM : RSS_EIO,
-                                 "rss_csv_hash_text: hipMalloc(%llu B): %s",
+                                 "rss_csv: hipMalloc(%llu B): %s",
                                  (unsigned long long)(count * sizeof(T)), hipGetErrorString(e));
         ptrs.push_back(p);
         *out = static_cast<T*>(p);
@@ -438,8 +611,15 @@ int exclusive_scan(const uint32_t* in, uint64_t n, uint64_t* out, uint64_t* h_to
 
 // One CSV job on the device: the body text (uploaded by the caller into text()) ->
 // rows -> hash / queue / counts -> formatted rows.  Buffers live until destruction.
+// Rows = RowsV4 (rss_hash_device, rows re-formatted from the tuples) or RowsV6
+// (rss_hash6_device, rows copied from their text spans).
+template <class Rows>
 class CsvJob {
   public:
+    static constexpr bool kV6 = std::is_same<Rows, RowsV6>::value;
+    using Tuple = typename Rows::Tuple;
+    using Key = typename std::conditional<kV6, rss_key6, rss_key>::type;
+
     CsvJob(hipStream_t s, const rss_csv_layout& layout, uint64_t blen) : s_(s), blen_(blen) {
         memcpy(lay_.col, layout.field_column, 4);
     }
@@ -472,17 +652,18 @@ class CsvJob {
         const uint64_t tail_start = nnl ? (uint64_t)last_nl + 1 : 0;
         const uint64_t nlines = nnl + (tail_start < blen_ ? 1 : 0);
 
-        rss_tuple4* d_lines;
+        Tuple* d_lines;
+        Span* d_line_spans = nullptr;
         uint32_t* d_is_row;
         unsigned long long* d_stat;  // [0] empty lines, [1] non-canonical lines
         if ((rc = buf_.alloc(&d_lines, nlines)) || (rc = buf_.alloc(&d_is_row, nlines)) ||
-            (rc = buf_.alloc(&d_stat, 2)))
+            (rc = buf_.alloc(&d_stat, 2)) || (kV6 && (rc = buf_.alloc(&d_line_spans, nlines))))
             return rc;
         CSV_HIP_CHECK(hipMemsetAsync(d_stat, 0, 2 * sizeof(unsigned long long), s_));
         if (nlines)
-            hipLaunchKernelGGL(parse_lines, dim3(blocks_for(nlines, kThreads)), dim3(kThreads), 0,
-                               s_, d_text_, blen_, d_pos, nnl, nlines, lay_, d_lines, d_is_row,
-                               d_stat, d_stat + 1);
+            hipLaunchKernelGGL(parse_lines<Rows>, dim3(blocks_for(nlines, kThreads)), dim3(kThreads),
+                               0, s_, d_text_, blen_, d_pos, nnl, nlines, lay_, d_lines,
+                               d_line_spans, d_is_row, d_stat, d_stat + 1);
         CSV_HIP_CHECK(hipGetLastError());
         unsigned long long stat[2];
         CSV_HIP_CHECK(hipMemcpyAsync(stat, d_stat, sizeof stat, hipMemcpyDeviceToHost, s_));
@@ -492,29 +673,39 @@ class CsvJob {
         n_ = nlines - stat[0];
         if (n_ == 0) return rss_set_error(RSS_ENOTSUP, "rss_csv: no data rows");
         d_tuples_ = d_lines;
+        d_spans_ = d_line_spans;
         if (stat[0]) {
             uint64_t* d_slot;
             uint64_t kept;
-            if ((rc = buf_.alloc(&d_slot, nlines)) || (rc = buf_.alloc(&d_tuples_, n_))) return rc;
+            if ((rc = buf_.alloc(&d_slot, nlines)) || (rc = buf_.alloc(&d_tuples_, n_)) ||
+                (kV6 && (rc = buf_.alloc(&d_spans_, n_))))
+                return rc;
             if ((rc = exclusive_scan(d_is_row, nlines, d_slot, &kept, buf_, s_))) return rc;
-            hipLaunchKernelGGL(compact_rows, dim3(blocks_for(nlines, kThreads)), dim3(kThreads), 0,
-                               s_, d_lines, d_is_row, d_slot, nlines, d_tuples_);
+            hipLaunchKernelGGL(compact_rows<Tuple>, dim3(blocks_for(nlines, kThreads)),
+                               dim3(kThreads), 0, s_, d_lines, d_line_spans, d_is_row, d_slot,
+                               nlines, d_tuples_, d_spans_);
             CSV_HIP_CHECK(hipGetLastError());
         }
         return RSS_OK;
     }
 
-    int hash(const rss_key* key, uint32_t htable, uint32_t nqueues, const uint32_t* reta,
+    int hash(const Key* key, uint32_t htable, uint32_t nqueues, const uint32_t* reta,
              bool want_rows, uint64_t* h_counts) {
         int rc;
         uint64_t* d_counts;
         if ((rc = buf_.alloc(&d_counts, nqueues))) return rc;
         if (want_rows && ((rc = buf_.alloc(&d_hash_, n_)) || (rc = buf_.alloc(&d_queue_, n_))))
             return rc;
-        rc = reta ? rss_hash_device_reta(key, d_tuples_, n_, htable, reta, nqueues, d_hash_,
-                                         d_queue_, d_counts, 0, s_)
-                  : rss_hash_device(key, d_tuples_, n_, htable, nqueues, d_hash_, d_queue_,
-                                    d_counts, 0, s_);
+        if constexpr (kV6)
+            rc = reta ? rss_hash6_device_reta(key, d_tuples_, n_, htable, reta, nqueues, d_hash_,
+                                              d_queue_, d_counts, 0, s_)
+                      : rss_hash6_device(key, d_tuples_, n_, htable, nqueues, d_hash_, d_queue_,
+                                         d_counts, 0, s_);
+        else
+            rc = reta ? rss_hash_device_reta(key, d_tuples_, n_, htable, reta, nqueues, d_hash_,
+                                             d_queue_, d_counts, 0, s_)
+                      : rss_hash_device(key, d_tuples_, n_, htable, nqueues, d_hash_, d_queue_,
+                                        d_counts, 0, s_);
         if (rc) return rc;
         CSV_HIP_CHECK(hipMemcpyAsync(h_counts, d_counts, sizeof(uint64_t) * nqueues,
                                      hipMemcpyDeviceToHost, s_));
@@ -528,13 +719,21 @@ class CsvJob {
         uint32_t* d_len;
         uint64_t* d_off;
         if ((rc = buf_.alloc(&d_len, n_)) || (rc = buf_.alloc(&d_off, n_))) return rc;
-        hipLaunchKernelGGL(row_lengths, dim3(blocks_for(n_, kThreads)), dim3(kThreads), 0, s_,
-                           d_tuples_, d_hash_, d_queue_, n_, d_len);
+        if constexpr (kV6)
+            hipLaunchKernelGGL(row_lengths6, dim3(blocks_for(n_, kThreads)), dim3(kThreads), 0, s_,
+                               d_spans_, d_hash_, d_queue_, n_, d_len);
+        else
+            hipLaunchKernelGGL(row_lengths, dim3(blocks_for(n_, kThreads)), dim3(kThreads), 0, s_,
+                               d_tuples_, d_hash_, d_queue_, n_, d_len);
         CSV_HIP_CHECK(hipGetLastError());
         if ((rc = exclusive_scan(d_len, n_, d_off, &rows_bytes_, buf_, s_))) return rc;
         if ((rc = buf_.alloc(&d_out_, rows_bytes_))) return rc;
-        hipLaunchKernelGGL(write_rows, dim3(blocks_for(n_, kThreads)), dim3(kThreads), 0, s_,
-                           d_tuples_, d_hash_, d_queue_, n_, lay_, d_off, rows_bytes_, d_out_);
+        if constexpr (kV6)
+            hipLaunchKernelGGL(write_rows6, dim3(blocks_for(n_, kThreads)), dim3(kThreads), 0, s_,
+                               d_text_, d_spans_, d_hash_, d_queue_, n_, d_off, rows_bytes_, d_out_);
+        else
+            hipLaunchKernelGGL(write_rows, dim3(blocks_for(n_, kThreads)), dim3(kThreads), 0, s_,
+                               d_tuples_, d_hash_, d_queue_, n_, lay_, d_off, rows_bytes_, d_out_);
         CSV_HIP_CHECK(hipGetLastError());
         return RSS_OK;
     }
@@ -549,14 +748,16 @@ class CsvJob {
     Layout lay_;
     DeviceBuffers buf_;
     uint8_t* d_text_ = nullptr;
-    rss_tuple4* d_tuples_ = nullptr;
+    Tuple* d_tuples_ = nullptr;
+    Span* d_spans_ = nullptr;
     uint32_t* d_hash_ = nullptr;
     uint32_t* d_queue_ = nullptr;
     uint8_t* d_out_ = nullptr;
     uint64_t n_ = 0, rows_bytes_ = 0;
 };
 
-int check_args(const rss_key* key, uint32_t htable, uint32_t nqueues) {
+template <class Key>
+int check_args(const Key* key, uint32_t htable, uint32_t nqueues) {
     if (!key) return rss_set_error(RSS_EINVAL, "rss_csv: key is NULL");
     if (htable < 1 || nqueues < 1)
         return rss_set_error(RSS_EINVAL, "rss_csv: htable (%u) and nqueues (%u) must be >= 1",
@@ -621,42 +822,30 @@ struct Fd {
     }
 };
 
-}  // namespace
-
-void rss_csv_release(rss_ctx* ctx) {
-    for (int b = 0; b < 2; ++b) {
-        if (ctx->stage[b]) (void)hipHostFree(ctx->stage[b]);
-        if (ctx->stage_done[b]) (void)hipEventDestroy(ctx->stage_done[b]);
-        ctx->stage[b] = nullptr;
-        ctx->stage_done[b] = nullptr;
-    }
-    ctx->stage_bytes = 0;
-}
-
-extern "C" {
-
-int rss_csv_hash_text(rss_ctx* ctx, const rss_key* key, const char* text, size_t len,
-                      uint32_t htable, uint32_t nqueues, const uint32_t* reta, uint32_t flags,
-                      const char** out, size_t* out_len, uint64_t* counts, size_t* n_rows) {
+template <class Rows>
+int csv_hash_text(const char* who, rss_ctx* ctx, const typename CsvJob<Rows>::Key* key,
+                  const char* text, size_t len, uint32_t htable, uint32_t nqueues,
+                  const uint32_t* reta, uint32_t flags, const char** out, size_t* out_len,
+                  uint64_t* counts, size_t* n_rows) {
     if (!ctx || !text || !counts || !n_rows)
-        return rss_set_error(RSS_EINVAL, "rss_csv_hash_text: NULL argument");
+        return rss_set_error(RSS_EINVAL, "%s: NULL argument", who);
     const bool want_file = !(flags & RSS_CSV_COUNTS_ONLY);
     if (want_file && (!out || !out_len))
-        return rss_set_error(RSS_EINVAL, "rss_csv_hash_text: out / out_len NULL");
+        return rss_set_error(RSS_EINVAL, "%s: out / out_len NULL", who);
     int rc = check_args(key, htable, nqueues);
     if (rc) return rc;
     *n_rows = 0;
     rss_csv_layout layout;
     size_t body_off;
     if (!rss_csv_header(text, len, &layout, &body_off))
-        return rss_set_error(RSS_ENOTSUP, "rss_csv_hash_text: header is not canonical");
+        return rss_set_error(RSS_ENOTSUP, "%s: header is not canonical", who);
     const uint64_t blen = len - body_off;
     if (blen >= 0xFFFFFFFFull)  // newline positions are 32-bit
-        return rss_set_error(RSS_ENOTSUP, "rss_csv_hash_text: body of %llu B exceeds 4 GiB",
+        return rss_set_error(RSS_ENOTSUP, "%s: body of %llu B exceeds 4 GiB", who,
                              (unsigned long long)blen);
     CSV_HIP_CHECK(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream[0];
-    CsvJob job(s, layout, blen);
+    CsvJob<Rows> job(s, layout, blen);
     if ((rc = job.alloc_text())) return rc;
     CSV_HIP_CHECK(hipMemcpyAsync(job.text(), text + body_off, blen, hipMemcpyHostToDevice, s));
     if ((rc = job.parse()) || (rc = job.hash(key, htable, nqueues, reta, want_file, counts)))
@@ -674,14 +863,15 @@ int rss_csv_hash_text(rss_ctx* ctx, const rss_key* key, const char* text, size_t
     return RSS_OK;
 }
 
-int rss_csv_hash_file(rss_ctx* ctx, const rss_key* key, const char* in_path, const char* out_path,
-                      uint32_t htable, uint32_t nqueues, const uint32_t* reta, uint32_t flags,
-                      uint64_t* counts, size_t* n_rows) {
+template <class Rows>
+int csv_hash_file(const char* who, rss_ctx* ctx, const typename CsvJob<Rows>::Key* key,
+                  const char* in_path, const char* out_path, uint32_t htable, uint32_t nqueues,
+                  const uint32_t* reta, uint32_t flags, uint64_t* counts, size_t* n_rows) {
     if (!ctx || !in_path || !counts || !n_rows)
-        return rss_set_error(RSS_EINVAL, "rss_csv_hash_file: NULL argument");
+        return rss_set_error(RSS_EINVAL, "%s: NULL argument", who);
     const bool want_file = !(flags & RSS_CSV_COUNTS_ONLY);
     if (want_file && !out_path)
-        return rss_set_error(RSS_EINVAL, "rss_csv_hash_file: out_path NULL");
+        return rss_set_error(RSS_EINVAL, "%s: out_path NULL", who);
     int rc = check_args(key, htable, nqueues);
     if (rc) return rc;
     *n_rows = 0;
@@ -692,16 +882,16 @@ int rss_csv_hash_file(rss_ctx* ctx, const rss_key* key, const char* in_path, con
     in.fd = open(in_path, O_RDONLY);
     struct stat st;
     if (in.fd < 0 || fstat(in.fd, &st) != 0 || !S_ISREG(st.st_mode))
-        return rss_set_error(RSS_ENOTSUP, "rss_csv_hash_file: cannot read %s", in_path);
+        return rss_set_error(RSS_ENOTSUP, "%s: cannot read %s", who, in_path);
     const uint64_t len = (uint64_t)st.st_size;
     // the header must sit in the first staging buffer (a canonical one is < 64 B)
     const size_t first = (size_t)(len < kStageBytes ? len : kStageBytes);
     if (!read_all(in.fd, ctx->stage[0], first, 0))
-        return rss_set_error(RSS_ENOTSUP, "rss_csv_hash_file: cannot read %s", in_path);
+        return rss_set_error(RSS_ENOTSUP, "%s: cannot read %s", who, in_path);
     rss_csv_layout layout;
     size_t body_off;
     if (!rss_csv_header(ctx->stage[0], first, &layout, &body_off))
-        return rss_set_error(RSS_ENOTSUP, "rss_csv_hash_file: header is not canonical");
+        return rss_set_error(RSS_ENOTSUP, "%s: header is not canonical", who);
     const uint64_t blen = len - body_off;
 
     // Stream the body up in line-aligned segments (each below 4 GiB: newline positions
@@ -711,17 +901,17 @@ int rss_csv_hash_file(rss_ctx* ctx, const rss_key* key, const char* in_path, con
     // Every segment is parsed, hashed (counts summed here) and formatted in HBM; the rows
     // are written only after the last one, since the file starts with the counts.
     const uint64_t seg_cap = segment_bytes();
-    std::vector<std::unique_ptr<CsvJob>> jobs;
+    std::vector<std::unique_ptr<CsvJob<Rows>>> jobs;
     std::vector<uint64_t> seg_counts(nqueues);
     memset(counts, 0, sizeof(uint64_t) * nqueues);
     uint64_t body_left = blen, dev_pos = 0;
     auto open_segment = [&]() -> int {
-        jobs.emplace_back(new CsvJob(s, layout, body_left < seg_cap ? body_left : seg_cap));
+        jobs.emplace_back(new CsvJob<Rows>(s, layout, body_left < seg_cap ? body_left : seg_cap));
         dev_pos = 0;
         return jobs.back()->alloc_text();
     };
     auto close_segment = [&]() -> int {
-        CsvJob& job = *jobs.back();
+        CsvJob<Rows>& job = *jobs.back();
         job.set_text_len(dev_pos);
         int r;
         if ((r = job.parse()) ||
@@ -750,7 +940,7 @@ int rss_csv_hash_file(rss_ctx* ctx, const rss_key* key, const char* in_path, con
             CSV_HIP_CHECK(hipEventSynchronize(ctx->stage_done[b]));  // buffer b is free again
             got = (size_t)(len - file_pos < kStageBytes ? len - file_pos : kStageBytes);
             if (!read_all(in.fd, ctx->stage[b], got, file_pos))
-                return rss_set_error(RSS_EIO, "rss_csv_hash_file: read of %s failed", in_path);
+                return rss_set_error(RSS_EIO, "%s: read of %s failed", who, in_path);
         }
         const char* chunk = ctx->stage[b] + (k == 0 ? body_off : 0);
         size_t bytes = got - (k == 0 ? body_off : 0);
@@ -759,7 +949,7 @@ int rss_csv_hash_file(rss_ctx* ctx, const rss_key* key, const char* in_path, con
             // cut after this chunk's last newline; the remainder opens the next segment
             const char* nl = static_cast<const char*>(memrchr(chunk, '\n', bytes));
             if (!nl)
-                return rss_set_error(RSS_ENOTSUP, "rss_csv_hash_file: a line spans %zu B",
+                return rss_set_error(RSS_ENOTSUP, "%s: a line spans %zu B", who,
                                      bytes);
             const size_t head = (size_t)(nl - chunk) + 1;
             if ((rc = upload(chunk, head)) || (rc = close_segment()) || (rc = open_segment()))
@@ -776,12 +966,12 @@ int rss_csv_hash_file(rss_ctx* ctx, const rss_key* key, const char* in_path, con
     Fd outf;
     outf.fd = open(out_path, O_WRONLY | O_CREAT | O_TRUNC, 0666);
     if (outf.fd < 0)  // the pandas path raises the reference's error for this path
-        return rss_set_error(RSS_ENOTSUP, "rss_csv_hash_file: cannot create %s", out_path);
+        return rss_set_error(RSS_ENOTSUP, "%s: cannot create %s", who, out_path);
     {
         std::vector<char> prefix(rss_csv_prefix_bound(nqueues));
         const size_t plen = rss_csv_format_prefix(counts, nqueues, &layout, prefix.data());
         if (!write_all(outf.fd, prefix.data(), plen))
-            return rss_set_error(RSS_EIO, "rss_csv_hash_file: write to %s failed", out_path);
+            return rss_set_error(RSS_EIO, "%s: write to %s failed", who, out_path);
     }
     // stream every segment's rows down: chunk k+1 copies into one pinned buffer while
     // chunk k is written from the other
@@ -803,15 +993,58 @@ int rss_csv_hash_file(rss_ctx* ctx, const rss_key* key, const char* in_path, con
             const uint64_t a = k * kStageBytes;
             const size_t bytes = (size_t)(total - a < kStageBytes ? total - a : kStageBytes);
             if (!write_all(outf.fd, ctx->stage[k & 1], bytes))
-                return rss_set_error(RSS_EIO, "rss_csv_hash_file: write to %s failed", out_path);
+                return rss_set_error(RSS_EIO, "%s: write to %s failed", who, out_path);
         }
     }
     if (close(outf.fd) != 0) {
         outf.fd = -1;
-        return rss_set_error(RSS_EIO, "rss_csv_hash_file: close of %s failed", out_path);
+        return rss_set_error(RSS_EIO, "%s: close of %s failed", who, out_path);
     }
     outf.fd = -1;
     return RSS_OK;
 }
 
+}  // namespace
+
+extern "C" {
+
+int rss_csv_hash_text(rss_ctx* ctx, const rss_key* key, const char* text, size_t len,
+                      uint32_t htable, uint32_t nqueues, const uint32_t* reta, uint32_t flags,
+                      const char** out, size_t* out_len, uint64_t* counts, size_t* n_rows) {
+    return csv_hash_text<RowsV4>("rss_csv_hash_text", ctx, key, text, len, htable, nqueues, reta,
+                                 flags, out, out_len, counts, n_rows);
+}
+
+int rss_csv6_hash_text(rss_ctx* ctx, const rss_key6* key, const char* text, size_t len,
+                       uint32_t htable, uint32_t nqueues, const uint32_t* reta, uint32_t flags,
+                       const char** out, size_t* out_len, uint64_t* counts, size_t* n_rows) {
+    return csv_hash_text<RowsV6>("rss_csv6_hash_text", ctx, key, text, len, htable, nqueues,
+                                 reta, flags, out, out_len, counts, n_rows);
+}
+
+int rss_csv_hash_file(rss_ctx* ctx, const rss_key* key, const char* in_path, const char* out_path,
+                      uint32_t htable, uint32_t nqueues, const uint32_t* reta, uint32_t flags,
+                      uint64_t* counts, size_t* n_rows) {
+    return csv_hash_file<RowsV4>("rss_csv_hash_file", ctx, key, in_path, out_path, htable,
+                                 nqueues, reta, flags, counts, n_rows);
+}
+
+int rss_csv6_hash_file(rss_ctx* ctx, const rss_key6* key, const char* in_path,
+                       const char* out_path, uint32_t htable, uint32_t nqueues,
+                       const uint32_t* reta, uint32_t flags, uint64_t* counts, size_t* n_rows) {
+    return csv_hash_file<RowsV6>("rss_csv6_hash_file", ctx, key, in_path, out_path, htable,
+                                 nqueues, reta, flags, counts, n_rows);
+}
+
 }  // extern "C"
+
+void rss_csv_release(rss_ctx* ctx) {
+    for (int b = 0; b < 2; ++b) {
+        if (ctx->stage[b]) (void)hipHostFree(ctx->stage[b]);
+        if (ctx->stage_done[b]) (void)hipEventDestroy(ctx->stage_done[b]);
+        ctx->stage[b] = nullptr;
+        ctx->stage_done[b] = nullptr;
+    }
+    ctx->stage_bytes = 0;
+}
+

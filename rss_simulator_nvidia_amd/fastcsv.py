@@ -97,9 +97,23 @@ def run_counts(hash_key, ips_file, htable, nqueues, threads=0, fields=_native.FI
 
 def run_csv6(hash_key, ips_file, htable, nqueues, output, threads=0, timings=None,
              fields=_native.FIELDS_ALL, reta=None):
-    """``--ipv6 --csv`` for a canonical IPv6 file: native parse (rss_csv_parse6) -> the
-    IPv6 kernel (rss_hash6_host) -> native format (rss_csv_format6, rows copied from the
-    input text).  False if the file needs the pandas path."""
+    """``--ipv6 --csv`` for a canonical IPv6 file: the whole job on the device
+    (rss_csv6_hash_file: newline index, parse, rss_hash6_device, rows copied from the
+    input text), or with RSS_CSV_DEVICE=0 native parse (rss_csv_parse6) -> the IPv6
+    kernel (rss_hash6_host) -> native format (rss_csv_format6).  False if the file needs
+    the pandas path."""
+    t = [time.perf_counter()]
+    key6 = _native.prepare_key6(hash_key, fields)
+    ctx = _native.default_context()
+    if device_text_enabled():
+        done = ctx.csv_hash_file(key6, ips_file, output, htable, nqueues, reta=reta)
+        if done is not None:
+            if timings is not None:
+                timings.update(device_file=time.perf_counter() - t[0], rows=done[1],
+                               bytes_in=os.path.getsize(ips_file),
+                               bytes_out=os.path.getsize(output), path="device6")
+            print("Wrote statistics to {csv}.".format(csv=output))
+            return True
     t = [time.perf_counter()]
     try:
         data = np.fromfile(ips_file, dtype=np.uint8)
@@ -111,8 +125,7 @@ def run_csv6(hash_key, ips_file, htable, nqueues, output, threads=0, timings=Non
         return False
     tuples, spans, layout = parsed
     t.append(time.perf_counter())
-    key6 = _native.prepare_key6(hash_key, fields)
-    h, q, c = _native.default_context().hash6(key6, tuples, htable, nqueues, reta=reta)
+    h, q, c = ctx.hash6(key6, tuples, htable, nqueues, reta=reta)
     t.append(time.perf_counter())
     out = _native.csv_format6(data, spans, h, q, c, layout, threads)
     t.append(time.perf_counter())
@@ -132,6 +145,12 @@ def run_csv6(hash_key, ips_file, htable, nqueues, output, threads=0, timings=Non
 def run_counts6(hash_key, ips_file, htable, nqueues, threads=0, fields=_native.FIELDS_ALL,
                 reta=None):
     """Per-queue counts of a canonical IPv6 file; None if it needs the pandas path."""
+    key6 = _native.prepare_key6(hash_key, fields)
+    ctx = _native.default_context()
+    if device_text_enabled():
+        done = ctx.csv_hash_file(key6, ips_file, None, htable, nqueues, reta=reta)
+        if done is not None:
+            return done[0]
     try:
         data = np.fromfile(ips_file, dtype=np.uint8)
     except (OSError, ValueError):
@@ -139,7 +158,6 @@ def run_counts6(hash_key, ips_file, htable, nqueues, threads=0, fields=_native.F
     parsed = _native.csv_parse6(data, threads)
     if parsed is None:
         return None
-    key6 = _native.prepare_key6(hash_key, fields)
-    _, _, counts = _native.default_context().hash6(key6, parsed[0], htable, nqueues,
-                                                   want_hash=False, want_queue=False, reta=reta)
+    _, _, counts = ctx.hash6(key6, parsed[0], htable, nqueues, want_hash=False,
+                             want_queue=False, reta=reta)
     return counts

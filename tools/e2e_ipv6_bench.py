@@ -1,6 +1,7 @@
-"""IPv6 CSV -> CSV rates (tool, not product): the native IPv6 path (rss_csv_parse6 ->
-IPv6 kernel -> rss_csv_format6) against the pandas path (RSS_CSV_FASTPATH=0) on a
-smaller file; both outputs of the small file must be identical.  Prints one JSON object.
+"""IPv6 CSV -> CSV rates (tool, not product): the device text path (rss_csv6_hash_file)
+and the host text path (RSS_CSV_DEVICE=0: rss_csv_parse6 -> IPv6 kernel ->
+rss_csv_format6) on the big file -- outputs must be identical -- and the pandas path
+(RSS_CSV_FASTPATH=0) on a smaller file.  Prints one JSON object.
 usage: python tools/e2e_ipv6_bench.py [ROWS] [PANDAS_ROWS] [WORKDIR]"""
 import json
 import os
@@ -43,21 +44,29 @@ key = [int(x, 16) for x in EXAMPLE_KEY.split(":")]
 H, Q = 128, 24
 result = {"rows": rows, "htable": H, "queues": Q, "generate_s": gen_s}
 _native.default_context()
-runs = []
-for _ in range(2):
-    out = os.path.join(work, "out_big6.csv")
-    if os.path.exists(out):
-        os.unlink(out)
-    t = {}
-    t0 = time.perf_counter()
-    assert fastcsv.run_csv6(key, big, H, Q, out, timings=t)
-    runs.append((time.perf_counter() - t0, t))
-wall, t = runs[-1]
-result["csv6_fastpath"] = {"wall_s": wall, "rows_per_s": rows / wall,
-                           "first_call_wall_s": runs[0][0],
-                           "stages_s": {k: v for k, v in t.items()
-                                        if k in ("read", "parse", "gpu", "format", "write")},
-                           "bytes_in": t["bytes_in"], "bytes_out": t["bytes_out"]}
+outputs = {}
+for dev, name in (("1", "csv6_device"), ("0", "csv6_fastpath")):
+    os.environ["RSS_CSV_DEVICE"] = dev
+    runs = []
+    out = os.path.join(work, "out_big6_%s.csv" % dev)
+    for _ in range(3):
+        if os.path.exists(out):
+            os.unlink(out)
+        t = {}
+        t0 = time.perf_counter()
+        assert fastcsv.run_csv6(key, big, H, Q, out, timings=t)
+        runs.append((time.perf_counter() - t0, t))
+    wall, t = min(runs[1:], key=lambda r: r[0])
+    result[name] = {"path": t["path"], "wall_s": wall, "rows_per_s": rows / wall,
+                    "first_call_wall_s": runs[0][0],
+                    "stages_s": {k: v for k, v in t.items()
+                                 if k in ("read", "parse", "gpu", "format", "write")},
+                    "bytes_in": t["bytes_in"], "bytes_out": t["bytes_out"]}
+    with open(out, "rb") as f:
+        outputs[dev] = hash(f.read())
+os.environ["RSS_CSV_DEVICE"] = "1"
+result["big_outputs_identical"] = outputs["1"] == outputs["0"]
+assert result["big_outputs_identical"]
 from rss_simulator_nvidia_amd.main import main as cli_main  # noqa: E402
 outs = {}
 for fast in ("1", "0"):
