@@ -24,10 +24,14 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <cerrno>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <thread>
 #include <type_traits>
 #include <vector>
 
@@ -569,24 +573,71 @@ inline unsigned blocks_for(uint64_t n, uint64_t per_block) {
     return (unsigned)((n + per_block - 1) / per_block);
 }
 
-// device allocations of one call, released on every exit path
+// Device allocations of one call, released on every exit path: back to the context's pool
+// (rss_ctx::csv_pool), where the next call finds them, rather than to hipFree.  A fresh
+// multi-GB hipMalloc maps new pages -- 10-25 ms of a 120 ms file job (RSS_CSV_TIMING) --
+// while a pooled block costs nothing.  The pool is trimmed to kPoolBytes after every call
+// (largest blocks first) and emptied when an allocation runs out of memory.  Reuse is
+// stream-ordered: every call on a context runs on its stream[0].
+constexpr size_t kPoolBytes = 8ull << 30;
+
+void trim_pool(rss_ctx* ctx, size_t cap) {
+    auto& pool = ctx->csv_pool;
+    size_t total = 0;
+    for (const auto& b : pool) total += b.second;
+    while (total > cap && !pool.empty()) {
+        size_t big = 0;
+        for (size_t k = 1; k < pool.size(); ++k)
+            if (pool[k].second > pool[big].second) big = k;
+        (void)hipFree(pool[big].first);
+        total -= pool[big].second;
+        pool.erase(pool.begin() + big);
+    }
+}
+
 struct DeviceBuffers {
-    std::vector<void*> ptrs;
+    explicit DeviceBuffers(rss_ctx* ctx) : ctx_(ctx) {}
+    DeviceBuffers(const DeviceBuffers&) = delete;
+    DeviceBuffers& operator=(const DeviceBuffers&) = delete;
     ~DeviceBuffers() {
-        for (void* p : ptrs) (void)hipFree(p);
+        for (const auto& b : blocks_) ctx_->csv_pool.push_back(b);
+        trim_pool(ctx_, kPoolBytes);
     }
     template <typename T>
     int alloc(T** out, uint64_t count) {
+        const size_t bytes = count ? count * sizeof(T) : 1;
+        // best fit among pooled blocks no more than twice (+1 MiB) the request
+        auto& pool = ctx_->csv_pool;
+        size_t pick = pool.size();
+        for (size_t k = 0; k < pool.size(); ++k)
+            if (pool[k].second >= bytes && pool[k].second <= 2 * bytes + (1u << 20) &&
+                (pick == pool.size() || pool[k].second < pool[pick].second))
+                pick = k;
+        if (pick < pool.size()) {
+            blocks_.push_back(pool[pick]);
+            pool.erase(pool.begin() + pick);
+            *out = static_cast<T*>(blocks_.back().first);
+            return RSS_OK;
+        }
         void* p = nullptr;
-        const hipError_t e = hipMalloc(&p, count ? count * sizeof(T) : 1);
+        hipError_t e = hipMalloc(&p, bytes);
+        if (e == hipErrorOutOfMemory && !pool.empty()) {
+            (void)hipGetLastError();
+            trim_pool(ctx_, 0);
+            e = hipMalloc(&p, bytes);
+        }
         if (e != hipSuccess)
             return rss_set_error(e == hipErrorOutOfMemory ? RSS_ENOMEM : RSS_EIO,
-                                 "rss_csv: hipMalloc(%llu B): %s",
-                                 (unsigned long long)(count * sizeof(T)), hipGetErrorString(e));
-        ptrs.push_back(p);
+                                 "rss_csv: hipMalloc(%llu B): %s", (unsigned long long)bytes,
+                                 hipGetErrorString(e));
+        blocks_.emplace_back(p, bytes);
         *out = static_cast<T*>(p);
         return RSS_OK;
     }
+
+  private:
+    rss_ctx* ctx_;
+    std::vector<std::pair<void*, size_t>> blocks_;
 };
 
 int exclusive_scan(const uint32_t* in, uint64_t n, uint64_t* out, uint64_t* h_total,
@@ -620,7 +671,8 @@ class CsvJob {
     using Tuple = typename Rows::Tuple;
     using Key = typename std::conditional<kV6, rss_key6, rss_key>::type;
 
-    CsvJob(hipStream_t s, const rss_csv_layout& layout, uint64_t blen) : s_(s), blen_(blen) {
+    CsvJob(rss_ctx* ctx, const rss_csv_layout& layout, uint64_t blen)
+        : s_(ctx->stream[0]), blen_(blen), buf_(ctx) {
         memcpy(lay_.col, layout.field_column, 4);
     }
     int alloc_text() { return buf_.alloc(&d_text_, blen_); }
@@ -804,6 +856,29 @@ bool read_all(int fd, char* dst, size_t len, uint64_t off) {
     return true;
 }
 
+// pread of [off, off + len) split over up to kReadThreads threads: page-cache reads scale
+// with threads (one thread ≈20 GB/s, four ≈60 GB/s on the GPU box; tools/io_probe.py), so
+// the file read stops being slower than the PCIe upload it feeds.  Writes do not scale
+// (≈10 GB/s from any number of threads) and stay single-threaded.
+constexpr int kReadThreads = 8;
+constexpr size_t kReadPiece = 4u << 20;
+
+bool read_parallel(int fd, char* dst, size_t len, uint64_t off) {
+    const size_t pieces = (len + kReadPiece - 1) / kReadPiece;
+    const int nt = (int)(pieces < (size_t)kReadThreads ? pieces : (size_t)kReadThreads);
+    if (nt <= 1) return read_all(fd, dst, len, off);
+    std::atomic<bool> ok{true};
+    std::vector<std::thread> pool;
+    pool.reserve(nt);
+    for (int t = 0; t < nt; ++t)
+        pool.emplace_back([&, t] {
+            const size_t a = len * t / nt, b = len * (t + 1) / nt;
+            if (!read_all(fd, dst + a, b - a, off + a)) ok = false;
+        });
+    for (auto& th : pool) th.join();
+    return ok;
+}
+
 bool write_all(int fd, const char* src, size_t len) {
     while (len) {
         const ssize_t w = write(fd, src, len);
@@ -814,6 +889,34 @@ bool write_all(int fd, const char* src, size_t len) {
     }
     return true;
 }
+
+// RSS_CSV_TIMING=1: rss_csv_hash_file prints its phase times to stderr (diagnostics)
+class PhaseTimer {
+  public:
+    explicit PhaseTimer(const char* who) : who_(who), on_(getenv("RSS_CSV_TIMING") != nullptr) {
+        last_ = std::chrono::steady_clock::now();
+    }
+    void mark(const char* phase) {
+        if (!on_) return;
+        const auto now = std::chrono::steady_clock::now();
+        const double ms = std::chrono::duration<double, std::milli>(now - last_).count();
+        last_ = now;
+        const int n = snprintf(line_ + used_, sizeof line_ - used_, " %s=%.2fms", phase, ms);
+        if (n > 0 && used_ + n < (int)sizeof line_) used_ += n;
+    }
+    ~PhaseTimer() {  // runs after the device buffers of the call are freed
+        if (!on_) return;
+        mark("free");
+        fprintf(stderr, "%s:%s\n", who_, line_);
+    }
+
+  private:
+    const char* who_;
+    bool on_;
+    std::chrono::steady_clock::time_point last_;
+    char line_[512] = {0};
+    int used_ = 0;
+};
 
 struct Fd {
     int fd = -1;
@@ -845,7 +948,7 @@ int csv_hash_text(const char* who, rss_ctx* ctx, const typename CsvJob<Rows>::Ke
                              (unsigned long long)blen);
     CSV_HIP_CHECK(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream[0];
-    CsvJob<Rows> job(s, layout, blen);
+    CsvJob<Rows> job(ctx, layout, blen);
     if ((rc = job.alloc_text())) return rc;
     CSV_HIP_CHECK(hipMemcpyAsync(job.text(), text + body_off, blen, hipMemcpyHostToDevice, s));
     if ((rc = job.parse()) || (rc = job.hash(key, htable, nqueues, reta, want_file, counts)))
@@ -875,6 +978,7 @@ int csv_hash_file(const char* who, rss_ctx* ctx, const typename CsvJob<Rows>::Ke
     int rc = check_args(key, htable, nqueues);
     if (rc) return rc;
     *n_rows = 0;
+    PhaseTimer timer(who);
     CSV_HIP_CHECK(hipSetDevice(ctx->device));
     if ((rc = reserve_stage(ctx))) return rc;
     hipStream_t s = ctx->stream[0];
@@ -886,7 +990,7 @@ int csv_hash_file(const char* who, rss_ctx* ctx, const typename CsvJob<Rows>::Ke
     const uint64_t len = (uint64_t)st.st_size;
     // the header must sit in the first staging buffer (a canonical one is < 64 B)
     const size_t first = (size_t)(len < kStageBytes ? len : kStageBytes);
-    if (!read_all(in.fd, ctx->stage[0], first, 0))
+    if (!read_parallel(in.fd, ctx->stage[0], first, 0))
         return rss_set_error(RSS_ENOTSUP, "%s: cannot read %s", who, in_path);
     rss_csv_layout layout;
     size_t body_off;
@@ -906,7 +1010,7 @@ int csv_hash_file(const char* who, rss_ctx* ctx, const typename CsvJob<Rows>::Ke
     memset(counts, 0, sizeof(uint64_t) * nqueues);
     uint64_t body_left = blen, dev_pos = 0;
     auto open_segment = [&]() -> int {
-        jobs.emplace_back(new CsvJob<Rows>(s, layout, body_left < seg_cap ? body_left : seg_cap));
+        jobs.emplace_back(new CsvJob<Rows>(ctx, layout, body_left < seg_cap ? body_left : seg_cap));
         dev_pos = 0;
         return jobs.back()->alloc_text();
     };
@@ -939,7 +1043,7 @@ int csv_hash_file(const char* who, rss_ctx* ctx, const typename CsvJob<Rows>::Ke
         } else {
             CSV_HIP_CHECK(hipEventSynchronize(ctx->stage_done[b]));  // buffer b is free again
             got = (size_t)(len - file_pos < kStageBytes ? len - file_pos : kStageBytes);
-            if (!read_all(in.fd, ctx->stage[b], got, file_pos))
+            if (!read_parallel(in.fd, ctx->stage[b], got, file_pos))
                 return rss_set_error(RSS_EIO, "%s: read of %s failed", who, in_path);
         }
         const char* chunk = ctx->stage[b] + (k == 0 ? body_off : 0);
@@ -961,7 +1065,9 @@ int csv_hash_file(const char* who, rss_ctx* ctx, const typename CsvJob<Rows>::Ke
         CSV_HIP_CHECK(hipEventRecord(ctx->stage_done[b], s));
     }
     if (jobs.empty()) return rss_set_error(RSS_ENOTSUP, "rss_csv: no data rows");
+    timer.mark("read+upload");
     if ((rc = close_segment())) return rc;
+    timer.mark("parse+hash+format");
     if (!want_file) return RSS_OK;
     Fd outf;
     outf.fd = open(out_path, O_WRONLY | O_CREAT | O_TRUNC, 0666);
@@ -973,6 +1079,7 @@ int csv_hash_file(const char* who, rss_ctx* ctx, const typename CsvJob<Rows>::Ke
         if (!write_all(outf.fd, prefix.data(), plen))
             return rss_set_error(RSS_EIO, "%s: write to %s failed", who, out_path);
     }
+    timer.mark("open+prefix");
     // stream every segment's rows down: chunk k+1 copies into one pinned buffer while
     // chunk k is written from the other
     for (const auto& job : jobs) {
@@ -996,11 +1103,13 @@ int csv_hash_file(const char* who, rss_ctx* ctx, const typename CsvJob<Rows>::Ke
                 return rss_set_error(RSS_EIO, "%s: write to %s failed", who, out_path);
         }
     }
+    timer.mark("download+write");
     if (close(outf.fd) != 0) {
         outf.fd = -1;
         return rss_set_error(RSS_EIO, "%s: close of %s failed", who, out_path);
     }
     outf.fd = -1;
+    timer.mark("close");
     return RSS_OK;
 }
 
@@ -1046,5 +1155,6 @@ void rss_csv_release(rss_ctx* ctx) {
         ctx->stage_done[b] = nullptr;
     }
     ctx->stage_bytes = 0;
+    trim_pool(ctx, 0);
 }
 

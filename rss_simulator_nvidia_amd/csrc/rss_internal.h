@@ -3,6 +3,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <utility>
 #include <vector>
 
 #include "rss_toeplitz.h"
@@ -33,9 +34,11 @@ struct rss_ctx {
     char* stage[2] = {nullptr, nullptr};
     hipEvent_t stage_done[2] = {nullptr, nullptr};
     size_t stage_bytes = 0;
+    // device blocks (pointer, bytes) the CSV device path keeps between calls
+    std::vector<std::pair<void*, size_t>> csv_pool;
 };
 
-// rss_csv_device.hip: release the rss_csv_hash_file staging of a context
+// rss_csv_device.hip: release the CSV device path's staging and pooled blocks of a context
 RSS_HIDDEN void rss_csv_release(rss_ctx* ctx);
 
 // Record the thread's rss_last_error() message; returns `code`.
