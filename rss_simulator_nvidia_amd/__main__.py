@@ -1,4 +1,5 @@
-"""``python -m rss_simulator_nvidia_amd`` == ``rss-simulator``."""
-from rss_simulator_nvidia_amd import main
+"""Entry point of ``python -m rss_simulator_nvidia_amd``: the same program as ``rss-simulator``."""
+from rss_simulator_nvidia_amd.main import main as _cli
 
-main()
+if __name__ == "__main__":
+    _cli()

@@ -1,21 +1,26 @@
-"""Positive-int argparse type (``rss_simulator/arg_parse_types/positive_int.py:8-30``)."""
+"""Positive-int argparse type (``rss_simulator/arg_parse_types/positive_int.py:8-30``).
+
+Used for ``--hash-table-size`` / ``--num-queues``; an argument that ``int()`` rejects
+reports ``int()``'s own message, one below 1 reports ``"Number must be positive."``.
+"""
 from argparse import ArgumentTypeError
+
+_NOT_POSITIVE = "Number must be positive."
+
+
+def _to_int(text):
+    try:
+        return int(text)
+    except ValueError as err:
+        raise ArgumentTypeError(err)
 
 
 class PositiveInt(object):
-    """Positive int argument class."""
+    """Namespace for the ``parse`` callable handed to argparse."""
 
     @staticmethod
     def parse(arg):
-        """Parse ``arg`` with ``int()`` and require a value >= 1.
-
-        Messages match the reference: ``int()``'s own ValueError text, or
-        ``"Number must be positive."``.
-        """
-        try:
-            num = int(arg)
-        except ValueError as v_err:
-            raise ArgumentTypeError(v_err)
-        if num < 1:
-            raise ArgumentTypeError("Number must be positive.")
-        return num
+        value = _to_int(arg)
+        if value >= 1:
+            return value
+        raise ArgumentTypeError(_NOT_POSITIVE)
