@@ -44,11 +44,12 @@ def parse_args():
     p.add_argument("--queues", type=int, default=24)
     p.add_argument("--queue-width", choices=["auto", "u8", "u16", "u32"], default="auto",
                    help="queue_number output dtype; auto = narrowest that holds every queue")
-    p.add_argument("--cpu-sample", type=int, default=20000,
-                   help="tuples for the CPU baseline (the 20k-tuple subsample of BASELINE.md; "
-                        "about 17 CPU-seconds)")
-    p.add_argument("--cpu-procs", type=int, default=16,
-                   help="worker processes for the CPU baseline (the box's CPU share)")
+    p.add_argument("--cpu-sample", type=int, default=0,
+                   help="tuples for the CPU baseline (default 0 = max(20000, 1500 per process): "
+                        "the 20k-tuple subsample of BASELINE.md, >= ~2 s of work per process)")
+    p.add_argument("--cpu-procs", type=int, default=0,
+                   help="worker processes for the CPU baseline (default 0 = every core this "
+                        "process may use: its CPU affinity, capped by a cgroup CPU quota)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extras", action="store_true",
                    help="skip the rank-0 secondary lines of the row-f kernels (IPv6 hash, key "
@@ -103,6 +104,39 @@ def _port_worker(args):
     return [compute_hash_port(key, s, d, sp, dp) for s, d, sp, dp in rows]
 
 
+def cpu_share():
+    """Cores this process may use: its CPU affinity, capped by a cgroup v2/v1 CPU quota
+    (``os.cpu_count()`` is the whole machine, which a container may not own)."""
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        cores = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(period)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                period = int(f.read())
+            if q > 0:
+                quota = q / period
+        except (OSError, ValueError):
+            pass
+    if quota is not None:
+        cores = min(cores, max(1, int(quota)))
+    # a scheduler that shares the machine without a quota states the share in
+    # OMP_NUM_THREADS (the GPU boxes set it to their CPU share)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        cores = min(cores, int(omp))
+    return max(1, cores)
+
+
 def cpu_baseline(key, n_sample, procs, distribution="uniform"):
     """Time the pure-Python restatement of the reference's per-tuple path (``oracle``).
 
@@ -125,9 +159,10 @@ def cpu_baseline(key, n_sample, procs, distribution="uniform"):
     dt = time.perf_counter() - t0
     assert sum(len(o) for o in out) == n_sample
     return {"value": n_sample / dt, "unit": "tuples/s", "cores": procs, "kind": "port",
+            "procs": procs, "cpu_share": cpu_share(), "host_cores": os.cpu_count(),
             "sample": "first %d tuples of the bench stream, pure-Python restatement of "
-                      "toeplitz.py:46-69 (rotating bit-string key) in %d processes, %.2f s wall"
-                      % (n_sample, procs, dt)}
+                      "toeplitz.py:46-69 (rotating bit-string key) in %d processes (one per "
+                      "core of this process's CPU share), %.2f s wall" % (n_sample, procs, dt)}
 
 
 def load_traffic(profile_dir, n, htable, queues, queue_width):
@@ -215,6 +250,9 @@ def main():
         raise SystemExit("bench: --steps must be >= 1 and --warmup >= 0")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(relaunch_distributed(args.gpus))
+    # under a launcher (torch.distributed.run sets WORLD_SIZE) a process group is created
+    # at every world size, so `--nproc-per-node 1` runs the same RCCL calls as N = 8
+    distributed = "WORLD_SIZE" in os.environ
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus != world:
         print("bench: --gpus %d but WORLD_SIZE=%d; reporting %d" % (args.gpus, world, world),
@@ -223,27 +261,32 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     key_bytes = [int(x, 16) for x in EXAMPLE_KEY.split(":")]
 
+    # rank 0 times the CPU baseline at every world size, before it (or any rank) joins the
+    # process group or touches the GPU: the other ranks wait in the rendezvous meanwhile
     baseline = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        baseline = cpu_baseline(key_bytes, args.cpu_sample, args.cpu_procs, args.distribution)
+    if rank == 0 and not args.no_cpu_baseline:
+        procs = args.cpu_procs or cpu_share()
+        baseline = cpu_baseline(key_bytes, args.cpu_sample or max(20000, 1500 * procs), procs,
+                                args.distribution)
 
     import torch
     import torch.distributed as dist
 
     from rss_simulator_nvidia_amd import _native
+    from rss_simulator_nvidia_amd.sharding import allreduce_counts
 
     # RSS_BENCH_DEVICE pins every rank to one device (rehearsing N>1 on a 1-GPU box)
     dev_index = int(os.environ.get("RSS_BENCH_DEVICE", local_rank))
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
-    if world > 1:
+    if distributed:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
 
     def barrier():
-        if world > 1:
+        if distributed:
             if args.dist_backend == "nccl":
                 dist.barrier(device_ids=[dev_index])
             else:
@@ -315,8 +358,8 @@ def main():
                 ev[1].record(stream)
         else:
             body(counts2[b], ev)
-        if world > 1:
-            pending[b] = dist.all_reduce(counts2[b], async_op=True)  # RCCL over xGMI
+        if distributed:  # RCCL over xGMI
+            pending[b] = allreduce_counts(counts2[b], async_op=True)
 
     def drain():
         for b in (0, 1):
@@ -371,7 +414,7 @@ def main():
     launch_ms = [a.elapsed_time(b) for a, b in events]
     kernel_ms = sum(launch_ms) / len(launch_ms)
     stats = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
-    if world > 1:
+    if distributed:
         dist.all_reduce(stats, op=dist.ReduceOp.MAX)
     elapsed, kernel_ms_max = float(stats[0]), float(stats[1])
 
@@ -392,8 +435,8 @@ def main():
 
     if rank == 0:
         value = n * world * args.steps / elapsed
-        kernel_s = kernel_ms / 1e3
-        achieved = n * (READ_BYTES + write_bytes) / kernel_s / 1e9
+        # the slowest rank's mean launch time: at N > 1 the fraction is the worst rank's
+        achieved = n * (READ_BYTES + write_bytes) / (kernel_ms_max / 1e3) / 1e9
         traffic = load_traffic(args.profile_dir, n, H, Q, qw)
         line = {
             "metric": METRIC,
@@ -422,9 +465,10 @@ def main():
                 "htable": H,
                 "queues": Q,
                 "queue_width": qw,
-                "parallelism": "tuple-sharded x%d, %s all-reduce of uint64[%d] counts "
-                               "(async, overlapped with the next step)"
-                               % (world, "RCCL" if args.dist_backend == "nccl" else "gloo", Q),
+                "parallelism": ("tuple-sharded x%d, %s all-reduce of uint64[%d] counts "
+                                "(async, overlapped with the next step)"
+                                % (world, "RCCL" if args.dist_backend == "nccl" else "gloo", Q))
+                               if distributed else "single process, one GPU (no process group)",
                 "step": "hipGraph replay (zero counts + hash kernel)" if graphs is not None
                         else "eager launches (zero counts + hash kernel)",
             },
@@ -437,11 +481,13 @@ def main():
                 "traffic": traffic,
                 "kernel": "rss_toeplitz_kernel",
                 "bytes_per_tuple": READ_BYTES + write_bytes,
-                "kernel_ms": kernel_ms,
+                "kernel_ms": kernel_ms_max,
+                "kernel_ms_rank0": kernel_ms,
                 "kernel_ms_max_rank": kernel_ms_max,
                 "kernel_ms_min_max": [min(launch_ms), max(launch_ms)],
                 "kernel_ms_median": sorted(launch_ms)[len(launch_ms) // 2],
-                "timing": "HIP events around each of the %d timed launches (launch stream)"
+                "timing": "HIP events around each of the %d timed launches (launch stream); "
+                          "achieved uses the slowest rank's mean (kernel_ms_max_rank)"
                           % args.steps,
             },
             # the HBM-read roofline is the counts-only mode's bound (12 B read
@@ -475,7 +521,7 @@ def main():
         if extras is not None:
             line["row_f_kernels"] = extras
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if distributed:
         barrier()  # ranks leave together (rank 0 ran the secondary timings alone)
         dist.destroy_process_group()
 

@@ -364,7 +364,8 @@ int rss_hash6_host_reta(rss_ctx* ctx, const rss_key6* key, const rss_tuple6* h_t
 /*
  * Multi-GPU host batch (replaces the same rows of Simulator.calc_hash /
  * calc_queue_number / write_statistics as rss_hash_host, simulator.py:74-113).  The n
- * tuples are split into nctx contiguous ranges of ceil(n / nctx) (the last shorter);
+ * tuples are split into nctx contiguous ranges as sharding.shard_range splits a batch over
+ * ranks (n / nctx each, the first n % nctx ranges one tuple longer);
  * context i hashes range i on its own device from its own host thread and copies the
  * hash / queue slice straight into the caller's output range (no collective), and the
  * per-queue counts of all ranges are summed on the host -- exact integers, so identical

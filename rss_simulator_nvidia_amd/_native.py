@@ -286,6 +286,45 @@ def _host_batch(tuples, nqueues, want_hash, want_queue, want_counts, out):
     return arr, n, h, q, c
 
 
+U32_MAX = 0xFFFFFFFF
+RETA_QUEUE_MAX = 0xFFFF  # an indirection-table entry travels as u16 (rss_hash_device_reta)
+
+
+def queue_modulus(htable, nqueues, reta=False):
+    """``(htable, nqueues)`` as the C ABI's ``uint32_t`` arguments, for the same
+    ``queue = hash % htable % nqueues`` (``simulator.py:96-98``) on every 32-bit hash.
+
+    ctypes would truncate a value >= 2**32 silently (4294967297 -> 1), so larger values
+    are rewritten exactly, never truncated:
+
+    * ``nqueues >= 2**32 > htable``: ``queue = hash % htable`` -> ``(htable, htable)``;
+    * ``htable >= 2**32``: ``hash % htable = hash`` (hash < 2**32), so ``queue = hash %
+      nqueues``; any multiple of ``nqueues`` as the table size gives the same remainder ->
+      ``((2**32 - 1) // nqueues * nqueues, nqueues)``;
+    * both ``>= 2**32``: ``queue = hash``, whose histogram would need 2**32 entries --
+      refused with ``ValueError`` (the one combination this build does not run);
+    * with an indirection table (``reta``) queues are table entries < 2**16, so an
+      ``nqueues >= 2**32`` only bounds them: it becomes 65536 (higher queues stay empty).
+
+    The per-queue counts then have ``nqueues'`` entries (queues past it are always empty).
+    """
+    H, Q = int(htable), int(nqueues)
+    if H < 0 or Q < 0:  # ctypes would wrap -1 to 2**32 - 1
+        raise ValueError("htable (%d) and nqueues (%d) must be >= 1" % (H, Q))
+    if H == 0 or Q == 0:
+        return H, Q  # the library refuses it (RSS_EINVAL, "must be >= 1")
+    if reta:
+        return H, (Q if Q <= U32_MAX else RETA_QUEUE_MAX + 1)
+    if H <= U32_MAX and Q <= U32_MAX:
+        return H, Q
+    if H <= U32_MAX:
+        return H, H
+    if Q <= U32_MAX:
+        return U32_MAX // Q * Q, Q
+    raise ValueError("htable %d and nqueues %d both >= 2**32: every hash would be its own queue "
+                     "(a 2**32-entry histogram); not supported" % (H, Q))
+
+
 def _reta_table(reta, htable):
     table = np.ascontiguousarray(reta, dtype=np.uint32)
     if len(table) != htable:
@@ -323,6 +362,7 @@ class HostContext:
         (page-locked tuples and outputs skip the staging copies).  Returns
         ``(hash_u32, queue_u32, counts_u64)``; disabled outputs are None.
         """
+        htable, nqueues = queue_modulus(htable, nqueues, reta is not None)
         arr, n, h, q, c = _host_batch(tuples, nqueues, want_hash, want_queue, want_counts, out)
         if reta is None:
             _check(self._lib.rss_hash_host(self._ctx, ctypes.byref(key), ptr(arr), n, htable,
@@ -339,6 +379,7 @@ class HostContext:
               want_counts=True, reta=None):
         """IPv6 batch (``TUPLE6_DTYPE`` or uint32 (n, 9)) -> (hash, queue, counts);
         ``reta`` as for :meth:`hash`."""
+        htable, nqueues = queue_modulus(htable, nqueues, reta is not None)
         arr = np.ascontiguousarray(tuples6)
         if arr.dtype != TUPLE6_DTYPE:
             arr = np.ascontiguousarray(arr, dtype=np.uint32).reshape(-1, 9)
@@ -356,12 +397,15 @@ class HostContext:
                                                  ptr(c), 0), "rss_hash6_host_reta")
         return h, q, c
 
-    def csv_hash_text(self, key, data, htable, nqueues, reta=None, counts_only=False):
+    def csv_hash_text(self, key, data, htable, nqueues, reta=None, counts_only=False,
+                      copy=True):
         """The whole ``--csv`` job on the device for a canonical file image
         (``rss_csv_hash_text``; ``rss_csv6_hash_text`` when ``key`` is an :class:`RssKey6`):
-        returns ``(file_image, counts, n_rows)`` -- file_image a uint8 view of
-        context-owned memory, valid until the next call on this context (None with
-        ``counts_only``) -- or None when the text is not canonical."""
+        returns ``(file_image, counts, n_rows)`` -- file_image a uint8 array (None with
+        ``counts_only``) -- or None when the text is not canonical.  ``copy=False`` returns
+        a zero-copy view of context-owned memory instead, valid only until the next call
+        on this context (which may resize or overwrite it)."""
+        htable, nqueues = queue_modulus(htable, nqueues, reta is not None)
         buf = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data
         counts = np.zeros(nqueues, dtype=np.uint64)
         out, out_len, n = ctypes.c_void_p(), ctypes.c_size_t(0), ctypes.c_size_t(0)
@@ -377,8 +421,13 @@ class HostContext:
         _check(rc, name)
         image = None
         if not counts_only:
-            image = np.ctypeslib.as_array(ctypes.cast(out, ctypes.POINTER(ctypes.c_uint8)),
-                                          shape=(out_len.value,))
+            if out_len.value:
+                image = np.ctypeslib.as_array(ctypes.cast(out, ctypes.POINTER(ctypes.c_uint8)),
+                                              shape=(out_len.value,))
+                if copy:
+                    image = image.copy()
+            else:
+                image = np.empty(0, dtype=np.uint8)
         return image, counts, n.value
 
     def csv_hash_file(self, key, in_path, out_path, htable, nqueues, reta=None):
@@ -387,6 +436,7 @@ class HostContext:
         ``out_path`` None = counts only.  Returns ``(counts, n_rows)``, or None when the
         file is not canonical or a path cannot be opened (the pandas path then raises the
         reference's error)."""
+        htable, nqueues = queue_modulus(htable, nqueues, reta is not None)
         counts = np.zeros(nqueues, dtype=np.uint64)
         n = ctypes.c_size_t(0)
         table = _csv_reta(reta, htable)
@@ -403,6 +453,7 @@ class HostContext:
 
     def key_search(self, keys, tuples, htable, nqueues):
         """Per-queue counts (uint64[len(keys), nqueues]) of ``tuples`` under each prepared key."""
+        htable, nqueues = queue_modulus(htable, nqueues)
         arr = np.ascontiguousarray(tuples)
         if arr.dtype != TUPLE_DTYPE:
             arr = np.ascontiguousarray(arr, dtype=np.uint32).reshape(-1, 3)
@@ -436,6 +487,7 @@ class MultiHostContext:
     def hash(self, key, tuples, htable, nqueues, want_hash=True, want_queue=True, want_counts=True,
              reta=None, out=None):
         """Same contract as :meth:`HostContext.hash`, over every context's device."""
+        htable, nqueues = queue_modulus(htable, nqueues, reta is not None)
         arr, n, h, q, c = _host_batch(tuples, nqueues, want_hash, want_queue, want_counts, out)
         handles = (ctypes.c_void_p * len(self.contexts))(*[x._ctx.value for x in self.contexts])
         table = _reta_table(reta, htable) if reta is not None else None
@@ -457,7 +509,9 @@ def default_context():
 # ------------------------------------------------------- device pointers ----
 def hash_device(key, tuples_ptr, n, htable, nqueues, hash_ptr=None, queue_ptr=None,
                 counts_ptr=None, flags=0, stream=None):
-    """Stream-ordered ``rss_hash_device`` on raw device pointers (ints)."""
+    """Stream-ordered ``rss_hash_device`` on raw device pointers (ints); ``counts_ptr``
+    holds ``queue_modulus(htable, nqueues)[1]`` entries."""
+    htable, nqueues = queue_modulus(htable, nqueues)
     _check(load().rss_hash_device(ctypes.byref(key), tuples_ptr, n, htable, nqueues, hash_ptr,
                                   queue_ptr, counts_ptr, flags, stream), "rss_hash_device")
 
@@ -465,6 +519,7 @@ def hash_device(key, tuples_ptr, n, htable, nqueues, hash_ptr=None, queue_ptr=No
 def hash_device_reta(key, tuples_ptr, n, htable, reta, nqueues, hash_ptr=None, queue_ptr=None,
                      counts_ptr=None, flags=0, stream=None):
     """Stream-ordered ``rss_hash_device_reta`` (``reta``: host sequence of htable queue ids)."""
+    htable, nqueues = queue_modulus(htable, nqueues, True)
     table = np.ascontiguousarray(reta, dtype=np.uint32)
     if len(table) != htable:
         raise ValueError("indirection table has %d entries, htable is %d" % (len(table), htable))
@@ -476,6 +531,7 @@ def hash_device_reta(key, tuples_ptr, n, htable, reta, nqueues, hash_ptr=None, q
 def hash6_device(key6, tuples_ptr, n, htable, nqueues, hash_ptr=None, queue_ptr=None,
                  counts_ptr=None, flags=0, stream=None):
     """Stream-ordered ``rss_hash6_device`` on raw device pointers (ints)."""
+    htable, nqueues = queue_modulus(htable, nqueues)
     _check(load().rss_hash6_device(ctypes.byref(key6), tuples_ptr, n, htable, nqueues, hash_ptr,
                                    queue_ptr, counts_ptr, flags, stream), "rss_hash6_device")
 
@@ -483,6 +539,7 @@ def hash6_device(key6, tuples_ptr, n, htable, nqueues, hash_ptr=None, queue_ptr=
 def hash6_device_reta(key6, tuples_ptr, n, htable, reta, nqueues, hash_ptr=None, queue_ptr=None,
                       counts_ptr=None, flags=0, stream=None):
     """Stream-ordered ``rss_hash6_device_reta`` (``reta``: host sequence of htable queue ids)."""
+    htable, nqueues = queue_modulus(htable, nqueues, True)
     table = _reta_table(reta, htable)
     _check(load().rss_hash6_device_reta(ctypes.byref(key6), tuples_ptr, n, htable,
                                         table.ctypes.data, nqueues, hash_ptr, queue_ptr,
@@ -492,6 +549,7 @@ def hash6_device_reta(key6, tuples_ptr, n, htable, reta, nqueues, hash_ptr=None,
 def key_search_device(windows_ptr, nkeys, tuples_ptr, n, htable, nqueues, counts_ptr,
                       stream=None):
     """Stream-ordered ``rss_key_search_device`` on raw device pointers (ints)."""
+    htable, nqueues = queue_modulus(htable, nqueues)
     _check(load().rss_key_search_device(windows_ptr, nkeys, tuples_ptr, n, htable, nqueues,
                                         counts_ptr, stream), "rss_key_search_device")
 

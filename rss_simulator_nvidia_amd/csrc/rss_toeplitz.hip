@@ -1661,13 +1661,15 @@ int rss_hash_host_multi(rss_ctx* const* ctxs, int nctx, const rss_key* key,
     if (htable < 1 || nqueues < 1)
         return set_error(RSS_EINVAL, "rss_hash_host_multi: htable (%u) and nqueues (%u) must be >= 1",
                          htable, nqueues);
-    // contiguous ranges, as sharding.shard_range: ceil(n / nctx) each, the last shorter
-    const size_t per = (n + (size_t)nctx - 1) / (size_t)nctx;
+    // contiguous ranges, exactly sharding.shard_range's: n / nctx each, the first n % nctx
+    // ranges one longer
+    const size_t base = n / (size_t)nctx, extra = n % (size_t)nctx;
     std::vector<std::vector<uint64_t>> part(nctx, std::vector<uint64_t>(h_counts ? nqueues : 0));
     std::vector<int> rcs(nctx, RSS_OK);
     std::vector<std::string> errs(nctx);
     auto work = [&](int i) {
-        const size_t a = std::min(n, per * (size_t)i), b = std::min(n, a + per);
+        const size_t a = base * (size_t)i + std::min((size_t)i, extra);
+        const size_t b = a + base + ((size_t)i < extra ? 1 : 0);
         const int rc = hash_host_impl(ctxs[i], key, h_tuples ? h_tuples + a : nullptr, b - a, htable,
                                       nqueues, h_hash ? h_hash + a : nullptr,
                                       h_queue ? h_queue + a : nullptr,

@@ -32,6 +32,8 @@ def figure(counts, hash_key_str, hash_table_size, num_queues):
     from matplotlib.ticker import MaxNLocator
 
     counts = np.asarray(counts, dtype=np.float64)
+    if len(counts) < num_queues:  # queues >= min(htable, 2**32) are never chosen
+        counts = np.concatenate([counts, np.zeros(num_queues - len(counts))])
     fig, ax = plt.subplots(figsize=(12, 8))
     ax.bar(np.arange(num_queues) + 0.05, counts, width=0.9, align="edge", color="#86bf91",
            zorder=2)

@@ -36,9 +36,15 @@ def _l4_arg(text):
 
 
 def indirection_table(args):
-    """The --reta-weights / --reta-file table, validated, or None (reference mapping)."""
+    """The --reta-weights / --reta-file table, validated, or None (reference mapping).
+    Raises ValueError (``main`` reports it as a usage error, exit status 2)."""
     if args.reta_weights is not None and args.reta_file is not None:
         raise ValueError("give either --reta-weights or --reta-file")
+    if args.reta_weights is None and args.reta_file is None:
+        return None
+    if args.htable_size > reta.MAX_ENTRIES:  # before a table of htable entries is built
+        raise ValueError("indirection tables hold at most %d entries, --htable-size is %d"
+                         % (reta.MAX_ENTRIES, args.htable_size))
     if args.reta_weights is not None:
         if len(args.reta_weights) != args.num_queues:
             raise ValueError("--reta-weights needs one weight per queue (%d)" % args.num_queues)
@@ -126,8 +132,13 @@ def parse_args(argv=None):
 
 def main(argv=None):
     """Invoke the RSS simulator (``main.py:54-64``)."""
-    args = parse_args(argv)
-    table = indirection_table(args)
+    parser = build_parser()
+    args = parser.parse_args(argv)
+    try:
+        table = indirection_table(args)
+        _native.queue_modulus(args.htable_size, args.num_queues, table is not None)
+    except ValueError as err:
+        parser.error(str(err))
     if args.pcap:
         return run_pcap(args, table)
     fast = fastcsv.enabled()

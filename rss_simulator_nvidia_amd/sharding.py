@@ -33,15 +33,19 @@ def world_info():
     return 0, 1
 
 
-def allreduce_counts(counts, group=None):
+def allreduce_counts(counts, group=None, async_op=False):
     """Sum per-queue counts over ranks in place (int64 tensor; uint64 bit pattern).
 
     Counts are exact integers, so the reduced histogram equals the single-device
-    histogram of the whole batch bit for bit.
+    histogram of the whole batch bit for bit.  Whenever a process group is
+    initialised the collective is issued, at world size 1 too (a no-op sum, but the
+    same RCCL call the N-GPU run makes); without one the counts are returned as they
+    are.  ``async_op`` returns the work handle (``None`` when nothing was issued).
     """
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
-        dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=group)
-    return counts
+    if dist.is_available() and dist.is_initialized():
+        work = dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
+        return work if async_op else counts
+    return None if async_op else counts
 
 
 def hash_shard(key, tuples, n, htable, nqueues, hashes=None, queues=None, counts=None,

@@ -70,6 +70,15 @@ def test_weights_cli(oracle_ctx, oracle_lib, golden_dir, tmp_path, capsys):
     with pytest.raises(SystemExit):
         main(["--key-file", key_file, "--ips-file", "x", "--htable-size", "16",
               "--num-queues", "4", "--reta-weights", "a,b"])
-    with pytest.raises(ValueError):
+    capsys.readouterr()
+    with pytest.raises(SystemExit) as exc:  # table problems are usage errors (exit 2)
         main(["--key-file", key_file, "--ips-file", os.path.join(golden_dir, "example_input",
               "ips.csv"), "--htable-size", "16", "--num-queues", "4", "--reta-weights", "1,2"])
+    assert exc.value.code == 2
+    assert "--reta-weights needs one weight per queue (4)" in capsys.readouterr().err
+    # the table size is checked before a table of --htable-size entries is built
+    with pytest.raises(SystemExit) as exc:
+        main(["--key-file", key_file, "--ips-file", "x", "--htable-size", str(10 ** 12),
+              "--num-queues", "4", "--reta-weights", "1,1,1,1"])
+    assert exc.value.code == 2
+    assert "at most 1024 entries" in capsys.readouterr().err
