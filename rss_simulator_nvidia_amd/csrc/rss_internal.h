@@ -29,6 +29,13 @@ struct rss_ctx {
     rss_tuple4* h_in[2] = {nullptr, nullptr};
     uint32_t* h_hash[2] = {nullptr, nullptr};
     uint32_t* h_queue[2] = {nullptr, nullptr};
+    // small batches (rss_hash_host, n <= kSmallBatch): device aliases of slot 0's pinned
+    // staging, read / written by the kernel in place, and a pinned landing buffer for the
+    // counts
+    void* alias_in = nullptr;
+    void* alias_hash = nullptr;
+    void* alias_queue = nullptr;
+    uint64_t* h_counts = nullptr;
     std::vector<char> csv_out;  // rss_csv_hash_text's statistics file image
     // rss_csv_hash_file: two pinned staging buffers for the streamed file I/O
     char* stage[2] = {nullptr, nullptr};

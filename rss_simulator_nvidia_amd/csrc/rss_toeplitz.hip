@@ -1556,6 +1556,7 @@ void rss_ctx_destroy(rss_ctx* ctx) {
         (void)hipHostFree(ctx->h_queue[b]);
         if (ctx->stream[b]) (void)hipStreamDestroy(ctx->stream[b]);
     }
+    (void)hipHostFree(ctx->h_counts);
     delete ctx;
 }
 
@@ -1610,6 +1611,9 @@ static int ctx_reserve(rss_ctx* ctx, size_t chunk, uint32_t nqueues) {
             RSS_HIP_CHECK(hipHostMalloc(&ctx->h_hash[b], chunk * sizeof(uint32_t), hipHostMallocDefault));
             RSS_HIP_CHECK(hipHostMalloc(&ctx->h_queue[b], chunk * sizeof(uint32_t), hipHostMallocDefault));
         }
+        RSS_HIP_CHECK(hipHostGetDevicePointer(&ctx->alias_in, ctx->h_in[0], 0));
+        RSS_HIP_CHECK(hipHostGetDevicePointer(&ctx->alias_hash, ctx->h_hash[0], 0));
+        RSS_HIP_CHECK(hipHostGetDevicePointer(&ctx->alias_queue, ctx->h_queue[0], 0));
         ctx->chunk = chunk;
     }
     if (ctx->counts_cap < nqueues) {
@@ -1617,10 +1621,46 @@ static int ctx_reserve(rss_ctx* ctx, size_t chunk, uint32_t nqueues) {
             (void)hipFree(ctx->d_counts[b]);
             ctx->d_counts[b] = nullptr;
         }
+        (void)hipHostFree(ctx->h_counts);
+        ctx->h_counts = nullptr;
         ctx->counts_cap = 0;
         for (int b = 0; b < 2; ++b)
             RSS_HIP_CHECK(hipMalloc(&ctx->d_counts[b], sizeof(uint64_t) * nqueues));
+        RSS_HIP_CHECK(hipHostMalloc(&ctx->h_counts, sizeof(uint64_t) * nqueues, hipHostMallocDefault));
         ctx->counts_cap = nqueues;
+    }
+    return RSS_OK;
+}
+
+// Small host batches -- a reference-style caller hashing one row per call
+// (Toeplitz.compute_hash from Simulator.__calc_entry_hash, simulator.py:80-92) -- are
+// bound by per-call overhead, not bytes: one stream, no pointer-attribute queries, the
+// kernel reading the tuples from and writing hash / queue straight into slot 0's pinned
+// staging (mapped into the device address space), the counts landing in pinned memory,
+// one synchronisation.  Same kernel and results as the pipelined path.
+constexpr size_t kSmallBatch = (size_t)1 << 14;
+
+static int hash_host_small(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples, size_t n,
+                           uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
+                           uint64_t* h_counts, uint32_t flags, const uint32_t* reta) {
+    int rc = ctx_reserve(ctx, std::max(ctx->chunk, kSmallBatch), h_counts ? nqueues : 1);
+    if (rc) return rc;
+    hipStream_t s = ctx->stream[0];
+    memcpy(ctx->h_in[0], h_tuples, n * sizeof(rss_tuple4));
+    rc = launch_hash(key, static_cast<const rss_tuple4*>(ctx->alias_in), n, htable, nqueues,
+                     h_hash ? static_cast<uint32_t*>(ctx->alias_hash) : nullptr,
+                     h_queue ? ctx->alias_queue : nullptr, h_counts ? ctx->d_counts[0] : nullptr,
+                     0, s, reta);
+    if (rc) return rc;
+    if (h_counts)
+        RSS_HIP_CHECK(hipMemcpyAsync(ctx->h_counts, ctx->d_counts[0], sizeof(uint64_t) * nqueues,
+                                     hipMemcpyDeviceToHost, s));
+    RSS_HIP_CHECK(hipStreamSynchronize(s));
+    if (h_hash) memcpy(h_hash, ctx->h_hash[0], n * 4);
+    if (h_queue) memcpy(h_queue, ctx->h_queue[0], n * 4);
+    if (h_counts) {
+        if (!(flags & RSS_FLAG_ACCUMULATE)) memset(h_counts, 0, sizeof(uint64_t) * nqueues);
+        for (uint32_t q = 0; q < nqueues; ++q) h_counts[q] += ctx->h_counts[q];
     }
     return RSS_OK;
 }
@@ -1737,6 +1777,9 @@ static int hash_host_impl(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_
         return set_error(RSS_EINVAL, "rss_hash_host: htable (%u) and nqueues (%u) must be >= 1",
                          htable, nqueues);
     RSS_HIP_CHECK(hipSetDevice(ctx->device));
+    if (n > 0 && n <= kSmallBatch)
+        return hash_host_small(ctx, key, h_tuples, n, htable, nqueues, h_hash, h_queue, h_counts,
+                               flags, reta);
     constexpr size_t kChunkMax = (size_t)1 << 22;  // 4M tuples: 48 MB in + 32 MB out per slot
     const size_t chunk = n < kChunkMax ? (n ? n : 1) : kChunkMax;
     int rc = ctx_reserve(ctx, chunk, nqueues);
