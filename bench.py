@@ -62,6 +62,11 @@ def parse_args():
     p.add_argument("--distribution", choices=["uniform", "flow"], default="uniform",
                    help="uniform = splitmix64 over all 96 bits (SURVEY.md 8d); flow = the "
                         "example_input/ips.csv shape: one IP pair, sequential source ports")
+    p.add_argument("--placement-probe", type=int, default=4, metavar="K",
+                   help="place the resident buffers by timing the kernel on 2 candidate input "
+                        "x K candidate output allocations before the timed region and keeping "
+                        "the fastest (rss_simulator_nvidia_amd/placement.py); 0 = first "
+                        "allocation, as allocated")
     p.add_argument("--profile-dir", default=os.path.join(ROOT, "profiles"),
                    help="where committed rocprofv3 PMC summaries (traffic) are looked up")
     return p.parse_args()
@@ -302,14 +307,36 @@ def main():
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
     key = _native.prepare_key(key_bytes)
-    tuples = torch.empty(3 * n, dtype=torch.int32, device=dev)
-    hashes = torch.empty(n, dtype=torch.int32, device=dev)
-    queues = torch.empty(n, dtype=torch.int32, device=dev)  # big enough for any width
     counts = torch.zeros(Q, dtype=torch.int64, device=dev)
-    if args.distribution == "uniform":
-        _native.generate_device(SEED, rank * n, n, tuples.data_ptr(), sp)
+
+    def fill_input(t):
+        if args.distribution == "uniform":
+            _native.generate_device(SEED, rank * n, n, t.data_ptr(), sp)
+        else:
+            flow_device(torch, t, rank * n, n, dev)
+
+    placement = None
+    if args.placement_probe > 0:
+        from rss_simulator_nvidia_amd.placement import choose_stream_buffers
+
+        def probe(t, h, q, ev):
+            if ev is not None:
+                ev[0].record(stream)
+            _native.hash_device(key, t.data_ptr(), n, H, Q, h.data_ptr(), q.data_ptr(),
+                                counts.data_ptr(), _native.FLAG_ACCUMULATE | qflag, sp)
+            if ev is not None:
+                ev[1].record(stream)
+
+        # queue buffers of 4n bytes, as the unplaced allocation: the u32 secondary line
+        # writes 4 B per tuple into the same buffer
+        tuples, hashes, queues, placement = choose_stream_buffers(
+            torch, dev, n, fill_input, probe, n_inputs=2, n_outputs=args.placement_probe,
+            queue_bytes=4)
     else:
-        flow_device(torch, tuples, rank * n, n, dev)
+        tuples = torch.empty(3 * n, dtype=torch.int32, device=dev)
+        hashes = torch.empty(n, dtype=torch.int32, device=dev)
+        queues = torch.empty(n, dtype=torch.int32, device=dev)  # big enough for any width
+        fill_input(tuples)
     torch.cuda.synchronize()
 
     # Two count buffers: step i hashes into counts[i % 2] while the RCCL all-reduce of
@@ -513,6 +540,7 @@ def main():
             "cpu_baseline": baseline,
         }
         line["secondary_min_median_max_ms"] = secondary_spread
+        line["placement"] = placement if placement is not None else "first allocation"
         if flow_ms is not None:
             line["flow_like"] = {
                 "kernel_ms": flow_ms, "tuples_per_s_per_gpu": n / (flow_ms / 1e3),

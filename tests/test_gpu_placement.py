@@ -1,0 +1,51 @@
+"""Placement of the resident stream buffers (``placement.choose_stream_buffers``): every
+candidate combination is probed with the real kernel, the fastest is returned, the
+returned input holds the generated tuples, and the kernel on the chosen buffers gives the
+oracle's results."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def test_choose_stream_buffers_probes_and_keeps_the_fastest(oracle_lib, example_key):
+    from rss_simulator_nvidia_amd import _native
+    from rss_simulator_nvidia_amd.placement import choose_stream_buffers
+    n, H, Q = (1 << 20) + 3, 128, 24
+    dev = torch.device("cuda:0")
+    stream = torch.cuda.current_stream(dev)
+    key = _native.prepare_key(example_key)
+    counts = torch.zeros(Q, dtype=torch.int64, device=dev)
+    seen = []
+
+    def fill(t):
+        _native.generate_device(0x5EED, 0, n, t.data_ptr(), stream.cuda_stream)
+
+    def probe(t, h, q, ev):
+        seen.append((t.data_ptr(), h.data_ptr(), q.data_ptr()))
+        if ev is not None:
+            ev[0].record(stream)
+        _native.hash_device(key, t.data_ptr(), n, H, Q, h.data_ptr(), q.data_ptr(),
+                            counts.data_ptr(), _native.FLAG_QUEUE_U8, stream.cuda_stream)
+        if ev is not None:
+            ev[1].record(stream)
+
+    tuples, hashes, queues, rep = choose_stream_buffers(torch, dev, n, fill, probe, n_inputs=2,
+                                                        n_outputs=3, probe_reps=4, probe_warm=1)
+    assert len(set(seen)) == 6 and len(seen) == 6 * 5
+    times = rep["probe_median_ms"]
+    assert set(times) == {"in%d_out%d" % (i, j) for i in range(2) for j in range(3)}
+    assert round(rep["chosen_ms"], 4) == min(times.values()) == times[rep["chosen"]]
+    assert tuples.numel() == 3 * n and hashes.numel() == n and queues.numel() == n
+    hashes.zero_()
+    _native.hash_device(key, tuples.data_ptr(), n, H, Q, hashes.data_ptr(), queues.data_ptr(),
+                        counts.data_ptr(), _native.FLAG_QUEUE_U8, stream.cuda_stream)
+    torch.cuda.synchronize()
+    tup = tuples.cpu().numpy().view(np.uint32).reshape(n, 3)
+    np.testing.assert_array_equal(tup, oracle_lib.generate(0x5EED, 0, n))
+    h, q, c = oracle_lib.run(example_key, tup, H, Q)
+    np.testing.assert_array_equal(hashes.cpu().numpy().view(np.uint32), h)
+    np.testing.assert_array_equal(queues.cpu().numpy(), q.astype(np.uint8))
+    np.testing.assert_array_equal(counts.cpu().numpy().view(np.uint64), c)

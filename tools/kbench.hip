@@ -72,6 +72,73 @@ __global__ __launch_bounds__(1024) void mem_ceiling_q8(Params p) {
     }
 }
 
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+// practical HBM ceilings for other read / write mixes on the same box: a float4 copy
+// (1 R : 1 W, the microarch guide's 6.29 TB/s shape) and a write-only fill
+__global__ __launch_bounds__(1024) void mem_copy16(const uint4* __restrict__ src,
+                                                   uint4* __restrict__ dst, uint64_t n16) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 1024 + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * 1024)
+        dst[i] = src[i];
+}
+__global__ __launch_bounds__(1024) void mem_fill16(uint4* __restrict__ dst, uint64_t n16) {
+    const u32x4v v = {threadIdx.x, blockIdx.x, 7u, 9u};
+    u32x4v* d = reinterpret_cast<u32x4v*>(dst);
+    for (uint64_t i = (uint64_t)blockIdx.x * 1024 + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * 1024)
+        __builtin_nontemporal_store(v, d + i);
+}
+
+// access-shape probes for the 12R+5W mix (outputs not meaningful: memory timing only).
+// kShape 0: the product's shape (lane reads its 4 tuples as 3 x 16 B at a 48-B stride);
+// 1: lane-contiguous loads (instruction k of a wave reads bytes [1024k, 1024k+1024) of the
+// wave's 3 KiB block), same 5 B/tuple of stores; 2: as 0 with the queue bytes of 4
+// consecutive groups kept in registers and written as one 16-B store (lane owns 16
+// consecutive tuples per iteration: 12 x 16-B loads, 4 x 16-B hash stores)
+template <int kShape>
+__global__ __launch_bounds__(1024) void mem_shape(Params p) {
+    const uint4* src = reinterpret_cast<const uint4*>(p.tuples);
+    const uint64_t ng = p.n >> 2;
+    const uint32_t lane = threadIdx.x & 63;
+    if constexpr (kShape == 2) {
+        const uint64_t ng16 = ng >> 2;
+        for (uint64_t g = (uint64_t)blockIdx.x * 1024 + threadIdx.x; g < ng16; g += (uint64_t)gridDim.x * 1024) {
+            uint32_t qv[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint64_t gg = 4 * g + j;
+                uint4 a = src[3 * gg], b = src[3 * gg + 1], c = src[3 * gg + 2];
+                uint32_t* o = p.hash_out + 4 * gg;
+                __builtin_nontemporal_store(a.x ^ a.y ^ a.z, o);
+                __builtin_nontemporal_store(a.w ^ b.x ^ b.y, o + 1);
+                __builtin_nontemporal_store(b.z ^ b.w ^ c.x, o + 2);
+                __builtin_nontemporal_store(c.y ^ c.z ^ c.w, o + 3);
+                qv[j] = (a.x ^ c.w) & 0x17171717u;
+            }
+            uint32_t* oq = p.queue_out + 4 * g;
+            __builtin_nontemporal_store(qv[0], oq);
+            __builtin_nontemporal_store(qv[1], oq + 1);
+            __builtin_nontemporal_store(qv[2], oq + 2);
+            __builtin_nontemporal_store(qv[3], oq + 3);
+        }
+        return;
+    }
+    for (uint64_t g = (uint64_t)blockIdx.x * 1024 + threadIdx.x; g < ng; g += (uint64_t)gridDim.x * 1024) {
+        uint4 a, b, c;
+        if constexpr (kShape == 0) {
+            a = src[3 * g]; b = src[3 * g + 1]; c = src[3 * g + 2];
+        } else {
+            const uint64_t w0 = 3 * (g - lane);  // the wave's first uint4
+            if (w0 + 192 > 3 * ng) { a = src[3 * g]; b = src[3 * g + 1]; c = src[3 * g + 2]; }
+            else { a = src[w0 + lane]; b = src[w0 + 64 + lane]; c = src[w0 + 128 + lane]; }
+        }
+        uint32_t* o = p.hash_out + 4 * g;
+        __builtin_nontemporal_store(a.x ^ a.y ^ a.z, o);
+        __builtin_nontemporal_store(a.w ^ b.x ^ b.y, o + 1);
+        __builtin_nontemporal_store(b.z ^ b.w ^ c.x, o + 2);
+        __builtin_nontemporal_store(c.y ^ c.z ^ c.w, o + 3);
+        __builtin_nontemporal_store((a.x ^ c.w) & 0x17171717u, p.queue_out + g);
+    }
+}
+
 // store-shape probes for the 12R+5W mix: kMode 0 = plain stores, 1 = hash only (12R+4W),
 // 2 = queue bytes gathered through LDS into one 16-B store per lane every 4th group
 template <int kMode>
@@ -606,6 +673,116 @@ int main(int argc, char** argv) {
         snprintf(name, sizeof name, "mem read+write grid=%dx", wpc);
         t = time_ms([&] { hipLaunchKernelGGL(mem_ceiling<true>, dim3(g_cus * wpc), dim3(1024), 0, 0, p); }, reps);
         printf("%-40s %8.3f ms  %7.1f Gt/s  %6.0f GB/s\n", name, t, n / t / 1e6, gb_rw / t * 1e3);
+    }
+
+    if (strstr("copy", filter)) {  // same-box ceilings of other mixes (1 GiB each way)
+        const uint64_t n16 = n / 4;  // n * 4 bytes
+        const double gb = n16 * 16e-9;
+        for (int wpc : {1, 2, 4}) {
+            t = time_ms([&] { hipLaunchKernelGGL(mem_copy16, dim3(g_cus * wpc), dim3(1024), 0, 0,
+                                                 (const uint4*)tup, (uint4*)h1, n16); }, reps);
+            printf("copy float4 1R:1W grid=%dx                %8.3f ms  %6.0f GB/s (R+W)\n", wpc, t,
+                   2 * gb / t * 1e3);
+            t = time_ms([&] { hipLaunchKernelGGL(mem_fill16, dim3(g_cus * wpc), dim3(1024), 0, 0,
+                                                 (uint4*)h1, n16); }, reps);
+            printf("fill float4 nt write-only grid=%dx        %8.3f ms  %6.0f GB/s\n", wpc, t, gb / t * 1e3);
+        }
+        t = time_ms([&] { CK(hipMemcpyAsync(h1, tup, n16 * 16, hipMemcpyDeviceToDevice, 0)); }, reps);
+        printf("hipMemcpy DtoD 1 GiB                       %8.3f ms  %6.0f GB/s (R+W)\n", t, 2 * gb / t * 1e3);
+        p.hash_out = h1;
+        p.queue_out = q1;
+        t = time_ms([&] { hipLaunchKernelGGL(mem_ceiling_q8, dim3(g_cus), dim3(1024), 0, 0, p); }, reps);
+        printf("mem 12R+5W nt grid=1x                      %8.3f ms  %6.0f GB/s\n", t, n * 17e-9 / t * 1e3);
+        t = time_ms([&] { prod(true, RSS_FLAG_QUEUE_U8); }, reps);
+        printf("product full u8 (again)                    %8.3f ms  %6.0f GB/s\n", t, n * 17e-9 / t * 1e3);
+    }
+
+    if (strstr("place", filter)) {
+        // physical placement: K output pairs (hash 4n B + queue n B) and two input copies
+        // allocated up front; the product and the 12R+5W streams timed on each combination
+        // in one process, so a placement-dependent rate shows up as a per-buffer difference
+        constexpr int K = 6;
+        uint32_t* hs[K];
+        uint32_t* qs[K];
+        for (int k = 0; k < K; ++k) {
+            CK(hipMalloc(&hs[k], n * 4));
+            CK(hipMalloc(&qs[k], n));
+        }
+        uint32_t* tup2;
+        CK(hipMalloc(&tup2, n * 12));
+        if (rss_generate_tuples(0x5EED, 0, n, (rss_tuple4*)tup2, nullptr)) return 1;
+        CK(hipDeviceSynchronize());
+        const uint32_t* ins[2] = {tup, tup2};
+        for (int in = 0; in < 2; ++in)
+            for (int k = 0; k < K; ++k) {
+                const float tp = time_ms([&] {
+                    if (rss_hash_device(&key, (const rss_tuple4*)ins[in], n, H, Q, hs[k], qs[k],
+                                        (uint64_t*)c0, RSS_FLAG_QUEUE_U8, nullptr)) exit(1);
+                }, reps);
+                Params pp = p;
+                pp.tuples = ins[in];
+                pp.hash_out = hs[k];
+                pp.queue_out = qs[k];
+                const float ts = time_ms([&] { hipLaunchKernelGGL(mem_ceiling_q8, dim3(g_cus), dim3(1024), 0, 0, pp); }, reps);
+                const float tc = time_ms([&] { hipLaunchKernelGGL((mem_stream<false, true, true>), dim3(g_cus), dim3(1024), 0, 0, pp); }, reps);
+                float tpol[4];
+                void (*pk[4])(Params) = {mem_policy<4, false, false>, mem_policy<1, false, false>,
+                                         mem_policy<2, false, false>, mem_policy<0, true, false>};
+                for (int v = 0; v < 4; ++v)
+                    tpol[v] = time_ms([&] { hipLaunchKernelGGL(pk[v], dim3(g_cus), dim3(1024), 0, 0, pp); }, reps);
+                printf("place in=%d out=%d (in %p h %p q %p)  product %.3f  stream %.3f  chunked %.3f  "
+                       "plain %.3f  sc1 %.3f  sc0sc1 %.3f  xcd %.3f ms\n",
+                       in, k, (const void*)ins[in], (void*)hs[k], (void*)qs[k], tp, ts, tc, tpol[0],
+                       tpol[1], tpol[2], tpol[3]);
+            }
+        // each buffer on its own: write-only fill and read-only sweep of hash buffer k, and
+        // the product with hash and queue buffers taken from different pairs
+        for (int k = 0; k < K; ++k) {
+            const uint64_t n16 = n / 4;
+            const float tf = time_ms([&] { hipLaunchKernelGGL(mem_fill16, dim3(g_cus), dim3(1024), 0, 0, (uint4*)hs[k], n16); }, reps);
+            Params pr = p;
+            pr.tuples = hs[k];
+            pr.n = n / 3 * 1;  // n/3 tuples of 12 B = 4n B = the hash buffer
+            const float tr = time_ms([&] { hipLaunchKernelGGL(mem_ceiling<false>, dim3(g_cus), dim3(1024), 0, 0, pr); }, reps);
+            printf("buffer h%d  fill %.3f ms (%.0f GB/s)  read %.3f ms (%.0f GB/s)\n", k, tf,
+                   n16 * 16e-9 / tf * 1e3, tr, (n / 3) * 12e-9 / tr * 1e3);
+        }
+        for (int kh = 0; kh < K; kh += K - 1)
+            for (int kq = 0; kq < K; kq += K - 1) {
+                const float tp = time_ms([&] {
+                    if (rss_hash_device(&key, (const rss_tuple4*)tup, n, H, Q, hs[kh], qs[kq],
+                                        (uint64_t*)c0, RSS_FLAG_QUEUE_U8, nullptr)) exit(1);
+                }, reps);
+                const float th = time_ms([&] {
+                    if (rss_hash_device(&key, (const rss_tuple4*)tup, n, H, Q, hs[kh], nullptr,
+                                        (uint64_t*)c0, 0, nullptr)) exit(1);
+                }, reps);
+                printf("mix h%d q%d  product %.3f ms   hash-only product %.3f ms\n", kh, kq, tp, th);
+            }
+        for (int k = 0; k < K; ++k) {
+            CK(hipFree(hs[k]));
+            CK(hipFree(qs[k]));
+        }
+        CK(hipFree(tup2));
+    }
+
+    if (strstr("shape", filter)) {
+        p.hash_out = h1;
+        p.queue_out = q1;
+        struct SV { const char* name; void (*k)(Params); int wpc; };
+        const SV vs[] = {{"shape 0 product access   grid=1x", mem_shape<0>, 1},
+                         {"shape 1 contiguous loads grid=1x", mem_shape<1>, 1},
+                         {"shape 2 16-B queue store grid=1x", mem_shape<2>, 1},
+                         {"shape 0 product access   grid=2x", mem_shape<0>, 2},
+                         {"shape 1 contiguous loads grid=2x", mem_shape<1>, 2},
+                         {"shape 2 16-B queue store grid=2x", mem_shape<2>, 2}};
+        for (int round = 0; round < 2; ++round)
+            for (const SV& v : vs) {
+                t = time_ms([&] { hipLaunchKernelGGL(v.k, dim3(g_cus * v.wpc), dim3(1024), 0, 0, p); }, reps);
+                printf("%-40s %8.3f ms  %6.0f GB/s\n", v.name, t, n * 17e-9 / t * 1e3);
+            }
+        t = time_ms([&] { prod(true, RSS_FLAG_QUEUE_U8); }, reps);
+        printf("product full u8 (again)                    %8.3f ms  %6.0f GB/s\n", t, n * 17e-9 / t * 1e3);
     }
 
     if (strstr("memq8", filter)) {
