@@ -62,7 +62,7 @@ def parse_args():
     p.add_argument("--distribution", choices=["uniform", "flow"], default="uniform",
                    help="uniform = splitmix64 over all 96 bits (SURVEY.md 8d); flow = the "
                         "example_input/ips.csv shape: one IP pair, sequential source ports")
-    p.add_argument("--placement-probe", type=int, default=4, metavar="K",
+    p.add_argument("--placement-probe", type=int, default=8, metavar="K",
                    help="place the resident buffers by timing the kernel on 2 candidate input "
                         "x K candidate output allocations before the timed region and keeping "
                         "the fastest (rss_simulator_nvidia_amd/placement.py); 0 = first "
@@ -315,28 +315,15 @@ def main():
         else:
             flow_device(torch, t, rank * n, n, dev)
 
-    placement = None
-    if args.placement_probe > 0:
-        from rss_simulator_nvidia_amd.placement import choose_stream_buffers
-
-        def probe(t, h, q, ev):
-            if ev is not None:
-                ev[0].record(stream)
-            _native.hash_device(key, t.data_ptr(), n, H, Q, h.data_ptr(), q.data_ptr(),
-                                counts.data_ptr(), _native.FLAG_ACCUMULATE | qflag, sp)
-            if ev is not None:
-                ev[1].record(stream)
-
-        # queue buffers of 4n bytes, as the unplaced allocation: the u32 secondary line
-        # writes 4 B per tuple into the same buffer
-        tuples, hashes, queues, placement = choose_stream_buffers(
-            torch, dev, n, fill_input, probe, n_inputs=2, n_outputs=args.placement_probe,
-            queue_bytes=4)
-    else:
-        tuples = torch.empty(3 * n, dtype=torch.int32, device=dev)
-        hashes = torch.empty(n, dtype=torch.int32, device=dev)
-        queues = torch.empty(n, dtype=torch.int32, device=dev)  # big enough for any width
-        fill_input(tuples)
+    # resident stream buffers, placed by probing candidate allocations with the real kernel
+    # (ResidentBatch / placement.py); queue buffers of 4n bytes, as the u32
+    # secondary line writes 4 B per tuple into the same buffer
+    from rss_simulator_nvidia_amd.resident import ResidentBatch
+    probe = (2, args.placement_probe) if args.placement_probe > 0 else (1, 1)
+    batch = ResidentBatch(n, key, H, Q, device=dev, fill=fill_input, queue_width=qw,
+                          placement=probe, queue_bytes=4, stream=stream)
+    tuples, hashes, queues = batch.tuples, batch.hashes, batch.queues
+    placement = batch.report
     torch.cuda.synchronize()
 
     # Two count buffers: step i hashes into counts[i % 2] while the RCCL all-reduce of
@@ -540,7 +527,7 @@ def main():
             "cpu_baseline": baseline,
         }
         line["secondary_min_median_max_ms"] = secondary_spread
-        line["placement"] = placement if placement is not None else "first allocation"
+        line["placement"] = placement
         if flow_ms is not None:
             line["flow_like"] = {
                 "kernel_ms": flow_ms, "tuples_per_s_per_gpu": n / (flow_ms / 1e3),

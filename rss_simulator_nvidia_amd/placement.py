@@ -2,20 +2,23 @@
 
 The hot kernel streams three arrays at once -- packed tuples in (12 B/tuple), hashes
 (4 B) and queues (1 B) out -- and runs at the rate of that 12 R + 5 W byte stream.
-Measured on MI355X (``tools/kbench.hip place``, ``profiles/r02/placement_*.log``), that
-rate depends on where the driver places the three allocations in physical HBM: the
-same kernel, inputs and sizes take 0.785, 0.81 or 0.865 ms per 2^28 tuples depending
-on which (input, hash, queue) allocations it is handed, every buffer alone reads and
-writes at full speed, and a plain 12 R + 5 W copy loop with no hashing shows the same
-tiers in the same process -- an interaction of the three streams in the memory system,
-not a property of the kernel, the store cache policy (nt / plain / sc1 / sc0 sc1) or
-the traversal (grid-stride / chunked / XCD-contiguous all move together).
+Measured on MI355X (``tools/kbench.hip place`` / ``contig``, ``profiles/r02/placement_*.log``,
+``profiles/r02/contig_*.log``), that rate depends on where the driver places the
+allocations in physical HBM: the same kernel, inputs and sizes take 0.785, 0.81 or
+0.865 ms per 2^28 tuples depending on which (input, hash, queue) allocations it is
+handed.  Every buffer alone reads and writes at full speed, and a plain 12 R + 5 W copy
+loop with no hashing shows the same tiers on the same buffers -- an interaction of the
+concurrent streams in the memory system, not a property of the kernel, the store cache
+policy (nt / plain / sc1 / sc0 sc1) or the traversal (grid-stride / chunked /
+XCD-contiguous all move together).  The tier follows the buffer, is stable for the life
+of the allocation, differs between 1 GiB regions of one large allocation, and physically
+contiguous allocations (``hipDeviceMallocContiguous``) land in all three tiers too.
 
 Physical addresses are not visible from user space, so a long-lived deployment places
 its resident buffers empirically, once: allocate a few candidate output (and input)
 buffers, time a few launches of the real kernel on each combination, keep the fastest,
 free the rest.  This is done before any timed work and does not change what is
-computed.
+computed.  ``rss_simulator_nvidia_amd.resident.ResidentBatch`` does it for callers.
 """
 import statistics
 
@@ -32,6 +35,8 @@ def choose_stream_buffers(torch, dev, n, fill_input, probe, n_inputs=2, n_output
     launch time, the chosen pair and the first-allocated pair's time (what an
     unplaced allocation would have run at).
     """
+    if n < 1:
+        raise ValueError("choose_stream_buffers: n must be >= 1")
     inputs = []
     for _ in range(max(1, n_inputs)):
         t = torch.empty(3 * n, dtype=torch.int32, device=dev)

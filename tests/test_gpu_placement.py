@@ -49,3 +49,32 @@ def test_choose_stream_buffers_probes_and_keeps_the_fastest(oracle_lib, example_
     np.testing.assert_array_equal(hashes.cpu().numpy().view(np.uint32), h)
     np.testing.assert_array_equal(queues.cpu().numpy(), q.astype(np.uint8))
     np.testing.assert_array_equal(counts.cpu().numpy().view(np.uint64), c)
+
+
+@pytest.mark.parametrize("width,placement", [("auto", (2, 3)), ("u16", (1, 1)), ("u32", (1, 2))])
+def test_resident_batch_equals_oracle(oracle_lib, example_key, width, placement):
+    """ResidentBatch: placed buffers, then batch after batch on the same buffers -- every
+    pass gives the oracle's hash / queue / counts, overwritten or accumulated."""
+    from rss_simulator_nvidia_amd import _native
+    from rss_simulator_nvidia_amd.resident import ResidentBatch
+    n, H, Q = (1 << 18) + 5, 512, 64
+    dev = torch.device("cuda:0")
+    key = _native.prepare_key(example_key)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    batch = ResidentBatch(n, key, H, Q, device=dev, queue_width=width, placement=placement,
+                          fill=lambda t: _native.generate_device(7, 0, n, t.data_ptr(), s))
+    assert batch.report["candidates"] == {"inputs": placement[0], "outputs": placement[1]}
+    counts = torch.full((Q,), 12345, dtype=torch.int64, device=dev)
+    for first in (0, n):  # a second batch written by the caller into the same input
+        _native.generate_device(7, first, n, batch.tuples.data_ptr(), s)
+        batch.hash(counts)
+        batch.hash(counts, accumulate=True)
+        torch.cuda.synchronize()
+        tup = oracle_lib.generate(7, first, n)
+        h, q, c = oracle_lib.run(example_key, tup, H, Q)
+        np.testing.assert_array_equal(batch.hashes.cpu().numpy().view(np.uint32), h)
+        qv = batch.queue_view().cpu().numpy()
+        qv = qv.view({1: np.uint8, 2: np.uint16, 4: np.uint32}[qv.itemsize])
+        np.testing.assert_array_equal(qv.astype(np.uint32), q)
+        np.testing.assert_array_equal(counts.cpu().numpy().view(np.uint64), 2 * c)
+

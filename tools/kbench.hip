@@ -766,6 +766,113 @@ int main(int argc, char** argv) {
         CK(hipFree(tup2));
     }
 
+    if (strstr("contig", filter)) {
+        // allocation kind vs the 12R+5W rate: K output pairs and one input from plain hipMalloc,
+        // the same from hipExtMallocWithFlags(hipDeviceMallocContiguous), and K output pairs carved
+        // at 1 GiB steps from one large hipMalloc pool; product + stream per combination
+        constexpr int K = 4;
+        uint32_t *hp[K], *qp[K], *hc[K] = {}, *qc[K] = {};
+        for (int k = 0; k < K; ++k) {
+            CK(hipMalloc(&hp[k], n * 4));
+            CK(hipMalloc(&qp[k], n));
+        }
+        uint32_t* tc = nullptr;
+        if (hipExtMallocWithFlags((void**)&tc, n * 12, hipDeviceMallocContiguous) != hipSuccess) {
+            printf("contiguous input allocation refused\n");
+            tc = nullptr;
+            (void)hipGetLastError();
+        }
+        for (int k = 0; k < K; ++k) {
+            if (hipExtMallocWithFlags((void**)&hc[k], n * 4, hipDeviceMallocContiguous) != hipSuccess ||
+                hipExtMallocWithFlags((void**)&qc[k], n, hipDeviceMallocContiguous) != hipSuccess) {
+                printf("contiguous output allocation %d refused\n", k);
+                (void)hipGetLastError();
+                hc[k] = qc[k] = nullptr;
+            }
+        }
+        const size_t pool_stride = size_t(1) << 30, pair = n * 5;
+        uint8_t* pool = nullptr;
+        CK(hipMalloc(&pool, pool_stride * (K - 1) + pair));
+        if (tc) {
+            CK(hipMemcpy(tc, tup, n * 12, hipMemcpyDeviceToDevice));
+        }
+        CK(hipDeviceSynchronize());
+        auto both = [&](const char* what, const uint32_t* in, uint32_t* h, uint32_t* q) {
+            if (!in || !h || !q) return;
+            const float tp = time_ms([&] {
+                if (rss_hash_device(&key, (const rss_tuple4*)in, n, H, Q, h, q, (uint64_t*)c0,
+                                    RSS_FLAG_QUEUE_U8, nullptr)) exit(1);
+            }, reps);
+            Params pp = p;
+            pp.tuples = in;
+            pp.hash_out = h;
+            pp.queue_out = q;
+            const float ts = time_ms([&] { hipLaunchKernelGGL(mem_ceiling_q8, dim3(g_cus), dim3(1024), 0, 0, pp); }, reps);
+            printf("contig %-28s (in %p h %p q %p)  product %.3f  stream %.3f ms\n", what,
+                   (const void*)in, (void*)h, (void*)q, tp, ts);
+        };
+        char name[64];
+        for (int round = 0; round < 2; ++round)
+            for (int k = 0; k < K; ++k) {
+                snprintf(name, sizeof name, "in=malloc out=malloc%d", k);
+                both(name, tup, hp[k], qp[k]);
+                snprintf(name, sizeof name, "in=malloc out=contig%d", k);
+                both(name, tup, hc[k], qc[k]);
+                snprintf(name, sizeof name, "in=contig out=malloc%d", k);
+                both(name, tc, hp[k], qp[k]);
+                snprintf(name, sizeof name, "in=contig out=contig%d", k);
+                both(name, tc, hc[k], qc[k]);
+                snprintf(name, sizeof name, "in=malloc out=pool+%dGiB", k);
+                both(name, tup, (uint32_t*)(pool + k * pool_stride), (uint32_t*)(pool + k * pool_stride + n * 4));
+            }
+        for (int k = 0; k < K; ++k) {
+            CK(hipFree(hp[k]));
+            CK(hipFree(qp[k]));
+            if (hc[k]) CK(hipFree(hc[k]));
+            if (qc[k]) CK(hipFree(qc[k]));
+        }
+        if (tc) CK(hipFree(tc));
+        CK(hipFree(pool));
+    }
+
+    if (strstr("offsets", filter)) {
+        // relative placement inside ONE allocation (physically contiguous when the driver
+        // grants hipDeviceMallocContiguous, else plain hipMalloc): tuples at 0, hashes at
+        // 12n + a, queues at 16n + a + b; scan a (b = 0) then b (a = 0) in 32 MiB steps
+        const size_t MiB = size_t(1) << 20, span = 1024 * MiB;
+        const size_t bytes = n * 17 + 2 * span + 64 * MiB;
+        for (int kind = 0; kind < 2; ++kind) {
+            uint8_t* pool = nullptr;
+            if (kind == 0) {
+                if (hipExtMallocWithFlags((void**)&pool, bytes, hipDeviceMallocContiguous) != hipSuccess) {
+                    (void)hipGetLastError();
+                    printf("offsets: contiguous pool refused\n");
+                    continue;
+                }
+            } else {
+                CK(hipMalloc(&pool, bytes));
+            }
+            CK(hipMemcpy(pool, tup, n * 12, hipMemcpyDeviceToDevice));
+            CK(hipDeviceSynchronize());
+            for (int scan = 0; scan < 2; ++scan)
+                for (size_t off = 0; off <= span; off += 32 * MiB) {
+                    const size_t a = scan == 0 ? off : 0, b = scan == 0 ? 0 : off;
+                    Params pp = p;
+                    pp.tuples = (const uint32_t*)pool;
+                    pp.hash_out = (uint32_t*)(pool + n * 12 + a);
+                    pp.queue_out = (uint32_t*)(pool + n * 16 + a + b);
+                    const float ts = time_ms([&] { hipLaunchKernelGGL(mem_ceiling_q8, dim3(g_cus), dim3(1024), 0, 0, pp); }, reps);
+                    const float tp = time_ms([&] {
+                        if (rss_hash_device(&key, (const rss_tuple4*)pp.tuples, n, H, Q, pp.hash_out,
+                                            pp.queue_out, (uint64_t*)c0, RSS_FLAG_QUEUE_U8, nullptr)) exit(1);
+                    }, reps);
+                    printf("offsets %s pool %p  hash +%4zu MiB  queue +%4zu MiB  stream %.3f  product %.3f ms\n",
+                           kind == 0 ? "contig" : "malloc", (void*)pool, a / MiB, b / MiB, ts, tp);
+                }
+            CK(hipFree(pool));
+        }
+    }
+
     if (strstr("shape", filter)) {
         p.hash_out = h1;
         p.queue_out = q1;
