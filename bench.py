@@ -137,6 +137,8 @@ def cpu_share():
     # a scheduler that shares the machine without a quota states the share in
     # OMP_NUM_THREADS (the GPU boxes set it to their CPU share)
     omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp == "1" and int(os.environ.get("LOCAL_WORLD_SIZE", "1")) > 1:
+        omp = ""  # torch.distributed.run's own default for nproc > 1, not a CPU share
     if omp.isdigit() and int(omp) > 0:
         cores = min(cores, int(omp))
     return max(1, cores)

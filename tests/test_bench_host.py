@@ -34,3 +34,19 @@ def test_load_traffic_only_for_matching_config(tmp_path):
     assert bench.load_traffic(str(tmp_path), 8, 128, 24, "u8") == 136.0
     assert bench.load_traffic(str(tmp_path), 8, 128, 24, "u32") is None
     assert bench.load_traffic(str(tmp_path / "missing"), 8, 128, 24, "u8") is None
+
+
+def test_cpu_share_ignores_torchrun_default_omp(monkeypatch):
+    """torch.distributed.run sets OMP_NUM_THREADS=1 for nproc > 1 when it is unset: that is
+    not the node's CPU share, so the N > 1 baseline is not cut to one core by it."""
+    import bench
+    monkeypatch.setenv("OMP_NUM_THREADS", "1")
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    free = bench.cpu_share()
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")
+    assert bench.cpu_share() == 1
+    monkeypatch.delenv("OMP_NUM_THREADS")
+    assert free == bench.cpu_share()
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    assert bench.cpu_share() == min(3, free)

@@ -13,3 +13,5 @@ cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
     python $R/bench.py --no-cpu-baseline "$@" > $OUT/prof.log 2>&1
 find $OUT/prof -name '*kernel_stats.csv' -exec cat {} \;
+python3 $R/tools/prof_timed.py $OUT/prof/run_kernel_trace.csv $OUT/prof.log > $OUT/prof_timed.json
+cat $OUT/prof_timed.json
