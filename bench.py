@@ -62,7 +62,7 @@ def parse_args():
     p.add_argument("--distribution", choices=["uniform", "flow"], default="uniform",
                    help="uniform = splitmix64 over all 96 bits (SURVEY.md 8d); flow = the "
                         "example_input/ips.csv shape: one IP pair, sequential source ports")
-    p.add_argument("--placement-probe", type=int, default=8, metavar="K",
+    p.add_argument("--placement-probe", type=int, default=12, metavar="K",
                    help="place the resident buffers by timing the kernel on 2 candidate input "
                         "x K candidate output allocations before the timed region and keeping "
                         "the fastest (rss_simulator_nvidia_amd/placement.py); 0 = first "
