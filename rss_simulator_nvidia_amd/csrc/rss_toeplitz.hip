@@ -23,6 +23,7 @@
 
 #include <cstdarg>
 #include <cstdint>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <algorithm>
@@ -367,6 +368,116 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
             }
             if (s) atomicAdd(&p.counts[q], (unsigned long long)s);
         }
+    }
+}
+
+// Counts only, power-of-two H <= 256 (histogram mode, `rss_hash_host` without per-tuple
+// outputs): the queue depends on hash & (H-1) alone, at most 8 bits, so every table term
+// fits a byte and the tables move from LDS into registers.  Each input byte is cut into
+// 3 + 3 + 2-bit fields (36 fields, field LSBs first as above); field f's <= 8-entry byte
+// table is two dwords, and v_perm_b32 looks up all four selector bytes of a dword in it at
+// once.  A lane's four tuples are byte-transposed (8 v_perm per word) so that one selector
+// dword holds the same field of the four tuples: one v_perm = one field of four tuples,
+// and the XOR of the 36 lookups is the four tuples' buckets, one per byte.  Per four
+// tuples ~170 VALU (60 v_perm) and 4 conflict-free `ds_add_u32` -- against 8 random-index
+// `ds_read_b32` per tuple in the LUT kernel, whose bank conflicts bind it in this mode
+// (DESIGN.md §3).  Measured 0.525-0.531 vs 0.545-0.548 ms per 2^28 tuples, read-only
+// stream 0.513-0.519 (profiles/r02/perm_counts.log).
+constexpr int kPermFields = 36;
+
+struct PermParams {
+    const rss_tuple4* tuples;
+    unsigned long long* counts;
+    uint64_t n;
+    uint32_t Q;
+    uint32_t q_mask;    // QM_MASK
+    uint32_t q_m16;     // QM_FAST8
+    uint32_t lo[kPermFields];  // field f: table entries 0..3 (v_perm selector 0..3)
+    uint32_t hi[kPermFields];  //          entries 4..7 (selector 4..7)
+};
+
+__device__ __forceinline__ uint32_t vperm(uint32_t s0, uint32_t s1, uint32_t sel) {
+    return __builtin_amdgcn_perm(s0, s1, sel);
+}
+
+// t_j = byte j of (x0, x1, x2, x3), tuple i in byte i
+__device__ __forceinline__ void transpose_bytes(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3,
+                                                uint32_t& t0, uint32_t& t1, uint32_t& t2,
+                                                uint32_t& t3) {
+    const uint32_t a = vperm(x1, x0, 0x05010400u), b = vperm(x1, x0, 0x07030602u);
+    const uint32_t c = vperm(x3, x2, 0x05010400u), d = vperm(x3, x2, 0x07030602u);
+    t0 = vperm(c, a, 0x05040100u);
+    t1 = vperm(c, a, 0x07060302u);
+    t2 = vperm(d, b, 0x05040100u);
+    t3 = vperm(d, b, 0x07060302u);
+}
+
+// XOR of the three field terms of byte-transposed dword t (fields kF .. kF+2)
+template <int kF>
+__device__ __forceinline__ uint32_t perm_byte_terms(const PermParams& p, uint32_t t) {
+    const uint32_t f0 = vperm(p.hi[kF], p.lo[kF], t & 0x07070707u);
+    const uint32_t f1 = vperm(p.hi[kF + 1], p.lo[kF + 1], (t >> 3) & 0x07070707u);
+    const uint32_t f2 = vperm(p.lo[kF + 2], p.lo[kF + 2], (t >> 6) & 0x03030303u);
+    return xor3(f0, f1, f2);
+}
+
+// acc ^ the terms of word kK of four tuples
+template <int kK>
+__device__ __forceinline__ uint32_t perm_word(const PermParams& p, uint32_t x0, uint32_t x1,
+                                              uint32_t x2, uint32_t x3, uint32_t acc) {
+    uint32_t t0, t1, t2, t3;
+    transpose_bytes(x0, x1, x2, x3, t0, t1, t2, t3);
+    return xor3(xor3(acc, perm_byte_terms<kK * 12 + 0>(p, t0), perm_byte_terms<kK * 12 + 3>(p, t1)),
+                perm_byte_terms<kK * 12 + 6>(p, t2), perm_byte_terms<kK * 12 + 9>(p, t3));
+}
+
+// buckets of four tuples (tuple i's hash & (H-1) in byte i)
+__device__ __forceinline__ uint32_t perm_buckets(const PermParams& p, const uint32_t (&w)[12]) {
+    uint32_t acc = perm_word<0>(p, w[0], w[3], w[6], w[9], 0u);
+    acc = perm_word<1>(p, w[1], w[4], w[7], w[10], acc);
+    return perm_word<2>(p, w[2], w[5], w[8], w[11], acc);
+}
+
+template <int kQMode>
+__device__ __forceinline__ uint32_t perm_queue(uint32_t b, const PermParams& p) {
+    if constexpr (kQMode == QM_MASK) return b & p.q_mask;
+    return b - __umul24(__umul24(b, p.q_m16) >> 16, p.Q);  // QM_FAST8: b, Q < 256
+}
+
+__device__ __forceinline__ void perm_count(uint32_t* bins, uint32_t q, uint32_t col) {
+    __hip_atomic_fetch_add(&bins[q * kBinCols + col], 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <int kQMode>
+__global__ __launch_bounds__(kBlock, 2) void rss_counts_perm_kernel(const PermParams p) {
+    extern __shared__ uint32_t bins[];  // Q x 32 private columns
+    const uint32_t tid = threadIdx.x, col = tid & (kBinCols - 1);
+    for (uint32_t e = tid; e < p.Q * kBinCols; e += kBlock) bins[e] = 0;
+    __syncthreads();
+    const uint4* __restrict__ src = reinterpret_cast<const uint4*>(p.tuples);
+    const uint64_t ngroups = p.n >> 2;
+    const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
+    for (uint64_t g = gtid; g < ngroups; g += (uint64_t)gridDim.x * kBlock) {
+        const uint4 a = src[3 * g], b = src[3 * g + 1], c = src[3 * g + 2];
+        const uint32_t w[12] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w};
+        const uint32_t bk = perm_buckets(p, w);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            perm_count(bins, perm_queue<kQMode>((bk >> (8 * i)) & 0xFFu, p), col);
+    }
+    // the last n % 4 tuples: one per lane of the first workgroup, in byte 0
+    const uint64_t i = (ngroups << 2) + gtid;
+    if (i < p.n) {
+        const uint32_t* t = reinterpret_cast<const uint32_t*>(p.tuples) + 3 * i;
+        const uint32_t w[12] = {t[0], t[1], t[2], 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        perm_count(bins, perm_queue<kQMode>(perm_buckets(p, w) & 0xFFu, p), col);
+    }
+    __syncthreads();
+    for (uint32_t q = tid; q < p.Q; q += kBlock) {  // rotated reads: conflict-free
+        uint32_t s = 0;
+        for (uint32_t c = 0; c < kBinCols; ++c) s += bins[q * kBinCols + ((c + q) & (kBinCols - 1))];
+        if (s) atomicAdd(&p.counts[q], (unsigned long long)s);
     }
 }
 
@@ -1152,6 +1263,50 @@ int check_reta(const uint32_t* reta, uint32_t htable, uint32_t nqueues, const ch
     return RSS_OK;
 }
 
+// RSS_COUNTS_PERM=0 routes counts-only launches to the LUT kernel too (A/B, tests)
+bool counts_perm_enabled() {
+    const char* e = getenv("RSS_COUNTS_PERM");
+    return !(e && e[0] == '0');
+}
+
+// Counts only, power-of-two H <= 256, 16-B aligned tuples: rss_counts_perm_kernel with the
+// 36 byte tables of (window & (H-1)) built here, from the same windows as the LUT.
+int launch_counts_perm(const rss_key* key, const LaunchParams& lp, int qmode, uint32_t bin_bytes,
+                       int cu_count, hipStream_t stream) {
+    PermParams pp;
+    memset(&pp, 0, sizeof pp);
+    pp.tuples = lp.tuples;
+    pp.counts = lp.counts;
+    pp.n = lp.n;
+    pp.Q = lp.Q;
+    pp.q_mask = lp.q_mask;
+    pp.q_m16 = lp.q_m16;
+    for (int k = 0; k < 3; ++k)          // word (src ip, dst ip, ports)
+        for (int j = 0; j < 4; ++j)      // byte of the word, least significant first
+            for (int f = 0; f < 3; ++f) {  // fields [0,3) [3,6) [6,8) of the byte
+                const int id = (k * 4 + j) * 3 + f, lsb = 8 * j + 3 * f, len = f < 2 ? 3 : 2;
+                uint8_t e[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                for (int v = 0; v < (1 << len); ++v)
+                    for (int b = 0; b < len; ++b)  // word k bit i is input bit 32k + 31 - i
+                        if ((v >> b) & 1) e[v] ^= (uint8_t)(key->window[32 * k + 31 - (lsb + b)] & lp.h_mask);
+                pp.lo[id] = e[0] | e[1] << 8 | e[2] << 16 | (uint32_t)e[3] << 24;
+                pp.hi[id] = e[4] | e[5] << 8 | e[6] << 16 | (uint32_t)e[7] << 24;
+            }
+    // 48 VGPRs and no LUT: two 1024-lane workgroups fit a CU (RSS_COUNTS_PERM_WGS=1|2)
+    const char* wgs_env = getenv("RSS_COUNTS_PERM_WGS");
+    const uint64_t wgs = wgs_env && wgs_env[0] == '1' ? 1 : 2;
+    const uint64_t want = (lp.n + 4 * kBlock - 1) / (4 * kBlock);
+    const unsigned grid = (unsigned)(want < wgs * cu_count ? want : wgs * cu_count);
+    if (qmode == QM_MASK)
+        hipLaunchKernelGGL(rss_counts_perm_kernel<QM_MASK>, dim3(grid), dim3(kBlock), bin_bytes,
+                           stream, pp);
+    else
+        hipLaunchKernelGGL(rss_counts_perm_kernel<QM_FAST8>, dim3(grid), dim3(kBlock), bin_bytes,
+                           stream, pp);
+    RSS_HIP_CHECK(hipGetLastError());
+    return RSS_OK;
+}
+
 int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32_t htable,
                 uint32_t nqueues, uint32_t* d_hash, void* d_queue, uint64_t* d_counts,
                 uint32_t flags, hipStream_t stream, const uint32_t* reta = nullptr) {
@@ -1203,12 +1358,15 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
     const uintptr_t qalign = qwidth == QW_U8 ? 4 : (qwidth == QW_U16 ? 8 : 16);
     const bool vec4 = aligned16(d_tuples) && (!d_hash || aligned16(d_hash)) &&
                       (!d_queue || ((uintptr_t)d_queue % qalign) == 0);
-    KernelFn fn = h_pow2 ? pick_queue<true>(qmode, hist, qwidth, vec4)
-                         : pick_queue<false>(qmode, hist, qwidth, vec4);
-
     DeviceInfo info;
     int rc = device_info(&info);
     if (rc) return rc;
+    if (!d_hash && !d_queue && d_counts && !reta && h_pow2 && htable <= 256u &&
+        hist == HIST_PRIVATE && (qmode == QM_MASK || qmode == QM_FAST8) && aligned16(d_tuples) &&
+        counts_perm_enabled())
+        return launch_counts_perm(key, p, qmode, bin_bytes, info.cu_count, stream);
+    KernelFn fn = h_pow2 ? pick_queue<true>(qmode, hist, qwidth, vec4)
+                         : pick_queue<false>(qmode, hist, qwidth, vec4);
     const uint64_t per_lane = vec4 ? 4 : 1;
     const uint64_t want = (n + per_lane * kBlock - 1) / (per_lane * kBlock);
     const uint64_t cap = (uint64_t)info.cu_count * kBlocksPerCU;

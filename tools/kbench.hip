@@ -607,6 +607,103 @@ static float time_ms(F launch, int reps) {
     return ms / reps;
 }
 
+// ------------------------------------------------ counts-only, no LDS tables
+// For a power-of-two H <= 256 the histogram needs only hash & (H-1), i.e. <= 8 bits: each
+// table term fits a byte.  Cut each input byte into 3 + 3 + 2-bit fields (36 fields); an
+// 8-entry byte table is two dwords, and v_perm_b32 looks up four selector bytes in it at
+// once.  A lane's four tuples are byte-transposed (8 v_perm per word) so that one selector
+// dword holds the same field of all four tuples: one v_perm = one field of four tuples.
+struct PermParams {
+    const uint32_t* tuples;
+    unsigned long long* counts;
+    uint64_t n;
+    uint32_t Q, q_m16;
+    uint32_t lo[36], hi[36];  // field f: entries 0..3 in lo[f], 4..7 in hi[f]
+};
+
+__device__ __forceinline__ uint32_t vperm(uint32_t s0, uint32_t s1, uint32_t sel) {
+    return __builtin_amdgcn_perm(s0, s1, sel);
+}
+
+__device__ __forceinline__ void transpose4(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3,
+                                           uint32_t& t0, uint32_t& t1, uint32_t& t2, uint32_t& t3) {
+    const uint32_t A = vperm(x1, x0, 0x05010400u), B = vperm(x1, x0, 0x07030602u);
+    const uint32_t C = vperm(x3, x2, 0x05010400u), D = vperm(x3, x2, 0x07030602u);
+    t0 = vperm(C, A, 0x05040100u);
+    t1 = vperm(C, A, 0x07060302u);
+    t2 = vperm(D, B, 0x05040100u);
+    t3 = vperm(D, B, 0x07060302u);
+}
+
+// the three fields of byte-transposed dword t (byte j of word k of four tuples)
+template <int kF>
+__device__ __forceinline__ uint32_t perm_byte(const PermParams& p, uint32_t t, uint32_t acc) {
+    const uint32_t f0 = vperm(p.hi[kF], p.lo[kF], t & 0x07070707u);
+    const uint32_t f1 = vperm(p.hi[kF + 1], p.lo[kF + 1], (t >> 3) & 0x07070707u);
+    const uint32_t f2 = vperm(p.lo[kF + 2], p.lo[kF + 2], (t >> 6) & 0x03030303u);
+    (void)acc;
+    return __builtin_amdgcn_bitop3_b32(f0, f1, f2, 0x96);
+}
+
+template <int kK>
+__device__ __forceinline__ uint32_t perm_word(const PermParams& p, uint32_t x0, uint32_t x1,
+                                              uint32_t x2, uint32_t x3, uint32_t acc) {
+    uint32_t t0, t1, t2, t3;
+    transpose4(x0, x1, x2, x3, t0, t1, t2, t3);
+    const uint32_t x = perm_byte<kK * 12 + 0>(p, t0, 0), y = perm_byte<kK * 12 + 3>(p, t1, 0);
+    const uint32_t z = perm_byte<kK * 12 + 6>(p, t2, 0), w = perm_byte<kK * 12 + 9>(p, t3, 0);
+    return __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(acc, x, y, 0x96), z, w, 0x96);
+}
+
+__global__ __launch_bounds__(1024) void perm_counts_kernel(const PermParams p) {
+    extern __shared__ uint32_t pbins[];
+    const uint32_t tid = threadIdx.x, col = tid & 31;
+    for (uint32_t e = tid; e < p.Q * 32; e += 1024) pbins[e] = 0;
+    __syncthreads();
+    const uint4* __restrict__ src = reinterpret_cast<const uint4*>(p.tuples);
+    const uint64_t ng = p.n >> 2;
+    for (uint64_t g = (uint64_t)blockIdx.x * 1024 + tid; g < ng; g += (uint64_t)gridDim.x * 1024) {
+        const uint4 a = src[3 * g], b = src[3 * g + 1], c = src[3 * g + 2];
+        uint32_t acc = perm_word<0>(p, a.x, a.w, b.z, c.y, 0u);
+        acc = perm_word<1>(p, a.y, b.x, b.w, c.z, acc);
+        acc = perm_word<2>(p, a.z, b.y, c.x, c.w, acc);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t bk = (acc >> (8 * i)) & 0xFFu;
+            const uint32_t q = bk - __umul24(__umul24(bk, p.q_m16) >> 16, p.Q);
+            __hip_atomic_fetch_add(&pbins[q * 32 + col], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+    __syncthreads();
+    for (uint32_t q = tid; q < p.Q; q += 1024) {
+        uint32_t s = 0;
+        for (uint32_t c2 = 0; c2 < 32; ++c2) s += pbins[q * 32 + ((c2 + q) & 31)];
+        if (s) atomicAdd(&p.counts[q], (unsigned long long)s);
+    }
+}
+
+static PermParams perm_params(const rss_key& key, const uint32_t* tup, unsigned long long* counts,
+                              uint64_t n, uint32_t H, uint32_t Q) {
+    PermParams pp{};
+    pp.tuples = tup;
+    pp.counts = counts;
+    pp.n = n;
+    pp.Q = Q;
+    pp.q_m16 = (65536u + Q - 1) / Q;
+    for (int k = 0; k < 3; ++k)
+        for (int j = 0; j < 4; ++j)
+            for (int f = 0; f < 3; ++f) {
+                const int id = (k * 4 + j) * 3 + f, s = 8 * j + 3 * f, len = f < 2 ? 3 : 2;
+                uint8_t e[8] = {};
+                for (int v = 0; v < (1 << len); ++v)
+                    for (int bb = 0; bb < len; ++bb)
+                        if ((v >> bb) & 1) e[v] ^= (uint8_t)(key.window[32 * k + 31 - (s + bb)] & (H - 1));
+                pp.lo[id] = e[0] | e[1] << 8 | e[2] << 16 | (uint32_t)e[3] << 24;
+                pp.hi[id] = e[4] | e[5] << 8 | e[6] << 16 | (uint32_t)e[7] << 24;
+            }
+    return pp;
+}
+
 int main(int argc, char** argv) {
     const uint64_t n = argc > 1 ? strtoull(argv[1], 0, 0) : (1ull << 28);
     const int reps = argc > 2 ? atoi(argv[2]) : 20;
@@ -833,6 +930,31 @@ int main(int argc, char** argv) {
         }
         if (tc) CK(hipFree(tc));
         CK(hipFree(pool));
+    }
+
+    if (strstr("perm", filter)) {
+        const PermParams pp = perm_params(key, tup, c1, n, H, Q);
+        for (int wpc : {1, 2}) {
+            CK(hipMemset(c1, 0, Q * 8));
+            hipLaunchKernelGGL(perm_counts_kernel, dim3(g_cus * wpc), dim3(1024), Q * 32 * 4, 0, pp);
+            CK(hipDeviceSynchronize());
+            CK(hipMemcpy(rc1.data(), c1, Q * 8, hipMemcpyDeviceToHost));
+            printf("perm counts grid=%dx check: %s\n", wpc, rc1 == rc0 ? "OK" : "MISMATCH");
+        }
+        for (int round = 0; round < 3; ++round) {
+            t = time_ms([&] { prod(false); }, reps);
+            printf("%-40s %8.3f ms  %7.1f Gt/s  %6.0f GB/s\n", "product counts", t, n / t / 1e6, gb_r / t * 1e3);
+            for (int wpc : {1, 2}) {
+                t = time_ms([&] {
+                    CK(hipMemsetAsync(c1, 0, Q * 8, 0));
+                    hipLaunchKernelGGL(perm_counts_kernel, dim3(g_cus * wpc), dim3(1024), Q * 32 * 4, 0, pp);
+                }, reps);
+                printf("perm counts grid=%dx                      %8.3f ms  %7.1f Gt/s  %6.0f GB/s\n", wpc, t,
+                       n / t / 1e6, gb_r / t * 1e3);
+            }
+            t = time_ms([&] { hipLaunchKernelGGL(mem_ceiling<false>, dim3(g_cus), dim3(1024), 0, 0, p); }, reps);
+            printf("%-40s %8.3f ms  %7.1f Gt/s  %6.0f GB/s\n", "mem read-only grid=1x", t, n / t / 1e6, gb_r / t * 1e3);
+        }
     }
 
     if (strstr("offsets", filter)) {
