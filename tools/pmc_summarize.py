@@ -20,7 +20,7 @@ ALGO = {"full_u8": 17, "counts_only": 12, "full_u32": 20}
 def per_dispatch(path):
     agg = collections.OrderedDict()
     for r in csv.DictReader(open(path)):
-        if "rss_toeplitz_kernel" not in r["Kernel_Name"]:
+        if not any(k in r["Kernel_Name"] for k in ("rss_toeplitz_kernel", "rss_counts_perm_kernel")):
             continue
         agg.setdefault(int(r["Dispatch_Id"]), collections.Counter())[r["Counter_Name"]] += \
             float(r["Counter_Value"])
