@@ -318,12 +318,12 @@ def main():
             flow_device(torch, t, rank * n, n, dev)
 
     # resident stream buffers, placed by probing candidate allocations with the real kernel
-    # (ResidentBatch / placement.py); queue buffers of 4n bytes, as the u32
-    # secondary line writes 4 B per tuple into the same buffer
+    # (ResidentBatch / placement.py); queue buffers of the queue width (the u32
+    # secondary line gets its own buffer after the timed region)
     from rss_simulator_nvidia_amd.resident import ResidentBatch
     probe = (2, args.placement_probe) if args.placement_probe > 0 else (1, 1)
     batch = ResidentBatch(n, key, H, Q, device=dev, fill=fill_input, queue_width=qw,
-                          placement=probe, queue_bytes=4, stream=stream)
+                          placement=probe, stream=stream)
     tuples, hashes, queues = batch.tuples, batch.hashes, batch.queues
     placement = batch.report
     torch.cuda.synchronize()
@@ -440,7 +440,10 @@ def main():
     if rank == 0:
         reps = max(5, args.steps // 2)
         co_ms = kernel_ms_of(None, None, 0, reps)
-        u32_ms = kernel_ms_of(hashes.data_ptr(), queues.data_ptr(), 0, reps)
+        queues32 = queues if queues.numel() >= 4 * n else torch.empty(n, dtype=torch.int32,
+                                                                        device=dev)
+        u32_ms = kernel_ms_of(hashes.data_ptr(), queues32.data_ptr(), 0, reps)
+        del queues32
         if args.distribution == "uniform":  # same kernel on SURVEY.md 8(d)'s flow-like input
             flow_device(torch, tuples, 0, n, dev)
             flow_ms = kernel_ms_of(hashes.data_ptr(), queues.data_ptr(), qflag, reps)

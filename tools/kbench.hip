@@ -932,6 +932,34 @@ int main(int argc, char** argv) {
         CK(hipFree(pool));
     }
 
+    if (strstr("qsize", filter)) {
+        // does the queue allocation's size (n B, as u8 queues need, vs 4n B, as the bench
+        // allocates for its u32 line) change how often a placement lands in the fast tier?
+        // K pairs of each kind, allocated alternately, all against the same input
+        constexpr int K = 6;
+        uint32_t *hs[2][K], *qs[2][K];
+        for (int k = 0; k < K; ++k)
+            for (int kind = 0; kind < 2; ++kind) {
+                CK(hipMalloc(&hs[kind][k], n * 4));
+                CK(hipMalloc(&qs[kind][k], kind == 0 ? n : 4 * n));
+            }
+        for (int round = 0; round < 2; ++round)
+            for (int kind = 0; kind < 2; ++kind)
+                for (int k = 0; k < K; ++k) {
+                    const float tp = time_ms([&] {
+                        if (rss_hash_device(&key, (const rss_tuple4*)tup, n, H, Q, hs[kind][k], qs[kind][k],
+                                            (uint64_t*)c0, RSS_FLAG_QUEUE_U8, nullptr)) exit(1);
+                    }, reps);
+                    printf("qsize %s pair %d (h %p q %p)  product %.3f ms\n", kind == 0 ? "q=n " : "q=4n", k,
+                           (void*)hs[kind][k], (void*)qs[kind][k], tp);
+                }
+        for (int k = 0; k < K; ++k)
+            for (int kind = 0; kind < 2; ++kind) {
+                CK(hipFree(hs[kind][k]));
+                CK(hipFree(qs[kind][k]));
+            }
+    }
+
     if (strstr("perm", filter)) {
         const PermParams pp = perm_params(key, tup, c1, n, H, Q);
         for (int wpc : {1, 2}) {
