@@ -166,10 +166,32 @@ def cpu_baseline(key, n_sample, procs, distribution="uniform"):
     dt = time.perf_counter() - t0
     assert sum(len(o) for o in out) == n_sample
     return {"value": n_sample / dt, "unit": "tuples/s", "cores": procs, "kind": "port",
+            "optimised_c": optimised_c_baseline(key, procs, distribution),
             "procs": procs, "cpu_share": cpu_share(), "host_cores": os.cpu_count(),
             "sample": "first %d tuples of the bench stream, pure-Python restatement of "
                       "toeplitz.py:46-69 (rotating bit-string key) in %d processes (one per "
                       "core of this process's CPU share), %.2f s wall" % (n_sample, procs, dt)}
+
+
+def optimised_c_baseline(key, threads, distribution="uniform", n=1 << 24):
+    """SURVEY.md 8(d)'s optional "optimised CPU" line: the C byte-table form
+    (``oracle_run_tables``: twelve 256-entry tables, hash % H % Q and the histogram, OpenMP
+    over ``threads``) on
+    ``n`` packed tuples of the same stream, best of three runs.  Reported beside the port,
+    never as the baseline."""
+    from oracle.oracle import OracleLib, generate_np
+    lib = OracleLib()
+    tup = generate_np(SEED, 0, n) if distribution == "uniform" else flow_np(0, n)
+    best = None
+    for _ in range(3):
+        t0 = time.perf_counter()
+        lib.run(key, tup, 128, 24, threads=threads, fn="oracle_run_tables")
+        dt = time.perf_counter() - t0
+        best = dt if best is None or dt < best else best
+    return {"value": n / best, "unit": "tuples/s", "threads": threads,
+            "sample": "%d tuples, hash u32 + queue u32 + counts (H=128, Q=24), oracle/"
+                      "toeplitz_oracle.c oracle_run_tables (12 byte tables, 12 lookups per "
+                      "tuple, OpenMP), best of 3" % n}
 
 
 def load_traffic(profile_dir, n, htable, queues, queue_width):

@@ -186,6 +186,8 @@ class OracleLib:
         lib.oracle_run.argtypes = [u8p, ctypes.c_size_t, u32p, ctypes.c_size_t, ctypes.c_uint32,
                                    ctypes.c_uint32, u32p, u32p, u64p, ctypes.c_int]
         lib.oracle_run.restype = ctypes.c_int
+        lib.oracle_run_tables.argtypes = lib.oracle_run.argtypes
+        lib.oracle_run_tables.restype = ctypes.c_int
         lib.oracle_windows_n.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, u32p]
         lib.oracle_windows_n.restype = ctypes.c_int
         lib.oracle_hash_bytes.argtypes = [u8p, ctypes.c_size_t, u8p, ctypes.c_size_t]
@@ -224,8 +226,10 @@ class OracleLib:
         d = (ctypes.c_uint8 * max(1, len(data)))(*bytearray(data))
         return self._lib.oracle_hash_bytes(k, n, d, len(data))
 
-    def run(self, key, tuples, htable, nqueues, threads=None, want_hash=True, want_queue=True):
-        """Returns (hash, queue, counts) for packed tuples of shape (n, 3)."""
+    def run(self, key, tuples, htable, nqueues, threads=None, want_hash=True, want_queue=True,
+            fn="oracle_run"):
+        """Returns (hash, queue, counts) for packed tuples of shape (n, 3).  ``fn`` =
+        ``oracle_run_tables`` runs the byte-table form (the bench's optimised-CPU line)."""
         tuples = np.ascontiguousarray(tuples, dtype=np.uint32).reshape(-1, 3)
         n = len(tuples)
         k, klen = self._key(key)
@@ -233,13 +237,13 @@ class OracleLib:
         q = np.empty(n, dtype=np.uint32) if want_queue else None
         c = np.zeros(nqueues, dtype=np.uint64)
         u32p = ctypes.POINTER(ctypes.c_uint32)
-        rc = self._lib.oracle_run(
+        rc = getattr(self._lib, fn)(
             k, klen, tuples.ctypes.data_as(u32p), n, htable, nqueues,
             h.ctypes.data_as(u32p) if h is not None else None,
             q.ctypes.data_as(u32p) if q is not None else None,
             c.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), threads or os.cpu_count() or 1)
         if rc:
-            raise ValueError("oracle_run failed (%d)" % rc)
+            raise ValueError("%s failed (%d)" % (fn, rc))
         return h, q, c
 
     def generate(self, seed, first_index, n):

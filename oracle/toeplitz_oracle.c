@@ -26,6 +26,7 @@
  */
 #include <stddef.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #ifdef _OPENMP
@@ -175,6 +176,63 @@ int oracle_run(const uint8_t* key, size_t len, const uint32_t* tuples, size_t n,
             for (uint32_t q = 0; q < nqueues; ++q) counts[q] += local[q];
         }
     }
+    return 0;
+}
+
+/*
+ * The bench's "optimised CPU" line, not a checker: the same batch as
+ * oracle_run with the 96 windows pre-summed into twelve 256-entry byte tables (12 KiB,
+ * L1-resident; entry v of table j = XOR of the windows of the bits set in input byte j),
+ * 12 lookups per tuple, OpenMP over tuples, per-thread histograms.  hash % htable %
+ * nqueues as the reference.  tests/test_oracle.py checks it against oracle_run.
+ */
+int oracle_run_tables(const uint8_t* key, size_t len, const uint32_t* tuples, size_t n,
+                      uint32_t htable, uint32_t nqueues, uint32_t* hash_out, uint32_t* queue_out,
+                      uint64_t* counts, int threads) {
+    uint32_t w[96];
+    if (oracle_windows(key, len, w)) return -22;
+    if (htable < 1 || nqueues < 1 || (counts && nqueues > 65536)) return -22;
+    uint32_t(*T)[256] = malloc(sizeof(uint32_t[12][256]));
+    if (!T) return -12;
+    for (int j = 0; j < 12; ++j)
+        for (int v = 0; v < 256; ++v) {
+            uint32_t x = 0;
+            for (int b = 0; b < 8; ++b)
+                if ((v >> (7 - b)) & 1) x ^= w[8 * j + b];  /* input bit 8j+b is the byte's bit 7-b */
+            T[j][v] = x;
+        }
+    if (counts) memset(counts, 0, sizeof(uint64_t) * nqueues);
+#ifdef _OPENMP
+    if (threads < 1) threads = 1;
+#pragma omp parallel num_threads(threads)
+#endif
+    {
+        uint64_t* local = counts ? calloc(nqueues, sizeof(uint64_t)) : NULL;
+#ifdef _OPENMP
+#pragma omp for schedule(static)
+#endif
+        for (int64_t i = 0; i < (int64_t)n; ++i) {
+            const uint32_t* t = tuples + 3 * i;
+            uint32_t h = 0;
+            for (int k = 0; k < 3; ++k) {
+                const uint32_t x = t[k];  /* byte 0 of the input is the word's top byte */
+                h ^= T[4 * k][x >> 24] ^ T[4 * k + 1][(x >> 16) & 255] ^
+                     T[4 * k + 2][(x >> 8) & 255] ^ T[4 * k + 3][x & 255];
+            }
+            const uint32_t q = (h % htable) % nqueues;
+            if (hash_out) hash_out[i] = h;
+            if (queue_out) queue_out[i] = q;
+            if (local) ++local[q];
+        }
+        if (local) {
+#ifdef _OPENMP
+#pragma omp critical
+#endif
+            for (uint32_t q = 0; q < nqueues; ++q) counts[q] += local[q];
+            free(local);
+        }
+    }
+    free(T);
     return 0;
 }
 

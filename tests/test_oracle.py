@@ -109,3 +109,16 @@ def test_short_keys_wrap_like_the_rotation(oracle_lib):
         np.testing.assert_array_equal(oracle_lib.windows(key), np.array(want, dtype=np.uint32))
         if length >= 16:
             np.testing.assert_array_equal(o.windows(key), np.array(want, dtype=np.uint32))
+
+
+def test_table_form_equals_window_form(random_golden, oracle_lib):
+    """oracle_run_tables (the bench's optimised-CPU line) == oracle_run == the reference's
+    F3 hashes, for every key and a few (H, Q) incl. non-powers of two and Q > 256."""
+    g = random_golden
+    for k, key in enumerate(g["key_list"]):
+        for H, Q in ((128, 24), (100, 7), (512, 64), (1 << 20, 1000)):
+            a = oracle_lib.run(key, g["tuples"], H, Q, threads=4, fn="oracle_run_tables")
+            b = oracle_lib.run(key, g["tuples"], H, Q, threads=4)
+            np.testing.assert_array_equal(a[0], g["hashes"][k])
+            for x, y in zip(a, b):
+                np.testing.assert_array_equal(x, y)
