@@ -462,8 +462,18 @@ def main():
     if rank == 0:
         reps = max(5, args.steps // 2)
         co_ms = kernel_ms_of(None, None, 0, reps)
-        queues32 = queues if queues.numel() >= 4 * n else torch.empty(n, dtype=torch.int32,
-                                                                        device=dev)
+        queues32, u32_probe = queues, None
+        if queues.numel() < 4 * n:  # the u32 line's queue buffer, placed like the others
+            from rss_simulator_nvidia_amd.placement import choose_buffer
+
+            def probe32(buf, ev):
+                if ev is not None:
+                    ev[0].record(stream)
+                _native.hash_device(key, tuples.data_ptr(), n, H, Q, hashes.data_ptr(),
+                                    buf.data_ptr(), counts.data_ptr(), _native.FLAG_ACCUMULATE, sp)
+                if ev is not None:
+                    ev[1].record(stream)
+            queues32, u32_probe = choose_buffer(torch, dev, 4 * n, probe32, candidates=4)
         u32_ms = kernel_ms_of(hashes.data_ptr(), queues32.data_ptr(), 0, reps)
         del queues32
         if args.distribution == "uniform":  # same kernel on SURVEY.md 8(d)'s flow-like input
@@ -548,6 +558,7 @@ def main():
             },
             "queue_u32": {
                 "kernel_ms": u32_ms,
+                "queue_buffer_probe_ms": u32_probe,
                 "tuples_per_s_per_gpu": n / (u32_ms / 1e3),
                 "achieved_GBs": n * 20 / (u32_ms / 1e3) / 1e9,
             },

@@ -68,3 +68,23 @@ def choose_stream_buffers(torch, dev, n, fill_input, probe, n_inputs=2, n_output
     del inputs, outputs
     torch.cuda.empty_cache()
     return tuples, hashes, queues, report
+
+
+def choose_buffer(torch, dev, nbytes, probe, candidates=3, probe_reps=5, probe_warm=2):
+    """One more placed buffer beside already chosen ones: ``candidates`` uint8 tensors of
+    ``nbytes``, ``probe(buf, events)`` enqueues one launch using ``buf`` between the two
+    events; returns ``(buffer, {candidate: median ms})`` with the fastest kept."""
+    bufs = [torch.empty(nbytes, dtype=torch.uint8, device=dev) for _ in range(max(1, candidates))]
+    times = []
+    for b in bufs:
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(probe_reps)]
+        for k in range(-probe_warm, probe_reps):
+            probe(b, ev[k] if k >= 0 else None)
+        torch.cuda.synchronize(dev)
+        times.append(statistics.median(a.elapsed_time(c) for a, c in ev))
+    best = min(range(len(bufs)), key=times.__getitem__)
+    chosen = bufs[best]
+    del bufs
+    torch.cuda.empty_cache()
+    return chosen, {"buf%d" % i: round(t, 4) for i, t in enumerate(times)}

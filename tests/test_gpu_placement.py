@@ -78,3 +78,23 @@ def test_resident_batch_equals_oracle(oracle_lib, example_key, width, placement)
         np.testing.assert_array_equal(qv.astype(np.uint32), q)
         np.testing.assert_array_equal(counts.cpu().numpy().view(np.uint64), 2 * c)
 
+
+
+def test_choose_buffer_keeps_the_fastest_candidate():
+    from rss_simulator_nvidia_amd.placement import choose_buffer
+    dev = torch.device("cuda:0")
+    s = torch.cuda.current_stream(dev)
+    seen = []
+
+    def probe(buf, ev):
+        seen.append(buf.data_ptr())
+        if ev is not None:
+            ev[0].record(s)
+        buf.fill_(7)
+        if ev is not None:
+            ev[1].record(s)
+
+    buf, times = choose_buffer(torch, dev, 1 << 20, probe, candidates=3, probe_reps=3,
+                               probe_warm=1)
+    assert len(set(seen)) == 3 and len(seen) == 12 and buf.data_ptr() in seen
+    assert buf.numel() == 1 << 20 and buf.dtype == torch.uint8 and set(times) == {"buf0", "buf1", "buf2"}
