@@ -67,6 +67,8 @@ def parse_args():
                         "x K candidate output allocations before the timed region and keeping "
                         "the fastest (rss_simulator_nvidia_amd/placement.py); 0 = first "
                         "allocation, as allocated")
+    p.add_argument("--secondary-warmup", type=int, default=30,
+                   help="untimed launches of each secondary line's own mode before its timed ones")
     p.add_argument("--profile-dir", default=os.path.join(ROOT, "profiles"),
                    help="where committed rocprofv3 PMC summaries (traffic) are looked up")
     return p.parse_args()
@@ -432,7 +434,7 @@ def main():
         (profiles/r01_runs/mode_switch_probe.json, bench_secondary_warmup.json)."""
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(reps)]
-        for i in range(-30, reps):
+        for i in range(-args.secondary_warmup, reps):
             if i >= 0:
                 ev[i][0].record(stream)
             _native.hash_device(key, tuples.data_ptr(), n, H, Q, hash_ptr, queue_ptr,
