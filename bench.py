@@ -3,7 +3,7 @@
 One step = one pass of the hot path (Toeplitz hash -> htable index -> queue
 modulo -> per-queue histogram, all outputs written) over this rank's resident
 shard of synthetic tuples (zero counts + one kernel launch; ``--graph`` replays the
-pair as a captured HIP graph), followed, when N > 1, by the RCCL all-reduce of the
+launch as a captured HIP graph), followed, under a launcher, by the RCCL all-reduce of the
 per-queue count vector, issued async so it overlaps the next step (double-buffered
 counts).  Weak scaling: every rank owns ``--tuples-per-gpu``
 tuples (default 2**28, BASELINE configs[2]) of one global splitmix64 stream.
@@ -304,7 +304,6 @@ def main():
     import torch.distributed as dist
 
     from rss_simulator_nvidia_amd import _native
-    from rss_simulator_nvidia_amd.sharding import allreduce_counts
 
     # RSS_BENCH_DEVICE pins every rank to one device (rehearsing N>1 on a 1-GPU box)
     dev_index = int(os.environ.get("RSS_BENCH_DEVICE", local_rank))
@@ -352,60 +351,48 @@ def main():
     placement = batch.report
     torch.cuda.synchronize()
 
-    # Two count buffers: step i hashes into counts[i % 2] while the RCCL all-reduce of
-    # step i-1's buffer (async, on the collective stream) overlaps it.
-    counts2 = [counts, torch.zeros(Q, dtype=torch.int64, device=dev)]
+    # Two count buffers: step i hashes into one while the RCCL all-reduce of step i-1's
+    # buffer (async, on the collective stream) overlaps it (sharding.CountsPipeline).
+    from rss_simulator_nvidia_amd.sharding import CountsPipeline
+    pipeline = CountsPipeline(Q, dev)
 
-    def body(c, ev=None):
-        c.zero_()
-        if ev is not None:
-            ev[0].record(stream)
+    def launch(c):
         _native.hash_device(key, tuples.data_ptr(), n, H, Q, hashes.data_ptr(), queues.data_ptr(),
                             c.data_ptr(), _native.FLAG_ACCUMULATE | qflag,
                             torch.cuda.current_stream(dev).cuda_stream)
-        if ev is not None:
-            ev[1].record(stream)
 
     graphs = None
     if args.graph:
-        try:  # capture zero + hash per buffer once; replay = one graph launch per step
+        try:  # capture one hash launch per count buffer; replay = one graph launch per step
             side = torch.cuda.Stream(dev)
             side.wait_stream(stream)
             with torch.cuda.stream(side):
-                body(counts2[0])
+                launch(pipeline.buffers[0])
             stream.wait_stream(side)
-            graphs = []
-            for c in counts2:
+            graphs = {}
+            for c in pipeline.buffers:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
-                    body(c)
-                graphs.append(g)
+                    launch(c)
+                graphs[c.data_ptr()] = g
         except Exception as err:  # eager fallback keeps the same work per step
             print("bench: graph capture unavailable (%s); launching eagerly" % err, file=sys.stderr)
             graphs = None
 
-    pending = [None, None]
-
     def step(i, ev=None):
-        b = i & 1
-        if pending[b] is not None:
-            pending[b].wait()  # buffer b's previous all-reduce must finish before reuse
-        if graphs is not None:
+        def timed_launch(c):
             if ev is not None:
                 ev[0].record(stream)
-            graphs[b].replay()
+            if graphs is not None:
+                graphs[c.data_ptr()].replay()
+            else:
+                launch(c)
             if ev is not None:
                 ev[1].record(stream)
-        else:
-            body(counts2[b], ev)
-        if distributed:  # RCCL over xGMI
-            pending[b] = allreduce_counts(counts2[b], async_op=True)
+        pipeline.step(timed_launch)
 
     def drain():
-        for b in (0, 1):
-            if pending[b] is not None:
-                pending[b].wait()
-                pending[b] = None
+        return pipeline.drain()
 
     for i in range(args.warmup):
         step(i)
@@ -419,11 +406,10 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i, events[i])
-    drain()
+    last = drain()
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
-    last = counts2[(args.steps - 1) & 1]
 
     # kernel-only timing (HIP events on the launch stream), for roofline.achieved
     def kernel_ms_of(hash_ptr, queue_ptr, flags, reps):
@@ -522,8 +508,8 @@ def main():
                                 "(async, overlapped with the next step)"
                                 % (world, "RCCL" if args.dist_backend == "nccl" else "gloo", Q))
                                if distributed else "single process, one GPU (no process group)",
-                "step": "hipGraph replay (zero counts + hash kernel)" if graphs is not None
-                        else "eager launches (zero counts + hash kernel)",
+                "step": "zero counts + hash kernel (hipGraph replay)" if graphs is not None
+                        else "zero counts + hash kernel (eager launches)",
             },
             "roofline": {
                 "bound": "hbm",

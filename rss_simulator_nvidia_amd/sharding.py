@@ -64,3 +64,41 @@ def hash_shard(key, tuples, n, htable, nqueues, hashes=None, queues=None, counts
     if counts is not None:
         allreduce_counts(counts, group)
     return hashes, queues, counts
+
+
+class CountsPipeline:
+    """Per-step histograms of a rank that hashes batch after batch (a weak-scaling job, a
+    service): step i zeroes count buffer ``i % 2``, enqueues the hash into it and issues
+    the all-reduce of that buffer asynchronously, so it overlaps step i+1's hash, which
+    writes the other buffer; a buffer's previous all-reduce is waited for before it is
+    reused.  Without a process group the collective is skipped (counts are the rank's).
+
+    ``launch(counts)`` enqueues one hash pass that accumulates into ``counts`` (int64
+    tensor of ``nqueues``) on the caller's stream.
+    """
+
+    def __init__(self, nqueues, device, group=None):
+        self.buffers = [torch.zeros(nqueues, dtype=torch.int64, device=device) for _ in range(2)]
+        self.pending = [None, None]
+        self.group = group
+        self.steps = 0
+
+    def step(self, launch):
+        b = self.steps & 1
+        if self.pending[b] is not None:
+            self.pending[b].wait()  # buffer b's previous all-reduce must finish before reuse
+            self.pending[b] = None
+        counts = self.buffers[b]
+        counts.zero_()
+        launch(counts)
+        self.pending[b] = allreduce_counts(counts, self.group, async_op=True)
+        self.steps += 1
+        return counts
+
+    def drain(self):
+        """Wait for every outstanding all-reduce; returns the last step's (reduced) counts."""
+        for b in (0, 1):
+            if self.pending[b] is not None:
+                self.pending[b].wait()
+                self.pending[b] = None
+        return self.buffers[(self.steps - 1) & 1] if self.steps else None

@@ -63,3 +63,48 @@ def test_gloo_sharded_counts_equal_single_process(world, tmp_path, oracle_lib, e
     np.testing.assert_array_equal(shards, h)
     for r in range(world):
         np.testing.assert_array_equal(np.load(tmp_path / ("c%d.npy" % r)).view(np.uint64), c)
+
+
+def _pipeline_worker(rank, world, port, steps, nq, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rss_simulator_nvidia_amd.sharding import CountsPipeline
+        pipe = CountsPipeline(nq, "cpu")
+        seen = []
+        for i in range(steps):
+            # step i adds (rank + 1) * (i + 1) to every queue of a freshly zeroed buffer
+            c = pipe.step(lambda counts, i=i: counts.add_((rank + 1) * (i + 1)))
+            seen.append(c.data_ptr())
+        last = pipe.drain()
+        assert len(set(seen)) == min(2, steps) and last.data_ptr() == seen[-1]
+        np.save(os.path.join(out_dir, "last%d.npy" % rank), last.numpy())
+        np.save(os.path.join(out_dir, "prev%d.npy" % rank), pipe.buffers[steps & 1].numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,steps", [(2, 5), (3, 4), (2, 1)])
+def test_counts_pipeline_reduces_every_step(world, steps, tmp_path):
+    """CountsPipeline (the bench's step shape): the double-buffered async all-reduce gives
+    each step's counts summed over ranks, the buffer reused two steps later is re-zeroed,
+    and drain() returns the last step's reduced counts."""
+    nq = 7
+    mp.start_processes(_pipeline_worker, args=(world, _free_port(), steps, nq, str(tmp_path)),
+                       nprocs=world, start_method="spawn")
+    ranks = sum(r + 1 for r in range(world))
+    for r in range(world):
+        np.testing.assert_array_equal(np.load(tmp_path / ("last%d.npy" % r)),
+                                      np.full(nq, ranks * steps))
+        if steps > 1:
+            np.testing.assert_array_equal(np.load(tmp_path / ("prev%d.npy" % r)),
+                                          np.full(nq, ranks * (steps - 1)))
+
+
+def test_counts_pipeline_without_group_keeps_local_counts():
+    from rss_simulator_nvidia_amd.sharding import CountsPipeline
+    pipe = CountsPipeline(3, "cpu")
+    for i in range(3):
+        pipe.step(lambda c, i=i: c.add_(i + 1))
+    np.testing.assert_array_equal(pipe.drain().numpy(), [3, 3, 3])
+    np.testing.assert_array_equal(pipe.buffers[1].numpy(), [2, 2, 2])
