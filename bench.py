@@ -553,7 +553,11 @@ def main():
             "cpu_baseline": baseline,
         }
         line["secondary_min_median_max_ms"] = secondary_spread
-        line["placement"] = placement
+        line["placement"] = dict(placement, first_allocation_tuples_per_s_per_gpu=n / (
+            placement["first_allocation_ms"] / 1e3),
+            note="resident buffers chosen among the probed candidate allocations before the "
+                 "timed region (ResidentBatch); first_allocation_* = the unplaced allocation's "
+                 "kernel-only rate")
         if flow_ms is not None:
             line["flow_like"] = {
                 "kernel_ms": flow_ms, "tuples_per_s_per_gpu": n / (flow_ms / 1e3),
