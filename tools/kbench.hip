@@ -932,6 +932,39 @@ int main(int argc, char** argv) {
         CK(hipFree(pool));
     }
 
+    if (strstr("parts", filter)) {
+        // is a placement tier a property of a whole allocation or of its sub-ranges?  For K
+        // output pairs: the product over all n tuples, then over each quarter of the tuples
+        // (writing the matching quarter of the hash / queue buffers), per-launch times
+        // scaled x4 for comparison
+        constexpr int K = 6;
+        uint32_t *hs[K], *qs[K];
+        for (int k = 0; k < K; ++k) {
+            CK(hipMalloc(&hs[k], n * 4));
+            CK(hipMalloc(&qs[k], n));
+        }
+        const uint64_t m = n / 4;
+        for (int k = 0; k < K; ++k) {
+            const float tf = time_ms([&] {
+                if (rss_hash_device(&key, (const rss_tuple4*)tup, n, H, Q, hs[k], qs[k], (uint64_t*)c0,
+                                    RSS_FLAG_QUEUE_U8, nullptr)) exit(1);
+            }, reps);
+            float tq[4];
+            for (int part = 0; part < 4; ++part)
+                tq[part] = 4 * time_ms([&] {
+                    if (rss_hash_device(&key, (const rss_tuple4*)tup + part * m, m, H, Q, hs[k] + part * m,
+                                        (uint8_t*)qs[k] + part * m, (uint64_t*)c0, RSS_FLAG_QUEUE_U8,
+                                        nullptr)) exit(1);
+                }, 4 * reps);
+            printf("parts pair %d  whole %.3f  quarters x4 %.3f %.3f %.3f %.3f ms\n", k, tf, tq[0], tq[1],
+                   tq[2], tq[3]);
+        }
+        for (int k = 0; k < K; ++k) {
+            CK(hipFree(hs[k]));
+            CK(hipFree(qs[k]));
+        }
+    }
+
     if (strstr("qsize", filter)) {
         // does the queue allocation's size (n B, as u8 queues need, vs 4n B, as the bench
         // allocates for its u32 line) change how often a placement lands in the fast tier?
