@@ -1,6 +1,7 @@
 """configs[3] on one GPU: 2**30 synthetic tuples (12 GiB of tuples, so every tuple past index
 357,913,941 sits beyond the 4 GiB byte offset) hashed in one launch and as the eight shards
-the N=8 bench hands its ranks (``sharding.shard_range``).
+the N=8 bench hands its ranks (``sharding.shard_range``); the shards and a whole-batch launch
+run counts-only (the register-table kernel), the single full-output launch the LDS-table one.
 
 Size-independent checks (large-N parity): the shards' per-queue counts sum to
 the single launch's counts and to N; the queue column equals ``hash % H % Q``
@@ -48,12 +49,16 @@ def test_1G_tuples_single_launch_and_eight_shards(native, oracle_lib, example_ke
         native.hash_device(key, tuples.data_ptr() + 12 * start, count, H, Q, None, None,
                            c.data_ptr(), 0, s)
         shard_counts.append(c)
+    # the whole batch counts-only in one launch (rss_counts_perm_kernel, 2^30 tuples)
+    whole = torch.empty(Q, dtype=torch.int64, device=dev)
+    native.hash_device(key, tuples.data_ptr(), N, H, Q, None, None, whole.data_ptr(), 0, s)
     torch.cuda.synchronize()
 
     total = counts.cpu().numpy().view(np.uint64)
     assert int(total.sum()) == N
     summed = sum(c.cpu().numpy().view(np.uint64) for c in shard_counts)
     np.testing.assert_array_equal(summed, total)
+    np.testing.assert_array_equal(whole.cpu().numpy().view(np.uint64), total)
 
     # element-wise against the oracle around shard boundaries, 4 GiB and the end
     starts = {0, N - WINDOW, (1 << 32) // 12 - WINDOW // 2}
