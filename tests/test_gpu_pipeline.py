@@ -1,0 +1,38 @@
+"""sharding.CountsPipeline on the GPU (no process group): the rotating count buffers are
+zeroed on a side stream while the previous hash pass runs, so every step's counts must be
+exactly that step's histogram -- never a leftover of the step three earlier -- and the
+previous step's counts must still hold when the next step has been issued."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def test_counts_pipeline_steps_equal_oracle(oracle_lib, example_key):
+    from rss_simulator_nvidia_amd import _native
+    from rss_simulator_nvidia_amd.sharding import CountsPipeline
+    n, H, Q = (1 << 20) + 1, 128, 24
+    dev = torch.device("cuda:0")
+    s = torch.cuda.current_stream(dev).cuda_stream
+    key = _native.prepare_key(example_key)
+    batches = []
+    for i in range(4):  # four different batches, used round-robin
+        host = oracle_lib.generate(100 + i, 0, n)
+        batches.append((torch.from_numpy(host.view(np.int32).reshape(-1)).to(dev),
+                        oracle_lib.run(example_key, host, H, Q, want_hash=False,
+                                       want_queue=False)[2]))
+    pipe = CountsPipeline(Q, dev)
+    prev = None
+    for i in range(11):
+        tup, want = batches[i % 4]
+        c = pipe.step(lambda counts, tup=tup: _native.hash_device(
+            key, tup.data_ptr(), n, H, Q, None, None, counts.data_ptr(), _native.FLAG_ACCUMULATE, s))
+        if prev is not None:  # step i-1's counts are still valid after step i is issued
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(prev[0].cpu().numpy().view(np.uint64), prev[1])
+        prev = (c, want)
+    last = pipe.drain()
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(last.cpu().numpy().view(np.uint64), batches[10 % 4][1])
