@@ -68,70 +68,37 @@ def hash_shard(key, tuples, n, htable, nqueues, hashes=None, queues=None, counts
 
 class CountsPipeline:
     """Per-step histograms of a rank that hashes batch after batch (a weak-scaling job, a
-    service).  Three count buffers rotate: step i enqueues the hash pass into buffer i % 3
-    and issues its all-reduce asynchronously, so the collective overlaps step i+1; meanwhile
-    a side stream zeroes the buffer step i+1 will use (last used by step i-2, once that
-    step's all-reduce has completed), so no zeroing kernel sits between two hash passes on
-    the compute stream.  The counts a step returns stay valid until the step two later is
-    issued.  Without a process group the collective is skipped (counts are the rank's); on
-    CPU tensors the buffer is zeroed in line.
+    service): step i zeroes count buffer ``i % 2``, enqueues the hash into it and issues
+    the all-reduce of that buffer asynchronously, so it overlaps step i+1's hash, which
+    writes the other buffer; a buffer's previous all-reduce is waited for before it is
+    reused.  Without a process group the collective is skipped (counts are the rank's).
 
     ``launch(counts)`` enqueues one hash pass that accumulates into ``counts`` (int64
-    tensor of ``nqueues``) on the caller's current stream.
+    tensor of ``nqueues``) on the caller's stream.
     """
 
-    DEPTH = 3
-
     def __init__(self, nqueues, device, group=None):
-        self.device = torch.device(device)
-        self.buffers = [torch.zeros(nqueues, dtype=torch.int64, device=self.device)
-                        for _ in range(self.DEPTH)]
-        self.pending = [None] * self.DEPTH
+        self.buffers = [torch.zeros(nqueues, dtype=torch.int64, device=device) for _ in range(2)]
+        self.pending = [None, None]
         self.group = group
         self.steps = 0
-        self.cuda = self.device.type == "cuda"
-        if self.cuda:
-            self.side = torch.cuda.Stream(self.device)
-            self.zeroed = [None] * self.DEPTH   # side-stream event: buffer b is zero
-            self.written = [None] * self.DEPTH  # compute-stream event: step into b enqueued
-
-    def _wait_reduce(self, b):
-        if self.pending[b] is not None:
-            self.pending[b].wait()  # the current stream waits for the collective
-            self.pending[b] = None
 
     def step(self, launch):
-        b = self.steps % self.DEPTH
+        b = self.steps & 1
+        if self.pending[b] is not None:
+            self.pending[b].wait()  # buffer b's previous all-reduce must finish before reuse
+            self.pending[b] = None
         counts = self.buffers[b]
-        if self.cuda:
-            cur = torch.cuda.current_stream(self.device)
-            if self.zeroed[b] is not None:
-                cur.wait_event(self.zeroed[b])
-            else:  # first use: zeroed at construction; order after any earlier reduce
-                self._wait_reduce(b)
-            launch(counts)
-            self.written[b] = cur.record_event()
-        else:
-            self._wait_reduce(b)
-            counts.zero_()
-            launch(counts)
+        counts.zero_()
+        launch(counts)
         self.pending[b] = allreduce_counts(counts, self.group, async_op=True)
         self.steps += 1
-        if self.cuda and self.steps >= self.DEPTH:
-            nxt = self.steps % self.DEPTH  # used by step i-2; needed next
-            with torch.cuda.stream(self.side):
-                self.side.wait_event(self.written[nxt])
-                self._wait_reduce(nxt)
-                self.buffers[nxt].zero_()
-                self.zeroed[nxt] = self.side.record_event()
         return counts
 
     def drain(self):
         """Wait for every outstanding all-reduce; returns the last step's (reduced) counts."""
-        for b in range(self.DEPTH):
-            self._wait_reduce(b)
-        if self.cuda:
-            for e in self.zeroed:
-                if e is not None:
-                    torch.cuda.current_stream(self.device).wait_event(e)
-        return self.buffers[(self.steps - 1) % self.DEPTH] if self.steps else None
+        for b in (0, 1):
+            if self.pending[b] is not None:
+                self.pending[b].wait()
+                self.pending[b] = None
+        return self.buffers[(self.steps - 1) & 1] if self.steps else None

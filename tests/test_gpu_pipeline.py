@@ -1,7 +1,8 @@
-"""sharding.CountsPipeline on the GPU (no process group): the rotating count buffers are
-zeroed on a side stream while the previous hash pass runs, so every step's counts must be
-exactly that step's histogram -- never a leftover of the step three earlier -- and the
-previous step's counts must still hold when the next step has been issued."""
+"""sharding.CountsPipeline on the GPU (no process group): the two count buffers alternate,
+so every step's counts must be exactly that step's histogram -- never a leftover of the
+step two earlier -- and the previous step's counts must still hold when the next step has
+been issued.  (A three-buffer variant that zeroed the next buffer on a side stream measured
+20 us per step of cross-stream overhead against 7 us for zeroing in line; not adopted.)"""
 import numpy as np
 import pytest
 
