@@ -383,17 +383,18 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
 // `ds_read_b32` per tuple in the LUT kernel, whose bank conflicts bind it in this mode
 // (DESIGN.md §3).  Measured 0.525-0.531 vs 0.545-0.548 ms per 2^28 tuples, read-only
 // stream 0.513-0.519 (profiles/r02/perm_counts.log).
-constexpr int kPermFields = 36;
-
+// The same kernel serves IPv6 (nine words, 108 fields, rss_hash6_device counts only).
+template <int kWords>
 struct PermParams {
-    const rss_tuple4* tuples;
+    static constexpr int kFields = kWords * 12;  // three fields per input byte
+    const uint32_t* tuples;  // kWords words per tuple
     unsigned long long* counts;
     uint64_t n;
     uint32_t Q;
     uint32_t q_mask;    // QM_MASK
     uint32_t q_m16;     // QM_FAST8
-    uint32_t lo[kPermFields];  // field f: table entries 0..3 (v_perm selector 0..3)
-    uint32_t hi[kPermFields];  //          entries 4..7 (selector 4..7)
+    uint32_t lo[kFields];  // field f: table entries 0..3 (v_perm selector 0..3)
+    uint32_t hi[kFields];  //          entries 4..7 (selector 4..7)
 };
 
 __device__ __forceinline__ uint32_t vperm(uint32_t s0, uint32_t s1, uint32_t sel) {
@@ -412,34 +413,32 @@ __device__ __forceinline__ void transpose_bytes(uint32_t x0, uint32_t x1, uint32
     t3 = vperm(d, b, 0x07060302u);
 }
 
-// XOR of the three field terms of byte-transposed dword t (fields kF .. kF+2)
-template <int kF>
-__device__ __forceinline__ uint32_t perm_byte_terms(const PermParams& p, uint32_t t) {
-    const uint32_t f0 = vperm(p.hi[kF], p.lo[kF], t & 0x07070707u);
-    const uint32_t f1 = vperm(p.hi[kF + 1], p.lo[kF + 1], (t >> 3) & 0x07070707u);
-    const uint32_t f2 = vperm(p.lo[kF + 2], p.lo[kF + 2], (t >> 6) & 0x03030303u);
+// XOR of the three field terms of byte-transposed dword t (fields f .. f+2)
+template <int kWords>
+__device__ __forceinline__ uint32_t perm_byte_terms(const PermParams<kWords>& p, int f, uint32_t t) {
+    const uint32_t f0 = vperm(p.hi[f], p.lo[f], t & 0x07070707u);
+    const uint32_t f1 = vperm(p.hi[f + 1], p.lo[f + 1], (t >> 3) & 0x07070707u);
+    const uint32_t f2 = vperm(p.lo[f + 2], p.lo[f + 2], (t >> 6) & 0x03030303u);
     return xor3(f0, f1, f2);
 }
 
-// acc ^ the terms of word kK of four tuples
-template <int kK>
-__device__ __forceinline__ uint32_t perm_word(const PermParams& p, uint32_t x0, uint32_t x1,
-                                              uint32_t x2, uint32_t x3, uint32_t acc) {
-    uint32_t t0, t1, t2, t3;
-    transpose_bytes(x0, x1, x2, x3, t0, t1, t2, t3);
-    return xor3(xor3(acc, perm_byte_terms<kK * 12 + 0>(p, t0), perm_byte_terms<kK * 12 + 3>(p, t1)),
-                perm_byte_terms<kK * 12 + 6>(p, t2), perm_byte_terms<kK * 12 + 9>(p, t3));
+// buckets of four tuples (tuple i's hash & (H-1) in byte i); w = 4 x kWords words, tuple-major
+template <int kWords>
+__device__ __forceinline__ uint32_t perm_buckets(const PermParams<kWords>& p,
+                                                 const uint32_t (&w)[4 * kWords]) {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < kWords; ++k) {  // fully unrolled: every field index is a constant
+        uint32_t t0, t1, t2, t3;
+        transpose_bytes(w[k], w[kWords + k], w[2 * kWords + k], w[3 * kWords + k], t0, t1, t2, t3);
+        acc = xor3(xor3(acc, perm_byte_terms(p, 12 * k + 0, t0), perm_byte_terms(p, 12 * k + 3, t1)),
+                   perm_byte_terms(p, 12 * k + 6, t2), perm_byte_terms(p, 12 * k + 9, t3));
+    }
+    return acc;
 }
 
-// buckets of four tuples (tuple i's hash & (H-1) in byte i)
-__device__ __forceinline__ uint32_t perm_buckets(const PermParams& p, const uint32_t (&w)[12]) {
-    uint32_t acc = perm_word<0>(p, w[0], w[3], w[6], w[9], 0u);
-    acc = perm_word<1>(p, w[1], w[4], w[7], w[10], acc);
-    return perm_word<2>(p, w[2], w[5], w[8], w[11], acc);
-}
-
-template <int kQMode>
-__device__ __forceinline__ uint32_t perm_queue(uint32_t b, const PermParams& p) {
+template <int kQMode, int kWords>
+__device__ __forceinline__ uint32_t perm_queue(uint32_t b, const PermParams<kWords>& p) {
     if constexpr (kQMode == QM_MASK) return b & p.q_mask;
     return b - __umul24(__umul24(b, p.q_m16) >> 16, p.Q);  // QM_FAST8: b, Q < 256
 }
@@ -449,8 +448,8 @@ __device__ __forceinline__ void perm_count(uint32_t* bins, uint32_t q, uint32_t 
                            __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-template <int kQMode>
-__global__ __launch_bounds__(kBlock, 2) void rss_counts_perm_kernel(const PermParams p) {
+template <int kQMode, int kWords>
+__global__ __launch_bounds__(kBlock, 2) void rss_counts_perm_kernel(const PermParams<kWords> p) {
     extern __shared__ uint32_t bins[];  // Q x 32 private columns
     const uint32_t tid = threadIdx.x, col = tid & (kBinCols - 1);
     for (uint32_t e = tid; e < p.Q * kBinCols; e += kBlock) bins[e] = 0;
@@ -459,8 +458,15 @@ __global__ __launch_bounds__(kBlock, 2) void rss_counts_perm_kernel(const PermPa
     const uint64_t ngroups = p.n >> 2;
     const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
     for (uint64_t g = gtid; g < ngroups; g += (uint64_t)gridDim.x * kBlock) {
-        const uint4 a = src[3 * g], b = src[3 * g + 1], c = src[3 * g + 2];
-        const uint32_t w[12] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w};
+        uint32_t w[4 * kWords];  // four tuples = kWords x 16 B, 16-B aligned
+#pragma unroll
+        for (int v = 0; v < kWords; ++v) {
+            const uint4 x = src[kWords * g + v];
+            w[4 * v] = x.x;
+            w[4 * v + 1] = x.y;
+            w[4 * v + 2] = x.z;
+            w[4 * v + 3] = x.w;
+        }
         const uint32_t bk = perm_buckets(p, w);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -469,8 +475,9 @@ __global__ __launch_bounds__(kBlock, 2) void rss_counts_perm_kernel(const PermPa
     // the last n % 4 tuples: one per lane of the first workgroup, in byte 0
     const uint64_t i = (ngroups << 2) + gtid;
     if (i < p.n) {
-        const uint32_t* t = reinterpret_cast<const uint32_t*>(p.tuples) + 3 * i;
-        const uint32_t w[12] = {t[0], t[1], t[2], 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        uint32_t w[4 * kWords] = {};
+#pragma unroll
+        for (int k = 0; k < kWords; ++k) w[k] = p.tuples[kWords * i + k];
         perm_count(bins, perm_queue<kQMode>(perm_buckets(p, w) & 0xFFu, p), col);
     }
     __syncthreads();
@@ -1270,39 +1277,41 @@ bool counts_perm_enabled() {
 }
 
 // Counts only, power-of-two H <= 256, 16-B aligned tuples: rss_counts_perm_kernel with the
-// 36 byte tables of (window & (H-1)) built here, from the same windows as the LUT.
-int launch_counts_perm(const rss_key* key, const LaunchParams& lp, int qmode, uint32_t bin_bytes,
-                       int cu_count, hipStream_t stream) {
-    PermParams pp;
+// byte tables of (window & (H-1)) built here from the key's windows (IPv4: 96, IPv6: 288).
+template <int kWords>
+int launch_counts_perm(const uint32_t* window, const void* tuples, uint64_t n, unsigned long long* counts,
+                       uint32_t h_mask, uint32_t Q, uint32_t q_mask, uint32_t q_m16, int qmode,
+                       uint32_t bin_bytes, int cu_count, hipStream_t stream) {
+    PermParams<kWords> pp;
     memset(&pp, 0, sizeof pp);
-    pp.tuples = lp.tuples;
-    pp.counts = lp.counts;
-    pp.n = lp.n;
-    pp.Q = lp.Q;
-    pp.q_mask = lp.q_mask;
-    pp.q_m16 = lp.q_m16;
-    for (int k = 0; k < 3; ++k)          // word (src ip, dst ip, ports)
-        for (int j = 0; j < 4; ++j)      // byte of the word, least significant first
-            for (int f = 0; f < 3; ++f) {  // fields [0,3) [3,6) [6,8) of the byte
+    pp.tuples = static_cast<const uint32_t*>(tuples);
+    pp.counts = counts;
+    pp.n = n;
+    pp.Q = Q;
+    pp.q_mask = q_mask;
+    pp.q_m16 = q_m16;
+    for (int k = 0; k < kWords; ++k)         // word
+        for (int j = 0; j < 4; ++j)          // byte of the word, least significant first
+            for (int f = 0; f < 3; ++f) {    // fields [0,3) [3,6) [6,8) of the byte
                 const int id = (k * 4 + j) * 3 + f, lsb = 8 * j + 3 * f, len = f < 2 ? 3 : 2;
                 uint8_t e[8] = {0, 0, 0, 0, 0, 0, 0, 0};
                 for (int v = 0; v < (1 << len); ++v)
                     for (int b = 0; b < len; ++b)  // word k bit i is input bit 32k + 31 - i
-                        if ((v >> b) & 1) e[v] ^= (uint8_t)(key->window[32 * k + 31 - (lsb + b)] & lp.h_mask);
+                        if ((v >> b) & 1) e[v] ^= (uint8_t)(window[32 * k + 31 - (lsb + b)] & h_mask);
                 pp.lo[id] = e[0] | e[1] << 8 | e[2] << 16 | (uint32_t)e[3] << 24;
                 pp.hi[id] = e[4] | e[5] << 8 | e[6] << 16 | (uint32_t)e[7] << 24;
             }
-    // 48 VGPRs and no LUT: two 1024-lane workgroups fit a CU (RSS_COUNTS_PERM_WGS=1|2)
+    // no LUT and <= 64 VGPRs: two 1024-lane workgroups fit a CU (RSS_COUNTS_PERM_WGS=1|2)
     const char* wgs_env = getenv("RSS_COUNTS_PERM_WGS");
     const uint64_t wgs = wgs_env && wgs_env[0] == '1' ? 1 : 2;
-    const uint64_t want = (lp.n + 4 * kBlock - 1) / (4 * kBlock);
+    const uint64_t want = (n + 4 * kBlock - 1) / (4 * kBlock);
     const unsigned grid = (unsigned)(want < wgs * cu_count ? want : wgs * cu_count);
     if (qmode == QM_MASK)
-        hipLaunchKernelGGL(rss_counts_perm_kernel<QM_MASK>, dim3(grid), dim3(kBlock), bin_bytes,
-                           stream, pp);
+        hipLaunchKernelGGL((rss_counts_perm_kernel<QM_MASK, kWords>), dim3(grid), dim3(kBlock),
+                           bin_bytes, stream, pp);
     else
-        hipLaunchKernelGGL(rss_counts_perm_kernel<QM_FAST8>, dim3(grid), dim3(kBlock), bin_bytes,
-                           stream, pp);
+        hipLaunchKernelGGL((rss_counts_perm_kernel<QM_FAST8, kWords>), dim3(grid), dim3(kBlock),
+                           bin_bytes, stream, pp);
     RSS_HIP_CHECK(hipGetLastError());
     return RSS_OK;
 }
@@ -1364,7 +1373,8 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
     if (!d_hash && !d_queue && d_counts && !reta && h_pow2 && htable <= 256u &&
         hist == HIST_PRIVATE && (qmode == QM_MASK || qmode == QM_FAST8) && aligned16(d_tuples) &&
         counts_perm_enabled())
-        return launch_counts_perm(key, p, qmode, bin_bytes, info.cu_count, stream);
+        return launch_counts_perm<3>(key->window, d_tuples, n, p.counts, p.h_mask, p.Q, p.q_mask,
+                                     p.q_m16, qmode, bin_bytes, info.cu_count, stream);
     KernelFn fn = h_pow2 ? pick_queue<true>(qmode, hist, qwidth, vec4)
                          : pick_queue<false>(qmode, hist, qwidth, vec4);
     const uint64_t per_lane = vec4 ? 4 : 1;
@@ -1463,10 +1473,16 @@ int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint
     const uintptr_t qalign = qwidth == QW_U8 ? 4 : (qwidth == QW_U16 ? 8 : 16);
     const bool vec4 = aligned16(d_tuples) && (!d_hash || aligned16(d_hash)) &&
                       (!d_queue || ((uintptr_t)d_queue % qalign) == 0);
-    KernelFn6 fn = h_pow2 ? pick6<true>(qmode, hist, vec4) : pick6<false>(qmode, hist, vec4);
     DeviceInfo info;
     int rc = device_info(&info);
     if (rc) return rc;
+    // counts only, power-of-two H <= 256: the register-table kernel (no LUT, so private bins
+    // up to Q = 256 fit beside it)
+    if (!d_hash && !d_queue && d_counts && !reta && h_pow2 && htable <= 256u && nqueues <= 256u &&
+        (qmode == QM_MASK || qmode == QM_FAST8) && aligned16(d_tuples) && counts_perm_enabled())
+        return launch_counts_perm<9>(key->window, d_tuples, n, p.counts, p.h_mask, p.Q, p.q_mask,
+                                     p.q_m16, qmode, nqueues * kBinCols * 4, info.cu_count, stream);
+    KernelFn6 fn = h_pow2 ? pick6<true>(qmode, hist, vec4) : pick6<false>(qmode, hist, vec4);
     const uint64_t per_lane = vec4 ? 4 : 1;
     const uint64_t want = (n + per_lane * kBlock - 1) / (per_lane * kBlock);
     const uint64_t cap = (uint64_t)info.cu_count * kBlocksPerCU6;

@@ -108,3 +108,27 @@ def test_flow_like_input(native, oracle_lib, example_key):
     key = native.prepare_key(example_key)
     _, _, want = oracle_lib.run(example_key, host, 128, 24, want_hash=False, want_queue=False)
     np.testing.assert_array_equal(_counts(native, key, tup.data_ptr(), n, 128, 24, True), want)
+
+
+@pytest.mark.parametrize("H,Q", [(128, 24), (256, 256), (64, 200), (2, 3), (16, 16), (512, 24)])
+@pytest.mark.parametrize("n", [1, 3, 4, 4097, (1 << 18) + 2])
+def test_ipv6_counts_equal_lut_kernel(native, example_key, H, Q, n):
+    """IPv6 counts only (rss_hash6_device): the register-table kernel (nine words, 108
+    fields) equals the LDS-table IPv6 kernel, which the Microsoft IPv6 KAT and the oracle pin
+    (tests/test_gpu_fields_ipv6.py); ragged n, every queue mode, and H > 256 (LDS kernel)."""
+    rng = np.random.default_rng(n * 1000 + H + Q)
+    words = torch.from_numpy(rng.integers(-2**31, 2**31, 9 * n, dtype=np.int64).astype(np.int32)).to("cuda:0")
+    key6 = native.prepare_key6(example_key)
+    s = torch.cuda.current_stream().cuda_stream
+    got = {}
+    for perm in (True, False):
+        c = torch.zeros(Q, dtype=torch.int64, device="cuda:0")
+        os.environ["RSS_COUNTS_PERM"] = "1" if perm else "0"
+        try:
+            native.hash6_device(key6, words.data_ptr(), n, H, Q, None, None, c.data_ptr(), 0, s)
+            torch.cuda.synchronize()
+        finally:
+            os.environ.pop("RSS_COUNTS_PERM", None)
+        got[perm] = c.cpu().numpy()
+    np.testing.assert_array_equal(got[True], got[False])
+    assert int(got[True].sum()) == n
