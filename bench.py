@@ -412,7 +412,7 @@ def main():
     elapsed = time.perf_counter() - t0
 
     # kernel-only timing (HIP events on the launch stream), for roofline.achieved
-    def kernel_ms_of(hash_ptr, queue_ptr, flags, reps):
+    def kernel_ms_of(hash_ptr, queue_ptr, flags, reps, tuples_ptr=None):
         """Mean launch time of `reps` launches of one output mode (HIP events on the
         launch stream around each launch), after 30 untimed launches of that mode: right
         after the memory-bound full-output steps, the LDS/VALU-heavier counts-only launches
@@ -423,7 +423,7 @@ def main():
         for i in range(-args.secondary_warmup, reps):
             if i >= 0:
                 ev[i][0].record(stream)
-            _native.hash_device(key, tuples.data_ptr(), n, H, Q, hash_ptr, queue_ptr,
+            _native.hash_device(key, tuples_ptr or tuples.data_ptr(), n, H, Q, hash_ptr, queue_ptr,
                                 counts.data_ptr(), flags | _native.FLAG_ACCUMULATE, sp)
             if i >= 0:
                 ev[i][1].record(stream)
@@ -449,7 +449,40 @@ def main():
     co_ms = u32_ms = flow_ms = None
     if rank == 0:
         reps = max(5, args.steps // 2)
-        co_ms = kernel_ms_of(None, None, 0, reps)
+        # counts only reads its input alone, and the read rate also depends a little on the
+        # input's placement (profiles/r02/co_placed_probe.log): a counts-only deployment places
+        # its input for that mode, so the line runs on the input kept by a counts-only probe of
+        # the placed input and three copies
+        co_input, co_probe = tuples, None
+        if args.placement_probe > 0:
+            def probe_co(buf, ev):
+                if ev is not None:
+                    ev[0].record(stream)
+                _native.hash_device(key, buf.data_ptr(), n, H, Q, None, None, counts.data_ptr(),
+                                    _native.FLAG_ACCUMULATE, sp)
+                if ev is not None:
+                    ev[1].record(stream)
+
+            cands = [tuples.view(torch.uint8)]
+            for _ in range(3):
+                cands.append(torch.empty(12 * n, dtype=torch.uint8, device=dev))
+                cands[-1].copy_(cands[0])
+            times = []
+            for b in cands:
+                ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                      for _ in range(5)]
+                for k in range(-5, 5):
+                    probe_co(b, ev[k] if k >= 0 else None)
+                torch.cuda.synchronize()
+                times.append(sorted(a.elapsed_time(c) for a, c in ev)[2])
+            best = min(range(len(cands)), key=times.__getitem__)
+            co_input = cands[best]
+            co_probe = {"input%d" % i: round(x, 4) for i, x in enumerate(times)}
+            co_probe["chosen"] = "input%d" % best
+            del cands
+        co_ms = kernel_ms_of(None, None, 0, reps, co_input.data_ptr())
+        del co_input
+        torch.cuda.empty_cache()
         queues32, u32_probe = queues, None
         if queues.numel() < 4 * n:  # the u32 line's queue buffer, placed like the others
             from rss_simulator_nvidia_amd.placement import choose_buffer
@@ -540,6 +573,7 @@ def main():
             },
             "counts_only": {
                 "kernel_ms": co_ms,
+                "input_probe_ms": co_probe,
                 "tuples_per_s_per_gpu": n / (co_ms / 1e3),
                 "hbm_read_GBs": n * READ_BYTES / (co_ms / 1e3) / 1e9,
                 "hbm_read_frac": n * READ_BYTES / (co_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
