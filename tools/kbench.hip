@@ -932,6 +932,32 @@ int main(int argc, char** argv) {
         CK(hipFree(pool));
     }
 
+    if (strstr("pads", filter)) {
+        // allocation size vs tier: K output pairs for each padding of the hash and queue
+        // allocations (0, 2 MiB, 64 MiB, 256 MiB extra), kinds allocated round-robin
+        constexpr int K = 5, P = 4;
+        const size_t pads[P] = {0, size_t(2) << 20, size_t(64) << 20, size_t(256) << 20};
+        uint32_t *hs[P][K], *qs[P][K];
+        for (int k = 0; k < K; ++k)
+            for (int pi = 0; pi < P; ++pi) {
+                CK(hipMalloc(&hs[pi][k], n * 4 + pads[pi]));
+                CK(hipMalloc(&qs[pi][k], n + pads[pi]));
+            }
+        for (int pi = 0; pi < P; ++pi)
+            for (int k = 0; k < K; ++k) {
+                const float tp = time_ms([&] {
+                    if (rss_hash_device(&key, (const rss_tuple4*)tup, n, H, Q, hs[pi][k], qs[pi][k],
+                                        (uint64_t*)c0, RSS_FLAG_QUEUE_U8, nullptr)) exit(1);
+                }, reps);
+                printf("pads pad=%zuMiB pair %d  product %.3f ms\n", pads[pi] >> 20, k, tp);
+            }
+        for (int k = 0; k < K; ++k)
+            for (int pi = 0; pi < P; ++pi) {
+                CK(hipFree(hs[pi][k]));
+                CK(hipFree(qs[pi][k]));
+            }
+    }
+
     if (strstr("parts", filter)) {
         // is a placement tier a property of a whole allocation or of its sub-ranges?  For K
         // output pairs: the product over all n tuples, then over each quarter of the tuples
