@@ -98,6 +98,48 @@ __global__ __launch_bounds__(1024) void mem_shape(Params p) {
     const uint4* src = reinterpret_cast<const uint4*>(p.tuples);
     const uint64_t ng = p.n >> 2;
     const uint32_t lane = threadIdx.x & 63;
+    if constexpr (kShape == 3 || kShape == 4) {
+        // whole tuples per load: a wave's block is 256 tuples; instruction j loads tuples
+        // 64j + lane (one 12-B dwordx3 per lane = 768 contiguous bytes per instruction).
+        // kShape 3: hash as 4 dword stores (tuples 64j + lane), queue as 4 byte stores;
+        // kShape 4: queue bytes regrouped through ds_bpermute so lane l stores the 4 queue
+        // bytes of tuples 4l..4l+3 as one dword (as the product), hashes as in 3
+        struct U3 { uint32_t x, y, z; };
+        const U3* t3 = reinterpret_cast<const U3*>(p.tuples);
+        const uint64_t wave = ((uint64_t)blockIdx.x * 1024 + threadIdx.x) >> 6;
+        const uint64_t nwaves = ((uint64_t)gridDim.x * 1024) >> 6;
+        const uint64_t nblocks = p.n >> 8;
+        uint8_t* q8 = reinterpret_cast<uint8_t*>(p.queue_out);
+        for (uint64_t b = wave; b < nblocks; b += nwaves) {
+            const uint64_t base = b << 8;
+            uint32_t h[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const U3 t = t3[base + 64 * j + lane];
+                h[j] = t.x ^ t.y ^ t.z;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) __builtin_nontemporal_store(h[j], p.hash_out + base + 64 * j + lane);
+            if constexpr (kShape == 3) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    __builtin_nontemporal_store((uint8_t)(h[j] & 0x17), q8 + base + 64 * j + lane);
+            } else {
+                // lane l needs queues of tuples 4l + i, held by lane (4l + i) % 64 in h[(4l + i) / 64]
+                uint32_t packed = 0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t src = (4 * lane + i) & 63, j = (4 * lane + i) >> 6;
+                    uint32_t v[4];
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj) v[jj] = __builtin_amdgcn_ds_bpermute(src << 2, h[jj] & 0x17);
+                    packed |= (j == 0 ? v[0] : j == 1 ? v[1] : j == 2 ? v[2] : v[3]) << (8 * i);
+                }
+                __builtin_nontemporal_store(packed, reinterpret_cast<uint32_t*>(q8) + (base >> 2) + lane);
+            }
+        }
+        return;
+    }
     if constexpr (kShape == 2) {
         const uint64_t ng16 = ng >> 2;
         for (uint64_t g = (uint64_t)blockIdx.x * 1024 + threadIdx.x; g < ng16; g += (uint64_t)gridDim.x * 1024) {
@@ -930,6 +972,42 @@ int main(int argc, char** argv) {
         }
         if (tc) CK(hipFree(tc));
         CK(hipFree(pool));
+    }
+
+    if (strstr("shapeplace", filter)) {
+        // the load shape on placements of every tier: product access (lane-owned 48 B) vs
+        // lane-contiguous 1 KiB wave loads, 12R+5W without compute, per output pair
+        constexpr int K = 6;
+        uint32_t *hs[K], *qs[K];
+        for (int k = 0; k < K; ++k) {
+            CK(hipMalloc(&hs[k], n * 4));
+            CK(hipMalloc(&qs[k], n));
+        }
+        for (int round = 0; round < 2; ++round)
+            for (int k = 0; k < K; ++k) {
+                Params pp = p;
+                pp.hash_out = hs[k];
+                pp.queue_out = qs[k];
+                const float tp = time_ms([&] {
+                    if (rss_hash_device(&key, (const rss_tuple4*)tup, n, H, Q, hs[k], qs[k], (uint64_t*)c0,
+                                        RSS_FLAG_QUEUE_U8, nullptr)) exit(1);
+                }, reps);
+                const float s0 = time_ms([&] { hipLaunchKernelGGL(mem_shape<0>, dim3(g_cus), dim3(1024), 0, 0, pp); }, reps);
+                const float s1 = time_ms([&] { hipLaunchKernelGGL(mem_shape<1>, dim3(g_cus), dim3(1024), 0, 0, pp); }, reps);
+                const float s1x2 = time_ms([&] { hipLaunchKernelGGL(mem_shape<1>, dim3(2 * g_cus), dim3(1024), 0, 0, pp); }, reps);
+                const float s0x2 = time_ms([&] { hipLaunchKernelGGL(mem_shape<0>, dim3(2 * g_cus), dim3(1024), 0, 0, pp); }, reps);
+                const float s3 = time_ms([&] { hipLaunchKernelGGL(mem_shape<3>, dim3(g_cus), dim3(1024), 0, 0, pp); }, reps);
+                const float s3x2 = time_ms([&] { hipLaunchKernelGGL(mem_shape<3>, dim3(2 * g_cus), dim3(1024), 0, 0, pp); }, reps);
+                const float s4 = time_ms([&] { hipLaunchKernelGGL(mem_shape<4>, dim3(g_cus), dim3(1024), 0, 0, pp); }, reps);
+                const float s4x2 = time_ms([&] { hipLaunchKernelGGL(mem_shape<4>, dim3(2 * g_cus), dim3(1024), 0, 0, pp); }, reps);
+                printf("shapeplace pair %d  product %.3f  shape0 %.3f  shape0x2 %.3f  shape1 %.3f  shape1x2 %.3f  "
+                       "shape3 %.3f  shape3x2 %.3f  shape4 %.3f  shape4x2 %.3f ms\n",
+                       k, tp, s0, s0x2, s1, s1x2, s3, s3x2, s4, s4x2);
+            }
+        for (int k = 0; k < K; ++k) {
+            CK(hipFree(hs[k]));
+            CK(hipFree(qs[k]));
+        }
     }
 
     if (strstr("pads", filter)) {
