@@ -78,7 +78,10 @@ static_assert(kBlock * 4 == (int)kTableEntries, "LUT build maps 4 entries per th
 
 enum QueueMode { QM_MASK = 0, QM_FAST16 = 1, QM_FAST32 = 2, QM_TABLE = 3, QM_FAST8 = 4 };
 constexpr uint32_t kRetaMax = 1024;  // indirection-table entries carried in the kernarg
-enum HistMode { HIST_PRIVATE = 0, HIST_SHARED = 1, HIST_GLOBAL = 2, HIST_NONE = 3 };
+enum HistMode { HIST_PRIVATE = 0, HIST_SHARED = 1, HIST_GLOBAL = 2, HIST_NONE = 3, HIST_RANGE = 4 };
+// HIST_RANGE: shared LDS bins for queues [q_lo, q_lo + q_span) only -- one pass of a
+// multi-pass launch for nqueues whose bins do not fit the LDS beside the tables
+// (launch_hash), instead of one global atomic per tuple (13x slower).
 enum QueueWidth { QW_U32 = 0, QW_U16 = 1, QW_U8 = 2 };
 
 // Everything a launch needs, passed by value in the kernarg segment.
@@ -99,6 +102,7 @@ struct LaunchParams {
     uint64_t q_m64;     // ceil(2^64 / Q): exact b % Q for any 32-bit b, Q
     uint32_t q_m16;     // ceil(2^16 / Q): exact b % Q for b < 256 (QM_FAST8, packed search)
     const uint32_t* key_windows;  // key search: nkeys x 96 windows in device memory
+    uint32_t q_lo, q_span;        // HIST_RANGE: the queues this pass counts
     uint16_t reta[kRetaMax];      // QM_TABLE: queue of bucket b (ethtool -X indirection)
 };
 
@@ -246,6 +250,10 @@ __device__ __forceinline__ void count_queue(uint32_t* bins, uint32_t q, uint32_t
         __hip_atomic_fetch_add(&bins[q], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     } else if constexpr (kHist == HIST_GLOBAL) {
         atomicAdd(&p.counts[q], 1ull);
+    } else if constexpr (kHist == HIST_RANGE) {
+        const uint32_t r = q - p.q_lo;  // wraps for q < q_lo
+        if (r < p.q_span)
+            __hip_atomic_fetch_add(&bins[r], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 }
 
@@ -305,8 +313,9 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
     const uint32_t tid = threadIdx.x;
 
     build_lut(lut, p.window, tid);
-    const uint32_t nbins =
-        kHist == HIST_PRIVATE ? p.Q * kBinCols : (kHist == HIST_SHARED ? p.Q : 0u);
+    const uint32_t nbins = kHist == HIST_PRIVATE ? p.Q * kBinCols
+                         : kHist == HIST_SHARED  ? p.Q
+                         : kHist == HIST_RANGE   ? p.q_span : 0u;
     for (uint32_t e = tid; e < nbins; e += kBlock) bins[e] = 0;
     uint32_t* reta_lds = bins + nbins;  // QM_TABLE: H entries after the bins
     if constexpr (kQMode == QM_TABLE)
@@ -368,7 +377,56 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
             }
             if (s) atomicAdd(&p.counts[q], (unsigned long long)s);
         }
+    } else if constexpr (kHist == HIST_RANGE) {
+        __syncthreads();
+        for (uint32_t r = tid; r < p.q_span; r += kBlock)
+            if (bins[r]) atomicAdd(&p.counts[p.q_lo + r], (unsigned long long)bins[r]);
     }
+}
+
+// HIST_RANGE passes after the first: histogram one range of queues straight from the
+// queue_number array the first pass wrote (2 or 4 B/tuple instead of re-reading 12 B and
+// rehashing): shared LDS bins for [q_lo, q_lo + q_span), 16-B loads when aligned.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void rss_queue_hist_kernel(const T* __restrict__ queues,
+                                                                uint64_t n, uint32_t q_lo,
+                                                                uint32_t q_span,
+                                                                unsigned long long* counts) {
+    extern __shared__ uint32_t bins[];
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t e = tid; e < q_span; e += kBlock) bins[e] = 0;
+    __syncthreads();
+    const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
+    const uint64_t gstride = (uint64_t)gridDim.x * kBlock;
+    auto add = [&](uint32_t q) {
+        const uint32_t r = q - q_lo;
+        if (r < q_span)
+            __hip_atomic_fetch_add(&bins[r], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    constexpr uint32_t kPer = 16 / sizeof(T);  // queues per 16-B load
+    uint64_t tail = 0;
+    if (((uintptr_t)queues & 15) == 0) {
+        const uint4* __restrict__ v = reinterpret_cast<const uint4*>(queues);
+        const uint64_t nv = n / kPer;
+        for (uint64_t i = gtid; i < nv; i += gstride) {
+            const uint4 x = v[i];
+            const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if constexpr (sizeof(T) == 2) {
+                    add(w[k] & 0xFFFFu);
+                    add(w[k] >> 16);
+                } else {
+                    add(w[k]);
+                }
+            }
+        }
+        tail = nv * kPer;
+    }
+    for (uint64_t i = tail + gtid; i < n; i += gstride) add(queues[i]);
+    __syncthreads();
+    for (uint32_t r = tid; r < q_span; r += kBlock)
+        if (bins[r]) atomicAdd(&counts[q_lo + r], (unsigned long long)bins[r]);
 }
 
 // Counts only, power-of-two H <= 256 (histogram mode, `rss_hash_host` without per-tuple
@@ -1091,6 +1149,7 @@ KernelFn pick_hist(int hist, int qwidth, bool vec4) {
         case HIST_PRIVATE: return pick_width<kHPow2, kQMode, HIST_PRIVATE>(qwidth, vec4);
         case HIST_SHARED: return pick_width<kHPow2, kQMode, HIST_SHARED>(qwidth, vec4);
         case HIST_GLOBAL: return pick_width<kHPow2, kQMode, HIST_GLOBAL>(qwidth, vec4);
+        case HIST_RANGE: return pick_width<kHPow2, kQMode, HIST_RANGE>(qwidth, vec4);
         default: return pick_width<kHPow2, kQMode, HIST_NONE>(qwidth, vec4);
     }
 }
@@ -1375,12 +1434,58 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
         counts_perm_enabled())
         return launch_counts_perm<3>(key->window, d_tuples, n, p.counts, p.h_mask, p.Q, p.q_mask,
                                      p.q_m16, qmode, bin_bytes, info.cu_count, stream);
-    KernelFn fn = h_pow2 ? pick_queue<true>(qmode, hist, qwidth, vec4)
-                         : pick_queue<false>(qmode, hist, qwidth, vec4);
+    // More queues than LDS bins: count them in ranges.  The first pass runs the hash kernel
+    // with shared LDS bins for queues [0, span) and writes the per-tuple outputs -- the
+    // queue column into the caller's buffer or, for a counts-only launch, into a stream-
+    // ordered scratch column; every further range is histogrammed from that column (2 or
+    // 4 B/tuple at the read stream's rate) instead of one global atomic per tuple (13x
+    // slower at 2^28 tuples, DESIGN.md §3 "Many queues").
     const uint64_t per_lane = vec4 ? 4 : 1;
     const uint64_t want = (n + per_lane * kBlock - 1) / (per_lane * kBlock);
     const uint64_t cap = (uint64_t)info.cu_count * kBlocksPerCU;
     const unsigned grid = (unsigned)(want < cap ? want : cap);
+    if (hist == HIST_GLOBAL && d_counts) {
+        const uint32_t span = (kBinBytesMax - reta_bytes) / 4;
+        const uint32_t qbytes = nqueues <= 65536u ? 2 : 4;
+        const uint64_t passes = ((uint64_t)nqueues + span - 1) / span;
+        if (passes <= (qbytes == 2 ? 64u : 32u)) {
+            void* qcol = d_queue;
+            int qw = qwidth;
+            bool scratch = false;
+            if (!qcol || qwidth == QW_U8) {  // (u8 queues always fit the bins: Q <= 256)
+                RSS_HIP_CHECK(hipMallocAsync(&qcol, (size_t)n * qbytes, stream));
+                scratch = true;
+                qw = qbytes == 2 ? QW_U16 : QW_U32;
+            }
+            p.queue_out = qcol;
+            p.q_lo = 0;
+            p.q_span = std::min<uint32_t>(span, nqueues);
+            const bool v4 = vec4 && ((uintptr_t)qcol % (qw == QW_U16 ? 8 : 16)) == 0;
+            KernelFn fn = h_pow2 ? pick_queue<true>(qmode, HIST_RANGE, qw, v4)
+                                 : pick_queue<false>(qmode, HIST_RANGE, qw, v4);
+            const unsigned g1 = v4 ? grid : (unsigned)std::min<uint64_t>((n + kBlock - 1) / kBlock, cap);
+            hipLaunchKernelGGL(fn, dim3(g1), dim3(kBlock), span * 4 + reta_bytes, stream, p);
+            RSS_HIP_CHECK(hipGetLastError());
+            const uint64_t qwant = (n + 8ull * kBlock - 1) / (8ull * kBlock);
+            const unsigned qgrid = (unsigned)std::min<uint64_t>(qwant, (uint64_t)info.cu_count * 2);
+            for (uint32_t lo = span; lo < nqueues; lo += span) {
+                const uint32_t sp = std::min<uint32_t>(span, nqueues - lo);
+                if (qw == QW_U16)
+                    hipLaunchKernelGGL(rss_queue_hist_kernel<uint16_t>, dim3(qgrid), dim3(kBlock),
+                                       sp * 4, stream, static_cast<const uint16_t*>(qcol), (uint64_t)n,
+                                       lo, sp, p.counts);
+                else
+                    hipLaunchKernelGGL(rss_queue_hist_kernel<uint32_t>, dim3(qgrid), dim3(kBlock),
+                                       sp * 4, stream, static_cast<const uint32_t*>(qcol), (uint64_t)n,
+                                       lo, sp, p.counts);
+                RSS_HIP_CHECK(hipGetLastError());
+            }
+            if (scratch) RSS_HIP_CHECK(hipFreeAsync(qcol, stream));
+            return RSS_OK;
+        }
+    }
+    KernelFn fn = h_pow2 ? pick_queue<true>(qmode, hist, qwidth, vec4)
+                         : pick_queue<false>(qmode, hist, qwidth, vec4);
     const uint32_t shmem = bin_bytes + reta_bytes;  // dynamic part; the 128 KiB LUT is static
     hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), shmem, stream, p);
     RSS_HIP_CHECK(hipGetLastError());

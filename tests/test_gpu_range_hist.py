@@ -1,0 +1,101 @@
+"""Large queue counts: when nqueues' bins do not fit the LDS beside the tables, the hash
+kernel counts queues [0, span) in LDS and writes the queue column (the caller's, or a
+stream-ordered scratch column for counts-only launches); every further range of queues is
+histogrammed from that column (rss_queue_hist_kernel) instead of one global atomic per
+tuple.  Bar: hash / queue / counts bit-exact to the C oracle across range counts 2..33 (u16
+and u32 queue columns, caller-owned and scratch), the fallback to global atomics past 32
+u32 ranges, RETA tables (whose LDS copy shrinks the range), misaligned input (the
+one-tuple-per-lane body and unaligned queue columns), ragged n and accumulation."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def native():
+    from rss_simulator_nvidia_amd import _native
+    if not torch.cuda.is_available():
+        pytest.fail("gpu tests need a gfx950 device")
+    return _native
+
+
+@pytest.mark.parametrize("H,Q", [(1 << 20, 8193), (1 << 20, 20000), (0xFFFFFFFF, 65536),
+                                 (1 << 30, 131072), (1 << 30, 131073), (99991, 50000),
+                                 (1 << 30, 8192 * 33)])
+@pytest.mark.parametrize("outputs", [True, False])
+def test_large_q_equals_oracle(native, oracle_lib, example_key, H, Q, outputs):
+    n = (1 << 20) + 7
+    host = oracle_lib.generate(21, 0, n)
+    dev = torch.device("cuda:0")
+    s = torch.cuda.current_stream(dev).cuda_stream
+    tup = torch.from_numpy(host.view(np.int32).reshape(-1)).to(dev)
+    h = torch.empty(n, dtype=torch.int32, device=dev) if outputs else None
+    q = torch.empty(n, dtype=torch.int16 if Q <= 65536 else torch.int32, device=dev) if outputs else None
+    c = torch.full((Q,), 5, dtype=torch.int64, device=dev)
+    flags = (native.FLAG_QUEUE_U16 if Q <= 65536 else 0) if outputs else 0
+    native.hash_device(native.prepare_key(example_key), tup.data_ptr(), n, H, Q,
+                       h.data_ptr() if outputs else None, q.data_ptr() if outputs else None,
+                       c.data_ptr(), flags, s)
+    torch.cuda.synchronize()
+    ho, qo, co = oracle_lib.run(example_key, host, H, Q)
+    np.testing.assert_array_equal(c.cpu().numpy().view(np.uint64), co)
+    if outputs:
+        np.testing.assert_array_equal(h.cpu().numpy().view(np.uint32), ho)
+        qv = q.cpu().numpy()
+        qv = qv.view(np.uint16) if qv.dtype == np.int16 else qv.view(np.uint32)
+        np.testing.assert_array_equal(qv.astype(np.uint32), qo)
+
+
+def test_large_q_misaligned_ragged_accumulate(native, oracle_lib, example_key):
+    n, H, Q = 300007, 1 << 24, 30000
+    host = oracle_lib.generate(22, 0, n)
+    flat = host.view(np.int32).reshape(-1)
+    buf = torch.zeros(flat.size + 1, dtype=torch.int32, device="cuda:0")
+    buf[1:] = torch.from_numpy(flat).to("cuda:0")  # 4-B offset: one tuple per lane
+    s = torch.cuda.current_stream().cuda_stream
+    c = torch.zeros(Q, dtype=torch.int64, device="cuda:0")
+    key = native.prepare_key(example_key)
+    for _ in range(2):
+        native.hash_device(key, buf.data_ptr() + 4, n, H, Q, None, None, c.data_ptr(),
+                           native.FLAG_ACCUMULATE, s)
+    torch.cuda.synchronize()
+    _, _, co = oracle_lib.run(example_key, host, H, Q, want_hash=False, want_queue=False)
+    np.testing.assert_array_equal(c.cpu().numpy().view(np.uint64), 2 * co)
+
+
+def test_large_q_with_reta(native, oracle_lib, example_key):
+    """RETA entries up to 20000 over 1024 buckets: bins share the LDS with the table"""
+    n, H, Q = 1 << 19, 1024, 20000
+    rng = np.random.default_rng(3)
+    reta = rng.integers(0, Q, H).astype(np.uint32)
+    host = oracle_lib.generate(23, 0, n)
+    tup = torch.from_numpy(host.view(np.int32).reshape(-1)).to("cuda:0")
+    q = torch.empty(n, dtype=torch.int32, device="cuda:0")
+    c = torch.zeros(Q, dtype=torch.int64, device="cuda:0")
+    native.hash_device_reta(native.prepare_key(example_key), tup.data_ptr(), n, H, reta, Q, None,
+                            q.data_ptr(), c.data_ptr(), 0, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    ho, _, _ = oracle_lib.run(example_key, host, 1, 1, want_queue=False)
+    want_q = reta[ho % H]
+    np.testing.assert_array_equal(q.cpu().numpy().view(np.uint32), want_q)
+    np.testing.assert_array_equal(c.cpu().numpy().view(np.uint64),
+                                  np.bincount(want_q, minlength=Q).astype(np.uint64))
+
+
+def test_large_q_unaligned_queue_column(native, oracle_lib, example_key):
+    """a caller queue column at a 2-byte offset: the range passes read it element-wise"""
+    n, H, Q = 200003, 1 << 20, 20000
+    host = oracle_lib.generate(24, 0, n)
+    tup = torch.from_numpy(host.view(np.int32).reshape(-1)).to("cuda:0")
+    qbuf = torch.zeros(n + 8, dtype=torch.int16, device="cuda:0")
+    c = torch.zeros(Q, dtype=torch.int64, device="cuda:0")
+    native.hash_device(native.prepare_key(example_key), tup.data_ptr(), n, H, Q, None,
+                       qbuf.data_ptr() + 2, c.data_ptr(), native.FLAG_QUEUE_U16,
+                       torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    _, qo, co = oracle_lib.run(example_key, host, H, Q)
+    np.testing.assert_array_equal(qbuf[1:n + 1].cpu().numpy().view(np.uint16).astype(np.uint32), qo)
+    np.testing.assert_array_equal(c.cpu().numpy().view(np.uint64), co)

@@ -1,0 +1,54 @@
+"""Kernel time across (H, Q) configurations on fixed buffers (tool, not product): full
+output (hash u32 + the narrowest queue width) and counts only, 2^28 tuples, medians of 10
+launches after 5 warm ones, against the same buffers' 12 R + 5 W / 12 R + 6 W / 12 R + 8 W
+byte counts.  Prints one JSON line per configuration."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from bench import EXAMPLE_KEY, SEED  # noqa: E402
+from rss_simulator_nvidia_amd import _native  # noqa: E402
+
+n = 1 << 28
+dev = torch.device("cuda:0")
+s = torch.cuda.current_stream(dev)
+key = _native.prepare_key([int(x, 16) for x in EXAMPLE_KEY.split(":")])
+tup = torch.empty(3 * n, dtype=torch.int32, device=dev)
+_native.generate_device(SEED, 0, n, tup.data_ptr(), s.cuda_stream)
+h = torch.empty(n, dtype=torch.int32, device=dev)
+q = torch.empty(n, dtype=torch.int32, device=dev)
+
+
+def timed(H, Q, outputs, flags, reps=10, warm=5):
+    c = torch.zeros(Q, dtype=torch.int64, device=dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(reps)]
+    hp, qp = (h.data_ptr(), q.data_ptr()) if outputs else (None, None)
+    for i in range(-warm, reps):
+        if i >= 0:
+            ev[i][0].record(s)
+        _native.hash_device(key, tup.data_ptr(), n, H, Q, hp, qp, c.data_ptr(),
+                            flags | _native.FLAG_ACCUMULATE, s.cuda_stream)
+        if i >= 0:
+            ev[i][1].record(s)
+    torch.cuda.synchronize()
+    x = sorted(a.elapsed_time(b) for a, b in ev)
+    return round(x[len(x) // 2], 4)
+
+
+for H, Q in [(128, 24), (128, 16), (512, 64), (100, 7), (1000, 24), (65536, 24),
+             (65536, 4096), (1 << 20, 1000), (1 << 20, 8193), (1 << 20, 20000),
+             (4294967295, 65536), (1 << 30, 131072), (1 << 30, 131073)]:
+    width = 1 if Q <= 256 else (2 if Q <= 65536 else 4)
+    fl = {1: _native.FLAG_QUEUE_U8, 2: _native.FLAG_QUEUE_U16, 4: 0}[width]
+    full = timed(H, Q, True, fl)
+    co = timed(H, Q, False, 0)
+    print(json.dumps({"H": H, "Q": Q, "queue_bytes": width, "full_ms": full,
+                      "full_GBs": round(n * (16 + width) / (full / 1e3) / 1e9),
+                      "counts_ms": co, "counts_read_GBs": round(n * 12 / (co / 1e3) / 1e9)}),
+          flush=True)
