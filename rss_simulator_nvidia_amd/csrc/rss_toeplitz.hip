@@ -890,6 +890,7 @@ struct LaunchParams6 {
     uint32_t qwidth;  // QueueWidth of queue_out (grid-uniform runtime switch)
     uint32_t q_m16;
     uint64_t q_m64;
+    uint32_t q_lo, q_span;    // HIST_RANGE, as LaunchParams
     uint16_t reta[kRetaMax];  // QM_TABLE: queue of bucket b, as LaunchParams::reta
 };
 
@@ -996,8 +997,11 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz6_kernel(const LaunchParam
     p.q_m32 = p6.q_m32;
     p.q_m16 = p6.q_m16;
     p.q_m64 = p6.q_m64;
-    const uint32_t nbins =
-        kHist == HIST_PRIVATE ? p.Q * kBinCols : (kHist == HIST_SHARED ? p.Q : 0u);
+    p.q_lo = p6.q_lo;
+    p.q_span = p6.q_span;
+    const uint32_t nbins = kHist == HIST_PRIVATE ? p.Q * kBinCols
+                         : kHist == HIST_SHARED  ? p.Q
+                         : kHist == HIST_RANGE   ? p.q_span : 0u;
     for (uint32_t e = tid; e < nbins; e += kBlock) bins[e] = 0;
     uint32_t* reta_lds = bins + nbins;  // QM_TABLE: H entries after the bins
     if constexpr (kQMode == QM_TABLE)
@@ -1081,6 +1085,10 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz6_kernel(const LaunchParam
             }
             if (s) atomicAdd(&p.counts[k], (unsigned long long)s);
         }
+    } else if constexpr (kHist == HIST_RANGE) {
+        __syncthreads();
+        for (uint32_t r = tid; r < p.q_span; r += kBlock)
+            if (bins[r]) atomicAdd(&p.counts[p.q_lo + r], (unsigned long long)bins[r]);
     }
 }
 
@@ -1375,6 +1383,25 @@ int launch_counts_perm(const uint32_t* window, const void* tuples, uint64_t n, u
     return RSS_OK;
 }
 
+// Queue ranges [span, nqueues) of a many-queues launch, histogrammed from the queue column
+// (u16 or u32) the first pass wrote.
+int launch_queue_ranges(const void* qcol, int qw, uint64_t n, uint32_t span, uint32_t nqueues,
+                        unsigned long long* counts, int cu_count, hipStream_t stream) {
+    const uint64_t qwant = (n + 8ull * kBlock - 1) / (8ull * kBlock);
+    const unsigned qgrid = (unsigned)std::min<uint64_t>(qwant, (uint64_t)cu_count * 2);
+    for (uint32_t lo = span; lo < nqueues; lo += span) {
+        const uint32_t sp = std::min<uint32_t>(span, nqueues - lo);
+        if (qw == QW_U16)
+            hipLaunchKernelGGL(rss_queue_hist_kernel<uint16_t>, dim3(qgrid), dim3(kBlock), sp * 4,
+                               stream, static_cast<const uint16_t*>(qcol), n, lo, sp, counts);
+        else
+            hipLaunchKernelGGL(rss_queue_hist_kernel<uint32_t>, dim3(qgrid), dim3(kBlock), sp * 4,
+                               stream, static_cast<const uint32_t*>(qcol), n, lo, sp, counts);
+        RSS_HIP_CHECK(hipGetLastError());
+    }
+    return RSS_OK;
+}
+
 int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32_t htable,
                 uint32_t nqueues, uint32_t* d_hash, void* d_queue, uint64_t* d_counts,
                 uint32_t flags, hipStream_t stream, const uint32_t* reta = nullptr) {
@@ -1466,22 +1493,9 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
             const unsigned g1 = v4 ? grid : (unsigned)std::min<uint64_t>((n + kBlock - 1) / kBlock, cap);
             hipLaunchKernelGGL(fn, dim3(g1), dim3(kBlock), span * 4 + reta_bytes, stream, p);
             RSS_HIP_CHECK(hipGetLastError());
-            const uint64_t qwant = (n + 8ull * kBlock - 1) / (8ull * kBlock);
-            const unsigned qgrid = (unsigned)std::min<uint64_t>(qwant, (uint64_t)info.cu_count * 2);
-            for (uint32_t lo = span; lo < nqueues; lo += span) {
-                const uint32_t sp = std::min<uint32_t>(span, nqueues - lo);
-                if (qw == QW_U16)
-                    hipLaunchKernelGGL(rss_queue_hist_kernel<uint16_t>, dim3(qgrid), dim3(kBlock),
-                                       sp * 4, stream, static_cast<const uint16_t*>(qcol), (uint64_t)n,
-                                       lo, sp, p.counts);
-                else
-                    hipLaunchKernelGGL(rss_queue_hist_kernel<uint32_t>, dim3(qgrid), dim3(kBlock),
-                                       sp * 4, stream, static_cast<const uint32_t*>(qcol), (uint64_t)n,
-                                       lo, sp, p.counts);
-                RSS_HIP_CHECK(hipGetLastError());
-            }
+            rc = launch_queue_ranges(qcol, qw, n, span, nqueues, p.counts, info.cu_count, stream);
             if (scratch) RSS_HIP_CHECK(hipFreeAsync(qcol, stream));
-            return RSS_OK;
+            return rc;
         }
     }
     KernelFn fn = h_pow2 ? pick_queue<true>(qmode, hist, qwidth, vec4)
@@ -1506,6 +1520,7 @@ KernelFn6 pick6_hist(int hist, bool vec4) {
         case HIST_PRIVATE: return pick6_vec<kHPow2, kQMode, HIST_PRIVATE>(vec4);
         case HIST_SHARED: return pick6_vec<kHPow2, kQMode, HIST_SHARED>(vec4);
         case HIST_GLOBAL: return pick6_vec<kHPow2, kQMode, HIST_GLOBAL>(vec4);
+        case HIST_RANGE: return pick6_vec<kHPow2, kQMode, HIST_RANGE>(vec4);
         default: return pick6_vec<kHPow2, kQMode, HIST_NONE>(vec4);
     }
 }
@@ -1587,11 +1602,38 @@ int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint
         (qmode == QM_MASK || qmode == QM_FAST8) && aligned16(d_tuples) && counts_perm_enabled())
         return launch_counts_perm<9>(key->window, d_tuples, n, p.counts, p.h_mask, p.Q, p.q_mask,
                                      p.q_m16, qmode, nqueues * kBinCols * 4, info.cu_count, stream);
-    KernelFn6 fn = h_pow2 ? pick6<true>(qmode, hist, vec4) : pick6<false>(qmode, hist, vec4);
     const uint64_t per_lane = vec4 ? 4 : 1;
     const uint64_t want = (n + per_lane * kBlock - 1) / (per_lane * kBlock);
     const uint64_t cap = (uint64_t)info.cu_count * kBlocksPerCU6;
     const unsigned grid = (unsigned)(want < cap ? want : cap);
+    // many queues: as launch_hash (first range in LDS + the queue column, then the column)
+    if (hist == HIST_GLOBAL && d_counts) {
+        const uint32_t span = budget / 4;
+        const uint32_t qbytes = nqueues <= 65536u ? 2 : 4;
+        const uint64_t passes = ((uint64_t)nqueues + span - 1) / span;
+        if (passes <= (qbytes == 2 ? 64u : 32u)) {
+            void* qcol = d_queue;
+            bool scratch = false;
+            if (!qcol || qwidth == QW_U8) {
+                RSS_HIP_CHECK(hipMallocAsync(&qcol, (size_t)n * qbytes, stream));
+                scratch = true;
+                p.qwidth = qbytes == 2 ? QW_U16 : QW_U32;
+            }
+            p.queue_out = qcol;
+            p.q_lo = 0;
+            p.q_span = std::min<uint32_t>(span, nqueues);
+            const uint32_t qw = p.qwidth;
+            const bool v4 = vec4 && ((uintptr_t)qcol % (qw == QW_U16 ? 8 : 16)) == 0;
+            KernelFn6 fn = h_pow2 ? pick6<true>(qmode, HIST_RANGE, v4) : pick6<false>(qmode, HIST_RANGE, v4);
+            const unsigned g1 = v4 ? grid : (unsigned)std::min<uint64_t>((n + kBlock - 1) / kBlock, cap);
+            hipLaunchKernelGGL(fn, dim3(g1), dim3(kBlock), span * 4 + reta_bytes, stream, p);
+            RSS_HIP_CHECK(hipGetLastError());
+            rc = launch_queue_ranges(qcol, (int)qw, n, span, nqueues, p.counts, info.cu_count, stream);
+            if (scratch) RSS_HIP_CHECK(hipFreeAsync(qcol, stream));
+            return rc;
+        }
+    }
+    KernelFn6 fn = h_pow2 ? pick6<true>(qmode, hist, vec4) : pick6<false>(qmode, hist, vec4);
     hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), bin_bytes + reta_bytes, stream, p);
     RSS_HIP_CHECK(hipGetLastError());
     return RSS_OK;

@@ -99,3 +99,28 @@ def test_large_q_unaligned_queue_column(native, oracle_lib, example_key):
     _, qo, co = oracle_lib.run(example_key, host, H, Q)
     np.testing.assert_array_equal(qbuf[1:n + 1].cpu().numpy().view(np.uint16).astype(np.uint32), qo)
     np.testing.assert_array_equal(c.cpu().numpy().view(np.uint64), co)
+
+
+@pytest.mark.parametrize("H,Q,outputs", [(1 << 20, 3073, True), (1 << 20, 20000, False),
+                                         (0xFFFFFFFF, 65536, True), (1 << 30, 100000, False)])
+def test_ipv6_large_q(native, example_key, H, Q, outputs):
+    """IPv6 (12 KiB of bins beside its tables, so ranges start at 3073 queues): queue and
+    counts equal hash % H % Q of the kernel's own hashes (pinned by the IPv6 KAT tests)"""
+    n = (1 << 18) + 3
+    rng = np.random.default_rng(Q)
+    words = torch.from_numpy(rng.integers(-2**31, 2**31, 9 * n, dtype=np.int64).astype(np.int32)).to("cuda:0")
+    key6 = native.prepare_key6(example_key)
+    s = torch.cuda.current_stream().cuda_stream
+    h = torch.empty(n, dtype=torch.int32, device="cuda:0")
+    native.hash6_device(key6, words.data_ptr(), n, 1, 1, h.data_ptr(), None, None, 0, s)
+    q = torch.empty(n, dtype=torch.int32, device="cuda:0") if outputs else None
+    c = torch.zeros(Q, dtype=torch.int64, device="cuda:0")
+    native.hash6_device(key6, words.data_ptr(), n, H, Q, None, q.data_ptr() if outputs else None,
+                        c.data_ptr(), 0, s)
+    torch.cuda.synchronize()
+    hv = h.cpu().numpy().view(np.uint32).astype(np.uint64)
+    want_q = (hv % np.uint64(H)) % np.uint64(Q)
+    np.testing.assert_array_equal(c.cpu().numpy().view(np.uint64),
+                                  np.bincount(want_q.astype(np.int64), minlength=Q).astype(np.uint64))
+    if outputs:
+        np.testing.assert_array_equal(q.cpu().numpy().view(np.uint32).astype(np.uint64), want_q)
