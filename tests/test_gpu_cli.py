@@ -40,3 +40,45 @@ def test_fast_path_equals_pandas_path_large(tmp_path, monkeypatch, capsys):
         outs[mode] = open(out, "rb").read()
     assert outs["1"] == outs["0"]
     assert outs["1"].count(b"\n") == 300000 + 1 + 24 + 1
+
+
+@pytest.mark.parametrize("device_csv", ["1", "0"])
+def test_many_queues_csv_paths_equal_pandas(tmp_path, monkeypatch, capsys, device_csv):
+    """--num-queues 20000 (the many-queues ranges on the device CSV path and on the host text
+    path) writes the same bytes as the pandas path."""
+    import os
+    import subprocess
+
+    from cli_cases import GOLDEN, run_main
+    root = os.path.dirname(GOLDEN.rstrip("/").rsplit("/", 1)[0])
+    gen = str(tmp_path / "gen_csv")
+    subprocess.run(["gcc", "-O2", "-o", gen, os.path.join(root, "tools", "gen_csv.c")], check=True)
+    src = str(tmp_path / "in.csv")
+    subprocess.run([gen, "50000", "77", src], check=True)
+    monkeypatch.setenv("RSS_CSV_DEVICE", device_csv)
+    outs = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("RSS_CSV_FASTPATH", mode)
+        out = str(tmp_path / ("out%s.csv" % mode))
+        status, _, _, exc = run_main(
+            ["--key-file", os.path.join(GOLDEN, "example_input", "hash_key.txt"),
+             "--ips-file", src, "--htable-size", "1048576", "--num-queues", "20000", "--csv", out],
+            capsys)
+        assert status == 0, exc
+        outs[mode] = open(out, "rb").read()
+    assert outs["1"] == outs["0"]
+    # the counts section is the bincount of the queue column, which is hash % H % Q
+    import io
+
+    import numpy as np
+    import pandas as pd
+    text = outs["1"].decode()
+    head, rows = text.split("src_ip,", 1)
+    table = pd.read_csv(io.StringIO("src_ip," + rows))
+    h = table["hash_result"].to_numpy().astype(np.uint64)
+    q = table["queue_number"].to_numpy()
+    np.testing.assert_array_equal(q, ((h % np.uint64(1048576)) % np.uint64(20000)).astype(q.dtype))
+    counts = pd.read_csv(io.StringIO(head))
+    bc = np.bincount(q, minlength=20000)
+    np.testing.assert_array_equal(counts["counts"].to_numpy(), bc[counts["queue_number"].to_numpy()])
+    assert int(counts["counts"].sum()) == len(q) == 50000
