@@ -1,6 +1,5 @@
 """Process start-up costs of the CLI (tool, not product): library load, first HIP call
 (device count), context creation, and a tiny hash, each timed from a fresh process."""
-import ctypes
 import json
 import os
 import sys
