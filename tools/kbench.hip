@@ -72,6 +72,26 @@ __global__ __launch_bounds__(1024) void mem_ceiling_q8(Params p) {
     }
 }
 
+// IPv6 byte mix: 36 B read (9 x 16-B loads per lane for 4 tuples) + 4 B hash + 1 B queue
+__global__ __launch_bounds__(1024) void mem_ceiling6_q8(Params p) {
+    const uint4* src = reinterpret_cast<const uint4*>(p.tuples);
+    const uint64_t ng = p.n >> 2;
+    for (uint64_t g = (uint64_t)blockIdx.x * 1024 + threadIdx.x; g < ng; g += (uint64_t)gridDim.x * 1024) {
+        uint32_t acc[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            const uint4 x = src[9 * g + k];
+            acc[k & 3] ^= x.x ^ x.y ^ x.z ^ x.w;
+        }
+        uint32_t* o = p.hash_out + 4 * g;
+        __builtin_nontemporal_store(acc[0], o);
+        __builtin_nontemporal_store(acc[1], o + 1);
+        __builtin_nontemporal_store(acc[2], o + 2);
+        __builtin_nontemporal_store(acc[3], o + 3);
+        __builtin_nontemporal_store((acc[0] ^ acc[3]) & 0x17171717u, p.queue_out + g);
+    }
+}
+
 typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
 // practical HBM ceilings for other read / write mixes on the same box: a float4 copy
 // (1 R : 1 W, the microarch guide's 6.29 TB/s shape) and a write-only fill
@@ -972,6 +992,34 @@ int main(int argc, char** argv) {
         }
         if (tc) CK(hipFree(tc));
         CK(hipFree(pool));
+    }
+
+    if (strstr("ipv6mem", filter)) {
+        // the IPv6 kernel (rss_hash6_device, u8 queues) against its 36 R + 5 W stream, same
+        // buffers: n/3 tuples of 36 B fill the 12n-byte tuple buffer
+        const uint64_t n6 = n / 3;
+        rss_key6 k6;
+        if (rss_key6_prepare(key_bytes, 40, &k6)) exit(1);
+        Params pp = p;
+        pp.n = n6;
+        pp.hash_out = h1;
+        pp.queue_out = q1;
+        for (int round = 0; round < 3; ++round) {
+            const float tk = time_ms([&] {
+                if (rss_hash6_device(&k6, (const rss_tuple6*)tup, n6, H, Q, h1, q1, (uint64_t*)c1,
+                                     RSS_FLAG_QUEUE_U8, nullptr)) exit(1);
+            }, reps);
+            const float tc = time_ms([&] {
+                if (rss_hash6_device(&k6, (const rss_tuple6*)tup, n6, H, Q, nullptr, nullptr, (uint64_t*)c1,
+                                     0, nullptr)) exit(1);
+            }, reps);
+            const float ts = time_ms([&] { hipLaunchKernelGGL(mem_ceiling6_q8, dim3(g_cus), dim3(1024), 0, 0, pp); }, reps);
+            const float tr = time_ms([&] { hipLaunchKernelGGL(mem_ceiling<false>, dim3(g_cus), dim3(1024), 0, 0, p); }, reps);
+            printf("ipv6mem  ipv6 full u8 %.3f ms (%.0f GB/s)  ipv6 counts %.3f ms (%.0f GB/s read)  "
+                   "stream 36R+5W %.3f ms (%.0f GB/s)  read-only 12n %.3f ms (%.0f GB/s)\n",
+                   tk, n6 * 41e-9 / tk * 1e3, tc, n6 * 36e-9 / tc * 1e3, ts, n6 * 41e-9 / ts * 1e3,
+                   tr, n * 12e-9 / tr * 1e3);
+        }
     }
 
     if (strstr("shapeplace", filter)) {
