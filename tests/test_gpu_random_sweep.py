@@ -3,6 +3,8 @@ C oracle: random sizes (incl. 0 and ragged tails), power-of-two and arbitrary ht
 nqueues (every modulo and histogram mode), key lengths 16..52, queue widths u8 / u16 /
 u32, NULL outputs, accumulation into non-zero counts and 4-byte-misaligned tuples.
 Bar: bit-exact (integer work)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -10,7 +12,9 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
-CASES = 48
+# RSS_SWEEP_CASES / RSS_SWEEP_SEED0 widen the sweep for a one-off deep run
+CASES = int(os.environ.get("RSS_SWEEP_CASES", "48"))
+SEED0 = int(os.environ.get("RSS_SWEEP_SEED0", "0"))
 
 
 @pytest.fixture(scope="module")
@@ -38,7 +42,7 @@ def _config(seed):
                 reta=bool(H <= 1024 and Q <= 65536 and rng.random() < 0.25))
 
 
-@pytest.mark.parametrize("seed", range(CASES))
+@pytest.mark.parametrize("seed", range(SEED0, SEED0 + CASES))
 def test_random_config_matches_oracle(native, oracle_lib, seed):
     c = _config(seed)
     rng, n, H, Q = c["rng"], c["n"], c["H"], c["Q"]
