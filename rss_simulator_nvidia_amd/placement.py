@@ -37,14 +37,29 @@ def choose_stream_buffers(torch, dev, n, fill_input, probe, n_inputs=2, n_output
     """
     if n < 1:
         raise ValueError("choose_stream_buffers: n must be >= 1")
-    inputs = []
-    for _ in range(max(1, n_inputs)):
+    oom = getattr(torch.cuda, "OutOfMemoryError", MemoryError)
+
+    def candidates(count, make):
+        # the first candidate must fit; later ones only while memory lasts (a batch near the
+        # HBM size gets fewer candidates, not an error)
+        got = [make()]
+        for _ in range(count - 1):
+            try:
+                got.append(make())
+            except oom:
+                torch.cuda.empty_cache()
+                break
+        return got
+
+    def make_input():
         t = torch.empty(3 * n, dtype=torch.int32, device=dev)
         fill_input(t)
-        inputs.append(t)
-    outputs = [(torch.empty(n, dtype=torch.int32, device=dev),
-                torch.empty(queue_bytes * n, dtype=torch.uint8, device=dev))
-               for _ in range(max(1, n_outputs))]
+        return t
+
+    inputs = candidates(max(1, n_inputs), make_input)
+    outputs = candidates(max(1, n_outputs),
+                         lambda: (torch.empty(n, dtype=torch.int32, device=dev),
+                                  torch.empty(queue_bytes * n, dtype=torch.uint8, device=dev)))
     torch.cuda.synchronize(dev)
     times = {}
     for i, t in enumerate(inputs):
