@@ -120,6 +120,10 @@ int rss_key_select_fields(rss_key* key, uint32_t fields);
  * (positive_int.py:27).  Launched on `stream` (hipStream_t) on the calling
  * thread's current device.  Any alignment works; 16-byte aligned tuples/hashes
  * (and 4/8/16-byte aligned u8/u16/u32 queues) take the 4-tuples-per-lane path.
+ * Counts-only launches with a power-of-two htable <= 256 run a table-free kernel;
+ * with more than ~8192 queues the counts are gathered range by range from the queue
+ * column -- d_queue when given, else a stream-ordered scratch column of 2 (nqueues <=
+ * 65536) or 4 bytes per tuple (hipMallocAsync / hipFreeAsync on `stream`).
  */
 int rss_hash_device(const rss_key* key, const rss_tuple4* d_tuples, size_t n,
                     uint32_t htable, uint32_t nqueues, uint32_t* d_hash,
