@@ -570,6 +570,9 @@ def main():
                 "bound_tuples_per_s_per_gpu": HBM_PEAK_GBS * 1e9 / READ_BYTES,
                 "counts_only_frac": n / (co_ms / 1e3) / (HBM_PEAK_GBS * 1e9 / READ_BYTES),
                 "full_value_frac": value / (world * HBM_PEAK_GBS * 1e9 / READ_BYTES),
+                # the same for the full-output kernel alone (slowest rank's mean launch), i.e.
+                # without the per-step counts zeroing, event records and launch gaps
+                "full_kernel_frac": n / (kernel_ms_max / 1e3) / (HBM_PEAK_GBS * 1e9 / READ_BYTES),
             },
             "counts_only": {
                 "kernel_ms": co_ms,
