@@ -1048,6 +1048,11 @@ int main(int argc, char** argv) {
                 const float s3x2 = time_ms([&] { hipLaunchKernelGGL(mem_shape<3>, dim3(2 * g_cus), dim3(1024), 0, 0, pp); }, reps);
                 const float s4 = time_ms([&] { hipLaunchKernelGGL(mem_shape<4>, dim3(g_cus), dim3(1024), 0, 0, pp); }, reps);
                 const float s4x2 = time_ms([&] { hipLaunchKernelGGL(mem_shape<4>, dim3(2 * g_cus), dim3(1024), 0, 0, pp); }, reps);
+                const float t9x2 = time_ms([&] {
+                    CK(hipMemsetAsync(c1, 0, Q * 8, 0));
+                    hipLaunchKernelGGL(lut9_kernel<true>, dim3(2 * g_cus), dim3(1024), 0, 0, pp);
+                }, reps);
+                printf("shapeplace pair %d  T9 x2 (60 KiB LUT, 2 WGs/CU) %.3f ms\n", k, t9x2);
                 printf("shapeplace pair %d  product %.3f  shape0 %.3f  shape0x2 %.3f  shape1 %.3f  shape1x2 %.3f  "
                        "shape3 %.3f  shape3x2 %.3f  shape4 %.3f  shape4x2 %.3f ms\n",
                        k, tp, s0, s0x2, s1, s1x2, s3, s3x2, s4, s4x2);
