@@ -2,8 +2,9 @@
 
 One step = one pass of the hot path (Toeplitz hash -> htable index -> queue
 modulo -> per-queue histogram, all outputs written) over this rank's resident
-shard of synthetic tuples (zero counts + one kernel launch; ``--graph`` replays the
-launch as a captured HIP graph), followed, under a launcher, by the RCCL all-reduce of the
+shard of synthetic tuples (one ``rss_hash_device_ws`` launch that also writes the step's
+counts from zero -- single-pass counts, no zeroing launch; ``--zero-counts`` = a zeroing launch
++ an accumulating one; ``--graph`` replays the launch as a captured HIP graph), followed, under a launcher, by the RCCL all-reduce of the
 per-queue count vector, issued async so it overlaps the next step (double-buffered
 counts).  Weak scaling: every rank owns ``--tuples-per-gpu``
 tuples (default 2**28, BASELINE configs[2]) of one global splitmix64 stream.
@@ -56,6 +57,9 @@ def parse_args():
                         "search), timed after the main measurement")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl = RCCL over xGMI; gloo only to rehearse N>1 on one GPU")
+    p.add_argument("--zero-counts", action="store_true",
+                   help="zero each step's counts with a separate launch (counts.zero_() + an "
+                        "accumulating rss_hash_device) instead of single-pass counts")
     p.add_argument("--graph", action="store_true",
                    help="replay each step as a captured HIP graph (measured: no gain over "
                         "eager launches at 2**28 tuples per step)")
@@ -354,12 +358,15 @@ def main():
     # Two count buffers: step i hashes into one while the RCCL all-reduce of step i-1's
     # buffer (async, on the collective stream) overlaps it (sharding.CountsPipeline).
     from rss_simulator_nvidia_amd.sharding import CountsPipeline
-    pipeline = CountsPipeline(Q, dev)
+    # Single-pass counts (rss_hash_device_ws): the launch writes the step's counts itself, no
+    # zeroing launch before it; --zero-counts = counts.zero_() + an accumulating launch
+    pipeline = CountsPipeline(Q, dev, single_pass=not args.zero_counts)
 
-    def launch(c):
+    def launch(c, ws=None):
         _native.hash_device(key, tuples.data_ptr(), n, H, Q, hashes.data_ptr(), queues.data_ptr(),
-                            c.data_ptr(), _native.FLAG_ACCUMULATE | qflag,
-                            torch.cuda.current_stream(dev).cuda_stream)
+                            c.data_ptr(), qflag | (0 if ws is not None else _native.FLAG_ACCUMULATE),
+                            torch.cuda.current_stream(dev).cuda_stream,
+                            ws.data_ptr() if ws is not None else None)
 
     graphs = None
     if args.graph:
@@ -367,26 +374,26 @@ def main():
             side = torch.cuda.Stream(dev)
             side.wait_stream(stream)
             with torch.cuda.stream(side):
-                launch(pipeline.buffers[0])
+                launch(pipeline.buffers[0], pipeline.workspace)
             stream.wait_stream(side)
             graphs = {}
             for c in pipeline.buffers:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
-                    launch(c)
+                    launch(c, pipeline.workspace)
                 graphs[c.data_ptr()] = g
         except Exception as err:  # eager fallback keeps the same work per step
             print("bench: graph capture unavailable (%s); launching eagerly" % err, file=sys.stderr)
             graphs = None
 
     def step(i, ev=None):
-        def timed_launch(c):
+        def timed_launch(c, ws=None):
             if ev is not None:
                 ev[0].record(stream)
             if graphs is not None:
                 graphs[c.data_ptr()].replay()
             else:
-                launch(c)
+                launch(c, ws)
             if ev is not None:
                 ev[1].record(stream)
         pipeline.step(timed_launch)
@@ -541,8 +548,10 @@ def main():
                                 "(async, overlapped with the next step)"
                                 % (world, "RCCL" if args.dist_backend == "nccl" else "gloo", Q))
                                if distributed else "single process, one GPU (no process group)",
-                "step": "zero counts + hash kernel (hipGraph replay)" if graphs is not None
-                        else "zero counts + hash kernel (eager launches)",
+                "step": ("zero counts + " if args.zero_counts else
+                         "single-pass counts (rss_hash_device_ws): ") +
+                        ("hash kernel (hipGraph replay)" if graphs is not None
+                         else "hash kernel (eager launches)"),
             },
             "roofline": {
                 "bound": "hbm",

@@ -131,6 +131,25 @@ int rss_hash_device(const rss_key* key, const rss_tuple4* d_tuples, size_t n,
                     void* stream);
 
 /*
+ * Single-pass counts: rss_hash_device with a caller-owned workspace, so that a batch's
+ * counts need no zeroing launch before it (the step of a job that hashes batch after
+ * batch into fresh counts, sharding.CountsPipeline).  Every workgroup adds its LDS bins
+ * into the workspace's accumulators and takes a ticket; the last one moves the sums into
+ * d_counts -- overwriting them, or adding with RSS_FLAG_ACCUMULATE -- and zeroes the
+ * workspace again.  d_workspace: rss_counts_workspace_bytes(nqueues) bytes of 8-byte
+ * aligned device memory, zero before its first use (every launch leaves it zero), used
+ * by one launch at a time (launches that may run concurrently need their own).  Launches
+ * whose counts are not gathered in LDS bins (more than ~8192 queues) leave the workspace
+ * untouched and zero d_counts first as rss_hash_device does.  Results are identical to
+ * rss_hash_device's.  With d_counts NULL the workspace is not used (may be NULL).
+ */
+int rss_counts_workspace_bytes(uint32_t nqueues, size_t* out);
+int rss_hash_device_ws(const rss_key* key, const rss_tuple4* d_tuples, size_t n,
+                       uint32_t htable, uint32_t nqueues, uint32_t* d_hash,
+                       void* d_queue, uint64_t* d_counts, uint32_t flags,
+                       uint64_t* d_workspace, void* stream);
+
+/*
  * Indirection table (RETA; `ethtool -X equal N / weight ...`, which the reference's
  * docs cite, docs/rss_general_explaination.md:9-11): queue = reta[hash % htable]
  * instead of (hash % htable) % nqueues.  reta: host array of htable entries, each

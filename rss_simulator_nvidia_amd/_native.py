@@ -37,6 +37,7 @@ EXPORTED_SYMBOLS = (
     "rss_csv_hash_file", "rss_host_alloc", "rss_host_free", "rss_hash_host_multi",
     "rss_pcap_parse6", "rss_hash6_device_reta", "rss_hash6_host_reta", "rss_csv_parse6",
     "rss_csv_format6_bound", "rss_csv_format6", "rss_csv6_hash_text", "rss_csv6_hash_file",
+    "rss_counts_workspace_bytes", "rss_hash_device_ws",
 )
 FIELD_SRC_IP, FIELD_DST_IP, FIELD_SRC_PORT, FIELD_DST_PORT = 1, 2, 4, 8
 FIELDS_IP, FIELDS_ALL = 3, 15
@@ -90,6 +91,8 @@ def _bind(lib):
         "rss_key_prepare": ([ctypes.POINTER(ctypes.c_uint8), sz, key_p], ctypes.c_int),
         "rss_device_count": ([ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
         "rss_hash_device": ([key_p, vp, sz, u32, u32, vp, vp, vp, u32, vp], ctypes.c_int),
+        "rss_hash_device_ws": ([key_p, vp, sz, u32, u32, vp, vp, vp, u32, vp, vp], ctypes.c_int),
+        "rss_counts_workspace_bytes": ([u32, ctypes.POINTER(sz)], ctypes.c_int),
         "rss_generate_tuples": ([u64, u64, sz, vp, vp], ctypes.c_int),
         "rss_ctx_create": ([ctypes.c_int, ctypes.POINTER(vp)], ctypes.c_int),
         "rss_ctx_destroy": ([vp], None),
@@ -508,12 +511,29 @@ def default_context():
 
 # ------------------------------------------------------- device pointers ----
 def hash_device(key, tuples_ptr, n, htable, nqueues, hash_ptr=None, queue_ptr=None,
-                counts_ptr=None, flags=0, stream=None):
+                counts_ptr=None, flags=0, stream=None, workspace_ptr=None):
     """Stream-ordered ``rss_hash_device`` on raw device pointers (ints); ``counts_ptr``
-    holds ``queue_modulus(htable, nqueues)[1]`` entries."""
+    holds ``queue_modulus(htable, nqueues)[1]`` entries.  With ``workspace_ptr`` (a zeroed
+    device buffer of :func:`counts_workspace_bytes` bytes, one launch at a time) the
+    launch is ``rss_hash_device_ws``: single-pass counts, no zeroing launch before it."""
     htable, nqueues = queue_modulus(htable, nqueues)
-    _check(load().rss_hash_device(ctypes.byref(key), tuples_ptr, n, htable, nqueues, hash_ptr,
-                                  queue_ptr, counts_ptr, flags, stream), "rss_hash_device")
+    if workspace_ptr is None:
+        _check(load().rss_hash_device(ctypes.byref(key), tuples_ptr, n, htable, nqueues,
+                                      hash_ptr, queue_ptr, counts_ptr, flags, stream),
+               "rss_hash_device")
+    else:
+        _check(load().rss_hash_device_ws(ctypes.byref(key), tuples_ptr, n, htable, nqueues,
+                                         hash_ptr, queue_ptr, counts_ptr, flags, workspace_ptr,
+                                         stream), "rss_hash_device_ws")
+
+
+def counts_workspace_bytes(htable, nqueues):
+    """Bytes of the single-pass counts workspace of ``rss_hash_device_ws`` for (H, Q)."""
+    nqueues = queue_modulus(htable, nqueues)[1]
+    out = ctypes.c_size_t()
+    _check(load().rss_counts_workspace_bytes(nqueues, ctypes.byref(out)),
+           "rss_counts_workspace_bytes")
+    return out.value
 
 
 def hash_device_reta(key, tuples_ptr, n, htable, reta, nqueues, hash_ptr=None, queue_ptr=None,

@@ -91,6 +91,8 @@ struct LaunchParams {
     uint32_t* hash_out;
     void* queue_out;
     unsigned long long* counts;
+    unsigned long long* ws;       // single-pass counts workspace (rss_hash_device_ws) or NULL
+    uint32_t accumulate;          // with ws: add into counts instead of overwriting them
     uint64_t n;
     uint64_t h_m64;     // ceil(2^64 / H) for the non-power-of-two htable path
     uint32_t h_mask;    // H - 1 when H is a power of two
@@ -294,6 +296,50 @@ __device__ __forceinline__ void store_queue4(void* out, uint64_t g, uint32_t q0,
     }
 }
 
+// Fold a workgroup's per-queue totals (`sum_of(q)`, q < Q) into the global uint64 counts.
+// Without a workspace: one atomicAdd per non-zero total (counts zeroed by the caller or by
+// a hipMemsetAsync before the launch).  With one (rss_hash_device_ws, single-pass counts):
+// the totals go into the accumulator ws[1..Q]; the workgroup then takes a ticket (ws[0]),
+// and the last of the gridDim.x workgroups moves the accumulated sums into `counts`
+// (overwriting, or adding when `accumulate`) and leaves the workspace zero for the next
+// launch -- so a batch's counts need no zeroing launch before it.  `flag` is one LDS word
+// the caller no longer reads (its bins, after every lane has summed them).
+// Ordering without fences: device-scope atomics are all performed at one coherence point,
+// and every lane waits for its adds' return values (the asm use below) before the barrier
+// that precedes the ticket, so a ticket is taken only after its workgroup's adds are
+// performed, and the last workgroup's exchanges read every add.  (An agent-scope
+// __threadfence here costs an L2 write-back per workgroup: +90 us per 2^28-tuple launch.)
+template <typename SumOf>
+__device__ __forceinline__ void fold_counts(SumOf sum_of, uint32_t Q, unsigned long long* counts,
+                                            unsigned long long* ws, bool accumulate,
+                                            uint32_t* flag) {
+    const uint32_t tid = threadIdx.x;
+    if (!ws) {
+        for (uint32_t q = tid; q < Q; q += blockDim.x) {
+            const uint32_t s = sum_of(q);
+            if (s) atomicAdd(&counts[q], (unsigned long long)s);
+        }
+        return;
+    }
+    for (uint32_t q = tid; q < Q; q += blockDim.x) {
+        const uint32_t s = sum_of(q);
+        if (s) {
+            const unsigned long long old = atomicAdd(&ws[1 + q], (unsigned long long)s);
+            asm volatile("" ::"v"((uint32_t)old));  // wait for the performed add
+        }
+    }
+    __syncthreads();   // every lane's adds performed, every lane done reading the bins
+    if (tid == 0) *flag = atomicAdd(&ws[0], 1ull) == (unsigned long long)gridDim.x - 1;
+    __syncthreads();
+    if (*flag) {       // uniform across the workgroup
+        for (uint32_t q = tid; q < Q; q += blockDim.x) {
+            const unsigned long long v = atomicExch(&ws[1 + q], 0ull);  // read + reset
+            counts[q] = accumulate ? counts[q] + v : v;
+        }
+        if (tid == 0) atomicExch(&ws[0], 0ull);
+    }
+}
+
 template <bool kHPow2, int kQMode, int kHist, int kQWidth>
 __device__ __forceinline__ void one_tuple(const uint32_t* lut, uint32_t* bins, uint64_t i,
                                           uint32_t col, uint32_t hi, const uint32_t* reta_lds,
@@ -366,17 +412,16 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
     // Epilogue: fold this workgroup's bins into the global uint64 counts.
     if constexpr (kHist == HIST_PRIVATE || kHist == HIST_SHARED) {
         __syncthreads();
-        for (uint32_t q = tid; q < p.Q; q += kBlock) {
-            uint32_t s;
+        fold_counts([&](uint32_t q) {
             if constexpr (kHist == HIST_PRIVATE) {
-                s = 0;
+                uint32_t s = 0;  // rotated column order: conflict-free
                 for (uint32_t c = 0; c < kBinCols; ++c)
                     s += bins[q * kBinCols + ((c + q) & (kBinCols - 1))];
+                return s;
             } else {
-                s = bins[q];
+                return bins[q];
             }
-            if (s) atomicAdd(&p.counts[q], (unsigned long long)s);
-        }
+        }, p.Q, p.counts, p.ws, p.accumulate != 0, bins);
     } else if constexpr (kHist == HIST_RANGE) {
         __syncthreads();
         for (uint32_t r = tid; r < p.q_span; r += kBlock)
@@ -447,6 +492,8 @@ struct PermParams {
     static constexpr int kFields = kWords * 12;  // three fields per input byte
     const uint32_t* tuples;  // kWords words per tuple
     unsigned long long* counts;
+    unsigned long long* ws;  // single-pass counts workspace or NULL (fold_counts)
+    uint32_t accumulate;
     uint64_t n;
     uint32_t Q;
     uint32_t q_mask;    // QM_MASK
@@ -539,11 +586,11 @@ __global__ __launch_bounds__(kBlock, 2) void rss_counts_perm_kernel(const PermPa
         perm_count(bins, perm_queue<kQMode>(perm_buckets(p, w) & 0xFFu, p), col);
     }
     __syncthreads();
-    for (uint32_t q = tid; q < p.Q; q += kBlock) {  // rotated reads: conflict-free
+    fold_counts([&](uint32_t q) {  // rotated reads: conflict-free
         uint32_t s = 0;
         for (uint32_t c = 0; c < kBinCols; ++c) s += bins[q * kBinCols + ((c + q) & (kBinCols - 1))];
-        if (s) atomicAdd(&p.counts[q], (unsigned long long)s);
-    }
+        return s;
+    }, p.Q, p.counts, p.ws, p.accumulate != 0, bins);
 }
 
 // Key search: per-queue counts of the same tuples under many
@@ -1348,11 +1395,14 @@ bool counts_perm_enabled() {
 template <int kWords>
 int launch_counts_perm(const uint32_t* window, const void* tuples, uint64_t n, unsigned long long* counts,
                        uint32_t h_mask, uint32_t Q, uint32_t q_mask, uint32_t q_m16, int qmode,
-                       uint32_t bin_bytes, int cu_count, hipStream_t stream) {
+                       uint32_t bin_bytes, int cu_count, hipStream_t stream,
+                       unsigned long long* ws = nullptr, bool accumulate = false) {
     PermParams<kWords> pp;
     memset(&pp, 0, sizeof pp);
     pp.tuples = static_cast<const uint32_t*>(tuples);
     pp.counts = counts;
+    pp.ws = ws;
+    pp.accumulate = accumulate;
     pp.n = n;
     pp.Q = Q;
     pp.q_mask = q_mask;
@@ -1402,9 +1452,13 @@ int launch_queue_ranges(const void* qcol, int qw, uint64_t n, uint32_t span, uin
     return RSS_OK;
 }
 
+// ws: rss_hash_device_ws's single-pass counts workspace, or NULL (counts zeroed by a
+// hipMemsetAsync unless RSS_FLAG_ACCUMULATE).  Used when the launch histograms in LDS bins
+// (private or shared); the many-queues range passes ignore it and zero the counts as before.
 int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32_t htable,
                 uint32_t nqueues, uint32_t* d_hash, void* d_queue, uint64_t* d_counts,
-                uint32_t flags, hipStream_t stream, const uint32_t* reta = nullptr) {
+                uint32_t flags, hipStream_t stream, const uint32_t* reta = nullptr,
+                uint64_t* ws = nullptr) {
     if (!key) return set_error(RSS_EINVAL, "rss_hash_device: key is NULL");
     if (key->len < RSS_KEY_MIN_BYTES)
         return set_error(RSS_EINVAL, "rss_hash_device: key not prepared (len=%u)", key->len);
@@ -1426,12 +1480,19 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
             return set_error(RSS_EINVAL, "rss_hash_device: RSS_FLAG_QUEUE_U16 needs nqueues <= 65536");
         qwidth = QW_U16;
     }
-    if (d_counts && !(flags & RSS_FLAG_ACCUMULATE))
+    LaunchParams p;
+    memset(&p, 0, sizeof p);
+    int qmode, hist;
+    uint32_t bin_bytes;
+    const uint32_t reta_bytes = reta ? htable * 4 : 0;
+    const bool h_pow2 = setup_modes(&p, htable, nqueues, d_counts != nullptr, &qmode, &hist,
+                                    &bin_bytes, kBinBytesMax - reta_bytes);
+    // single pass: the kernel's last workgroup writes the counts (fold_counts)
+    const bool single_pass = ws && d_counts && n > 0 && (hist == HIST_PRIVATE || hist == HIST_SHARED);
+    if (d_counts && !(flags & RSS_FLAG_ACCUMULATE) && !single_pass)
         RSS_HIP_CHECK(hipMemsetAsync(d_counts, 0, sizeof(uint64_t) * nqueues, stream));
     if (n == 0) return RSS_OK;
 
-    LaunchParams p;
-    memset(&p, 0, sizeof p);
     memcpy(p.window, key->window, sizeof p.window);
     p.tuples = d_tuples;
     p.hash_out = d_hash;
@@ -1439,11 +1500,10 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
 
     p.counts = reinterpret_cast<unsigned long long*>(d_counts);
     p.n = n;
-    int qmode, hist;
-    uint32_t bin_bytes;
-    const uint32_t reta_bytes = reta ? htable * 4 : 0;
-    const bool h_pow2 = setup_modes(&p, htable, nqueues, d_counts != nullptr, &qmode, &hist,
-                                    &bin_bytes, kBinBytesMax - reta_bytes);
+    if (single_pass) {
+        p.ws = reinterpret_cast<unsigned long long*>(ws);
+        p.accumulate = (flags & RSS_FLAG_ACCUMULATE) ? 1u : 0u;
+    }
     if (reta) {
         qmode = QM_TABLE;
         for (uint32_t b = 0; b < htable; ++b) p.reta[b] = (uint16_t)reta[b];
@@ -1460,7 +1520,8 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
         hist == HIST_PRIVATE && (qmode == QM_MASK || qmode == QM_FAST8) && aligned16(d_tuples) &&
         counts_perm_enabled())
         return launch_counts_perm<3>(key->window, d_tuples, n, p.counts, p.h_mask, p.Q, p.q_mask,
-                                     p.q_m16, qmode, bin_bytes, info.cu_count, stream);
+                                     p.q_m16, qmode, bin_bytes, info.cu_count, stream, p.ws,
+                                     p.accumulate != 0);
     // More queues than LDS bins: count them in ranges.  The first pass runs the hash kernel
     // with shared LDS bins for queues [0, span) and writes the per-tuple outputs -- the
     // queue column into the caller's buffer or, for a counts-only launch, into a stream-
@@ -1828,6 +1889,22 @@ int rss_hash_device(const rss_key* key, const rss_tuple4* d_tuples, size_t n, ui
                     uint32_t flags, void* stream) {
     return launch_hash(key, d_tuples, n, htable, nqueues, d_hash, d_queue, d_counts, flags,
                        static_cast<hipStream_t>(stream));
+}
+
+int rss_counts_workspace_bytes(uint32_t nqueues, size_t* out) {
+    if (!out) return set_error(RSS_EINVAL, "rss_counts_workspace_bytes: NULL argument");
+    if (nqueues < 1) return set_error(RSS_EINVAL, "rss_counts_workspace_bytes: nqueues must be >= 1");
+    *out = sizeof(uint64_t) * ((size_t)nqueues + 1);  // ticket + one accumulator per queue
+    return RSS_OK;
+}
+
+int rss_hash_device_ws(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32_t htable,
+                       uint32_t nqueues, uint32_t* d_hash, void* d_queue, uint64_t* d_counts,
+                       uint32_t flags, uint64_t* d_workspace, void* stream) {
+    if (d_counts && (!d_workspace || ((uintptr_t)d_workspace & 7u)))
+        return set_error(RSS_EINVAL, "rss_hash_device_ws: workspace NULL or not 8-byte aligned");
+    return launch_hash(key, d_tuples, n, htable, nqueues, d_hash, d_queue, d_counts, flags,
+                       static_cast<hipStream_t>(stream), nullptr, d_workspace);
 }
 
 int rss_hash_device_reta(const rss_key* key, const rss_tuple4* d_tuples, size_t n,

@@ -68,17 +68,31 @@ def hash_shard(key, tuples, n, htable, nqueues, hashes=None, queues=None, counts
 
 class CountsPipeline:
     """Per-step histograms of a rank that hashes batch after batch (a weak-scaling job, a
-    service): step i zeroes count buffer ``i % 2``, enqueues the hash into it and issues
-    the all-reduce of that buffer asynchronously, so it overlaps step i+1's hash, which
-    writes the other buffer; a buffer's previous all-reduce is waited for before it is
-    reused.  Without a process group the collective is skipped (counts are the rank's).
+    service): step i produces its counts in buffer ``i % 2`` and issues the all-reduce of
+    that buffer asynchronously, so it overlaps step i+1's hash, which writes the other
+    buffer; a buffer's previous all-reduce is waited for before it is reused.  Without a
+    process group the collective is skipped (counts are the rank's).
 
-    ``launch(counts)`` enqueues one hash pass that accumulates into ``counts`` (int64
-    tensor of ``nqueues``) on the caller's stream.
+    Two ways to start a step's counts from zero:
+
+    * ``single_pass=True`` (default on a GPU): ``launch(counts, workspace)`` enqueues one
+      ``rss_hash_device_ws`` launch that overwrites ``counts`` itself -- the kernel's last
+      workgroup writes them from the zero-initialised ``workspace`` (int64 tensor of
+      ``nqueues + 1``, shared by the steps: their launches run one after another on the
+      caller's stream) -- so a step is one kernel launch and no zeroing launch;
+    * ``single_pass=False``: the pipeline zeroes ``counts`` and ``launch(counts)``
+      enqueues one pass that accumulates into them.
+
+    ``counts`` is an int64 tensor of ``nqueues``.
     """
 
-    def __init__(self, nqueues, device, group=None):
+    def __init__(self, nqueues, device, group=None, single_pass=None):
+        device = torch.device(device)
         self.buffers = [torch.zeros(nqueues, dtype=torch.int64, device=device) for _ in range(2)]
+        if single_pass is None:
+            single_pass = device.type == "cuda"
+        self.workspace = (torch.zeros(nqueues + 1, dtype=torch.int64, device=device)
+                          if single_pass else None)
         self.pending = [None, None]
         self.group = group
         self.steps = 0
@@ -89,8 +103,11 @@ class CountsPipeline:
             self.pending[b].wait()  # buffer b's previous all-reduce must finish before reuse
             self.pending[b] = None
         counts = self.buffers[b]
-        counts.zero_()
-        launch(counts)
+        if self.workspace is not None:
+            launch(counts, self.workspace)
+        else:
+            counts.zero_()
+            launch(counts)
         self.pending[b] = allreduce_counts(counts, self.group, async_op=True)
         self.steps += 1
         return counts
