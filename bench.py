@@ -362,7 +362,8 @@ def main():
     # zeroing launch before it; --zero-counts = counts.zero_() + an accumulating launch
     pipeline = CountsPipeline(Q, dev, single_pass=not args.zero_counts)
 
-    def launch(c, ws=None):
+    def launch(c, workspace=None):
+        ws = workspace
         _native.hash_device(key, tuples.data_ptr(), n, H, Q, hashes.data_ptr(), queues.data_ptr(),
                             c.data_ptr(), qflag | (0 if ws is not None else _native.FLAG_ACCUMULATE),
                             torch.cuda.current_stream(dev).cuda_stream,
@@ -374,26 +375,26 @@ def main():
             side = torch.cuda.Stream(dev)
             side.wait_stream(stream)
             with torch.cuda.stream(side):
-                launch(pipeline.buffers[0], pipeline.workspace)
+                launch(pipeline.buffers[0], workspace=pipeline.workspace)
             stream.wait_stream(side)
             graphs = {}
             for c in pipeline.buffers:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
-                    launch(c, pipeline.workspace)
+                    launch(c, workspace=pipeline.workspace)
                 graphs[c.data_ptr()] = g
         except Exception as err:  # eager fallback keeps the same work per step
             print("bench: graph capture unavailable (%s); launching eagerly" % err, file=sys.stderr)
             graphs = None
 
     def step(i, ev=None):
-        def timed_launch(c, ws=None):
+        def timed_launch(c, workspace=None):
             if ev is not None:
                 ev[0].record(stream)
             if graphs is not None:
                 graphs[c.data_ptr()].replay()
             else:
-                launch(c, ws)
+                launch(c, workspace)
             if ev is not None:
                 ev[1].record(stream)
         pipeline.step(timed_launch)

@@ -60,6 +60,9 @@ class ResidentBatch:
         self.stream = stream or torch.cuda.current_stream(self.device)
         self._fill = fill or (lambda t: None)
         self._probe_counts = torch.zeros(self.counts_len, dtype=torch.int64, device=self.device)
+        # single-pass counts workspace of this batch's launches (rss_hash_device_ws; they all
+        # run in order on self.stream, so one suffices)
+        self.workspace = torch.zeros(self.counts_len + 1, dtype=torch.int64, device=self.device)
         n_in, n_out = placement
         self.tuples, self.hashes, self.queues, self.report = choose_stream_buffers(
             torch, self.device, self.n, self._fill, self._probe, n_inputs=n_in,
@@ -67,12 +70,13 @@ class ResidentBatch:
         if n_in * n_out == 1:
             self.report["chosen"] = "first allocation"
 
-    def _launch(self, tuples, hashes, queues, counts, flags):
+    def _launch(self, tuples, hashes, queues, counts, flags, workspace=None):
         _native.hash_device(self.key, tuples.data_ptr(), self.n, self.htable, self.nqueues,
                             hashes.data_ptr() if hashes is not None else None,
                             queues.data_ptr() if queues is not None else None,
                             counts.data_ptr() if counts is not None else None,
-                            flags, self.stream.cuda_stream)
+                            flags, self.stream.cuda_stream,
+                            workspace.data_ptr() if workspace is not None else None)
 
     def _probe(self, tuples, hashes, queues, events):
         if events is not None:
@@ -82,13 +86,18 @@ class ResidentBatch:
         if events is not None:
             events[1].record(self.stream)
 
-    def hash(self, counts=None, accumulate=False, outputs=True):
+    def hash(self, counts=None, accumulate=False, outputs=True, workspace=None):
         """Enqueue one pass over the resident batch on :attr:`stream`: ``hashes`` /
         ``queues`` (when ``outputs``) and ``counts`` (int64[counts_len]; summed into when
-        ``accumulate``, else overwritten).  Returns ``counts``."""
+        ``accumulate``, else overwritten).  Counts are single-pass (``rss_hash_device_ws``:
+        one launch, no zeroing launch before it) on ``workspace`` -- a zeroed int64 tensor of
+        ``counts_len + 1`` no other launch uses at the same time -- or on the batch's own
+        :attr:`workspace`.  Returns ``counts``."""
         flags = QUEUE_FLAGS[self.queue_width] | (_native.FLAG_ACCUMULATE if accumulate else 0)
         self._launch(self.tuples, self.hashes if outputs else None,
-                     self.queues if outputs else None, counts, flags)
+                     self.queues if outputs else None, counts, flags,
+                     (workspace if workspace is not None else self.workspace)
+                     if counts is not None else None)
         return counts
 
     def queue_view(self):

@@ -75,7 +75,7 @@ class CountsPipeline:
 
     Two ways to start a step's counts from zero:
 
-    * ``single_pass=True`` (default on a GPU): ``launch(counts, workspace)`` enqueues one
+    * ``single_pass=True`` (default on a GPU): ``launch(counts, workspace=ws)`` enqueues one
       ``rss_hash_device_ws`` launch that overwrites ``counts`` itself -- the kernel's last
       workgroup writes them from the zero-initialised ``workspace`` (int64 tensor of
       ``nqueues + 1``, shared by the steps: their launches run one after another on the
@@ -104,7 +104,7 @@ class CountsPipeline:
             self.pending[b] = None
         counts = self.buffers[b]
         if self.workspace is not None:
-            launch(counts, self.workspace)
+            launch(counts, workspace=self.workspace)
         else:
             counts.zero_()
             launch(counts)

@@ -32,8 +32,9 @@ def test_counts_pipeline_steps_equal_oracle(oracle_lib, example_key, single_pass
     for i in range(11):
         tup, want = batches[i % 4]
         if single_pass:  # rss_hash_device_ws overwrites the buffer: no zeroing launch
-            launch = lambda counts, ws, tup=tup: _native.hash_device(  # noqa: E731
-                key, tup.data_ptr(), n, H, Q, None, None, counts.data_ptr(), 0, s, ws.data_ptr())
+            launch = lambda counts, workspace, tup=tup: _native.hash_device(  # noqa: E731
+                key, tup.data_ptr(), n, H, Q, None, None, counts.data_ptr(), 0, s,
+                workspace.data_ptr())
         else:
             launch = lambda counts, tup=tup: _native.hash_device(  # noqa: E731
                 key, tup.data_ptr(), n, H, Q, None, None, counts.data_ptr(),

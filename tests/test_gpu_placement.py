@@ -77,6 +77,31 @@ def test_resident_batch_equals_oracle(oracle_lib, example_key, width, placement)
         qv = qv.view({1: np.uint8, 2: np.uint16, 4: np.uint32}[qv.itemsize])
         np.testing.assert_array_equal(qv.astype(np.uint32), q)
         np.testing.assert_array_equal(counts.cpu().numpy().view(np.uint64), 2 * c)
+    assert int(batch.workspace.abs().sum()) == 0  # single-pass workspace left zero
+
+
+def test_counts_pipeline_steps_a_resident_batch(oracle_lib, example_key):
+    """INTEGRATION.md's loop: ``CountsPipeline.step(batch.hash)`` -- single-pass counts on the
+    pipeline's workspace, batch after batch -- gives each batch's oracle counts."""
+    from rss_simulator_nvidia_amd import _native
+    from rss_simulator_nvidia_amd.resident import ResidentBatch
+    from rss_simulator_nvidia_amd.sharding import CountsPipeline
+    n, H, Q = (1 << 18) + 3, 128, 24
+    dev = torch.device("cuda:0")
+    key = _native.prepare_key(example_key)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    batch = ResidentBatch(n, key, H, Q, device=dev, placement=(1, 2))
+    pipe = CountsPipeline(Q, dev)
+    assert pipe.workspace is not None
+    for first in (0, n, 2 * n, 0):
+        _native.generate_device(11, first, n, batch.tuples.data_ptr(), s)
+        counts = pipe.step(batch.hash)
+        torch.cuda.synchronize()
+        want = oracle_lib.run(example_key, oracle_lib.generate(11, first, n), H, Q,
+                              want_hash=False, want_queue=False)[2]
+        np.testing.assert_array_equal(counts.cpu().numpy().view(np.uint64), want)
+    np.testing.assert_array_equal(pipe.drain().cpu().numpy().view(np.uint64), want)
+    assert int(pipe.workspace.abs().sum()) == 0
 
 
 
