@@ -60,6 +60,9 @@ def parse_args():
     p.add_argument("--zero-counts", action="store_true",
                    help="zero each step's counts with a separate launch (counts.zero_() + an "
                         "accumulating rss_hash_device) instead of single-pass counts")
+    p.add_argument("--settle-ms", type=float, default=600,
+                   help="untimed launches of the step for this long before the warmup steps "
+                        "(clock settle; 0 = none)")
     p.add_argument("--graph", action="store_true",
                    help="replay each step as a captured HIP graph (measured: no gain over "
                         "eager launches at 2**28 tuples per step)")
@@ -402,18 +405,38 @@ def main():
     def drain():
         return pipeline.drain()
 
+    # Clock settle (untimed, rank-local, no collective): the first ~0.4 s of back-to-back
+    # launches run ~0.8 % slower than sustained ones, and a box left idle for 0.3 s drops
+    # back (tools/drift_probe.py, profiles/r02/drift_probe.jsonl) -- a service hashing batch
+    # after batch runs in the settled state, so the timed steps should too.
+    settle_launches, t_settle = 0, time.perf_counter()
+    while args.settle_ms > 0:
+        for _ in range(16):
+            _native.hash_device(key, tuples.data_ptr(), n, H, Q, hashes.data_ptr(),
+                                queues.data_ptr(), counts.data_ptr(),
+                                _native.FLAG_ACCUMULATE | qflag, sp)
+        settle_launches += 16
+        torch.cuda.synchronize()
+        if time.perf_counter() - t_settle >= args.settle_ms / 1e3:
+            break
+    settle_s = time.perf_counter() - t_settle
+
     for i in range(args.warmup):
         step(i)
     drain()
     barrier()
     torch.cuda.synchronize()
-    # HIP events on the launch stream bracket every timed hash launch: roofline.achieved
-    # is the algorithmic bytes over the mean launch time inside the timed region
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(args.steps)]
+    # One pair of HIP events on the launch stream brackets the K timed launches:
+    # roofline.achieved = algorithmic bytes over that GPU time per step (the launches plus
+    # the gaps between them -- no per-launch events inside the timed region: a pair around
+    # every launch costs ~7 us per step, profiles/r02/drift_probe.jsonl).  The per-launch
+    # spread comes from K event-bracketed launches after the timed region.
+    region = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     t0 = time.perf_counter()
+    region[0].record(stream)
     for i in range(args.steps):
-        step(i, events[i])
+        step(i)
+    region[1].record(stream)
     last = drain()
     torch.cuda.synchronize()
     barrier()
@@ -445,8 +468,16 @@ def main():
     total = int(last.sum().item())
     if total != n * world:
         raise SystemExit("bench: per-queue counts sum to %d, expected %d" % (total, n * world))
-    launch_ms = [a.elapsed_time(b) for a, b in events]
-    kernel_ms = sum(launch_ms) / len(launch_ms)
+    kernel_ms = region[0].elapsed_time(region[1]) / args.steps
+    # per-launch spread: K launches of the same step, each bracketed by its own events
+    spread_ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                 for _ in range(args.steps)]
+    for e in spread_ev:
+        e[0].record(stream)
+        launch(counts, workspace=pipeline.workspace)
+        e[1].record(stream)
+    torch.cuda.synchronize()
+    launch_ms = sorted(a.elapsed_time(b) for a, b in spread_ev)
     stats = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
     if distributed:
         dist.all_reduce(stats, op=dist.ReduceOp.MAX)
@@ -566,11 +597,15 @@ def main():
                 "kernel_ms": kernel_ms_max,
                 "kernel_ms_rank0": kernel_ms,
                 "kernel_ms_max_rank": kernel_ms_max,
-                "kernel_ms_min_max": [min(launch_ms), max(launch_ms)],
-                "kernel_ms_median": sorted(launch_ms)[len(launch_ms) // 2],
-                "timing": "HIP events around each of the %d timed launches (launch stream); "
-                          "achieved uses the slowest rank's mean (kernel_ms_max_rank)"
-                          % args.steps,
+                "kernel_ms_min_max": [launch_ms[0], launch_ms[-1]],
+                "kernel_ms_median": launch_ms[len(launch_ms) // 2],
+                "kernel_ms_events_mean": sum(launch_ms) / len(launch_ms),
+                "timing": "kernel_ms = GPU time per step on the launch stream: one pair of HIP "
+                          "events around the %d timed launches (launches + the gaps between "
+                          "them), slowest rank (kernel_ms_max_rank); min_max / median / "
+                          "events_mean: %d launches each bracketed by HIP events, after the "
+                          "timed region"
+                          % (args.steps, args.steps),
             },
             # the HBM-read roofline is the counts-only mode's bound (12 B read
             # per tuple, 666.7 G tuples/s per GPU); the full-output `value` also writes
@@ -600,6 +635,9 @@ def main():
             "cpu_baseline": baseline,
         }
         line["secondary_min_median_max_ms"] = secondary_spread
+        line["settle"] = {"launches": settle_launches, "s": round(settle_s, 3),
+                          "note": "untimed launches of the step before the warmup steps "
+                                  "(--settle-ms; clock settle, rank-local)"}
         line["placement"] = dict(placement, first_allocation_tuples_per_s_per_gpu=n / (
             placement["first_allocation_ms"] / 1e3),
             note="resident buffers chosen among the probed candidate allocations before the "

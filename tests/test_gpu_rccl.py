@@ -101,7 +101,9 @@ def test_bench_under_torchrun_nproc1_reports_baseline_and_roofline(tmp_path):
     assert "RCCL all-reduce" in rec["config"]["parallelism"]
     base = rec["cpu_baseline"]
     assert base is not None and base["value"] > 0 and base["cores"] == 2
+    assert rec["settle"]["launches"] >= 16  # clock-settle launches before the warmup
     roof = rec["roofline"]
     assert roof["kernel_ms"] == roof["kernel_ms_max_rank"]
+    assert roof["kernel_ms_min_max"][0] <= roof["kernel_ms_median"] <= roof["kernel_ms_min_max"][1]
     want = (1 << 22) * roof["bytes_per_tuple"] / (roof["kernel_ms_max_rank"] / 1e3) / 1e9
     assert abs(roof["achieved"] - want) < 1e-6 * want

@@ -6,7 +6,8 @@ probe's launches on all candidate buffers, the warmup, the timed steps and the s
 lines.  The bench's ``roofline.kernel_ms`` is the mean over the K timed launches, so the
 comparable profiler figure is the mean duration of exactly those dispatches.  With the bench
 line of the same profiled run (``prof.log``), the full-output kernel's dispatches are, in
-order: the probe (inputs x outputs x (3 warm + 5 timed)), W warmup steps, K timed steps.
+order: the probe (inputs x outputs x (3 warm + 5 timed)), the clock-settle launches
+(``settle.launches``), W warmup steps, K timed steps.
 
     python tools/prof_timed.py TRACE_CSV PROF_LOG > summary.json
 """
@@ -28,6 +29,7 @@ def main(trace_path, log_path):
     cand = line["placement"]["candidates"]
     probe = cand["inputs"] * cand["outputs"] * PROBE_LAUNCHES
     w, k = line["warmup"], line["steps"]
+    probe += line.get("settle", {}).get("launches", 0)
     name = "rss_toeplitz_kernel<true, 4, 0, 2, true>"  # full output, u8 queues
     durs = []
     with open(trace_path) as f:
@@ -43,7 +45,7 @@ def main(trace_path, log_path):
     out = {
         "kernel": name,
         "launches_in_trace": len(durs),
-        "probe_launches": probe, "warmup": w, "timed": k,
+        "probe_and_settle_launches": probe, "warmup": w, "timed": k,
         "rocprof_timed_mean_ms": mean_ms,
         "rocprof_timed_min_max_ms": [min(timed) / 1e6, max(timed) / 1e6],
         "bench_kernel_ms_same_run": line["roofline"]["kernel_ms"],
