@@ -60,6 +60,11 @@ def parse_args():
     p.add_argument("--zero-counts", action="store_true",
                    help="zero each step's counts with a separate launch (counts.zero_() + an "
                         "accumulating rss_hash_device) instead of single-pass counts")
+    p.add_argument("--allreduce", choices=["overlap", "stream", "rccl"], default="rccl",
+                   help="per-step count all-reduce (sharding.CountsPipeline): torch.distributed "
+                        "async on its own stream (overlap), torch.distributed stream-ordered "
+                        "(stream), or ncclAllReduce through rccl.RcclComm on the launch stream "
+                        "(rccl)")
     p.add_argument("--settle-ms", type=float, default=600,
                    help="untimed launches of the step for this long before the warmup steps "
                         "(clock settle; 0 = none)")
@@ -363,7 +368,18 @@ def main():
     from rss_simulator_nvidia_amd.sharding import CountsPipeline
     # Single-pass counts (rss_hash_device_ws): the launch writes the step's counts itself, no
     # zeroing launch before it; --zero-counts = counts.zero_() + an accumulating launch
-    pipeline = CountsPipeline(Q, dev, single_pass=not args.zero_counts)
+    comm = None
+    if distributed and args.allreduce == "rccl" and args.dist_backend != "nccl":
+        args.allreduce = "overlap"  # the gloo rehearsal: torch.distributed's exchange
+    if distributed and args.allreduce == "rccl":
+        from rss_simulator_nvidia_amd.rccl import RcclComm, RcclError
+        try:
+            comm = RcclComm(dev)
+        except RcclError as err:  # keep the run: torch.distributed's exchange instead
+            print("bench: RcclComm unavailable (%s); --allreduce overlap" % err, file=sys.stderr)
+            args.allreduce = "overlap"
+    pipeline = CountsPipeline(Q, dev, single_pass=not args.zero_counts,
+                              allreduce=args.allreduce if distributed else "overlap", comm=comm)
 
     def launch(c, workspace=None):
         ws = workspace
@@ -576,9 +592,14 @@ def main():
                 "htable": H,
                 "queues": Q,
                 "queue_width": qw,
-                "parallelism": ("tuple-sharded x%d, %s all-reduce of uint64[%d] counts "
-                                "(async, overlapped with the next step)"
-                                % (world, "RCCL" if args.dist_backend == "nccl" else "gloo", Q))
+                "parallelism": ("tuple-sharded x%d, %s all-reduce of uint64[%d] counts %s"
+                                % (world, "RCCL" if args.dist_backend == "nccl" else "gloo", Q,
+                                   {"overlap": "(torch.distributed async, overlapped with the "
+                                               "next step)",
+                                    "stream": "(torch.distributed, stream-ordered after each "
+                                              "step's launch)",
+                                    "rccl": "(ncclAllReduce via rccl.RcclComm, stream-ordered "
+                                            "after each step's launch)"}[args.allreduce]))
                                if distributed else "single process, one GPU (no process group)",
                 "step": ("zero counts + " if args.zero_counts else
                          "single-pass counts (rss_hash_device_ws): ") +
@@ -653,6 +674,9 @@ def main():
         print(json.dumps(line), flush=True)
     if distributed:
         barrier()  # ranks leave together (rank 0 ran the secondary timings alone)
+        if comm is not None:
+            torch.cuda.synchronize()
+            comm.destroy()
         dist.destroy_process_group()
 
 

@@ -2,8 +2,9 @@
 (torch's ``nccl`` backend is RCCL on ROCm) runs every collective the N-GPU bench makes --
 ``init_process_group("nccl", device_id=...)``, the synchronous and the async
 ``all_reduce`` of the ``uint64[Q]`` counts from ``rss_hash_device``, the MAX all-reduce of
-the timings, ``barrier(device_ids=...)`` and ``destroy_process_group`` -- and the reduced
-counts must equal the oracle's.  A second test runs ``bench.py`` itself under
+the timings, ``barrier(device_ids=...)`` and ``destroy_process_group``, and the bench's
+default per-step exchange, ``ncclAllReduce`` through ``rccl.RcclComm`` on the launch stream
+-- and the reduced counts must equal the oracle's.  A second test runs ``bench.py`` itself under
 ``torch.distributed.run --nproc-per-node 1``: its line must carry the CPU baseline and the
 max-over-ranks roofline, as every N > 1 line of the driver's scaling run will.
 
@@ -59,6 +60,25 @@ def _rccl_worker(rank, port, key, n, htable, nqueues, out_dir):
         work = allreduce_counts(counts2, async_op=True)
         assert work is not None
         work.wait()
+        # the bench's default form: ncclAllReduce through rccl.RcclComm on the launch stream,
+        # through CountsPipeline with single-pass counts, batch after batch
+        from rss_simulator_nvidia_amd.rccl import RcclComm
+        from rss_simulator_nvidia_amd.sharding import CountsPipeline
+        comm = RcclComm(dev)
+        assert (comm.rank, comm.world) == (0, 1)
+        pipe = CountsPipeline(nqueues, dev, allreduce="rccl", comm=comm)
+        k = _native.prepare_key(key)
+        for _ in range(5):
+            c3 = pipe.step(lambda c, workspace: _native.hash_device(
+                k, tuples.data_ptr(), n, htable, nqueues, None, None, c.data_ptr(), 0, s,
+                workspace.data_ptr()))
+        c3 = pipe.drain()
+        direct = counts2.clone()
+        comm.all_reduce_counts(direct)
+        torch.cuda.synchronize()
+        comm.destroy()
+        np.save(os.path.join(out_dir, "c3.npy"), c3.cpu().numpy())
+        np.save(os.path.join(out_dir, "c4.npy"), direct.cpu().numpy())
         stats = torch.tensor([1.5, 2.5], dtype=torch.float64, device=dev)
         dist.all_reduce(stats, op=dist.ReduceOp.MAX)
         dist.barrier(device_ids=[0])
@@ -81,6 +101,8 @@ def test_nccl_world1_allreduce_counts_equal_oracle(tmp_path, oracle_lib, example
     np.testing.assert_array_equal(np.load(tmp_path / "h.npy").view(np.uint32), ho)
     np.testing.assert_array_equal(np.load(tmp_path / "c.npy").view(np.uint64), co)
     np.testing.assert_array_equal(np.load(tmp_path / "c2.npy").view(np.uint64), co)
+    np.testing.assert_array_equal(np.load(tmp_path / "c3.npy").view(np.uint64), co)
+    np.testing.assert_array_equal(np.load(tmp_path / "c4.npy").view(np.uint64), co)
     np.testing.assert_array_equal(np.load(tmp_path / "stats.npy"), [1.5, 2.5])
 
 
@@ -99,6 +121,7 @@ def test_bench_under_torchrun_nproc1_reports_baseline_and_roofline(tmp_path):
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 1 and rec["steps"] == 3 and rec["warmup"] == 1
     assert "RCCL all-reduce" in rec["config"]["parallelism"]
+    assert "rccl.RcclComm" in rec["config"]["parallelism"]  # the default per-step exchange
     base = rec["cpu_baseline"]
     assert base is not None and base["value"] > 0 and base["cores"] == 2
     assert rec["settle"]["launches"] >= 16  # clock-settle launches before the warmup

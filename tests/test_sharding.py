@@ -65,12 +65,25 @@ def test_gloo_sharded_counts_equal_single_process(world, tmp_path, oracle_lib, e
         np.testing.assert_array_equal(np.load(tmp_path / ("c%d.npy" % r)).view(np.uint64), c)
 
 
-def _pipeline_worker(rank, world, port, steps, nq, out_dir):
+class _GlooComm:
+    """Stands in for rccl.RcclComm on CPU: the same in-place sum over the default group."""
+
+    def __init__(self):
+        self.calls = 0
+
+    def all_reduce_counts(self, counts, stream=None):
+        self.calls += 1
+        dist.all_reduce(counts)
+        return counts
+
+
+def _pipeline_worker(rank, world, port, steps, nq, out_dir, allreduce="overlap"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from rss_simulator_nvidia_amd.sharding import CountsPipeline
-        pipe = CountsPipeline(nq, "cpu")
+        comm = _GlooComm() if allreduce == "rccl" else None
+        pipe = CountsPipeline(nq, "cpu", allreduce=allreduce, comm=comm)
         seen = []
         for i in range(steps):
             # step i adds (rank + 1) * (i + 1) to every queue of a freshly zeroed buffer
@@ -78,19 +91,23 @@ def _pipeline_worker(rank, world, port, steps, nq, out_dir):
             seen.append(c.data_ptr())
         last = pipe.drain()
         assert len(set(seen)) == min(2, steps) and last.data_ptr() == seen[-1]
+        assert comm is None or comm.calls == steps
         np.save(os.path.join(out_dir, "last%d.npy" % rank), last.numpy())
         np.save(os.path.join(out_dir, "prev%d.npy" % rank), pipe.buffers[steps & 1].numpy())
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,steps", [(2, 5), (3, 4), (2, 1)])
-def test_counts_pipeline_reduces_every_step(world, steps, tmp_path):
-    """CountsPipeline (the bench's step shape): the double-buffered async all-reduce gives
-    each step's counts summed over ranks, the buffer reused two steps later is re-zeroed,
-    and drain() returns the last step's reduced counts."""
+@pytest.mark.parametrize("world,steps,allreduce", [(2, 5, "overlap"), (3, 4, "overlap"),
+                                                   (2, 1, "overlap"), (2, 5, "stream"),
+                                                   (3, 4, "rccl")])
+def test_counts_pipeline_reduces_every_step(world, steps, allreduce, tmp_path):
+    """CountsPipeline (the bench's step shape), with each all-reduce mode: every step's
+    counts summed over ranks, the buffer reused two steps later is re-zeroed, and drain()
+    returns the last step's reduced counts ("rccl" through a stand-in comm over gloo)."""
     nq = 7
-    mp.start_processes(_pipeline_worker, args=(world, _free_port(), steps, nq, str(tmp_path)),
+    mp.start_processes(_pipeline_worker, args=(world, _free_port(), steps, nq, str(tmp_path),
+                                               allreduce),
                        nprocs=world, start_method="spawn")
     ranks = sum(r + 1 for r in range(world))
     for r in range(world):
@@ -99,6 +116,20 @@ def test_counts_pipeline_reduces_every_step(world, steps, tmp_path):
         if steps > 1:
             np.testing.assert_array_equal(np.load(tmp_path / ("prev%d.npy" % r)),
                                           np.full(nq, ranks * (steps - 1)))
+
+
+def test_counts_pipeline_rejects_bad_modes():
+    from rss_simulator_nvidia_amd.sharding import CountsPipeline
+    with pytest.raises(ValueError, match="overlap, stream or rccl"):
+        CountsPipeline(3, "cpu", allreduce="ring")
+    with pytest.raises(ValueError, match="needs comm"):
+        CountsPipeline(3, "cpu", allreduce="rccl")
+
+
+def test_rccl_comm_needs_a_process_group():
+    from rss_simulator_nvidia_amd.rccl import RcclComm, RcclError
+    with pytest.raises(RcclError, match="process group"):
+        RcclComm("cpu")
 
 
 def test_counts_pipeline_without_group_keeps_local_counts():
