@@ -60,6 +60,9 @@ def parse_args():
     p.add_argument("--zero-counts", action="store_true",
                    help="zero each step's counts with a separate launch (counts.zero_() + an "
                         "accumulating rss_hash_device) instead of single-pass counts")
+    p.add_argument("--placement-rounds", type=int, default=3, metavar="R",
+                   help="up to R rounds of --placement-probe more output candidates while no "
+                        "probed set is clearly faster than the rest (no faster tier found)")
     p.add_argument("--allreduce", choices=["overlap", "stream", "rccl"], default="rccl",
                    help="per-step count all-reduce (sharding.CountsPipeline): torch.distributed "
                         "async on its own stream (overlap), torch.distributed stream-ordered "
@@ -356,7 +359,8 @@ def main():
     # (ResidentBatch / placement.py); queue buffers of the queue width (the u32
     # secondary line gets its own buffer after the timed region)
     from rss_simulator_nvidia_amd.resident import ResidentBatch
-    probe = (2, args.placement_probe) if args.placement_probe > 0 else (1, 1)
+    probe = ((2, args.placement_probe, args.placement_rounds) if args.placement_probe > 0
+             else (1, 1))
     batch = ResidentBatch(n, key, H, Q, device=dev, fill=fill_input, queue_width=qw,
                           placement=probe, stream=stream)
     tuples, hashes, queues = batch.tuples, batch.hashes, batch.queues

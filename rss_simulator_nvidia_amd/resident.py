@@ -32,8 +32,9 @@ class ResidentBatch:
     ``fill(tuples)`` (optional) writes the first batch into the int32[3n] input tensor;
     without it the input is left for the caller to write (``batch.tuples``).  The
     candidate inputs are filled the same way before probing, so the probe times the
-    kernel on real data.  ``placement=(inputs, outputs)`` candidate allocations are
-    probed (``(1, 1)`` = no probe: the first allocation, as allocated); ``queue_bytes``
+    kernel on real data.  ``placement=(inputs, outputs[, rounds])`` candidate allocations
+    are probed (``rounds``: up to that many rounds of ``outputs`` more output candidates
+    while none is clearly faster than the rest, placement.choose_stream_buffers) (``(1, 1)`` = no probe: the first allocation, as allocated); ``queue_bytes``
     sizes the queue buffer per tuple (4 holds any width).  ``report`` records the probe.
     """
 
@@ -63,10 +64,11 @@ class ResidentBatch:
         # single-pass counts workspace of this batch's launches (rss_hash_device_ws; they all
         # run in order on self.stream, so one suffices)
         self.workspace = torch.zeros(self.counts_len + 1, dtype=torch.int64, device=self.device)
-        n_in, n_out = placement
+        n_in, n_out = placement[0], placement[1]
+        rounds = placement[2] if len(placement) > 2 else 1
         self.tuples, self.hashes, self.queues, self.report = choose_stream_buffers(
             torch, self.device, self.n, self._fill, self._probe, n_inputs=n_in,
-            n_outputs=n_out, queue_bytes=qbytes)
+            n_outputs=n_out, queue_bytes=qbytes, max_rounds=rounds)
         if n_in * n_out == 1:
             self.report["chosen"] = "first allocation"
 
