@@ -1,4 +1,4 @@
-"""Seeded randomised parity sweep of the device API (rss_hash_device / _reta) against the
+"""Seeded randomised parity sweep of the device API (rss_hash_device / _ws / _reta) against the
 C oracle: random sizes (incl. 0 and ragged tails), power-of-two and arbitrary htable /
 nqueues (every modulo and histogram mode), key lengths 16..52, queue widths u8 / u16 /
 u32, NULL outputs, accumulation into non-zero counts and 4-byte-misaligned tuples.
@@ -72,8 +72,18 @@ def test_random_config_matches_oracle(native, oracle_lib, seed):
                                 flags, stream)
     else:
         reta = None
-        native.hash_device(key, tup_ptr, n, H, Q, h_ptr, q_ptr, counts.data_ptr(), flags, stream)
+        # half the cases as single-pass counts (rss_hash_device_ws; own generator, so the
+        # configurations above stay what they were), the workspace followed by guard words
+        single_pass = bool(np.random.default_rng(5000 + seed).random() < 0.5)
+        ws = torch.zeros(Q + 1 + 8, dtype=torch.int64, device=dev)
+        ws[Q + 1:] = -7
+        native.hash_device(key, tup_ptr, n, H, Q, h_ptr, q_ptr, counts.data_ptr(), flags, stream,
+                           ws.data_ptr() if single_pass else None)
     torch.cuda.synchronize()
+    if reta is None:
+        wsh = ws.cpu().numpy()
+        assert (wsh[:Q + 1] == 0).all(), "workspace not left zero"
+        assert (wsh[Q + 1:] == -7).all(), "workspace written past Q + 1"
 
     eh, eq, ec = oracle_lib.run(c["key"], host, H, Q, threads=8)
     if reta is not None:
