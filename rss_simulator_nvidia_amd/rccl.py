@@ -15,6 +15,7 @@ torch loaded.  The reference is single-process; this module is new.
 """
 import ctypes
 import os
+import threading
 
 import torch
 import torch.distributed as dist
@@ -69,9 +70,15 @@ def _check(rc, what):
 
 class RcclComm:
     """RCCL communicator over the ranks of ``group`` (default: the default group), one GPU
-    (``device``) per rank.  Collective over the group: every rank constructs it."""
+    (``device``) per rank.  Collective over the group: every rank constructs it.
 
-    def __init__(self, device, group=None):
+    ``ncclCommInitRank`` runs on a helper thread and is given ``timeout_s``: a rank whose
+    init has not finished by then (or failed) reports it, the ranks agree over the process
+    group (a MIN all-reduce of the outcome), and if any rank failed every rank raises
+    ``RcclError`` -- so callers fall back together instead of hanging in the bootstrap.
+    """
+
+    def __init__(self, device, group=None, timeout_s=120.0):
         if not (dist.is_available() and dist.is_initialized()):
             raise RcclError("RcclComm needs an initialised torch.distributed process group")
         lib = _library()
@@ -79,18 +86,44 @@ class RcclComm:
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         uid = _UniqueId()
-        if self.rank == 0:
-            _check(lib.ncclGetUniqueId(ctypes.byref(uid)), "ncclGetUniqueId")
-        blob = [ctypes.string_at(ctypes.addressof(uid), 128) if self.rank == 0 else None]
+        blob = [None]
+        if self.rank == 0:  # a failure here still reaches the other ranks (as no id)
+            rc = lib.ncclGetUniqueId(ctypes.byref(uid))
+            blob = [ctypes.string_at(ctypes.addressof(uid), 128) if rc == 0 else ("rc", rc)]
         src = dist.get_global_rank(group, 0) if group is not None else 0
         dist.broadcast_object_list(blob, src=src, group=group, device=self.device)
         if not isinstance(blob[0], bytes) or len(blob[0]) != 128:
-            raise RcclError("bad ncclUniqueId from rank 0")
+            raise RcclError("no ncclUniqueId from rank 0 (%r)" % (blob[0],))
         uid = _UniqueId.from_buffer_copy(blob[0])
-        self._comm = ctypes.c_void_p()
-        with torch.cuda.device(self.device):
-            _check(lib.ncclCommInitRank(ctypes.byref(self._comm), self.world, uid, self.rank),
-                   "ncclCommInitRank")
+        comm = ctypes.c_void_p()
+        result = {}
+
+        def init():
+            try:
+                torch.cuda.set_device(self.device)  # the HIP device is per thread
+                result["rc"] = lib.ncclCommInitRank(ctypes.byref(comm), self.world, uid, self.rank)
+            except Exception as err:  # reported below, on the caller's thread
+                result["err"] = err
+
+        worker = threading.Thread(target=init, name="rccl-init", daemon=True)
+        worker.start()
+        worker.join(timeout_s)
+        if worker.is_alive():
+            why = "ncclCommInitRank did not finish in %.0f s" % timeout_s
+        elif "err" in result:
+            why = "ncclCommInitRank raised %r" % result["err"]
+        elif result.get("rc", -1) != 0:
+            msg = lib.ncclGetErrorString(result["rc"])
+            why = "ncclCommInitRank failed (%d): %s" % (result["rc"], msg.decode() if msg else "?")
+        else:
+            why = None
+        ok = torch.tensor([0 if why else 1], dtype=torch.int32, device=self.device)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)  # every rank's outcome
+        self._comm = comm if why is None else None
+        if int(ok.item()) == 0:
+            if self._comm is not None:
+                self.destroy()
+            raise RcclError(why or "ncclCommInitRank failed on another rank")
 
     def all_reduce_counts(self, counts, stream=None):
         """Sum the int64 (uint64 bit pattern) tensor ``counts`` over the ranks in place,
@@ -106,6 +139,6 @@ class RcclComm:
         return counts
 
     def destroy(self):
-        if self._comm is not None and self._comm.value:
+        if getattr(self, "_comm", None) is not None and self._comm.value:
             _check(_library().ncclCommDestroy(self._comm), "ncclCommDestroy")
         self._comm = None

@@ -139,3 +139,30 @@ def test_counts_pipeline_without_group_keeps_local_counts():
         pipe.step(lambda c, i=i: c.add_(i + 1))
     np.testing.assert_array_equal(pipe.drain().numpy(), [3, 3, 3])
     np.testing.assert_array_equal(pipe.buffers[1].numpy(), [2, 2, 2])
+
+
+def _rccl_fail_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rss_simulator_nvidia_amd.rccl import RcclComm, RcclError
+        try:
+            RcclComm("cpu", timeout_s=30)
+            outcome = "constructed"
+        except RcclError as err:
+            outcome = "RcclError: %s" % err
+        with open(os.path.join(out_dir, "r%d.txt" % rank), "w") as f:
+            f.write(outcome)
+        dist.barrier()  # every rank got here: nobody is left in the bootstrap
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_comm_fails_together_without_a_gpu(tmp_path):
+    """Without a GPU, RcclComm must fail on every rank with RcclError -- whether rank 0's
+    ncclGetUniqueId or the per-rank init fails -- and no rank may hang waiting for another."""
+    world = 2
+    mp.start_processes(_rccl_fail_worker, args=(world, _free_port(), str(tmp_path)),
+                       nprocs=world, start_method="spawn")
+    for r in range(world):
+        assert (tmp_path / ("r%d.txt" % r)).read_text().startswith("RcclError"), r
