@@ -83,6 +83,8 @@ class RcclComm:
             raise RcclError("RcclComm needs an initialised torch.distributed process group")
         lib = _library()
         self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         uid = _UniqueId()
