@@ -252,3 +252,30 @@ def test_workspace_required_with_counts(native, example_key):
         native.hash_device(key, None, 0, 128, 24, None, None, counts.data_ptr(), 0, s,
                            ws.data_ptr() + 4)
     native.hash_device(key, None, 0, 128, 24, None, None, None, 0, s, 0)
+
+
+def test_stress_one_workspace_many_launches(native, oracle_lib, example_key):
+    """1800 back-to-back launches on one workspace over batches of 1000, 2^20 + 3 and 2^22
+    tuples (grids of one and of every CU), with and without per-tuple outputs: every launch's
+    counts exact (``tools/ws_stress.py`` runs the same at 6300 launches)."""
+    H, Q = 128, 24
+    key = native.prepare_key(example_key)
+    s = torch.cuda.current_stream().cuda_stream
+    batches = []
+    for seed, n in ((1, 1000), (2, (1 << 20) + 3), (3, 1 << 22)):
+        host = oracle_lib.generate(seed, 0, n)
+        want = oracle_lib.run(example_key, host, H, Q, want_hash=False, want_queue=False)[2]
+        batches.append((n, torch.from_numpy(host.view(np.int32).reshape(-1)).to(DEV), want))
+    ws = _ws(native, H, Q)
+    h = torch.empty(1 << 22, dtype=torch.int32, device=DEV)
+    outs = torch.zeros((600, Q), dtype=torch.int64, device=DEV)
+    for _ in range(3):
+        for i in range(600):
+            n, t, _ = batches[i % 3]
+            native.hash_device(key, t.data_ptr(), n, H, Q, h.data_ptr() if i % 2 else None, None,
+                               outs[i].data_ptr(), 0, s, ws.data_ptr())
+        got = outs.cpu().numpy().view(np.uint64)
+        for i in range(600):
+            np.testing.assert_array_equal(got[i], batches[i % 3][2])
+        outs.zero_()
+    assert int(ws.abs().sum()) == 0
