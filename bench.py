@@ -68,6 +68,10 @@ def parse_args():
                         "async on its own stream (overlap), torch.distributed stream-ordered "
                         "(stream), or ncclAllReduce through rccl.RcclComm on the launch stream "
                         "(rccl)")
+    p.add_argument("--allreduce-bucket", type=int, default=8, metavar="B",
+                   help="steps per count all-reduce at N > 1: each step's uint64[Q] counts are "
+                        "a row of a [B, Q] bucket reduced by one collective after its B-th "
+                        "step (sharding.CountsPipeline bucket; 1 = one collective per step)")
     p.add_argument("--settle-ms", type=float, default=600,
                    help="untimed launches of the step for this long before the warmup steps "
                         "(clock settle; 0 = none)")
@@ -382,8 +386,11 @@ def main():
         except RcclError as err:  # keep the run: torch.distributed's exchange instead
             print("bench: RcclComm unavailable (%s); --allreduce overlap" % err, file=sys.stderr)
             args.allreduce = "overlap"
+    if args.allreduce_bucket < 1:
+        raise SystemExit("bench: --allreduce-bucket must be >= 1")
     pipeline = CountsPipeline(Q, dev, single_pass=not args.zero_counts,
-                              allreduce=args.allreduce if distributed else "overlap", comm=comm)
+                              allreduce=args.allreduce if distributed else "overlap", comm=comm,
+                              bucket=args.allreduce_bucket if distributed else 1)
 
     def launch(c, workspace=None):
         ws = workspace
@@ -456,6 +463,7 @@ def main():
     region[0].record(stream)
     for i in range(args.steps):
         step(i)
+    pipeline.flush()  # a partly filled bucket's collective belongs to the timed steps
     region[1].record(stream)
     last = drain()
     torch.cuda.synchronize()
@@ -596,14 +604,16 @@ def main():
                 "htable": H,
                 "queues": Q,
                 "queue_width": qw,
-                "parallelism": ("tuple-sharded x%d, %s all-reduce of uint64[%d] counts %s"
+                "parallelism": ("tuple-sharded x%d, %s all-reduce of every step's uint64[%d] "
+                                "counts, %d steps per collective (rows of a [%d, %d] bucket) %s"
                                 % (world, "RCCL" if args.dist_backend == "nccl" else "gloo", Q,
+                                   pipeline.bucket, pipeline.bucket, Q,
                                    {"overlap": "(torch.distributed async, overlapped with the "
                                                "next step)",
-                                    "stream": "(torch.distributed, stream-ordered after each "
-                                              "step's launch)",
+                                    "stream": "(torch.distributed, stream-ordered after the "
+                                              "bucket's last launch)",
                                     "rccl": "(ncclAllReduce via rccl.RcclComm, stream-ordered "
-                                            "after each step's launch)"}[args.allreduce]))
+                                            "after the bucket's last launch)"}[args.allreduce]))
                                if distributed else "single process, one GPU (no process group)",
                 "step": ("zero counts + " if args.zero_counts else
                          "single-pass counts (rss_hash_device_ws): ") +

@@ -96,50 +96,93 @@ class CountsPipeline:
       stream after the launch and nothing else: no markers on the launch stream, buffer
       reuse ordered by the stream.  Per-step cost at world size 1 on MI355X: overlap 22 us,
       stream 8 us, rccl ~0 (``profiles/r02/rccl_step_overhead.log``).
+
+    ``bucket`` = steps per all-reduce (default 1: every step's counts reduced on their own).
+    With ``bucket=B > 1`` the count buffers are the rows of two ``[B, nqueues]`` buckets: step
+    i writes row ``i % B`` of bucket ``(i // B) % 2`` and the bucket's ``B`` rows are summed
+    over the ranks by ONE collective after its last step -- fewer, larger exchanges, as a
+    gradient bucket batches its parameters.  Every step's counts are still reduced on their
+    own (the rows are separate histograms, the sum is element-wise); a row holds the reduced
+    counts once its bucket's collective has run: after the bucket's last step on the launch
+    stream ("rccl" / "stream"), after ``drain()`` in any mode.  ``flush()`` issues the
+    collective of a partly filled bucket (``drain()`` calls it).  At world size N > 1 each
+    collective joins a step (a few tens of us over xGMI against a ~0.79 ms step) and makes
+    every rank wait for the slowest one's launch, so B batches per collective divide both
+    by B; a batch's histogram arrives at most B - 1 steps later.
     """
 
     def __init__(self, nqueues, device, group=None, single_pass=None, allreduce="overlap",
-                 comm=None):
+                 comm=None, bucket=1):
         if allreduce not in ("overlap", "stream", "rccl"):
             raise ValueError("allreduce must be overlap, stream or rccl")
         if allreduce == "rccl" and comm is None:
             raise ValueError("allreduce='rccl' needs comm (an rccl.RcclComm)")
+        bucket = int(bucket)
+        if bucket < 1:
+            raise ValueError("bucket must be >= 1")
         device = torch.device(device)
-        self.buffers = [torch.zeros(nqueues, dtype=torch.int64, device=device) for _ in range(2)]
+        self.bucket = bucket
+        self.buckets = [torch.zeros(bucket, nqueues, dtype=torch.int64, device=device)
+                        for _ in range(2)]
+        # buffers[k * bucket + r] = row r of bucket k (bucket=1: the two count buffers)
+        self.buffers = [b[r] for b in self.buckets for r in range(bucket)]
         if single_pass is None:
             single_pass = device.type == "cuda"
         self.workspace = (torch.zeros(nqueues + 1, dtype=torch.int64, device=device)
                           if single_pass else None)
         self.pending = [None, None]
+        self._open = 0   # rows of the current bucket written and not yet exchanged
+        self._slot = 0   # row slot of the next step (bucket = slot // B % 2, row = slot % B)
+        self._last = None
         self.group = group
         self.allreduce = allreduce
         self.comm = comm
         self.steps = 0
 
+    def _exchange(self, k, rows):
+        """Issue the all-reduce of bucket k's first ``rows`` rows (one collective)."""
+        counts = self.buckets[k][:rows]  # leading rows of a contiguous bucket: contiguous
+        if self.allreduce == "overlap":
+            self.pending[k] = allreduce_counts(counts, self.group, async_op=True)
+        elif self.allreduce == "stream":
+            allreduce_counts(counts, self.group)
+        else:
+            self.comm.all_reduce_counts(counts)
+
     def step(self, launch):
-        b = self.steps & 1
-        if self.pending[b] is not None:
-            self.pending[b].wait()  # buffer b's previous all-reduce must finish before reuse
-            self.pending[b] = None
-        counts = self.buffers[b]
+        k, r = (self._slot // self.bucket) & 1, self._slot % self.bucket
+        if r == 0 and self.pending[k] is not None:
+            self.pending[k].wait()  # bucket k's previous all-reduce must finish before reuse
+            self.pending[k] = None
+        counts = self.buckets[k][r]
         if self.workspace is not None:
             launch(counts, workspace=self.workspace)
         else:
             counts.zero_()
             launch(counts)
-        if self.allreduce == "overlap":
-            self.pending[b] = allreduce_counts(counts, self.group, async_op=True)
-        elif self.allreduce == "stream":
-            allreduce_counts(counts, self.group)
-        else:
-            self.comm.all_reduce_counts(counts)
         self.steps += 1
+        self._slot += 1
+        self._last = counts
+        self._open = r + 1  # rows of bucket k written and not yet exchanged
+        if self._open == self.bucket:
+            self._exchange(k, self._open)
+            self._open = 0
         return counts
 
+    def flush(self):
+        """Issue the collective of a partly filled bucket (no wait); the next step starts
+        the other bucket, so no row is ever exchanged twice."""
+        if self._open:
+            self._exchange(((self._slot - 1) // self.bucket) & 1, self._open)
+            self._slot += self.bucket - self._open
+            self._open = 0
+
     def drain(self):
-        """Wait for every outstanding all-reduce; returns the last step's (reduced) counts."""
+        """Flush, then wait for every outstanding all-reduce; returns the last step's
+        (reduced) counts."""
+        self.flush()
         for b in (0, 1):
             if self.pending[b] is not None:
                 self.pending[b].wait()
                 self.pending[b] = None
-        return self.buffers[(self.steps - 1) & 1] if self.steps else None
+        return self._last

@@ -73,12 +73,24 @@ def _rccl_worker(rank, port, key, n, htable, nqueues, out_dir):
                 k, tuples.data_ptr(), n, htable, nqueues, None, None, c.data_ptr(), 0, s,
                 workspace.data_ptr()))
         c3 = pipe.drain()
+        # bucketed (the bench's N > 1 default): one ncclAllReduce per [3, Q] bucket, a
+        # drain between phases closes a partly filled one
+        pipe_b = CountsPipeline(nqueues, dev, allreduce="rccl", comm=comm, bucket=3)
+        rows = []
+        for steps in (2, 5):
+            for _ in range(steps):
+                rows.append(pipe_b.step(lambda c, workspace: _native.hash_device(
+                    k, tuples.data_ptr(), n, htable, nqueues, None, None, c.data_ptr(), 0, s,
+                    workspace.data_ptr())))
+            pipe_b.drain()
+        c5 = torch.stack(rows[-5:])  # the last five steps' rows: all distinct, none reused
         direct = counts2.clone()
         comm.all_reduce_counts(direct)
         torch.cuda.synchronize()
         comm.destroy()
         np.save(os.path.join(out_dir, "c3.npy"), c3.cpu().numpy())
         np.save(os.path.join(out_dir, "c4.npy"), direct.cpu().numpy())
+        np.save(os.path.join(out_dir, "c5.npy"), c5.cpu().numpy())
         stats = torch.tensor([1.5, 2.5], dtype=torch.float64, device=dev)
         dist.all_reduce(stats, op=dist.ReduceOp.MAX)
         dist.barrier(device_ids=[0])
@@ -103,6 +115,8 @@ def test_nccl_world1_allreduce_counts_equal_oracle(tmp_path, oracle_lib, example
     np.testing.assert_array_equal(np.load(tmp_path / "c2.npy").view(np.uint64), co)
     np.testing.assert_array_equal(np.load(tmp_path / "c3.npy").view(np.uint64), co)
     np.testing.assert_array_equal(np.load(tmp_path / "c4.npy").view(np.uint64), co)
+    for row in np.load(tmp_path / "c5.npy").view(np.uint64):
+        np.testing.assert_array_equal(row, co)
     np.testing.assert_array_equal(np.load(tmp_path / "stats.npy"), [1.5, 2.5])
 
 
@@ -122,6 +136,7 @@ def test_bench_under_torchrun_nproc1_reports_baseline_and_roofline(tmp_path):
     assert rec["n_gpus"] == 1 and rec["steps"] == 3 and rec["warmup"] == 1
     assert "RCCL all-reduce" in rec["config"]["parallelism"]
     assert "rccl.RcclComm" in rec["config"]["parallelism"]  # the default per-step exchange
+    assert "8 steps per collective" in rec["config"]["parallelism"]  # --allreduce-bucket 8
     base = rec["cpu_baseline"]
     assert base is not None and base["value"] > 0 and base["cores"] == 2
     assert rec["settle"]["launches"] >= 16  # clock-settle launches before the warmup

@@ -118,12 +118,60 @@ def test_counts_pipeline_reduces_every_step(world, steps, allreduce, tmp_path):
                                           np.full(nq, ranks * (steps - 1)))
 
 
+def _bucket_worker(rank, world, port, phases, bucket, nq, out_dir, allreduce):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rss_simulator_nvidia_amd.sharding import CountsPipeline
+        comm = _GlooComm() if allreduce == "rccl" else None
+        pipe = CountsPipeline(nq, "cpu", allreduce=allreduce, comm=comm, bucket=bucket)
+        latest, i = {}, 0
+        for steps in phases:  # e.g. the bench's warmup steps, drain, timed steps, drain
+            for _ in range(steps):
+                c = pipe.step(lambda counts, i=i: counts.add_((rank + 1) * (i + 1)))
+                latest[c.data_ptr()] = (i, c)
+                i += 1
+            last = pipe.drain()
+            assert last.data_ptr() == c.data_ptr()
+        if comm is not None:
+            assert comm.calls == sum(-(-s // bucket) for s in phases)
+        rows = sorted(latest.values(), key=lambda v: v[0])
+        np.save(os.path.join(out_dir, "rows%d.npy" % rank), np.stack([r.numpy() for _, r in rows]))
+        np.save(os.path.join(out_dir, "idx%d.npy" % rank), np.array([j for j, _ in rows]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,phases,bucket,allreduce", [
+    (2, (5,), 8, "rccl"), (2, (3, 20), 8, "rccl"), (3, (7, 9), 4, "overlap"),
+    (2, (2, 11), 3, "stream"), (2, (16,), 8, "overlap"), (3, (1, 1, 5), 2, "rccl")])
+def test_counts_pipeline_bucketed_exchange(world, phases, bucket, allreduce, tmp_path):
+    """bucket=B (the bench's N > 1 default B = 8): every step's counts are still reduced on
+    their own -- each row that was written last by step i holds the sum over ranks of step
+    i's counts, never a row reduced twice (a drain between phases closes a partly filled
+    bucket and the next step starts the other one) -- with one collective per B steps."""
+    nq = 5
+    mp.start_processes(_bucket_worker, args=(world, _free_port(), phases, bucket, nq,
+                                             str(tmp_path), allreduce),
+                       nprocs=world, start_method="spawn")
+    ranks = sum(r + 1 for r in range(world))
+    for r in range(world):
+        idx = np.load(tmp_path / ("idx%d.npy" % r))
+        rows = np.load(tmp_path / ("rows%d.npy" % r))
+        assert idx[-1] == sum(phases) - 1
+        assert len(idx) == min(sum(phases), 2 * bucket)
+        for j, row in zip(idx, rows):
+            np.testing.assert_array_equal(row, np.full(nq, ranks * (j + 1)))
+
+
 def test_counts_pipeline_rejects_bad_modes():
     from rss_simulator_nvidia_amd.sharding import CountsPipeline
     with pytest.raises(ValueError, match="overlap, stream or rccl"):
         CountsPipeline(3, "cpu", allreduce="ring")
     with pytest.raises(ValueError, match="needs comm"):
         CountsPipeline(3, "cpu", allreduce="rccl")
+    with pytest.raises(ValueError, match="bucket"):
+        CountsPipeline(3, "cpu", bucket=0)
 
 
 def test_rccl_comm_needs_a_process_group():
