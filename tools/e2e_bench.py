@@ -66,14 +66,20 @@ result["device_host_outputs_identical"] = \
 # the device text path from a host file image (rss_csv_hash_text, file already in memory)
 data = np.fromfile(big, dtype=np.uint8)
 k0 = _native.prepare_key(key)
-_native.default_context().csv_hash_text(k0, data, H, Q)
-t0 = time.perf_counter()
-img, _, _ = _native.default_context().csv_hash_text(k0, data, H, Q)
-result["csv_hash_text_in_memory"] = {"wall_s": time.perf_counter() - t0,
-                                     "rows_per_s": rows / (time.perf_counter() - t0),
-                                     "note": "file image in host memory -> statistics image in "
-                                             "host memory (PCIe-inclusive, no file I/O)"}
-del img, data
+ctx = _native.default_context()
+ctx.csv_hash_text(k0, data, H, Q, copy=False)
+for copy in (False, True):  # the context-owned image (zero-copy view) / the default copy
+    t0 = time.perf_counter()
+    img, _, _ = ctx.csv_hash_text(k0, data, H, Q, copy=copy)
+    wall = time.perf_counter() - t0
+    result["csv_hash_text_in_memory" + ("_copy" if copy else "")] = {
+        "wall_s": wall, "rows_per_s": rows / wall,
+        "note": "file image in host memory -> statistics image in host memory (PCIe-inclusive, "
+                "no file I/O)" + ("; plus the copy of the output image out of the context "
+                                  "(csv_hash_text's default copy=True)" if copy else
+                                  "; the image as a view of the context's buffer (copy=False)")}
+    del img
+del data
 
 # the CLI as a user runs it: a fresh process (interpreter start, imports, GPU init)
 cli = [sys.executable, "-m", "rss_simulator_nvidia_amd", "--key-file",
