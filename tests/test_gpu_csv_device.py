@@ -215,3 +215,20 @@ def test_file_to_file_in_segments(native, ctx, oracle_lib, example_key, tmp_path
     c2, n2 = ctx.csv_hash_file(key, str(src), None, 128, 24)  # counts only, segmented too
     np.testing.assert_array_equal(c2, want[1])
     assert n2 == n
+
+
+def test_default_image_is_an_owned_copy(native, ctx, example_key):
+    """csv_hash_text's default image (copied out on several threads when large) equals the
+    context's own image (copy=False) and outlives the next call on the context."""
+    rng = random.Random(11)
+    base = _random_canonical(rng, 100_000, (0, 1, 2, 3), False, False, True)
+    header, body = base.split("\n", 1)
+    text = header + "\n" + body * 16  # 1.6M rows, a statistics image above 64 MiB
+    key = native.prepare_key(example_key)
+    owned = ctx.csv_hash_text(key, _bytes(text), 128, 24)[0]
+    view = ctx.csv_hash_text(key, _bytes(text), 128, 24, copy=False)[0]
+    assert owned.size > (64 << 20) and owned.tobytes() == view.tobytes()
+    assert owned.ctypes.data != view.ctypes.data
+    before = owned.tobytes()
+    ctx.csv_hash_text(key, _bytes(text[:len(text) // 3].rsplit("\n", 1)[0] + "\n"), 100, 7)
+    assert owned.tobytes() == before

@@ -138,3 +138,12 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     monkeypatch.setattr(_native, "_lib", None)
     with pytest.raises(NativeLibraryError, match="no CPU fallback"):
         _native.load()
+
+
+@pytest.mark.parametrize("n", [0, 1, 4097, (64 << 20) + 5, (3 << 26) + 1])
+def test_copy_out_is_an_exact_owned_copy(n):
+    """csv_hash_text's copy of a context-owned image (_native._copy_out, threaded slices)."""
+    a = (np.arange(n, dtype=np.uint32) * 2654435761 % 251).astype(np.uint8)
+    b = _native._copy_out(a)
+    assert b.dtype == np.uint8 and b.shape == a.shape and np.array_equal(a, b)
+    assert n == 0 or b.ctypes.data != a.ctypes.data
