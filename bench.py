@@ -388,7 +388,7 @@ def main():
             args.allreduce = "overlap"
     if args.allreduce_bucket < 1:
         raise SystemExit("bench: --allreduce-bucket must be >= 1")
-    pipeline = CountsPipeline(Q, dev, single_pass=not args.zero_counts,
+    pipeline = CountsPipeline(Q, dev, single_pass=not args.zero_counts, htable=H,
                               allreduce=args.allreduce if distributed else "overlap", comm=comm,
                               bucket=args.allreduce_bucket if distributed else 1)
 

@@ -294,22 +294,24 @@ RETA_QUEUE_MAX = 0xFFFF  # an indirection-table entry travels as u16 (rss_hash_d
 
 
 def queue_modulus(htable, nqueues, reta=False):
-    """``(htable, nqueues)`` as the C ABI's ``uint32_t`` arguments, for the same
-    ``queue = hash % htable % nqueues`` (``simulator.py:96-98``) on every 32-bit hash.
+    """``(htable, nqueues')`` as the C ABI's ``uint32_t`` arguments, for the same
+    ``queue = hash % htable % nqueues`` (``simulator.py:96-98``) on every 32-bit hash,
+    with ``nqueues'`` the number of queues a tuple can actually get -- the length of every
+    per-queue count vector (queues past it are always empty).
 
-    ctypes would truncate a value >= 2**32 silently (4294967297 -> 1), so larger values
-    are rewritten exactly, never truncated:
-
-    * ``nqueues >= 2**32 > htable``: ``queue = hash % htable`` -> ``(htable, htable)``;
+    * ``nqueues >= htable``: ``bucket = hash % htable < htable <= nqueues``, so ``queue =
+      bucket`` -> ``(htable, htable)``: bins, counts and the queue column's width are sized
+      by ``min(htable, nqueues)``, never by ``nqueues`` (``--num-queues 4000000000`` with
+      ``--htable-size 128`` needs 128 counts, not 32 GB);
     * ``htable >= 2**32``: ``hash % htable = hash`` (hash < 2**32), so ``queue = hash %
       nqueues``; any multiple of ``nqueues`` as the table size gives the same remainder ->
-      ``((2**32 - 1) // nqueues * nqueues, nqueues)``;
+      ``((2**32 - 1) // nqueues * nqueues, nqueues)`` (ctypes would truncate 4294967297 to
+      1 silently: values are rewritten exactly, never truncated);
     * both ``>= 2**32``: ``queue = hash``, whose histogram would need 2**32 entries --
-      refused with ``ValueError`` (the one combination this build does not run);
+      ``ValueError`` here (``Simulator`` counts that case's queues sparsely on the host);
     * with an indirection table (``reta``) queues are table entries < 2**16, so an
-      ``nqueues >= 2**32`` only bounds them: it becomes 65536 (higher queues stay empty).
-
-    The per-queue counts then have ``nqueues'`` entries (queues past it are always empty).
+      ``nqueues >= 2**32`` only bounds them: it becomes 65536 (higher queues stay empty);
+      the library sizes its bins by ``max(reta) + 1``.
     """
     H, Q = int(htable), int(nqueues)
     if H < 0 or Q < 0:  # ctypes would wrap -1 to 2**32 - 1
@@ -318,14 +320,18 @@ def queue_modulus(htable, nqueues, reta=False):
         return H, Q  # the library refuses it (RSS_EINVAL, "must be >= 1")
     if reta:
         return H, (Q if Q <= U32_MAX else RETA_QUEUE_MAX + 1)
-    if H <= U32_MAX and Q <= U32_MAX:
-        return H, Q
     if H <= U32_MAX:
-        return H, H
+        return H, min(H, Q)
     if Q <= U32_MAX:
         return U32_MAX // Q * Q, Q
     raise ValueError("htable %d and nqueues %d both >= 2**32: every hash would be its own queue "
                      "(a 2**32-entry histogram); not supported" % (H, Q))
+
+
+def queues_are_hashes(htable, nqueues, reta=None):
+    """True when ``hash % htable % nqueues == hash`` for every 32-bit hash (both >= 2**32,
+    no table): the one case :func:`queue_modulus` refuses, whose queues are the hashes."""
+    return reta is None and int(htable) > U32_MAX and int(nqueues) > U32_MAX
 
 
 def _reta_table(reta, htable):

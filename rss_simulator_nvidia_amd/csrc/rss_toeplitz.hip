@@ -105,6 +105,7 @@ struct LaunchParams {
     uint32_t q_m16;     // ceil(2^16 / Q): exact b % Q for b < 256 (QM_FAST8, packed search)
     const uint32_t* key_windows;  // key search: nkeys x 96 windows in device memory
     uint32_t q_lo, q_span;        // HIST_RANGE: the queues this pass counts
+    uint32_t q_stride;            // key search: row stride of the [keys, nqueues] counts (>= Q)
     uint16_t reta[kRetaMax];      // QM_TABLE: queue of bucket b (ethtool -X indirection)
 };
 
@@ -723,8 +724,8 @@ __global__ __launch_bounds__(kBlock) void rss_key_search_kernel(const LaunchPara
     __syncthreads();
 
     LaunchParams qa = p, qb = p;  // per-key counts rows
-    qa.counts = p.counts + (size_t)key_a * p.Q;
-    qb.counts = p.counts + (size_t)key_b * p.Q;
+    qa.counts = p.counts + (size_t)key_a * p.q_stride;
+    qb.counts = p.counts + (size_t)key_b * p.q_stride;
     uint32_t* bins_a = bins;
     uint32_t* bins_b = bins + per_key;
     const uint32_t col = tid & (kBinCols - 1);
@@ -887,7 +888,7 @@ __global__ __launch_bounds__(kBlock) void rss_key_search_packed_kernel(const Lau
         if (key0 + k >= p.nkeys) continue;
         uint32_t s = 0;
         for (uint32_t c = 0; c < kBinCols; ++c) s += bins[e * kBinCols + ((c + e) & (kBinCols - 1))];
-        if (s) atomicAdd(&p.counts[(size_t)(key0 + k) * p.Q + q], (unsigned long long)s);
+        if (s) atomicAdd(&p.counts[(size_t)(key0 + k) * p.q_stride + q], (unsigned long long)s);
     }
 }
 
@@ -1228,6 +1229,28 @@ bool aligned16(const void* ptr) { return ((uintptr_t)ptr & 15u) == 0; }
 uint64_t magic64(uint32_t d) { return UINT64_MAX / d + 1; }
 uint32_t magic32(uint32_t d) { return UINT32_MAX / d + 1; }
 
+// The queues a launch can produce.  Without an indirection table queue = bucket % Q with
+// bucket < H (simulator.py:96-98), so every queue is < min(H, Q); with one, < max(reta) + 1.
+// Bins, the queue-width check and the counts the kernels write are sized by this; counts
+// [q_eff, nqueues) of the caller's vector are always zero (zero_counts_tail).
+uint32_t effective_queues(uint32_t htable, uint32_t nqueues, const uint32_t* reta) {
+    if (reta) {
+        uint32_t m = 0;
+        for (uint32_t b = 0; b < htable; ++b) m = std::max(m, reta[b]);
+        return m + 1;  // <= nqueues (check_reta)
+    }
+    return nqueues < htable ? nqueues : htable;
+}
+
+// counts[q_eff, nqueues) of a non-accumulating launch: queues no tuple can have
+int zero_counts_tail(uint64_t* d_counts, uint32_t q_eff, uint32_t nqueues, uint32_t flags,
+                     hipStream_t stream) {
+    if (d_counts && q_eff < nqueues && !(flags & RSS_FLAG_ACCUMULATE))
+        RSS_HIP_CHECK(hipMemsetAsync(d_counts + q_eff, 0, sizeof(uint64_t) * (nqueues - q_eff),
+                                     stream));
+    return RSS_OK;
+}
+
 // Modulo strategy (mask / exact 16-bit magic / exact 64-bit magic) and histogram
 // placement (private LDS columns / shared LDS bins / global atomics) for H and Q.
 // Returns whether H is a power of two.
@@ -1324,9 +1347,11 @@ int launch_search(const uint32_t* d_windows, size_t nkeys, const rss_tuple4* d_t
     memset(&p, 0, sizeof p);
     p.tuples = d_tuples;
     p.n = n;
+    p.q_stride = nqueues;  // rows keep the caller's nqueues; queues >= min(H, Q) stay zero
+    const uint32_t q_eff = effective_queues(htable, nqueues, nullptr);
     int qmode, hist;
     uint32_t bin_bytes;  // per key; a workgroup holds the bins of its two keys
-    const bool h_pow2 = setup_modes(&p, htable, nqueues, true, &qmode, &hist, &bin_bytes,
+    const bool h_pow2 = setup_modes(&p, htable, q_eff, true, &qmode, &hist, &bin_bytes,
                                     kPairBinBytesMax / 2, false);
     const bool vec4 = aligned16(d_tuples);
     DeviceInfo info;
@@ -1334,12 +1359,12 @@ int launch_search(const uint32_t* d_windows, size_t nkeys, const rss_tuple4* d_t
     if (rc) return rc;
     // packed buckets (8 keys per table entry for H <= 256, 4 for H <= 65536) whenever
     // their private bins fit (8 keys: Q <= 40, 4 keys: Q <= 80); else pairs of full hashes
-    const bool bytes_fit = (uint64_t)nqueues * 8 * kBinCols * 4 <= kPairBinBytesMax;
+    const bool bytes_fit = (uint64_t)q_eff * 8 * kBinCols * 4 <= kPairBinBytesMax;
     const int lane_bits = htable <= 256u && bytes_fit ? 8 : 16;
     const uint32_t keys_per_wg = 64 / lane_bits;
-    const uint64_t packed_bins = (uint64_t)nqueues * keys_per_wg * kBinCols * 4;
+    const uint64_t packed_bins = (uint64_t)q_eff * keys_per_wg * kBinCols * 4;
     if (h_pow2 && htable <= 65536u && packed_bins <= kPairBinBytesMax) {
-        p.q_m16 = 65536u / nqueues + (65536u % nqueues != 0);
+        p.q_m16 = 65536u / q_eff + (65536u % q_eff != 0);
         KernelFn fn = pick_packed(lane_bits, qmode, vec4);
         const unsigned gx = search_grid_x(n, info.cu_count);
         const uint32_t shmem = (uint32_t)std::max<uint64_t>(packed_bins, kPackedPrepBytes);
@@ -1470,14 +1495,18 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
         const int rc = check_reta(reta, htable, nqueues, "rss_hash_device_reta");
         if (rc) return rc;
     }
+    // every queue is < q_eff = min(H, Q) (or max(reta) + 1): bins and widths by q_eff
+    const uint32_t q_eff = effective_queues(htable, nqueues, reta);
     int qwidth = QW_U32;
     if (flags & RSS_FLAG_QUEUE_U8) {
-        if (nqueues > 256)
-            return set_error(RSS_EINVAL, "rss_hash_device: RSS_FLAG_QUEUE_U8 needs nqueues <= 256");
+        if (q_eff > 256)
+            return set_error(RSS_EINVAL, "rss_hash_device: RSS_FLAG_QUEUE_U8 needs min(htable, nqueues) <= 256 "
+                                         "(got %u)", q_eff);
         qwidth = QW_U8;
     } else if (flags & RSS_FLAG_QUEUE_U16) {
-        if (nqueues > 65536)
-            return set_error(RSS_EINVAL, "rss_hash_device: RSS_FLAG_QUEUE_U16 needs nqueues <= 65536");
+        if (q_eff > 65536)
+            return set_error(RSS_EINVAL, "rss_hash_device: RSS_FLAG_QUEUE_U16 needs min(htable, nqueues) <= 65536 "
+                                         "(got %u)", q_eff);
         qwidth = QW_U16;
     }
     LaunchParams p;
@@ -1485,12 +1514,16 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
     int qmode, hist;
     uint32_t bin_bytes;
     const uint32_t reta_bytes = reta ? htable * 4 : 0;
-    const bool h_pow2 = setup_modes(&p, htable, nqueues, d_counts != nullptr, &qmode, &hist,
+    const bool h_pow2 = setup_modes(&p, htable, q_eff, d_counts != nullptr, &qmode, &hist,
                                     &bin_bytes, kBinBytesMax - reta_bytes);
     // single pass: the kernel's last workgroup writes the counts (fold_counts)
     const bool single_pass = ws && d_counts && n > 0 && (hist == HIST_PRIVATE || hist == HIST_SHARED);
     if (d_counts && !(flags & RSS_FLAG_ACCUMULATE) && !single_pass)
         RSS_HIP_CHECK(hipMemsetAsync(d_counts, 0, sizeof(uint64_t) * nqueues, stream));
+    else if (single_pass) {
+        const int trc = zero_counts_tail(d_counts, q_eff, nqueues, flags, stream);
+        if (trc) return trc;
+    }
     if (n == 0) return RSS_OK;
 
     memcpy(p.window, key->window, sizeof p.window);
@@ -1534,29 +1567,43 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
     const unsigned grid = (unsigned)(want < cap ? want : cap);
     if (hist == HIST_GLOBAL && d_counts) {
         const uint32_t span = (kBinBytesMax - reta_bytes) / 4;
-        const uint32_t qbytes = nqueues <= 65536u ? 2 : 4;
-        const uint64_t passes = ((uint64_t)nqueues + span - 1) / span;
+        const uint32_t qbytes = q_eff <= 65536u ? 2 : 4;
+        const uint64_t passes = ((uint64_t)q_eff + span - 1) / span;
         if (passes <= (qbytes == 2 ? 64u : 32u)) {
             void* qcol = d_queue;
             int qw = qwidth;
-            bool scratch = false;
-            if (!qcol || qwidth == QW_U8) {  // (u8 queues always fit the bins: Q <= 256)
-                RSS_HIP_CHECK(hipMallocAsync(&qcol, (size_t)n * qbytes, stream));
-                scratch = true;
-                qw = qbytes == 2 ? QW_U16 : QW_U32;
+            bool scratch = false, ranged = true;
+            if (!qcol || qwidth == QW_U8) {  // (u8 queues always fit the bins: q_eff <= 256)
+                if (hipMallocAsync(&qcol, (size_t)n * qbytes, stream) == hipSuccess) {
+                    scratch = true;
+                    qw = qbytes == 2 ? QW_U16 : QW_U32;
+                } else {
+                    (void)hipGetLastError();  // no room for a scratch column: one global
+                    ranged = false;           // atomic per tuple below (HIST_GLOBAL) instead
+                }
             }
-            p.queue_out = qcol;
-            p.q_lo = 0;
-            p.q_span = std::min<uint32_t>(span, nqueues);
-            const bool v4 = vec4 && ((uintptr_t)qcol % (qw == QW_U16 ? 8 : 16)) == 0;
-            KernelFn fn = h_pow2 ? pick_queue<true>(qmode, HIST_RANGE, qw, v4)
-                                 : pick_queue<false>(qmode, HIST_RANGE, qw, v4);
-            const unsigned g1 = v4 ? grid : (unsigned)std::min<uint64_t>((n + kBlock - 1) / kBlock, cap);
-            hipLaunchKernelGGL(fn, dim3(g1), dim3(kBlock), span * 4 + reta_bytes, stream, p);
-            RSS_HIP_CHECK(hipGetLastError());
-            rc = launch_queue_ranges(qcol, qw, n, span, nqueues, p.counts, info.cu_count, stream);
-            if (scratch) RSS_HIP_CHECK(hipFreeAsync(qcol, stream));
-            return rc;
+            if (ranged) {
+                p.queue_out = qcol;
+                p.q_lo = 0;
+                p.q_span = std::min<uint32_t>(span, q_eff);
+                const bool v4 = vec4 && ((uintptr_t)qcol % (qw == QW_U16 ? 8 : 16)) == 0;
+                KernelFn fn = h_pow2 ? pick_queue<true>(qmode, HIST_RANGE, qw, v4)
+                                     : pick_queue<false>(qmode, HIST_RANGE, qw, v4);
+                const unsigned g1 = v4 ? grid : (unsigned)std::min<uint64_t>((n + kBlock - 1) / kBlock, cap);
+                hipLaunchKernelGGL(fn, dim3(g1), dim3(kBlock), span * 4 + reta_bytes, stream, p);
+                const hipError_t le = hipGetLastError();
+                rc = le == hipSuccess
+                         ? launch_queue_ranges(qcol, qw, n, span, q_eff, p.counts, info.cu_count, stream)
+                         : set_error(RSS_EIO, "rss_hash_device: range launch failed: %s",
+                                     hipGetErrorString(le));
+                // the scratch column goes back on every path (stream-ordered after its readers)
+                if (scratch) {
+                    const hipError_t fe = hipFreeAsync(qcol, stream);
+                    if (fe != hipSuccess && rc == RSS_OK)
+                        rc = set_error(RSS_EIO, "hipFreeAsync failed: %s", hipGetErrorString(fe));
+                }
+                return rc;
+            }
         }
     }
     KernelFn fn = h_pow2 ? pick_queue<true>(qmode, hist, qwidth, vec4)
@@ -1610,14 +1657,17 @@ int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint
         const int rc = check_reta(reta, htable, nqueues, "rss_hash6_device_reta");
         if (rc) return rc;
     }
+    const uint32_t q_eff = effective_queues(htable, nqueues, reta);  // as launch_hash
     uint32_t qwidth = QW_U32;
     if (flags & RSS_FLAG_QUEUE_U8) {
-        if (nqueues > 256)
-            return set_error(RSS_EINVAL, "rss_hash6_device: RSS_FLAG_QUEUE_U8 needs nqueues <= 256");
+        if (q_eff > 256)
+            return set_error(RSS_EINVAL, "rss_hash6_device: RSS_FLAG_QUEUE_U8 needs min(htable, nqueues) <= 256 "
+                                         "(got %u)", q_eff);
         qwidth = QW_U8;
     } else if (flags & RSS_FLAG_QUEUE_U16) {
-        if (nqueues > 65536)
-            return set_error(RSS_EINVAL, "rss_hash6_device: RSS_FLAG_QUEUE_U16 needs nqueues <= 65536");
+        if (q_eff > 65536)
+            return set_error(RSS_EINVAL, "rss_hash6_device: RSS_FLAG_QUEUE_U16 needs min(htable, nqueues) <= 65536 "
+                                         "(got %u)", q_eff);
         qwidth = QW_U16;
     }
     if (d_counts && !(flags & RSS_FLAG_ACCUMULATE))
@@ -1629,7 +1679,7 @@ int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint
     uint32_t bin_bytes;
     const uint32_t reta_bytes = reta ? htable * 4 : 0;  // the table in LDS after the bins
     const uint32_t budget = kBinBytesMax6 - reta_bytes;   // bins share the LDS with the LUT
-    const bool h_pow2 = setup_modes(&tmp, htable, nqueues, d_counts != nullptr, &qmode, &hist,
+    const bool h_pow2 = setup_modes(&tmp, htable, q_eff, d_counts != nullptr, &qmode, &hist,
                                     &bin_bytes, budget);
     if (reta) qmode = QM_TABLE;
     LaunchParams6 p;
@@ -1659,10 +1709,10 @@ int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint
     if (rc) return rc;
     // counts only, power-of-two H <= 256: the register-table kernel (no LUT, so private bins
     // up to Q = 256 fit beside it)
-    if (!d_hash && !d_queue && d_counts && !reta && h_pow2 && htable <= 256u && nqueues <= 256u &&
+    if (!d_hash && !d_queue && d_counts && !reta && h_pow2 && htable <= 256u && q_eff <= 256u &&
         (qmode == QM_MASK || qmode == QM_FAST8) && aligned16(d_tuples) && counts_perm_enabled())
         return launch_counts_perm<9>(key->window, d_tuples, n, p.counts, p.h_mask, p.Q, p.q_mask,
-                                     p.q_m16, qmode, nqueues * kBinCols * 4, info.cu_count, stream);
+                                     p.q_m16, qmode, q_eff * kBinCols * 4, info.cu_count, stream);
     const uint64_t per_lane = vec4 ? 4 : 1;
     const uint64_t want = (n + per_lane * kBlock - 1) / (per_lane * kBlock);
     const uint64_t cap = (uint64_t)info.cu_count * kBlocksPerCU6;
@@ -1670,28 +1720,41 @@ int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint
     // many queues: as launch_hash (first range in LDS + the queue column, then the column)
     if (hist == HIST_GLOBAL && d_counts) {
         const uint32_t span = budget / 4;
-        const uint32_t qbytes = nqueues <= 65536u ? 2 : 4;
-        const uint64_t passes = ((uint64_t)nqueues + span - 1) / span;
+        const uint32_t qbytes = q_eff <= 65536u ? 2 : 4;
+        const uint64_t passes = ((uint64_t)q_eff + span - 1) / span;
         if (passes <= (qbytes == 2 ? 64u : 32u)) {
             void* qcol = d_queue;
-            bool scratch = false;
+            bool scratch = false, ranged = true;
             if (!qcol || qwidth == QW_U8) {
-                RSS_HIP_CHECK(hipMallocAsync(&qcol, (size_t)n * qbytes, stream));
-                scratch = true;
-                p.qwidth = qbytes == 2 ? QW_U16 : QW_U32;
+                if (hipMallocAsync(&qcol, (size_t)n * qbytes, stream) == hipSuccess) {
+                    scratch = true;
+                    p.qwidth = qbytes == 2 ? QW_U16 : QW_U32;
+                } else {
+                    (void)hipGetLastError();  // as launch_hash: global atomics below instead
+                    ranged = false;
+                }
             }
-            p.queue_out = qcol;
-            p.q_lo = 0;
-            p.q_span = std::min<uint32_t>(span, nqueues);
-            const uint32_t qw = p.qwidth;
-            const bool v4 = vec4 && ((uintptr_t)qcol % (qw == QW_U16 ? 8 : 16)) == 0;
-            KernelFn6 fn = h_pow2 ? pick6<true>(qmode, HIST_RANGE, v4) : pick6<false>(qmode, HIST_RANGE, v4);
-            const unsigned g1 = v4 ? grid : (unsigned)std::min<uint64_t>((n + kBlock - 1) / kBlock, cap);
-            hipLaunchKernelGGL(fn, dim3(g1), dim3(kBlock), span * 4 + reta_bytes, stream, p);
-            RSS_HIP_CHECK(hipGetLastError());
-            rc = launch_queue_ranges(qcol, (int)qw, n, span, nqueues, p.counts, info.cu_count, stream);
-            if (scratch) RSS_HIP_CHECK(hipFreeAsync(qcol, stream));
-            return rc;
+            if (ranged) {
+                p.queue_out = qcol;
+                p.q_lo = 0;
+                p.q_span = std::min<uint32_t>(span, q_eff);
+                const uint32_t qw = p.qwidth;
+                const bool v4 = vec4 && ((uintptr_t)qcol % (qw == QW_U16 ? 8 : 16)) == 0;
+                KernelFn6 fn = h_pow2 ? pick6<true>(qmode, HIST_RANGE, v4) : pick6<false>(qmode, HIST_RANGE, v4);
+                const unsigned g1 = v4 ? grid : (unsigned)std::min<uint64_t>((n + kBlock - 1) / kBlock, cap);
+                hipLaunchKernelGGL(fn, dim3(g1), dim3(kBlock), span * 4 + reta_bytes, stream, p);
+                const hipError_t le = hipGetLastError();
+                rc = le == hipSuccess
+                         ? launch_queue_ranges(qcol, (int)qw, n, span, q_eff, p.counts, info.cu_count, stream)
+                         : set_error(RSS_EIO, "rss_hash6_device: range launch failed: %s",
+                                     hipGetErrorString(le));
+                if (scratch) {
+                    const hipError_t fe = hipFreeAsync(qcol, stream);
+                    if (fe != hipSuccess && rc == RSS_OK)
+                        rc = set_error(RSS_EIO, "hipFreeAsync failed: %s", hipGetErrorString(fe));
+                }
+                return rc;
+            }
         }
     }
     KernelFn6 fn = h_pow2 ? pick6<true>(qmode, hist, vec4) : pick6<false>(qmode, hist, vec4);

@@ -136,12 +136,17 @@ def main(argv=None):
     args = parser.parse_args(argv)
     try:
         table = indirection_table(args)
-        _native.queue_modulus(args.htable_size, args.num_queues, table is not None)
+        # --csv with htable and num-queues both >= 2**32: queue = hash (simulator.py:97), the
+        # Simulator path counts those queues sparsely; histogram mode would need 2**32+ bins
+        hashes_are_queues = args.csv and _native.queues_are_hashes(args.htable_size,
+                                                                   args.num_queues, table)
+        if not hashes_are_queues:
+            _native.queue_modulus(args.htable_size, args.num_queues, table is not None)
     except ValueError as err:
         parser.error(str(err))
     if args.pcap:
         return run_pcap(args, table)
-    fast = fastcsv.enabled()
+    fast = fastcsv.enabled() and not hashes_are_queues
     run_csv = fastcsv.run_csv6 if args.ipv6 else fastcsv.run_csv
     run_counts = fastcsv.run_counts6 if args.ipv6 else fastcsv.run_counts
     if args.csv and fast and run_csv(args.key, args.ips_file, args.htable_size, args.num_queues,

@@ -28,7 +28,14 @@ class _UniqueId(ctypes.Structure):
 
 
 class RcclError(RuntimeError):
-    pass
+    """An RCCL call failed.  ``stuck`` is True when a communicator init timed out: its
+    ``ncclCommInitRank`` may still be blocked on a helper thread of this process (holding
+    bootstrap sockets and a half-built communicator), so falling back to another collective
+    on the same ``librccl`` is not safe -- callers should end the process instead."""
+
+    def __init__(self, msg, stuck=False):
+        super().__init__(msg)
+        self.stuck = stuck
 
 
 _LIB = None
@@ -54,9 +61,11 @@ def _library():
         lib.ncclCommInitRank.argtypes = [ctypes.POINTER(vp), ctypes.c_int, _UniqueId, ctypes.c_int]
         lib.ncclAllReduce.argtypes = [vp, vp, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, vp, vp]
         lib.ncclCommDestroy.argtypes = [vp]
+        lib.ncclCommAbort.argtypes = [vp]
         lib.ncclGetErrorString.argtypes = [ctypes.c_int]
         lib.ncclGetErrorString.restype = ctypes.c_char_p
-        for fn in ("ncclGetUniqueId", "ncclCommInitRank", "ncclAllReduce", "ncclCommDestroy"):
+        for fn in ("ncclGetUniqueId", "ncclCommInitRank", "ncclAllReduce", "ncclCommDestroy",
+                   "ncclCommAbort"):
             getattr(lib, fn).restype = ctypes.c_int
         _LIB = lib
     return _LIB
@@ -74,8 +83,11 @@ class RcclComm:
 
     ``ncclCommInitRank`` runs on a helper thread and is given ``timeout_s``: a rank whose
     init has not finished by then (or failed) reports it, the ranks agree over the process
-    group (a MIN all-reduce of the outcome), and if any rank failed every rank raises
-    ``RcclError`` -- so callers fall back together instead of hanging in the bootstrap.
+    group (a MAX all-reduce of [failed, timed out]), and if any rank failed every rank raises
+    ``RcclError`` -- so callers fall back together instead of hanging in the bootstrap.  If
+    any rank's init timed out the error is ``stuck``: the blocked init cannot be cancelled
+    (a communicator handle that was already returned is ``ncclCommAbort``-ed), so the
+    process must not fall back to RCCL through ``torch.distributed`` -- it should exit.
     """
 
     def __init__(self, device, group=None, timeout_s=120.0):
@@ -110,7 +122,8 @@ class RcclComm:
         worker = threading.Thread(target=init, name="rccl-init", daemon=True)
         worker.start()
         worker.join(timeout_s)
-        if worker.is_alive():
+        stuck = worker.is_alive()
+        if stuck:
             why = "ncclCommInitRank did not finish in %.0f s" % timeout_s
         elif "err" in result:
             why = "ncclCommInitRank raised %r" % result["err"]
@@ -119,13 +132,17 @@ class RcclComm:
             why = "ncclCommInitRank failed (%d): %s" % (result["rc"], msg.decode() if msg else "?")
         else:
             why = None
-        ok = torch.tensor([0 if why else 1], dtype=torch.int32, device=self.device)
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)  # every rank's outcome
+        flags = torch.tensor([1 if why else 0, 1 if stuck else 0], dtype=torch.int32,
+                             device=self.device)
+        dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=group)  # every rank's outcome
+        failed, any_stuck = (int(x) for x in flags.tolist())
         self._comm = comm if why is None else None
-        if int(ok.item()) == 0:
+        if failed:
             if self._comm is not None:
                 self.destroy()
-            raise RcclError(why or "ncclCommInitRank failed on another rank")
+            elif stuck and comm.value:  # a handle exists but init has not returned: abort it
+                lib.ncclCommAbort(comm)
+            raise RcclError(why or "ncclCommInitRank failed on another rank", stuck=bool(any_stuck))
 
     def all_reduce_counts(self, counts, stream=None):
         """Sum the int64 (uint64 bit pattern) tensor ``counts`` over the ranks in place,

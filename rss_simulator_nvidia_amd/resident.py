@@ -63,7 +63,8 @@ class ResidentBatch:
         self._probe_counts = torch.zeros(self.counts_len, dtype=torch.int64, device=self.device)
         # single-pass counts workspace of this batch's launches (rss_hash_device_ws; they all
         # run in order on self.stream, so one suffices)
-        self.workspace = torch.zeros(self.counts_len + 1, dtype=torch.int64, device=self.device)
+        self.workspace = torch.zeros(_native.counts_workspace_bytes(self.htable, self.nqueues) // 8,
+                                     dtype=torch.int64, device=self.device)
         n_in, n_out = placement[0], placement[1]
         rounds = placement[2] if len(placement) > 2 else 1
         self.tuples, self.hashes, self.queues, self.report = choose_stream_buffers(
@@ -93,8 +94,8 @@ class ResidentBatch:
         ``queues`` (when ``outputs``) and ``counts`` (int64[counts_len]; summed into when
         ``accumulate``, else overwritten).  Counts are single-pass (``rss_hash_device_ws``:
         one launch, no zeroing launch before it) on ``workspace`` -- a zeroed int64 tensor of
-        ``counts_len + 1`` no other launch uses at the same time -- or on the batch's own
-        :attr:`workspace`.  Returns ``counts``."""
+        ``_native.counts_workspace_bytes(htable, nqueues) // 8`` no other launch uses at the
+        same time -- or on the batch's own :attr:`workspace`.  Returns ``counts``."""
         flags = QUEUE_FLAGS[self.queue_width] | (_native.FLAG_ACCUMULATE if accumulate else 0)
         self._launch(self.tuples, self.hashes if outputs else None,
                      self.queues if outputs else None, counts, flags,

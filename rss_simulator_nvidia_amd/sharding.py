@@ -78,12 +78,14 @@ class CountsPipeline:
     * ``single_pass=True`` (default on a GPU): ``launch(counts, workspace=ws)`` enqueues one
       ``rss_hash_device_ws`` launch that overwrites ``counts`` itself -- the kernel's last
       workgroup writes them from the zero-initialised ``workspace`` (int64 tensor of
-      ``nqueues + 1``, shared by the steps: their launches run one after another on the
-      caller's stream) -- so a step is one kernel launch and no zeroing launch;
+      ``_native.counts_workspace_bytes(htable, nqueues) // 8`` -- the library's own size --
+      shared by the steps: their launches run one after another on the caller's stream) --
+      so a step is one kernel launch and no zeroing launch; it needs ``htable``;
     * ``single_pass=False``: the pipeline zeroes ``counts`` and ``launch(counts)``
       enqueues one pass that accumulates into them.
 
-    ``counts`` is an int64 tensor of ``nqueues``.
+    ``counts`` is an int64 tensor of ``nqueues`` -- of ``_native.queue_modulus(htable,
+    nqueues)[1]`` (= min(htable, nqueues): no queue >= htable exists) when ``htable`` is given.
 
     How each step's all-reduce is issued (``allreduce``):
 
@@ -112,7 +114,7 @@ class CountsPipeline:
     """
 
     def __init__(self, nqueues, device, group=None, single_pass=None, allreduce="overlap",
-                 comm=None, bucket=1):
+                 comm=None, bucket=1, htable=None):
         if allreduce not in ("overlap", "stream", "rccl"):
             raise ValueError("allreduce must be overlap, stream or rccl")
         if allreduce == "rccl" and comm is None:
@@ -121,14 +123,24 @@ class CountsPipeline:
         if bucket < 1:
             raise ValueError("bucket must be >= 1")
         device = torch.device(device)
+        if single_pass is None:
+            single_pass = device.type == "cuda"
+        if single_pass and htable is None:
+            raise ValueError("single_pass counts need htable: the workspace is sized by "
+                             "_native.counts_workspace_bytes(htable, nqueues)")
+        ws_len = None
+        if htable is not None:
+            from rss_simulator_nvidia_amd import _native
+            if single_pass:
+                ws_len = _native.counts_workspace_bytes(htable, nqueues) // 8
+            nqueues = _native.queue_modulus(htable, nqueues)[1]
+        self.nqueues = nqueues
         self.bucket = bucket
         self.buckets = [torch.zeros(bucket, nqueues, dtype=torch.int64, device=device)
                         for _ in range(2)]
         # buffers[k * bucket + r] = row r of bucket k (bucket=1: the two count buffers)
         self.buffers = [b[r] for b in self.buckets for r in range(bucket)]
-        if single_pass is None:
-            single_pass = device.type == "cuda"
-        self.workspace = (torch.zeros(nqueues + 1, dtype=torch.int64, device=device)
+        self.workspace = (torch.zeros(ws_len, dtype=torch.int64, device=device)
                           if single_pass else None)
         self.pending = [None, None]
         self._open = 0   # rows of the current bucket written and not yet exchanged

@@ -22,7 +22,7 @@ import numpy as np
 import pandas as pd
 from pandas.errors import ParserError as pd_ParserError
 
-from rss_simulator_nvidia_amd import histogram
+from rss_simulator_nvidia_amd import _native, histogram
 from rss_simulator_nvidia_amd.column_names import INPUT_COLUMNS, ColumnNames
 from rss_simulator_nvidia_amd.exceptions import ParseException
 from rss_simulator_nvidia_amd.ingest import pack_frame, pack_frame6
@@ -50,6 +50,7 @@ class Simulator(object):
         self.__queue_num = queue_number
         self.__queues = None
         self.__counts = None
+        self.__count_rows = None  # sparse (queue, count) rows when queues are the hashes
 
     @property
     def data_frame(self):
@@ -88,13 +89,20 @@ class Simulator(object):
             # the reference's DataFrame.apply on zero rows fails the same way
             raise ValueError("Cannot set a DataFrame with multiple columns to the single column "
                              "hash_result")
+        H, Q = self.__hash_table_size, self.__queue_num
+        sparse = _native.queues_are_hashes(H, Q, self.__reta)
+        if sparse:  # H, Q >= 2**32: hash % H % Q = hash (simulator.py:97); hashes only
+            H = Q = 1
         if self.__ipv6:
-            h, q, c = self.__toeplitz.compute_queues6(pack_frame6(df), self.__hash_table_size,
-                                                      self.__queue_num, self.__reta)
+            h, q, c = self.__toeplitz.compute_queues6(pack_frame6(df), H, Q, self.__reta)
         else:
-            h, q, c = self.__toeplitz.compute_queues(pack_frame(df), self.__hash_table_size,
-                                                     self.__queue_num, self.__reta)
+            h, q, c = self.__toeplitz.compute_queues(pack_frame(df), H, Q, self.__reta)
         df[_HASH] = h.astype(np.int64)
+        self.__count_rows = None
+        if sparse:  # a 2**32-entry histogram: the non-empty queues only (value_counts)
+            q, c = h, None
+            values, freq = np.unique(h, return_counts=True)
+            self.__count_rows = [(int(v), int(f)) for v, f in zip(values, freq)]
         self.__queues = q
         self.__counts = c
 
@@ -106,6 +114,8 @@ class Simulator(object):
 
     def queue_count_rows(self):
         """``[(queue, count)]`` for non-empty queues, ascending (value_counts().sort_index())."""
+        if self.__count_rows is not None:
+            return self.__count_rows
         counts = self.__counts
         nz = np.flatnonzero(counts)
         return [(int(q), int(counts[q])) for q in nz]

@@ -52,13 +52,37 @@ MS_VECTORS = [
 SWEEP = [(h, q) for h in (128, 512) for q in (8, 16, 24, 64)] + [(100, 7), (1000, 3), (1, 1), (65536, 1000)]
 
 
+def assert_reference_module(mod, ref=REF):
+    """Refuse to generate anything unless ``mod`` was imported from the reference tree.
+
+    This repository ships its own ``rss_simulator`` import shim (a re-export of the build):
+    a path mishap that imported it instead would make every fixture a self-comparison."""
+    path = os.path.realpath(getattr(mod, "__file__", "") or "")
+    root = os.path.realpath(ref) + os.sep
+    if not path.startswith(root):
+        raise RuntimeError("golden generator: %s was imported from %r, not from the reference "
+                           "tree %r; refusing to generate fixtures" % (mod.__name__, path, root))
+    return path
+
+
+# the same check inside every CLI subprocess (run_cli), before the reference's main runs
+GUARD_EXIT = 97
+CLI_GUARD = ("import os, rss_simulator\n"
+             "if not os.path.realpath(rss_simulator.__file__).startswith("
+             "os.path.realpath(%r) + os.sep):\n"
+             "    sys.stderr.write('golden generator guard: rss_simulator from %%s\\n' %% "
+             "rss_simulator.__file__)\n"
+             "    sys.exit(%d)\n" % (REF, GUARD_EXIT))
+
+
 def import_reference():
     env_ns = {}
     exec(SHIM, env_ns)
-    from rss_simulator.toeplitz import Toeplitz  # noqa: E402
-    from rss_simulator.simulator import Simulator  # noqa: E402
-    from rss_simulator.hash_key import HashKey  # noqa: E402
-    return Toeplitz, Simulator, HashKey
+    import rss_simulator  # noqa: E402
+    from rss_simulator import hash_key, simulator, toeplitz  # noqa: E402
+    for mod in (rss_simulator, toeplitz, simulator, hash_key):
+        assert_reference_module(mod)
+    return toeplitz.Toeplitz, simulator.Simulator, hash_key.HashKey
 
 
 def ip_str(n):
@@ -70,9 +94,12 @@ def key_text(kb):
 
 
 def run_cli(args, cwd):
-    code = SHIM + "sys.argv = ['rss-simulator'] + %r\nfrom rss_simulator import main\nmain()\n" % (args,)
+    code = (SHIM + CLI_GUARD +
+            "sys.argv = ['rss-simulator'] + %r\nfrom rss_simulator import main\nmain()\n" % (args,))
     env = dict(os.environ, PYTHONDONTWRITEBYTECODE="1", MPLBACKEND="Agg")
     p = subprocess.run([sys.executable, "-c", code], cwd=cwd, capture_output=True, text=True, env=env)
+    if p.returncode == GUARD_EXIT and "golden generator guard" in p.stderr:
+        raise RuntimeError(p.stderr.strip())
     if "Traceback" not in p.stderr:
         return p.returncode, p.stdout, p.stderr  # argparse usage errors: keep them whole
     err_lines = [ln for ln in p.stderr.strip().splitlines() if ln.strip()]

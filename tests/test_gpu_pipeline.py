@@ -26,7 +26,7 @@ def test_counts_pipeline_steps_equal_oracle(oracle_lib, example_key, single_pass
         batches.append((torch.from_numpy(host.view(np.int32).reshape(-1)).to(dev),
                         oracle_lib.run(example_key, host, H, Q, want_hash=False,
                                        want_queue=False)[2]))
-    pipe = CountsPipeline(Q, dev, single_pass=single_pass)
+    pipe = CountsPipeline(Q, dev, single_pass=single_pass, htable=H)
     assert (pipe.workspace is not None) == single_pass
     prev = None
     for i in range(11):

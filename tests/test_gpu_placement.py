@@ -91,7 +91,7 @@ def test_counts_pipeline_steps_a_resident_batch(oracle_lib, example_key):
     key = _native.prepare_key(example_key)
     s = torch.cuda.current_stream(dev).cuda_stream
     batch = ResidentBatch(n, key, H, Q, device=dev, placement=(1, 2))
-    pipe = CountsPipeline(Q, dev)
+    pipe = CountsPipeline(Q, dev, htable=H)
     assert pipe.workspace is not None
     for first in (0, n, 2 * n, 0):
         _native.generate_device(11, first, n, batch.tuples.data_ptr(), s)

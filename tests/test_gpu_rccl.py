@@ -66,7 +66,7 @@ def _rccl_worker(rank, port, key, n, htable, nqueues, out_dir):
         from rss_simulator_nvidia_amd.sharding import CountsPipeline
         comm = RcclComm(dev)
         assert (comm.rank, comm.world) == (0, 1)
-        pipe = CountsPipeline(nqueues, dev, allreduce="rccl", comm=comm)
+        pipe = CountsPipeline(nqueues, dev, allreduce="rccl", comm=comm, htable=htable)
         k = _native.prepare_key(key)
         for _ in range(5):
             c3 = pipe.step(lambda c, workspace: _native.hash_device(
@@ -75,7 +75,8 @@ def _rccl_worker(rank, port, key, n, htable, nqueues, out_dir):
         c3 = pipe.drain()
         # bucketed (the bench's N > 1 default): one ncclAllReduce per [3, Q] bucket, a
         # drain between phases closes a partly filled one
-        pipe_b = CountsPipeline(nqueues, dev, allreduce="rccl", comm=comm, bucket=3)
+        pipe_b = CountsPipeline(nqueues, dev, allreduce="rccl", comm=comm, bucket=3,
+                                htable=htable)
         rows = []
         for steps in (2, 5):
             for _ in range(steps):

@@ -94,3 +94,39 @@ def test_cli_both_beyond_u32_is_a_usage_error(golden_dir, capsys):
               "--ips-file", "x.csv", "--htable-size", str(U32), "--num-queues", str(U32)])
     assert exc.value.code == 2
     assert "both >= 2**32" in capsys.readouterr().err
+
+
+@pytest.mark.parametrize("H,Q,want", [(128, 129, (128, 128)), (128, 20000, (128, 128)),
+                                      (128, 300000, (128, 128)), (128, 4 * 10 ** 9, (128, 128)),
+                                      (128, U32 + 1, (128, 128)), (128, 24, (128, 24)),
+                                      (128, 128, (128, 128)), (U32 - 1, U32, (U32 - 1, U32 - 1))])
+def test_counts_sized_by_min_of_htable_and_queues(H, Q, want):
+    """VERDICT r02 "Fix the Q >= H path": queue = bucket % Q < min(H, Q) (simulator.py:96-98),
+    so every count vector is min(H, Q) long -- not 32 GB for --num-queues 4e9."""
+    assert _native.queue_modulus(H, Q) == want
+    h2, q2 = want
+    for h in HASHES[:200]:
+        assert h % h2 % q2 == h % H % Q
+
+
+def test_cli_both_beyond_u32_csv_counts_hashes(golden_dir, tmp_path, monkeypatch, oracle_lib):
+    """--csv with htable and num-queues both >= 2**32: queue = hash (the reference's pandas
+    arithmetic), counted sparsely on the host (no usage error in CSV mode)."""
+    import pandas as pd
+    ctx = RecordingContext(oracle_lib)
+    monkeypatch.setattr(_native, "default_context", lambda: ctx)
+    out = tmp_path / "o.csv"
+    main(["--key-file", os.path.join(golden_dir, "example_input", "hash_key.txt"),
+          "--ips-file", os.path.join(golden_dir, "example_input", "ips.csv"),
+          "--htable-size", str(U32 + 5), "--num-queues", str(2 ** 40), "--csv", str(out)])
+    text = out.read_text().splitlines()
+    start = text.index("src_ip,dst_ip,src_port,dst_port,hash_result,queue_number")
+    body = pd.read_csv(out, skiprows=start)
+    assert (body.queue_number == body.hash_result).all()
+    ref_path = os.path.join(golden_dir, "example", "out_h128_q24.csv")
+    ref = pd.read_csv(ref_path, skiprows=open(ref_path).read().splitlines().index(text[start]))
+    assert (body.hash_result == ref.hash_result).all()
+    counts = pd.read_csv(out, nrows=start - 1)
+    want = body.hash_result.value_counts().sort_index()
+    assert list(counts.queue_number) == list(want.index)
+    assert list(counts.counts) == list(want.values)

@@ -87,10 +87,18 @@ def test_argument_validation_before_any_device_work(lib, example_key):
         _native.hash_device(key, 0, 16, 128, 0)
     with pytest.raises(DeviceError, match="tuples is NULL"):
         _native.hash_device(key, None, 16, 128, 24)
-    with pytest.raises(DeviceError, match="QUEUE_U8 needs nqueues <= 256"):
+    with pytest.raises(DeviceError, match=r"QUEUE_U8 needs min\(htable, nqueues\) <= 256"):
         _native.hash_device(key, 0, 0, 1024, 257, None, None, None, _native.FLAG_QUEUE_U8)
-    with pytest.raises(DeviceError, match="QUEUE_U16 needs nqueues <= 65536"):
+    with pytest.raises(DeviceError, match=r"QUEUE_U16 needs min\(htable, nqueues\) <= 65536"):
         _native.hash_device(key, 0, 0, 2**20, 65537, None, None, None, _native.FLAG_QUEUE_U16)
+    # queues are < min(htable, nqueues): a u8 column holds them for any nqueues when
+    # htable <= 256 (the queue step is sized by min(Q, H)) -- validated, no error
+    # before the (absent) device is needed for n = 0
+    for q in (257, 20000, 2**32 - 1):
+        try:
+            _native.hash_device(key, 0, 0, 128, q, None, None, None, _native.FLAG_QUEUE_U8)
+        except DeviceError as err:
+            assert "QUEUE_U8" not in str(err), err
     empty = _native.RssKey()
     with pytest.raises(DeviceError, match="key not prepared"):
         _native.hash_device(empty, 0, 16, 128, 24)

@@ -11,7 +11,7 @@ def test_resident_batch_refuses_bad_sizes(example_key):
     with pytest.raises(ValueError):
         ResidentBatch(0, key, 128, 24, device="cpu")
     with pytest.raises(ValueError):
-        ResidentBatch(16, key, 128, 300, device="cpu", queue_width="u8")
+        ResidentBatch(16, key, 1024, 300, device="cpu", queue_width="u8")  # 300 queues
     with pytest.raises(ValueError):
         ResidentBatch(16, key, 128, 24, device="cpu", queue_width="u64")
     with pytest.raises(ValueError):
