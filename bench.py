@@ -90,6 +90,15 @@ def parse_args():
                    help="untimed launches of each secondary line's own mode before its timed ones")
     p.add_argument("--profile-dir", default=os.path.join(ROOT, "profiles"),
                    help="where committed rocprofv3 PMC summaries (traffic) are looked up")
+    p.add_argument("--configs3-tuples", type=int, default=1 << 30, metavar="T",
+                   help="BASELINE configs[3]: T global tuples split over the ranks by "
+                        "sharding.shard_range, one RCCL all-reduce of the counts per batch "
+                        "(the `configs3` block; 0 = skip)")
+    p.add_argument("--configs3-steps", type=int, default=0, metavar="K",
+                   help="timed configs[3] batches (default 0 = --steps)")
+    p.add_argument("--no-verify", action="store_true",
+                   help="skip the untimed check of the timed work against "
+                        "tests/golden/bench_digest.npz")
     return p.parse_args()
 
 
@@ -228,6 +237,206 @@ def load_traffic(profile_dir, n, htable, queues, queue_width):
             (n, htable, queues, queue_width):
         return rec.get("hbm_bytes_per_launch")
     return None
+
+
+# ------------------------------------------------------ output verification --
+DIGEST_PATH = os.path.join(ROOT, "tests", "golden", "bench_digest.npz")
+DIGEST_BLOCK = 1 << 20   # tuples per digest block (tests/golden/make_bench_digest.py)
+
+
+def load_digest(path=DIGEST_PATH):
+    """The C oracle's digests of the bench stream (tests/golden/make_bench_digest.py), or
+    None when the file is absent."""
+    import numpy as np
+    try:
+        with np.load(path, allow_pickle=False) as d:
+            return {k: d[k] for k in d.files}
+    except OSError:
+        return None
+
+
+def digest_applies(gold, key_bytes, htable, nqueues, distribution):
+    return (gold is not None and distribution == "uniform" and htable == int(gold["htable"])
+            and nqueues == int(gold["queues"]) and list(gold["key"]) == list(key_bytes))
+
+
+def block_digests(torch, hashes, queues, nblocks, block=DIGEST_BLOCK, chunk=64):
+    """Per ``block``-tuple block of the resident outputs (hash_result int32 view, queue_number
+    uint8): ``(hash_xor, hash_wsum, queue_wsum)`` as Python ints -- the XOR of the block's
+    hashes, sum_j hash[j] * (j + 1) mod 2^64 and sum_j queue[j] * (j + 1) mod 2^64, exactly
+    as tests/golden/make_bench_digest.py computes them with numpy.  Sums are split into
+    16-bit halves so no int64 partial sum overflows."""
+    dev = hashes.device
+    w = torch.arange(1, block + 1, dtype=torch.int64, device=dev)
+    hx, hw, qw = [], [], []
+    for b0 in range(0, nblocks, chunk):
+        nb = min(chunk, nblocks - b0)
+        h = hashes[b0 * block:(b0 + nb) * block].view(nb, block)
+        x = h
+        while x.shape[1] > 1:
+            half = x.shape[1] // 2
+            x = torch.bitwise_xor(x[:, :half], x[:, half:2 * half])
+        hx += [v & 0xFFFFFFFF for v in x[:, 0].tolist()]
+        h64 = h.to(torch.int64) & 0xFFFFFFFF
+        lo = ((h64 & 0xFFFF) * w).sum(dim=1).tolist()
+        hi = ((h64 >> 16) * w).sum(dim=1).tolist()
+        hw += [((a << 16) + b) % (1 << 64) for a, b in zip(hi, lo)]
+        del h64
+        q = queues[b0 * block:(b0 + nb) * block].view(nb, block).to(torch.int64)
+        if queues.dtype != torch.uint8:  # int16 / int32 views of u16 / u32 queues
+            q &= 0xFFFF if queues.dtype == torch.int16 else 0xFFFFFFFF
+        qw += [v % (1 << 64) for v in (q * w).sum(dim=1).tolist()]
+    return hx, hw, qw
+
+
+def verify_outputs(torch, gold, hashes, queues, first, n):
+    """Compare the resident outputs of tuples [first, first + n) (the rank's shard of the
+    bench stream) with the golden digests; returns a dict with ``ok`` and what was checked
+    (``ok`` None when the shard is not made of whole digest blocks inside the golden range)."""
+    B = int(gold["block"])
+    if first % B or n % B or first + n > int(gold["total"]):
+        return {"ok": None, "why": "shard not whole %d-tuple blocks of the golden range" % B}
+    b0, nb = first // B, n // B
+    hx, hw, qw = block_digests(torch, hashes, queues, nb, B)
+    bad = [b0 + i for i in range(nb)
+           if (hx[i], hw[i], qw[i]) != (int(gold["hash_xor"][b0 + i]),
+                                        int(gold["hash_wsum"][b0 + i]),
+                                        int(gold["queue_wsum"][b0 + i]))]
+    return {"ok": not bad, "blocks": nb, "first_block": b0, "bad_blocks": bad[:8]}
+
+
+def golden_counts(gold, first, n):
+    """Per-queue counts of tuples [first, first + n) from the golden chunk counts, or None
+    when the range is not made of whole chunks."""
+    C = int(gold["counts_chunk"])
+    if first % C or n % C or first + n > int(gold["total"]):
+        return None
+    return [int(v) for v in gold["counts"][first // C:(first + n) // C].sum(axis=0)]
+
+
+def _okcode(v):
+    """1 / 0 / -1 for a verification record that passed / failed / could not be checked."""
+    if not v or v.get("ok") is None:
+        return -1.0
+    return 1.0 if v["ok"] and v.get("counts_ok") is not False else 0.0
+
+
+def gather_rows(torch, dist, row, device, distributed, world):
+    """Every rank's ``row`` (floats), in rank order (all_gather; rank-local without a group)."""
+    t = torch.tensor(row, dtype=torch.float64, device=device)
+    if not distributed:
+        return [t.tolist()]
+    out = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [o.tolist() for o in out]
+
+
+def run_configs3(args, torch, dist, _native, dev, stream, key, comm, rank, world, distributed,
+                 barrier, qw, qflag, probe, gold):
+    """BASELINE configs[3] as a strong-scaling batch: ``--configs3-tuples`` global tuples of
+    the bench stream split over the ranks by ``sharding.shard_range``; one batch = one
+    ``rss_hash_device_ws`` launch per rank over its resident shard + ONE all-reduce of the
+    batch's counts (``CountsPipeline(bucket=1)``, RCCL on the launch stream under a launcher).
+    Returns the ``configs3`` block of the line (+ this rank's values for ``per_rank``)."""
+    from rss_simulator_nvidia_amd.resident import ResidentBatch
+    from rss_simulator_nvidia_amd.sharding import CountsPipeline, shard_range
+    total, H, Q = args.configs3_tuples, args.htable, args.queues
+    first, n3 = shard_range(total, rank, world)
+    sp = stream.cuda_stream
+
+    def fill(t):
+        if args.distribution == "uniform":
+            _native.generate_device(SEED, first, n3, t.data_ptr(), sp)
+        else:
+            flow_device(torch, t, first, n3, dev)
+
+    # placed like the main line's buffers, with fewer candidates (a 2^30-tuple shard's output
+    # pair is 5 GiB)
+    probe3 = (probe[0], min(8, probe[1]), probe[2]) if len(probe) > 2 else probe
+    batch = ResidentBatch(n3, key, H, Q, device=dev, fill=fill, queue_width=qw,
+                          placement=probe3, stream=stream)
+    allreduce = args.allreduce if distributed else "overlap"
+    pipe = CountsPipeline(Q, dev, single_pass=True, htable=H, allreduce=allreduce, comm=comm,
+                          bucket=1)
+    steps = args.configs3_steps or args.steps
+
+    def launch(c, workspace):
+        batch.hash(counts=c, workspace=workspace)
+
+    for _ in range(max(3, args.warmup)):
+        pipe.step(launch)
+    pipe.drain()
+    barrier()
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    t0 = time.perf_counter()
+    ev[0].record(stream)
+    for _ in range(steps):
+        pipe.step(launch)
+    pipe.flush()
+    ev[1].record(stream)
+    last = pipe.drain()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    step_ms = ev[0].elapsed_time(ev[1]) / steps  # launch + exchange, on the launch stream
+    # the kernel alone (no collective), one event pair around `steps` launches
+    local = torch.zeros(batch.counts_len, dtype=torch.int64, device=dev)
+    ev[2].record(stream)
+    for _ in range(steps):
+        batch.hash(counts=local)
+    ev[3].record(stream)
+    torch.cuda.synchronize()
+    kernel_ms = ev[2].elapsed_time(ev[3]) / steps
+    stats = torch.tensor([elapsed, step_ms, kernel_ms, float(n3)], dtype=torch.float64,
+                         device=dev if args.dist_backend == "nccl" else "cpu")
+    if distributed:
+        dist.all_reduce(stats, op=dist.ReduceOp.MAX)
+    elapsed_max, step_max, kernel_max, n3_max = (float(x) for x in stats.tolist())
+    counts = [int(x) & ((1 << 64) - 1) for x in last.tolist()]
+    if sum(counts) != total:
+        raise SystemExit("bench: configs[3] counts sum to %d, expected %d" % (sum(counts), total))
+    verified = None
+    if gold is not None:
+        verified = verify_outputs(torch, gold, batch.hashes, batch.queue_view(), first, n3)
+        want = golden_counts(gold, 0, total)
+        verified["counts_ok"] = None if want is None else counts[:len(want)] == want
+    write_bytes = HASH_BYTES + QUEUE_BYTES[qw]
+    achieved = n3_max * (READ_BYTES + write_bytes) / (kernel_max / 1e3) / 1e9
+    out = {
+        "workload": "configs[3]: %d global synthetic 4-tuples split over %d rank(s) by "
+                    "sharding.shard_range (contiguous shards), htable=%d, queues=%d; one batch "
+                    "= one rss_hash_device_ws launch per rank + ONE %s of the batch's uint64[%d] "
+                    "counts" % (total, world, H, Q,
+                                {"rccl": "ncclAllReduce (rccl.RcclComm, launch stream)",
+                                 "overlap": "torch.distributed all-reduce" if distributed
+                                 else "local histogram (no process group)",
+                                 "stream": "torch.distributed all-reduce"}[allreduce], Q),
+        "global_tuples": total,
+        "tuples_per_rank_max": int(n3_max),
+        "steps": steps,
+        "scaling": "strong",
+        "ms_per_batch": elapsed_max * 1e3 / steps,
+        "tuples_per_s": total * steps / elapsed_max,
+        "step_ms_max_rank": step_max,
+        "kernel_ms_max_rank": kernel_max,
+        "exchange_ms_est": step_max - kernel_max,
+        "timing": "ms_per_batch = wall time of the timed batches (barrier + synchronize on "
+                  "both sides, slowest rank) / steps; step_ms = one HIP event pair on the "
+                  "launch stream around the timed batches (launch + all-reduce); kernel_ms = "
+                  "the same number of launches without the collective, after the region",
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "bytes_per_tuple": READ_BYTES + write_bytes},
+        "placement_rank0": dict(batch.report),
+        "verified": verified,
+        "kernel_ms_rank": kernel_ms,
+        "placement_rank": {"chosen_ms": batch.report["chosen_ms"],
+                           "first_allocation_ms": batch.report["first_allocation_ms"]},
+    }
+    del batch, pipe, local
+    torch.cuda.empty_cache()
+    return out
 
 
 # ------------------------------------------------------------------- main -----
@@ -383,7 +592,11 @@ def main():
         from rss_simulator_nvidia_amd.rccl import RcclComm, RcclError
         try:
             comm = RcclComm(dev)
-        except RcclError as err:  # keep the run: torch.distributed's exchange instead
+        except RcclError as err:
+            if err.stuck:  # an init still blocked inside RCCL: no safe fallback in-process
+                raise SystemExit("bench: RcclComm init timed out (%s); exiting instead of "
+                                 "falling back to torch.distributed on the same RCCL" % err)
+            # a clean failure on every rank: keep the run on torch.distributed's exchange
             print("bench: RcclComm unavailable (%s); --allreduce overlap" % err, file=sys.stderr)
             args.allreduce = "overlap"
     if args.allreduce_bucket < 1:
@@ -510,6 +723,41 @@ def main():
     if distributed:
         dist.all_reduce(stats, op=dist.ReduceOp.MAX)
     elapsed, kernel_ms_max = float(stats[0]), float(stats[1])
+
+    # The timed work itself, checked after the timed region (untimed): the resident outputs
+    # of this rank's shard against the C oracle's per-block digests and the reduced counts
+    # against the oracle's (tests/golden/make_bench_digest.py; simulator.py:94-113).
+    gold = None if args.no_verify else load_digest()
+    verify_ok = digest_applies(gold, key_bytes, H, Q, args.distribution)
+    verified = {"main": None, "configs3": None}
+    if verify_ok:
+        v = verify_outputs(torch, gold, hashes, batch.queue_view(), rank * n, n)
+        want = golden_counts(gold, 0, n * world)
+        v["counts_ok"] = None if want is None else \
+            [int(x) & ((1 << 64) - 1) for x in last.tolist()] == want
+        verified["main"] = v
+
+    # BASELINE configs[3]: 2^30 global tuples split over the ranks (sharding.shard_range),
+    # one batch = one rss_hash_device_ws launch per rank + ONE all-reduce of its counts
+    # (bucket 1) -- the reference's unit of work, one histogram per batch
+    # (simulator.py:100-116) -- strong scaling over N.
+    c3 = None
+    if args.configs3_tuples > 0:
+        c3 = run_configs3(args, torch, dist, _native, dev, stream, key, comm, rank, world,
+                          distributed, barrier, qw, qflag, probe, gold if verify_ok else None)
+        verified["configs3"] = c3.pop("verified")
+
+    # every rank's timings and placement, gathered for the line (rank 0 prints it)
+    row = [float(rank), kernel_ms, placement["chosen_ms"], placement["first_allocation_ms"],
+           c3["kernel_ms_rank"] if c3 else -1.0, c3["placement_rank"]["chosen_ms"] if c3 else -1.0,
+           c3["placement_rank"]["first_allocation_ms"] if c3 else -1.0,
+           _okcode(verified["main"]), _okcode(verified["configs3"])]
+    rows = gather_rows(torch, dist, row, dev if args.dist_backend == "nccl" else "cpu",
+                       distributed, world)
+    # True: every rank's checks passed; False: any failed; None: nothing was checkable
+    codes = [r[7] for r in rows] + ([r[8] for r in rows] if c3 is not None else [])
+    verified_all = False if 0.0 in codes else (True if 1.0 in codes and -1.0 not in codes
+                                               else None)
 
     # secondary lines (rank 0, after the timed region): counts-only mode (12 B/tuple,
     # the HBM-read roofline) and u32 queue outputs (20 B/tuple)
@@ -678,6 +926,22 @@ def main():
             note="resident buffers chosen among the probed candidate allocations before the "
                  "timed region (ResidentBatch); first_allocation_* = the unplaced allocation's "
                  "kernel-only rate")
+        line["per_rank"] = [
+            {"rank": int(r[0]), "kernel_ms": r[1], "chosen_ms": r[2], "first_allocation_ms": r[3],
+             "configs3_kernel_ms": r[4] if c3 else None,
+             "configs3_chosen_ms": r[5] if c3 else None,
+             "configs3_first_allocation_ms": r[6] if c3 else None,
+             "verified_main": {1.0: True, 0.0: False}.get(r[7]),
+             "verified_configs3": {1.0: True, 0.0: False}.get(r[8])} for r in rows]
+        if c3 is not None:
+            c3.pop("kernel_ms_rank", None)
+            c3.pop("placement_rank", None)
+            line["configs3"] = c3
+        line["verification"] = dict(verified, source="tests/golden/bench_digest.npz (C oracle, "
+                                    "tests/golden/make_bench_digest.py): per-2^20-block hash / "
+                                    "queue digests of every rank's resident outputs + the "
+                                    "reduced counts, checked after the timed region")
+        line["verified"] = verified_all
         if flow_ms is not None:
             line["flow_like"] = {
                 "kernel_ms": flow_ms, "tuples_per_s_per_gpu": n / (flow_ms / 1e3),
@@ -686,12 +950,17 @@ def main():
         if extras is not None:
             line["row_f_kernels"] = extras
         print(json.dumps(line), flush=True)
+    if verified_all is False:
+        print("bench: the timed work does not match the oracle's digests (see `verification`)",
+              file=sys.stderr)
     if distributed:
         barrier()  # ranks leave together (rank 0 ran the secondary timings alone)
         if comm is not None:
             torch.cuda.synchronize()
             comm.destroy()
         dist.destroy_process_group()
+    if verified_all is False:
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -114,9 +114,13 @@ int rss_key_select_fields(rss_key* key, uint32_t fields);
  *     (counts[q] = number of tuples with queue q, for q < nqueues).
  * d_tuples: n packed tuples in device memory.  d_hash: n uint32 or NULL.
  * d_queue: n queue numbers or NULL -- uint32 by default, uint16 / uint8 with
- * RSS_FLAG_QUEUE_U16 / RSS_FLAG_QUEUE_U8 (same values, narrower stores; the
- * flag is rejected if nqueues does not fit).  d_counts: nqueues uint64 or NULL;
- * overwritten unless RSS_FLAG_ACCUMULATE.  htable >= 1, nqueues >= 1
+ * RSS_FLAG_QUEUE_U16 / RSS_FLAG_QUEUE_U8 (same values, narrower stores; the flag is
+ * rejected if the queues do not fit).  Every queue is < min(htable, nqueues) (bucket <
+ * htable), so bins, the width check and the counts the kernel writes are sized by
+ * min(htable, nqueues): --num-queues 4e9 with htable 128 fits a u8 column and 128 bins.
+ * d_counts: nqueues uint64 or NULL; overwritten unless RSS_FLAG_ACCUMULATE (entries
+ * [min(htable, nqueues), nqueues) are then zero -- callers may size counts by
+ * min(htable, nqueues) and pass that as nqueues).  htable >= 1, nqueues >= 1
  * (positive_int.py:27).  Launched on `stream` (hipStream_t) on the calling
  * thread's current device.  Any alignment works; 16-byte aligned tuples/hashes
  * (and 4/8/16-byte aligned u8/u16/u32 queues) take the 4-tuples-per-lane path.
@@ -142,6 +146,13 @@ int rss_hash_device(const rss_key* key, const rss_tuple4* d_tuples, size_t n,
  * whose counts are not gathered in LDS bins (more than ~8192 queues) leave the workspace
  * untouched and zero d_counts first as rss_hash_device does.  Results are identical to
  * rss_hash_device's.  With d_counts NULL the workspace is not used (may be NULL).
+ * Hardware assumption (default): the hand-off from the workgroups to the last one uses
+ * relaxed device-scope atomics only -- each workgroup waits for its adds' return values,
+ * then takes its ticket -- relying on gfx950 performing every device-scope atomic at one
+ * coherence point beyond the XCDs' L2s.  That holds on MI355X (stress-tested in
+ * tests/test_gpu_single_pass.py) but is not promised by the HIP memory model;
+ * RSS_WS_ORDER=acqrel in the environment switches to a release ticket + acquire fence
+ * (the model's own hand-off; costs an L2 write-back per workgroup).
  */
 int rss_counts_workspace_bytes(uint32_t nqueues, size_t* out);
 int rss_hash_device_ws(const rss_key* key, const rss_tuple4* d_tuples, size_t n,

@@ -92,7 +92,7 @@ struct LaunchParams {
     void* queue_out;
     unsigned long long* counts;
     unsigned long long* ws;       // single-pass counts workspace (rss_hash_device_ws) or NULL
-    uint32_t accumulate;          // with ws: add into counts instead of overwriting them
+    uint32_t accumulate;          // with ws: fold mode (kFoldAccumulate | kFoldOrdered)
     uint64_t n;
     uint64_t h_m64;     // ceil(2^64 / H) for the non-power-of-two htable path
     uint32_t h_mask;    // H - 1 when H is a power of two
@@ -106,6 +106,8 @@ struct LaunchParams {
     const uint32_t* key_windows;  // key search: nkeys x 96 windows in device memory
     uint32_t q_lo, q_span;        // HIST_RANGE: the queues this pass counts
     uint32_t q_stride;            // key search: row stride of the [keys, nqueues] counts (>= Q)
+    uint32_t tail_rows;           // balanced tail: rows handed out as units (0 = static grid-stride)
+    uint32_t bal_off;             // balanced tail: byte offset of its LDS slot (dynamic LDS)
     uint16_t reta[kRetaMax];      // QM_TABLE: queue of bucket b (ethtool -X indirection)
 };
 
@@ -302,18 +304,26 @@ __device__ __forceinline__ void store_queue4(void* out, uint64_t g, uint32_t q0,
 // a hipMemsetAsync before the launch).  With one (rss_hash_device_ws, single-pass counts):
 // the totals go into the accumulator ws[1..Q]; the workgroup then takes a ticket (ws[0]),
 // and the last of the gridDim.x workgroups moves the accumulated sums into `counts`
-// (overwriting, or adding when `accumulate`) and leaves the workspace zero for the next
-// launch -- so a batch's counts need no zeroing launch before it.  `flag` is one LDS word
-// the caller no longer reads (its bins, after every lane has summed them).
-// Ordering without fences: device-scope atomics are all performed at one coherence point,
-// and every lane waits for its adds' return values (the asm use below) before the barrier
-// that precedes the ticket, so a ticket is taken only after its workgroup's adds are
-// performed, and the last workgroup's exchanges read every add.  (An agent-scope
-// __threadfence here costs an L2 write-back per workgroup: +90 us per 2^28-tuple launch.)
+// (overwriting, or adding when `mode & kFoldAccumulate`) and leaves the workspace zero for
+// the next launch -- so a batch's counts need no zeroing launch before it.  `flag` is one
+// LDS word the caller no longer reads (its bins, after every lane has summed them).
+// Ordering.  Default: no fences.  The workspace is touched only by device-scope atomics,
+// which gfx950 performs at one coherence point past the XCDs' L2s, and every lane waits for
+// its adds' return values (the asm use below) before the barrier that precedes the ticket:
+// a ticket is taken only after its workgroup's adds are performed, so the last workgroup's
+// exchanges read every add.  That is a property of the hardware, not a guarantee of the
+// HIP/AMDGPU memory model (which orders relaxed atomics on different addresses only through
+// release/acquire); include/rss_toeplitz.h states the assumption and
+// tests/test_gpu_single_pass.py stress-tests it.  `mode & kFoldOrdered` (RSS_WS_ORDER=acqrel)
+// takes the ticket with an agent-scope RELEASE and fences the last workgroup with an
+// agent-scope ACQUIRE instead: the memory model's own hand-off, at the price of an L2
+// write-back per workgroup (measured: DESIGN.md §3 "Single-pass counts").
+constexpr uint32_t kFoldAccumulate = 1u, kFoldOrdered = 2u;
+
 template <typename SumOf>
 __device__ __forceinline__ void fold_counts(SumOf sum_of, uint32_t Q, unsigned long long* counts,
-                                            unsigned long long* ws, bool accumulate,
-                                            uint32_t* flag) {
+                                            unsigned long long* ws, uint32_t mode,
+                                            uint32_t* flag, unsigned long long* reset = nullptr) {
     const uint32_t tid = threadIdx.x;
     if (!ws) {
         for (uint32_t q = tid; q < Q; q += blockDim.x) {
@@ -330,14 +340,27 @@ __device__ __forceinline__ void fold_counts(SumOf sum_of, uint32_t Q, unsigned l
         }
     }
     __syncthreads();   // every lane's adds performed, every lane done reading the bins
-    if (tid == 0) *flag = atomicAdd(&ws[0], 1ull) == (unsigned long long)gridDim.x - 1;
+    if (tid == 0) {
+        const unsigned long long ticket =
+            (mode & kFoldOrdered)
+                ? __hip_atomic_fetch_add(&ws[0], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT)
+                : atomicAdd(&ws[0], 1ull);
+        *flag = ticket == (unsigned long long)gridDim.x - 1;
+    }
     __syncthreads();
     if (*flag) {       // uniform across the workgroup
+        if (mode & kFoldOrdered) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        const bool accumulate = (mode & kFoldAccumulate) != 0;
         for (uint32_t q = tid; q < Q; q += blockDim.x) {
             const unsigned long long v = atomicExch(&ws[1 + q], 0ull);  // read + reset
             counts[q] = accumulate ? counts[q] + v : v;
         }
-        if (tid == 0) atomicExch(&ws[0], 0ull);
+        if (tid == 0) {
+            atomicExch(&ws[0], 0ull);
+            // the balanced tail's unit counter (ws[Q + 1]): every workgroup made its last
+            // claim before its ticket, so no claim of this launch can follow the reset
+            if (reset) atomicExch(reset, 0ull);
+        }
     }
 }
 
@@ -380,7 +403,7 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
         // 4 consecutive tuples per lane: 48 B = 3 x dwordx4, 16-B aligned.
         const uint4* __restrict__ src = reinterpret_cast<const uint4*>(p.tuples);
         const uint64_t ngroups = p.n >> 2;
-        for (uint64_t g = gtid; g < ngroups; g += gstride) {
+        auto group = [&](uint64_t g) {
             const uint4 a = src[3 * g + 0];
             const uint4 b = src[3 * g + 1];
             const uint4 c = src[3 * g + 2];
@@ -404,6 +427,39 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
             count_queue<kHist>(bins, q1, col, p);
             count_queue<kHist>(bins, q2, col, p);
             count_queue<kHist>(bins, q3, col, p);
+        };
+        if (p.tail_rows) {
+            // Balanced tail (single-pass launches, DESIGN.md §3 "Balanced tail").  A row is
+            // one grid-stride step of the whole grid (gstride groups).  Rows [0, srows) go
+            // as above, statically; the last tail_rows rows are handed out in order as units
+            // of one workgroup slot (kBlock groups) through the workspace counter ws[Q + 1],
+            // one claim per workgroup in flight (issued one unit ahead), so the XCDs that
+            // stream faster (measured: even XCDs finish ~4 % before odd ones) take more of
+            // the tail and every XCD ends together.  The whole grid still sweeps one window
+            // of the arrays at a time.  The counter is reset by fold_counts' last workgroup.
+            unsigned long long* next = p.ws + 1 + p.Q;
+            unsigned long long* slot = reinterpret_cast<unsigned long long*>(
+                reinterpret_cast<char*>(bins) + p.bal_off);
+            const uint64_t nrows = (ngroups + gstride - 1) / gstride;
+            const uint64_t srows = nrows - p.tail_rows;  // launch_hash: tail_rows < nrows
+            unsigned long long claim = 0;
+            if (tid == 0) claim = atomicAdd(next, 1ull);  // first tail unit, in flight meanwhile
+            for (uint64_t row = 0; row < srows; ++row) group(row * gstride + gtid);
+            if (tid == 0) *slot = claim;
+            __syncthreads();
+            const uint64_t first = srows * gridDim.x, nunits = nrows * gridDim.x;
+            uint64_t u = first + *slot;
+            while (u < nunits) {
+                __syncthreads();  // every lane has read the slot
+                if (tid == 0) claim = atomicAdd(next, 1ull);  // the next unit, during this one
+                const uint64_t g = (u / gridDim.x) * gstride + (u % gridDim.x) * kBlock + tid;
+                if (g < ngroups) group(g);
+                if (tid == 0) *slot = claim;
+                __syncthreads();
+                u = first + *slot;
+            }
+        } else {
+            for (uint64_t g = gtid; g < ngroups; g += gstride) group(g);
         }
         tail_begin = ngroups << 2;
     }
@@ -422,7 +478,7 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
             } else {
                 return bins[q];
             }
-        }, p.Q, p.counts, p.ws, p.accumulate != 0, bins);
+        }, p.Q, p.counts, p.ws, p.accumulate, bins, p.tail_rows ? p.ws + 1 + p.Q : nullptr);
     } else if constexpr (kHist == HIST_RANGE) {
         __syncthreads();
         for (uint32_t r = tid; r < p.q_span; r += kBlock)
@@ -591,7 +647,7 @@ __global__ __launch_bounds__(kBlock, 2) void rss_counts_perm_kernel(const PermPa
         uint32_t s = 0;
         for (uint32_t c = 0; c < kBinCols; ++c) s += bins[q * kBinCols + ((c + q) & (kBinCols - 1))];
         return s;
-    }, p.Q, p.counts, p.ws, p.accumulate != 0, bins);
+    }, p.Q, p.counts, p.ws, p.accumulate, bins);
 }
 
 // Key search: per-queue counts of the same tuples under many
@@ -1409,6 +1465,20 @@ int check_reta(const uint32_t* reta, uint32_t htable, uint32_t nqueues, const ch
     return RSS_OK;
 }
 
+// RSS_WS_ORDER=acqrel: single-pass counts hand off with release/acquire (fold_counts);
+// read at every launch (tens of ns) so one process can A/B both orders on the same buffers
+bool ws_order_acqrel() {
+    const char* e = getenv("RSS_WS_ORDER");
+    return e && strcmp(e, "acqrel") == 0;
+}
+
+// RSS_BALANCE=0: single-pass launches keep the static grid-stride to the end (A/B, tests);
+// read at every launch like RSS_WS_ORDER
+bool balance_enabled() {
+    const char* e = getenv("RSS_BALANCE");
+    return !(e && e[0] == '0');
+}
+
 // RSS_COUNTS_PERM=0 routes counts-only launches to the LUT kernel too (A/B, tests)
 bool counts_perm_enabled() {
     const char* e = getenv("RSS_COUNTS_PERM");
@@ -1421,13 +1491,13 @@ template <int kWords>
 int launch_counts_perm(const uint32_t* window, const void* tuples, uint64_t n, unsigned long long* counts,
                        uint32_t h_mask, uint32_t Q, uint32_t q_mask, uint32_t q_m16, int qmode,
                        uint32_t bin_bytes, int cu_count, hipStream_t stream,
-                       unsigned long long* ws = nullptr, bool accumulate = false) {
+                       unsigned long long* ws = nullptr, uint32_t fold_mode = 0) {
     PermParams<kWords> pp;
     memset(&pp, 0, sizeof pp);
     pp.tuples = static_cast<const uint32_t*>(tuples);
     pp.counts = counts;
     pp.ws = ws;
-    pp.accumulate = accumulate;
+    pp.accumulate = fold_mode;  // kFoldAccumulate | kFoldOrdered
     pp.n = n;
     pp.Q = Q;
     pp.q_mask = q_mask;
@@ -1535,7 +1605,8 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
     p.n = n;
     if (single_pass) {
         p.ws = reinterpret_cast<unsigned long long*>(ws);
-        p.accumulate = (flags & RSS_FLAG_ACCUMULATE) ? 1u : 0u;
+        p.accumulate = ((flags & RSS_FLAG_ACCUMULATE) ? kFoldAccumulate : 0u) |
+                       (ws_order_acqrel() ? kFoldOrdered : 0u);
     }
     if (reta) {
         qmode = QM_TABLE;
@@ -1554,7 +1625,7 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
         counts_perm_enabled())
         return launch_counts_perm<3>(key->window, d_tuples, n, p.counts, p.h_mask, p.Q, p.q_mask,
                                      p.q_m16, qmode, bin_bytes, info.cu_count, stream, p.ws,
-                                     p.accumulate != 0);
+                                     p.accumulate);
     // More queues than LDS bins: count them in ranges.  The first pass runs the hash kernel
     // with shared LDS bins for queues [0, span) and writes the per-tuple outputs -- the
     // queue column into the caller's buffer or, for a counts-only launch, into a stream-
@@ -1608,7 +1679,17 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
     }
     KernelFn fn = h_pow2 ? pick_queue<true>(qmode, hist, qwidth, vec4)
                          : pick_queue<false>(qmode, hist, qwidth, vec4);
-    const uint32_t shmem = bin_bytes + reta_bytes;  // dynamic part; the 128 KiB LUT is static
+    uint32_t shmem = bin_bytes + reta_bytes;  // dynamic part; the 128 KiB LUT is static
+    // Balanced tail (single-pass launches: the workspace holds its unit counter and is used
+    // by one launch at a time): the last ~1/10 of the grid-stride rows handed out per
+    // workgroup slot, so the XCDs finish together.  Needs 8 bytes of LDS beside the bins.
+    const uint64_t rows = (n / 4 + (uint64_t)grid * kBlock - 1) / ((uint64_t)grid * kBlock);
+    const uint32_t bal_off = (shmem + 7u) & ~7u;
+    if (single_pass && vec4 && rows >= 16 && bal_off + 8 <= kBinBytesMax && balance_enabled()) {
+        p.tail_rows = (uint32_t)std::max<uint64_t>(1, rows / 10);
+        p.bal_off = bal_off;
+        shmem = bal_off + 8;
+    }
     hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), shmem, stream, p);
     RSS_HIP_CHECK(hipGetLastError());
     return RSS_OK;
@@ -1957,7 +2038,8 @@ int rss_hash_device(const rss_key* key, const rss_tuple4* d_tuples, size_t n, ui
 int rss_counts_workspace_bytes(uint32_t nqueues, size_t* out) {
     if (!out) return set_error(RSS_EINVAL, "rss_counts_workspace_bytes: NULL argument");
     if (nqueues < 1) return set_error(RSS_EINVAL, "rss_counts_workspace_bytes: nqueues must be >= 1");
-    *out = sizeof(uint64_t) * ((size_t)nqueues + 1);  // ticket + one accumulator per queue
+    // ticket + one accumulator per queue + the balanced tail's unit counter
+    *out = sizeof(uint64_t) * ((size_t)nqueues + 2);
     return RSS_OK;
 }
 

@@ -50,3 +50,61 @@ def test_cpu_share_ignores_torchrun_default_omp(monkeypatch):
     monkeypatch.setenv("OMP_NUM_THREADS", "3")
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
     assert bench.cpu_share() == min(3, free)
+
+
+def _make_bench_digest():
+    import importlib.util
+    import os
+    path = os.path.join(os.path.dirname(__file__), "golden", "make_bench_digest.py")
+    spec = importlib.util.spec_from_file_location("make_bench_digest_under_test", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_block_digests_match_the_generator():
+    """bench.block_digests (torch, what the GPU run computes) == the generator's numpy form,
+    incl. all-ones hashes (the largest partial sums) and u8 / u16 / u32 queue views."""
+    gen = _make_bench_digest()
+    rng = np.random.default_rng(5)
+    B, nb = 1024, 6
+    h = rng.integers(0, 1 << 32, B * nb, dtype=np.uint64).astype(np.uint32)
+    h[:B] = 0xFFFFFFFF
+    for qmax, dt in ((24, torch.uint8), (60000, torch.int16), (3_000_000_000, torch.int32)):
+        q = rng.integers(0, qmax, B * nb, dtype=np.uint64).astype(np.uint32)
+        q[B:2 * B] = qmax - 1
+        want = gen.block_digests_np(h, q, block=B)
+        qv = {torch.uint8: q.astype(np.uint8), torch.int16: q.astype(np.uint16).view(np.int16),
+              torch.int32: q.view(np.int32)}[dt]
+        got = bench.block_digests(torch, torch.from_numpy(h.view(np.int32)),
+                                  torch.from_numpy(qv), nb, block=B, chunk=4)
+        assert got[0] == [int(x) for x in want[0]]
+        assert got[1] == [int(x) for x in want[1]]
+        assert got[2] == [int(x) for x in want[2]]
+
+
+def test_bench_digest_is_pinned_to_the_oracle(oracle_lib, example_key):
+    """The committed digests of blocks 0 and 2047 (first and last 2^20 tuples of the 2^31
+    stream) recomputed here by the C oracle; verify_outputs accepts them and flags one
+    changed hash or queue; the chunk counts cover 2^27 tuples each."""
+    gold = bench.load_digest()
+    assert gold is not None and bench.digest_applies(gold, example_key, 128, 24, "uniform")
+    assert not bench.digest_applies(gold, example_key, 128, 24, "flow")
+    B = int(gold["block"])
+    for b in (0, int(gold["total"]) // B - 1):
+        tup = oracle_lib.generate(bench.SEED, b * B, B)
+        h, q, _ = oracle_lib.run(example_key, tup, 128, 24, fn="oracle_run_tables")
+        ht = torch.from_numpy(h.view(np.int32).copy())
+        qt = torch.from_numpy(q.astype(np.uint8))
+        v = bench.verify_outputs(torch, gold, ht, qt, b * B, B)
+        assert v["ok"] is True and v["blocks"] == 1, v
+        ht[B // 2] ^= 1
+        assert bench.verify_outputs(torch, gold, ht, qt, b * B, B)["bad_blocks"] == [b]
+        ht[B // 2] ^= 1
+        qt[7], qt[8] = qt[8].item(), qt[7].item() + (1 if qt[7] == qt[8] else 0)
+        assert bench.verify_outputs(torch, gold, ht, qt, b * B, B)["ok"] is False
+    assert (gold["counts"].sum(axis=1) == int(gold["counts_chunk"])).all()
+    assert bench.golden_counts(gold, 0, 1 << 28) == \
+        [int(x) for x in gold["counts"][:2].sum(axis=0)]
+    assert bench.golden_counts(gold, 1 << 20, 1 << 27) is None   # not whole chunks
+    assert bench.verify_outputs(torch, gold, ht, qt, 5, B)["ok"] is None

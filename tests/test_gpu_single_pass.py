@@ -34,7 +34,7 @@ def _dev_tuples(host, offset_bytes=0):
 
 def _ws(native, H, Q):
     nbytes = native.counts_workspace_bytes(H, Q)
-    assert nbytes == 8 * (Q + 1)
+    assert nbytes == 8 * (min(H, Q) + 2)  # ticket, sums, balanced-tail counter
     return torch.zeros(nbytes // 8, dtype=torch.int64, device=DEV)
 
 
@@ -278,4 +278,107 @@ def test_stress_one_workspace_many_launches(native, oracle_lib, example_key):
         for i in range(600):
             np.testing.assert_array_equal(got[i], batches[i % 3][2])
         outs.zero_()
+    assert int(ws.abs().sum()) == 0
+
+
+ACQREL_SCRIPT = r"""
+import sys
+import numpy as np
+import torch
+sys.path.insert(0, %(root)r)
+from oracle.oracle import OracleLib
+from rss_simulator_nvidia_amd import _native
+lib = OracleLib()
+key_bytes = %(key)r
+H, Q, n = 128, 24, (1 << 20) + 3
+host = lib.generate(7, 0, n)
+want = lib.run(key_bytes, host, H, Q, want_hash=False, want_queue=False)[2]
+dev = torch.device("cuda:0")
+t = torch.from_numpy(host.view(np.int32).reshape(-1)).to(dev)
+ws = torch.zeros(_native.counts_workspace_bytes(H, Q) // 8, dtype=torch.int64, device=dev)
+outs = torch.zeros((300, Q), dtype=torch.int64, device=dev)
+key = _native.prepare_key(key_bytes)
+s = torch.cuda.current_stream().cuda_stream
+for i in range(300):
+    _native.hash_device(key, t.data_ptr(), n, H, Q, None, None, outs[i].data_ptr(), 0, s,
+                        ws.data_ptr())
+got = outs.cpu().numpy().view(np.uint64)
+assert (got == want[None, :]).all(), "mismatch"
+assert int(ws.abs().sum()) == 0
+print("acqrel ok")
+"""
+
+
+def test_acqrel_ordering_variant(example_key):
+    """RSS_WS_ORDER=acqrel (release ticket + acquire fence, the memory model's own hand-off;
+    ADVICE r02) gives the same counts launch after launch (in a child process, so the
+    variable never leaks into this one)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ACQREL_SCRIPT % {"root": root, "key": list(example_key)}
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240,
+                       env=dict(os.environ, RSS_WS_ORDER="acqrel"))
+    assert p.returncode == 0 and "acqrel ok" in p.stdout, p.stdout + p.stderr
+
+
+@pytest.mark.parametrize("n", [1 << 24, (1 << 24) + 4099, 3 * (1 << 23) + 5, (1 << 25) + 1234567])
+def test_balanced_tail_equals_oracle(native, oracle_lib, example_key, n):
+    """Single-pass launches of >= 16 grid rows hand their last ~1/10 of the rows out per
+    workgroup slot (the balanced tail): every tuple is hashed exactly once --
+    hashes and u8 queues element-wise equal to the oracle, counts exact, launch after launch
+    on one workspace (left zero, its tail counter included) -- and equal to the static
+    grid-stride launch (RSS_BALANCE=0) on the same buffers."""
+    import os
+    H, Q = 128, 24
+    key = native.prepare_key(example_key)
+    s = torch.cuda.current_stream().cuda_stream
+    host = oracle_lib.generate(41, 0, n)
+    h_want, q_want, c_want = oracle_lib.run(example_key, host, H, Q, fn="oracle_run_tables")
+    t = torch.from_numpy(host.view(np.int32).reshape(-1)).to(DEV)
+    ws = _ws(native, H, Q)
+    hashes = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    queues = torch.full((n,), 255, dtype=torch.uint8, device=DEV)
+    outs = torch.zeros((12, Q), dtype=torch.int64, device=DEV)
+    for i in range(12):
+        if i == 6:  # static launches on the same workspace in between
+            os.environ["RSS_BALANCE"] = "0"
+        elif i == 9:
+            os.environ.pop("RSS_BALANCE", None)
+        native.hash_device(key, t.data_ptr(), n, H, Q, hashes.data_ptr(), queues.data_ptr(),
+                           outs[i].data_ptr(), native.FLAG_QUEUE_U8, s, ws.data_ptr())
+    os.environ.pop("RSS_BALANCE", None)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(hashes.cpu().numpy().view(np.uint32), h_want)
+    np.testing.assert_array_equal(queues.cpu().numpy(), q_want.astype(np.uint8))
+    got = outs.cpu().numpy().view(np.uint64)
+    for i in range(12):
+        np.testing.assert_array_equal(got[i], c_want)
+    assert int(ws.abs().sum()) == 0
+
+
+def test_balanced_tail_stress(native, oracle_lib, example_key):
+    """300 back-to-back balanced single-pass launches of 2^24 + 3 tuples (and 300 of a
+    small batch in between, whose launches keep the static loop) on one workspace: every
+    launch's counts exact."""
+    H, Q = 128, 24
+    key = native.prepare_key(example_key)
+    s = torch.cuda.current_stream().cuda_stream
+    batches = []
+    for seed, n in ((5, (1 << 24) + 3), (6, 4099)):
+        host = oracle_lib.generate(seed, 0, n)
+        want = oracle_lib.run(example_key, host, H, Q, want_hash=False, want_queue=False,
+                              fn="oracle_run_tables")[2]
+        batches.append((n, torch.from_numpy(host.view(np.int32).reshape(-1)).to(DEV), want))
+    ws = _ws(native, H, Q)
+    h = torch.empty((1 << 24) + 3, dtype=torch.int32, device=DEV)
+    outs = torch.zeros((600, Q), dtype=torch.int64, device=DEV)
+    for i in range(600):
+        n, t, _ = batches[i % 2]
+        native.hash_device(key, t.data_ptr(), n, H, Q, h.data_ptr() if i % 4 < 2 else None,
+                           None, outs[i].data_ptr(), 0, s, ws.data_ptr())
+    got = outs.cpu().numpy().view(np.uint64)
+    for i in range(600):
+        np.testing.assert_array_equal(got[i], batches[i % 2][2])
     assert int(ws.abs().sum()) == 0

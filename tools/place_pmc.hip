@@ -34,6 +34,102 @@
         }                                                                                  \
     } while (0)
 
+// The bench's byte mix without hashing (12 B read, 4 + 1 B written with nt stores,
+// grid-stride, 4 tuples per lane -- the product kernel's access shape), recording for every
+// workgroup its XCD (HW_REG_XCC_ID) and its start / end wall clock (100 MHz): does a slow
+// placement slow every XCD, or do some XCDs finish late while the others idle?
+__global__ __launch_bounds__(1024) void stream_trace(const uint4* __restrict__ src,
+                                                     uint32_t* __restrict__ hash_out,
+                                                     uint32_t* __restrict__ queue_out, uint64_t n,
+                                                     unsigned long long* rec) {
+    __shared__ unsigned long long t0;
+    if (threadIdx.x == 0) t0 = wall_clock64();
+    __syncthreads();
+    const uint64_t ng = n >> 2;
+    for (uint64_t g = (uint64_t)blockIdx.x * 1024 + threadIdx.x; g < ng; g += (uint64_t)gridDim.x * 1024) {
+        const uint4 a = src[3 * g], b = src[3 * g + 1], c = src[3 * g + 2];
+        uint32_t* o = hash_out + 4 * g;
+        __builtin_nontemporal_store(a.x ^ a.y ^ a.z, o);
+        __builtin_nontemporal_store(a.w ^ b.x ^ b.y, o + 1);
+        __builtin_nontemporal_store(b.z ^ b.w ^ c.x, o + 2);
+        __builtin_nontemporal_store(c.y ^ c.z ^ c.w, o + 3);
+        __builtin_nontemporal_store((a.x ^ c.w) & 0x17171717u, queue_out + g);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        rec[3 * blockIdx.x + 0] = xcc & 0xFu;
+        rec[3 * blockIdx.x + 1] = t0;
+        rec[3 * blockIdx.x + 2] = wall_clock64();
+    }
+}
+
+// The same stream with its tail balanced between workgroups: rows (one grid-stride step
+// of the whole grid) [0, static_rows) are processed as above; the rest are handed out as
+// units (one row x one workgroup slot = 1024 lane-groups) in increasing order through a
+// global counter, one claim per workgroup in flight (prefetched one unit ahead), so a
+// workgroup (an XCD) that streams faster takes more of the tail.  ctl[0] = next unit,
+// ctl[1] = workgroups done; the last workgroup to finish resets both (self-resetting).
+// rec as stream_trace, plus rec[3 * gridDim.x + w] = units workgroup w claimed.
+__global__ __launch_bounds__(1024) void stream_bal(const uint4* __restrict__ src,
+                                                   uint32_t* __restrict__ hash_out,
+                                                   uint32_t* __restrict__ queue_out, uint64_t n,
+                                                   unsigned long long* rec,
+                                                   unsigned long long* ctl, uint64_t static_rows) {
+    __shared__ unsigned long long t0, s_unit;
+    const uint32_t tid = threadIdx.x;
+    if (tid == 0) t0 = wall_clock64();
+    const uint64_t ng = n >> 2;
+    const uint64_t G = (uint64_t)gridDim.x * 1024;
+    const uint64_t nrows = (ng + G - 1) / G;
+    const uint64_t srows = static_rows < nrows ? static_rows : nrows;
+    const uint64_t first_unit = srows * gridDim.x, nunits = nrows * gridDim.x;
+    auto body = [&](uint64_t g) {
+        const uint4 a = src[3 * g], b = src[3 * g + 1], c = src[3 * g + 2];
+        uint32_t* o = hash_out + 4 * g;
+        __builtin_nontemporal_store(a.x ^ a.y ^ a.z, o);
+        __builtin_nontemporal_store(a.w ^ b.x ^ b.y, o + 1);
+        __builtin_nontemporal_store(b.z ^ b.w ^ c.x, o + 2);
+        __builtin_nontemporal_store(c.y ^ c.z ^ c.w, o + 3);
+        __builtin_nontemporal_store((a.x ^ c.w) & 0x17171717u, queue_out + g);
+    };
+    unsigned long long claim = 0;
+    if (tid == 0) claim = atomicAdd(&ctl[0], 1ull);  // first tail unit, in flight meanwhile
+    for (uint64_t row = 0; row < srows; ++row) {
+        const uint64_t g = row * G + (uint64_t)blockIdx.x * 1024 + tid;
+        if (g < ng) body(g);
+    }
+    if (tid == 0) s_unit = claim;
+    __syncthreads();
+    uint64_t u = first_unit + s_unit;
+    uint64_t mine = 0;
+    while (u < nunits) {
+        __syncthreads();  // every lane has read s_unit
+        if (tid == 0) claim = atomicAdd(&ctl[0], 1ull);  // the next unit, while this one streams
+        const uint64_t g = (u / gridDim.x) * G + (u % gridDim.x) * 1024 + tid;
+        if (g < ng) body(g);
+        ++mine;
+        if (tid == 0) s_unit = claim;
+        __syncthreads();
+        u = first_unit + s_unit;
+    }
+    if (tid == 0) {
+        // this workgroup's last claim was past the end: it claims no more; the last one
+        // to get here resets the counters for the next launch
+        if (atomicAdd(&ctl[1], 1ull) == gridDim.x - 1) {
+            atomicExch(&ctl[0], 0ull);
+            atomicExch(&ctl[1], 0ull);
+        }
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        rec[3 * blockIdx.x + 0] = xcc & 0xFu;
+        rec[3 * blockIdx.x + 1] = t0;
+        rec[3 * blockIdx.x + 2] = wall_clock64();
+        rec[3 * gridDim.x + blockIdx.x] = mine;
+    }
+}
+
 int main(int argc, char** argv) {
     const int K = argc > 1 ? atoi(argv[1]) : 12;      // output pairs
     const int R = argc > 2 ? atoi(argv[2]) : 5;       // timed launches per mode
@@ -96,6 +192,121 @@ int main(int argc, char** argv) {
         std::sort(t.begin(), t.end());
         return t[R / 2];
     };
+
+    const bool baltrace = argc > 4 && strcmp(argv[4], "balance") == 0;
+    if (baltrace) {
+        // per candidate: static stream vs tail-balanced stream at several static fractions
+        // (same buffers, alternating), per-XCD last end and units taken
+        int cus = 0;
+        CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+        unsigned long long *rec, *ctl;
+        CK(hipMalloc(&rec, (size_t)cus * 4 * 8));
+        CK(hipMalloc(&ctl, 16));
+        CK(hipMemset(ctl, 0, 16));
+        std::vector<unsigned long long> h(cus * 4);
+        const uint64_t G = (uint64_t)cus * 1024, nrows = ((n >> 2) + G - 1) / G;
+        const double fracs[4] = {1.0, 0.95, 0.90, 0.85};
+        auto summarize = [&](const char* name, float ms, bool units) {
+            CK(hipMemcpy(h.data(), rec, h.size() * 8, hipMemcpyDeviceToHost));
+            unsigned long long tmin = ~0ull;
+            for (int w = 0; w < cus; ++w) tmin = std::min(tmin, h[3 * w + 1]);
+            double last[8] = {0};
+            unsigned long long u[8] = {0};
+            for (int w = 0; w < cus; ++w) {
+                const int x = (int)(h[3 * w] & 7);
+                last[x] = std::max(last[x], (h[3 * w + 2] - tmin) / 100.0);
+                if (units) u[x] += h[3 * cus + w];
+            }
+            printf("  %-16s %.4f ms  last:", name, ms);
+            for (int x = 0; x < 8; ++x) printf(" %.1f", last[x]);
+            if (units) {
+                printf("  units:");
+                for (int x = 0; x < 8; ++x) printf(" %llu", u[x]);
+            }
+            printf("\n");
+        };
+        int cand = 0;
+        for (int i = 0; i < 2; ++i)
+            for (int k = 0; k < K; ++k, ++cand) {
+                printf("bal cand %d in=%d out=%d full_ms=%.4f rows=%llu\n", cand, i, k,
+                       median_of(i, k, true, true), (unsigned long long)nrows);
+                for (int rep = 0; rep < 2; ++rep)
+                    for (double f : fracs) {
+                        const uint64_t srows = (uint64_t)(f * nrows);
+                        std::vector<float> ts(R);
+                        for (int r = 0; r < R; ++r) {
+                            CK(hipEventRecord(e0, nullptr));
+                            if (f >= 1.0)
+                                hipLaunchKernelGGL(stream_trace, dim3(cus), dim3(1024), 0, nullptr,
+                                                   (const uint4*)in[i], (uint32_t*)hs[k],
+                                                   (uint32_t*)qs[k], n, rec);
+                            else
+                                hipLaunchKernelGGL(stream_bal, dim3(cus), dim3(1024), 0, nullptr,
+                                                   (const uint4*)in[i], (uint32_t*)hs[k],
+                                                   (uint32_t*)qs[k], n, rec, ctl, srows);
+                            CK(hipEventRecord(e1, nullptr));
+                            CK(hipEventSynchronize(e1));
+                            CK(hipEventElapsedTime(&ts[r], e0, e1));
+                        }
+                        std::sort(ts.begin(), ts.end());
+                        char name[32];
+                        snprintf(name, sizeof name, f >= 1.0 ? "static" : "tail %.2f", 1.0 - f);
+                        summarize(name, ts[R / 2], f < 1.0);
+                    }
+                fflush(stdout);
+            }
+        CK(hipFree(rec));
+        CK(hipFree(ctl));
+        return 0;
+    }
+    const bool wgtrace = argc > 4 && strcmp(argv[4], "wgtrace") == 0;
+    if (wgtrace) {
+        // per candidate: the product's full-u8 median, then the traced stream; per XCD the
+        // number of workgroups, their mean duration and the last end, in us from the
+        // earliest start (wall clock: 100 MHz)
+        int cus = 0;
+        CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+        unsigned long long* rec;
+        CK(hipMalloc(&rec, (size_t)cus * 3 * 8));
+        std::vector<unsigned long long> h(cus * 3);
+        int cand = 0;
+        for (int i = 0; i < 2; ++i)
+            for (int k = 0; k < K; ++k, ++cand) {
+                launch(i, k, true, true);
+                launch(i, k, true, true);
+                const float full = median_of(i, k, true, true);
+                std::vector<float> ts(R);
+                for (int r = 0; r < R; ++r) {
+                    CK(hipEventRecord(e0, nullptr));
+                    hipLaunchKernelGGL(stream_trace, dim3(cus), dim3(1024), 0, nullptr,
+                                       (const uint4*)in[i], (uint32_t*)hs[k], (uint32_t*)qs[k], n, rec);
+                    CK(hipEventRecord(e1, nullptr));
+                    CK(hipEventSynchronize(e1));
+                    CK(hipEventElapsedTime(&ts[r], e0, e1));
+                }
+                std::sort(ts.begin(), ts.end());
+                CK(hipMemcpy(h.data(), rec, h.size() * 8, hipMemcpyDeviceToHost));
+                unsigned long long tmin = ~0ull;
+                for (int w = 0; w < cus; ++w) tmin = std::min(tmin, h[3 * w + 1]);
+                double dur[8] = {0}, last[8] = {0};
+                int cnt[8] = {0};
+                for (int w = 0; w < cus; ++w) {
+                    const int x = (int)(h[3 * w] & 7);
+                    cnt[x]++;
+                    dur[x] += (h[3 * w + 2] - h[3 * w + 1]) / 100.0;
+                    last[x] = std::max(last[x], (h[3 * w + 2] - tmin) / 100.0);
+                }
+                printf("wg cand %d in=%d out=%d full_ms=%.4f stream_ms=%.4f xcd:", cand, i, k, full,
+                       ts[R / 2]);
+                for (int x = 0; x < 8; ++x)
+                    printf(" [%d n=%d mean=%.1f last=%.1f]", x, cnt[x], cnt[x] ? dur[x] / cnt[x] : 0.0,
+                           last[x]);
+                printf("\n");
+                fflush(stdout);
+            }
+        CK(hipFree(rec));
+        return 0;
+    }
 
     printf("place_pmc n=%llu K=%d R=%d launches_per_candidate=%d "
            "(2 warm full, %d full, %d hash-only, %d queue-only; rss_toeplitz_kernel only)\n",

@@ -27,7 +27,7 @@ for seed, n in ((1, 1000), (2, (1 << 20) + 3), (3, 1 << 22)):
     host = ora.generate(seed, 0, n)
     want = ora.run(kb, host, H, Q, want_hash=False, want_queue=False)[2]
     batches.append((n, torch.from_numpy(host.view(np.int32).reshape(-1)).to(dev), want))
-ws = torch.zeros(Q + 1, dtype=torch.int64, device=dev)
+ws = torch.zeros(_native.counts_workspace_bytes(H, Q) // 8, dtype=torch.int64, device=dev)
 outs = torch.zeros((600, Q), dtype=torch.int64, device=dev)
 h = torch.empty(1 << 22, dtype=torch.int32, device=dev)
 bad = 0
