@@ -141,18 +141,20 @@ int rss_hash_device(const rss_key* key, const rss_tuple4* d_tuples, size_t n,
  * into the workspace's accumulators and takes a ticket; the last one moves the sums into
  * d_counts -- overwriting them, or adding with RSS_FLAG_ACCUMULATE -- and zeroes the
  * workspace again.  d_workspace: rss_counts_workspace_bytes(nqueues) bytes of 8-byte
- * aligned device memory, zero before its first use (every launch leaves it zero), used
+ * aligned device memory (ticket + one sum per queue + the balanced tail's unit counter),
+ * zero before its first use (every launch leaves it zero), used
  * by one launch at a time (launches that may run concurrently need their own).  Launches
  * whose counts are not gathered in LDS bins (more than ~8192 queues) leave the workspace
  * untouched and zero d_counts first as rss_hash_device does.  Results are identical to
  * rss_hash_device's.  With d_counts NULL the workspace is not used (may be NULL).
- * Hardware assumption (default): the hand-off from the workgroups to the last one uses
- * relaxed device-scope atomics only -- each workgroup waits for its adds' return values,
- * then takes its ticket -- relying on gfx950 performing every device-scope atomic at one
- * coherence point beyond the XCDs' L2s.  That holds on MI355X (stress-tested in
- * tests/test_gpu_single_pass.py) but is not promised by the HIP memory model;
- * RSS_WS_ORDER=acqrel in the environment switches to a release ticket + acquire fence
- * (the model's own hand-off; costs an L2 write-back per workgroup).
+ * Ordering: each workgroup takes its ticket with an agent-scope release and the last one
+ * fences with an agent-scope acquire before reading the sums (the HIP memory model's
+ * hand-off; ~1.5 us per 2^28-tuple launch).  RSS_WS_ORDER=relaxed in the environment drops
+ * both and relies on gfx950 performing every device-scope atomic at one coherence point
+ * beyond the XCDs' L2s (true on MI355X, stress-tested in tests/test_gpu_single_pass.py,
+ * but not promised by the memory model).  Launches of >= 2^24 tuples also take the last
+ * tenth of their work from a counter in the workspace (the balanced tail: the XCDs finish
+ * together), so a workspace must never be shared by two launches in flight.
  */
 int rss_counts_workspace_bytes(uint32_t nqueues, size_t* out);
 int rss_hash_device_ws(const rss_key* key, const rss_tuple4* d_tuples, size_t n,

@@ -307,17 +307,15 @@ __device__ __forceinline__ void store_queue4(void* out, uint64_t g, uint32_t q0,
 // (overwriting, or adding when `mode & kFoldAccumulate`) and leaves the workspace zero for
 // the next launch -- so a batch's counts need no zeroing launch before it.  `flag` is one
 // LDS word the caller no longer reads (its bins, after every lane has summed them).
-// Ordering.  Default: no fences.  The workspace is touched only by device-scope atomics,
-// which gfx950 performs at one coherence point past the XCDs' L2s, and every lane waits for
-// its adds' return values (the asm use below) before the barrier that precedes the ticket:
-// a ticket is taken only after its workgroup's adds are performed, so the last workgroup's
-// exchanges read every add.  That is a property of the hardware, not a guarantee of the
-// HIP/AMDGPU memory model (which orders relaxed atomics on different addresses only through
-// release/acquire); include/rss_toeplitz.h states the assumption and
-// tests/test_gpu_single_pass.py stress-tests it.  `mode & kFoldOrdered` (RSS_WS_ORDER=acqrel)
-// takes the ticket with an agent-scope RELEASE and fences the last workgroup with an
-// agent-scope ACQUIRE instead: the memory model's own hand-off, at the price of an L2
-// write-back per workgroup (measured: DESIGN.md §3 "Single-pass counts").
+// Ordering.  Default (`mode & kFoldOrdered`): the ticket is taken with an agent-scope
+// RELEASE and the last workgroup fences with an agent-scope ACQUIRE before reading the sums
+// -- the HIP/AMDGPU memory model's own hand-off between workgroups.  It costs 1.3-1.5 us per
+// 2^28-tuple launch (tools/ws_order_ab.py; a full __threadfence around the ticket cost
+// 90 us).  RSS_WS_ORDER=relaxed drops both: the workspace is touched only by device-scope
+// atomics, which gfx950 performs at one coherence point past the XCDs' L2s, and every lane
+// waits for its adds' return values (the asm use below) before the barrier that precedes the
+// ticket, so on this hardware the last workgroup's exchanges read every add even without
+// release/acquire (stress-tested both ways in tests/test_gpu_single_pass.py).
 constexpr uint32_t kFoldAccumulate = 1u, kFoldOrdered = 2u;
 
 template <typename SumOf>
@@ -529,6 +527,81 @@ __global__ __launch_bounds__(kBlock) void rss_queue_hist_kernel(const T* __restr
     __syncthreads();
     for (uint32_t r = tid; r < q_span; r += kBlock)
         if (bins[r]) atomicAdd(&counts[q_lo + r], (unsigned long long)bins[r]);
+}
+
+// Queue ranges past the first pass's LDS bins, wide: ONE pass over the queue column per
+// range of up to kWideSpan queues (instead of one per 8192).  Bins are u16 in LDS, two per
+// dword, with a guard bit: the add that returns 0x7FFF (so the bin now holds 0x8000) moves
+// 2^15 out of the bin into the global counts itself.  Exactly one add sees 0x7FFF per wrap,
+// and the bin cannot reach 0x10000 (a carry into its neighbour) before that lane's subtract
+// lands: the other adds in flight meanwhile are bounded by the workgroup's lanes, far below
+// 2^15.  Each workgroup then stores its bins as one row of a u16 [grid][stride] matrix with
+// plain coalesced stores -- not Q atomics per workgroup, which would cost more than the pass
+// at Q = 65536 -- and rss_partial_reduce_kernel sums the rows into the counts.
+constexpr uint32_t kWideSpan = 65536;  // 128 KiB of u16 bins: one workgroup per CU
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void rss_queue_hist_wide_kernel(
+        const T* __restrict__ queues, uint64_t n, uint32_t q_lo, uint32_t q_span,
+        uint32_t* __restrict__ partial, uint32_t stride_words, unsigned long long* counts) {
+    extern __shared__ uint32_t bins[];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t words = (q_span + 1) / 2;
+    for (uint32_t e = tid; e < words; e += kBlock) bins[e] = 0;
+    __syncthreads();
+    const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
+    const uint64_t gstride = (uint64_t)gridDim.x * kBlock;
+    auto add = [&](uint32_t q) {
+        const uint32_t r = q - q_lo;  // wraps for q < q_lo
+        if (r < q_span) {
+            const uint32_t sh = (r & 1u) * 16u;
+            const uint32_t old = __hip_atomic_fetch_add(&bins[r >> 1], 1u << sh, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (((old >> sh) & 0xFFFFu) == 0x7FFFu) {  // this add set the guard bit
+                __hip_atomic_fetch_sub(&bins[r >> 1], 0x8000u << sh, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+                atomicAdd(&counts[q], 0x8000ull);
+            }
+        }
+    };
+    constexpr uint32_t kPer = 16 / sizeof(T);  // queues per 16-B load
+    uint64_t tail = 0;
+    if (((uintptr_t)queues & 15) == 0) {
+        const uint4* __restrict__ v = reinterpret_cast<const uint4*>(queues);
+        const uint64_t nv = n / kPer;
+        for (uint64_t i = gtid; i < nv; i += gstride) {
+            const uint4 x = v[i];
+            const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if constexpr (sizeof(T) == 2) {
+                    add(w[k] & 0xFFFFu);
+                    add(w[k] >> 16);
+                } else {
+                    add(w[k]);
+                }
+            }
+        }
+        tail = nv * kPer;
+    }
+    for (uint64_t i = tail + gtid; i < n; i += gstride) add(queues[i]);
+    __syncthreads();
+    uint32_t* row = partial + (size_t)blockIdx.x * stride_words;
+    for (uint32_t e = tid; e < words; e += kBlock) row[e] = bins[e];
+}
+
+// counts[q_lo + q] += sum over the rows of the u16 partial matrix (column q); one thread per
+// queue, rows read coalesced across the threads.  The wide pass's guard-bit adds have landed
+// already (previous launch on the stream), so a plain read-modify-write suffices.
+__global__ __launch_bounds__(256) void rss_partial_reduce_kernel(const uint16_t* __restrict__ partial,
+                                                                 uint32_t rows, uint32_t stride,
+                                                                 uint32_t q_lo, uint32_t q_span,
+                                                                 unsigned long long* counts) {
+    const uint32_t q = blockIdx.x * 256 + threadIdx.x;
+    if (q >= q_span) return;
+    unsigned long long s = 0;
+    for (uint32_t r = 0; r < rows; ++r) s += partial[(size_t)r * stride + q];
+    if (s) counts[q_lo + q] += s;
 }
 
 // Counts only, power-of-two H <= 256 (histogram mode, `rss_hash_host` without per-tuple
@@ -1465,11 +1538,12 @@ int check_reta(const uint32_t* reta, uint32_t htable, uint32_t nqueues, const ch
     return RSS_OK;
 }
 
-// RSS_WS_ORDER=acqrel: single-pass counts hand off with release/acquire (fold_counts);
-// read at every launch (tens of ns) so one process can A/B both orders on the same buffers
+// Single-pass counts hand off with release/acquire (fold_counts, kFoldOrdered) unless
+// RSS_WS_ORDER=relaxed; read at every launch (tens of ns) so one process can A/B both orders
+// on the same buffers (tools/ws_order_ab.py: +1.3-1.5 us per 2^28-tuple launch)
 bool ws_order_acqrel() {
     const char* e = getenv("RSS_WS_ORDER");
-    return e && strcmp(e, "acqrel") == 0;
+    return !(e && strcmp(e, "relaxed") == 0);
 }
 
 // RSS_BALANCE=0: single-pass launches keep the static grid-stride to the end (A/B, tests);
@@ -1528,10 +1602,61 @@ int launch_counts_perm(const uint32_t* window, const void* tuples, uint64_t n, u
     return RSS_OK;
 }
 
+bool wide_hist_enabled() {
+    const char* e = getenv("RSS_WIDE_HIST");
+    return !(e && e[0] == '0');
+}
+
+// Whether a many-queues launch counts its queues from the queue column (launch_queue_ranges)
+// rather than with one global atomic per tuple: up to 64 wide passes (4M queues), or 64 / 32
+// narrow passes of `span` queues (u16 / u32 column) with RSS_WIDE_HIST=0.
+bool ranged_histogram_ok(uint32_t q_eff, uint32_t span, uint32_t qbytes) {
+    if (wide_hist_enabled()) return (uint64_t)q_eff <= 64ull * kWideSpan;
+    return ((uint64_t)q_eff + span - 1) / span <= (qbytes == 2 ? 64u : 32u);
+}
+
 // Queue ranges [span, nqueues) of a many-queues launch, histogrammed from the queue column
-// (u16 or u32) the first pass wrote.
+// (u16 or u32) the first pass wrote: one wide pass (u16 LDS bins, rows of a u16 partial
+// matrix, then a reduce) per kWideSpan queues; RSS_WIDE_HIST=0 (or no memory for the
+// partial matrix) keeps one rss_queue_hist_kernel pass per `span` queues.
 int launch_queue_ranges(const void* qcol, int qw, uint64_t n, uint32_t span, uint32_t nqueues,
                         unsigned long long* counts, int cu_count, hipStream_t stream) {
+    if (span >= nqueues) return RSS_OK;
+    if (wide_hist_enabled()) {
+        const uint64_t want = (n + 8ull * kBlock - 1) / (8ull * kBlock);
+        const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, cu_count));
+        const uint32_t stride_words = kWideSpan / 2;
+        void* partial = nullptr;
+        if (hipMallocAsync(&partial, (size_t)grid * stride_words * 4, stream) == hipSuccess) {
+            int rc = RSS_OK;
+            for (uint32_t lo = span; lo < nqueues && rc == RSS_OK; lo += std::min(kWideSpan, nqueues - lo)) {
+                const uint32_t sp = std::min<uint32_t>(kWideSpan, nqueues - lo);
+                const uint32_t lds = ((sp + 1) / 2) * 4;
+                if (qw == QW_U16)
+                    hipLaunchKernelGGL(rss_queue_hist_wide_kernel<uint16_t>, dim3(grid), dim3(kBlock), lds,
+                                       stream, static_cast<const uint16_t*>(qcol), n, lo, sp,
+                                       static_cast<uint32_t*>(partial), stride_words, counts);
+                else
+                    hipLaunchKernelGGL(rss_queue_hist_wide_kernel<uint32_t>, dim3(grid), dim3(kBlock), lds,
+                                       stream, static_cast<const uint32_t*>(qcol), n, lo, sp,
+                                       static_cast<uint32_t*>(partial), stride_words, counts);
+                hipError_t e = hipGetLastError();
+                if (e == hipSuccess) {
+                    hipLaunchKernelGGL(rss_partial_reduce_kernel, dim3((sp + 255) / 256), dim3(256), 0,
+                                       stream, static_cast<const uint16_t*>(partial), grid,
+                                       2 * stride_words, lo, sp, counts);
+                    e = hipGetLastError();
+                }
+                if (e != hipSuccess)
+                    rc = set_error(RSS_EIO, "wide queue histogram launch failed: %s", hipGetErrorString(e));
+            }
+            const hipError_t fe = hipFreeAsync(partial, stream);
+            if (fe != hipSuccess && rc == RSS_OK)
+                rc = set_error(RSS_EIO, "hipFreeAsync failed: %s", hipGetErrorString(fe));
+            return rc;
+        }
+        (void)hipGetLastError();  // no room for the partial matrix: the narrow passes below
+    }
     const uint64_t qwant = (n + 8ull * kBlock - 1) / (8ull * kBlock);
     const unsigned qgrid = (unsigned)std::min<uint64_t>(qwant, (uint64_t)cu_count * 2);
     for (uint32_t lo = span; lo < nqueues; lo += span) {
@@ -1639,8 +1764,7 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
     if (hist == HIST_GLOBAL && d_counts) {
         const uint32_t span = (kBinBytesMax - reta_bytes) / 4;
         const uint32_t qbytes = q_eff <= 65536u ? 2 : 4;
-        const uint64_t passes = ((uint64_t)q_eff + span - 1) / span;
-        if (passes <= (qbytes == 2 ? 64u : 32u)) {
+        if (ranged_histogram_ok(q_eff, span, qbytes)) {
             void* qcol = d_queue;
             int qw = qwidth;
             bool scratch = false, ranged = true;
@@ -1802,8 +1926,7 @@ int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint
     if (hist == HIST_GLOBAL && d_counts) {
         const uint32_t span = budget / 4;
         const uint32_t qbytes = q_eff <= 65536u ? 2 : 4;
-        const uint64_t passes = ((uint64_t)q_eff + span - 1) / span;
-        if (passes <= (qbytes == 2 ? 64u : 32u)) {
+        if (ranged_histogram_ok(q_eff, span, qbytes)) {
             void* qcol = d_queue;
             bool scratch = false, ranged = true;
             if (!qcol || qwidth == QW_U8) {

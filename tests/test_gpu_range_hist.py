@@ -124,3 +124,60 @@ def test_ipv6_large_q(native, example_key, H, Q, outputs):
                                   np.bincount(want_q.astype(np.int64), minlength=Q).astype(np.uint64))
     if outputs:
         np.testing.assert_array_equal(q.cpu().numpy().view(np.uint32).astype(np.uint64), want_q)
+
+
+@pytest.mark.parametrize("H,Q", [(1 << 20, 20000), (1 << 30, 65536), (1 << 30, 131072),
+                                 (1 << 30, 65536 * 3 + 17)])
+def test_wide_equals_narrow_passes(native, oracle_lib, example_key, H, Q):
+    """The wide pass (u16 guard-bit LDS bins + partial-matrix reduce, one pass per 65536
+    queues) and the round-2 narrow passes (RSS_WIDE_HIST=0, one per 8192) give the oracle's
+    counts on the same launch, with and without per-tuple outputs."""
+    import os
+    n = (1 << 22) + 3
+    host = oracle_lib.generate(27, 0, n)
+    dev = torch.device("cuda:0")
+    s = torch.cuda.current_stream(dev).cuda_stream
+    tup = torch.from_numpy(host.view(np.int32).reshape(-1)).to(dev)
+    want = oracle_lib.run(example_key, host, H, Q, want_hash=False, want_queue=False)[2]
+    key = native.prepare_key(example_key)
+    for wide in ("1", "0"):
+        os.environ["RSS_WIDE_HIST"] = wide
+        try:
+            for outputs in (True, False):
+                q = (torch.empty(n, dtype=torch.int16 if Q <= 65536 else torch.int32, device=dev)
+                     if outputs else None)
+                c = torch.full((Q,), 3, dtype=torch.int64, device=dev)
+                native.hash_device(key, tup.data_ptr(), n, H, Q, None,
+                                   q.data_ptr() if outputs else None, c.data_ptr(),
+                                   (native.FLAG_QUEUE_U16 if Q <= 65536 else 0) if outputs else 0, s)
+                torch.cuda.synchronize()
+                np.testing.assert_array_equal(c.cpu().numpy().view(np.uint64), want)
+        finally:
+            os.environ.pop("RSS_WIDE_HIST", None)
+
+
+@pytest.mark.parametrize("Q", [40000, 100000])
+def test_wide_guard_bit_on_one_hot_queue(native, oracle_lib, example_key, Q):
+    """2^25 identical tuples plus 4099 random ones: every workgroup of the wide pass counts
+    ~2^17 adds into one u16 bin, so the guard bit moves 2^15 out of it again and again; the
+    counts stay exact (the identical tuples' queue gets all 2^25)."""
+    n_same, n_rand = 1 << 25, 4099
+    H = 1 << 30
+    rnd = oracle_lib.generate(28, 0, n_rand)
+    _, q_rnd, _ = oracle_lib.run(example_key, rnd, H, Q)
+    pick = int(np.flatnonzero(q_rnd >= 8192)[0])  # a queue past the hash pass's LDS range
+    one = rnd[pick:pick + 1]
+    host = np.concatenate([np.repeat(one, n_same, axis=0), rnd])
+    dev = torch.device("cuda:0")
+    s = torch.cuda.current_stream(dev).cuda_stream
+    tup = torch.from_numpy(host.view(np.int32).reshape(-1)).to(dev)
+    c = torch.zeros(Q, dtype=torch.int64, device=dev)
+    native.hash_device(native.prepare_key(example_key), tup.data_ptr(), len(host), H, Q, None,
+                       None, c.data_ptr(), 0, s)
+    torch.cuda.synchronize()
+    _, q1, _ = oracle_lib.run(example_key, one, H, Q)
+    want = oracle_lib.run(example_key, rnd, H, Q, want_hash=False, want_queue=False)[2]
+    want[int(q1[0])] += n_same
+    got = c.cpu().numpy().view(np.uint64)
+    np.testing.assert_array_equal(got, want)
+    assert int(got[int(q1[0])]) >= n_same

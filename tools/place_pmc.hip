@@ -146,6 +146,17 @@ int main(int argc, char** argv) {
     rss_key key;
     if (rss_key_prepare(key_bytes, 40, &key)) return 1;
 
+    // "ballast G": hold G GiB allocated (and touched) before the candidates, to see whether
+    // the tier follows the allocation order / the physical range the allocator hands out
+    const bool ballast_mode = argc > 4 && strcmp(argv[4], "ballast") == 0;
+    const double ballast_gib = ballast_mode && argc > 5 ? atof(argv[5]) : 0.0;
+    std::vector<void*> ballast;
+    for (double got = 0; got + 0.5 <= ballast_gib; got += 1.0) {
+        void* b;
+        CK(hipMalloc(&b, 1ull << 30));
+        CK(hipMemset(b, 0, 1ull << 30));
+        ballast.push_back(b);
+    }
     // allocation order as ResidentBatch: input 0, the output pairs (hash then queue), input 1
     int order = 0;
     void* in[2];
@@ -193,6 +204,23 @@ int main(int argc, char** argv) {
         return t[R / 2];
     };
 
+    if (ballast_mode) {  // full-u8 medians only, per candidate, with the ballast held
+        const bool free_first = argc > 6 && strcmp(argv[6], "free") == 0;
+        if (free_first) {  // release the ballast before timing (the candidates stay put)
+            for (void* b : ballast) CK(hipFree(b));
+            ballast.clear();
+        }
+        printf("ballast %.0f GiB%s:", ballast_gib, free_first ? " (freed)" : "");
+        for (int i = 0; i < 2; ++i)
+            for (int k = 0; k < K; ++k) {
+                launch(i, k, true, true);
+                launch(i, k, true, true);
+                printf(" %.3f", median_of(i, k, true, true));
+            }
+        printf("\n");
+        for (void* b : ballast) CK(hipFree(b));
+        return 0;
+    }
     const bool baltrace = argc > 4 && strcmp(argv[4], "balance") == 0;
     if (baltrace) {
         // per candidate: static stream vs tail-balanced stream at several static fractions
