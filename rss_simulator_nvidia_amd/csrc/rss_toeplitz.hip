@@ -362,6 +362,53 @@ __device__ __forceinline__ void fold_counts(SumOf sum_of, uint32_t Q, unsigned l
     }
 }
 
+// The grid's walk over `ngroups` groups of 4 tuples (`group(g)`), one grid-stride row at a
+// time: row r = groups [r * gstride, (r + 1) * gstride), workgroup w takes slot w of it.
+// With `tail_rows` (single-pass launches, DESIGN.md §3 "Balanced tail") rows [0, srows) go
+// statically and the last tail_rows rows are handed out in order as units of one workgroup
+// slot (kBlock groups) through the workspace counter `next`, one claim per workgroup in
+// flight (issued one unit ahead, broadcast through the LDS word `slot`), so the workgroups
+// -- the XCDs -- that stream faster (measured: even XCDs finish ~4 % before odd ones) take
+// more of the tail and every XCD ends together, while the whole grid still sweeps one
+// window of the arrays at a time.  `next` is reset by fold_counts' last workgroup.
+template <typename Group>
+__device__ __forceinline__ void walk_rows(Group group, uint64_t ngroups, uint32_t tail_rows,
+                                          unsigned long long* next, unsigned long long* slot) {
+    const uint32_t tid = threadIdx.x;
+    const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
+    const uint64_t gstride = (uint64_t)gridDim.x * kBlock;
+    if (!tail_rows) {
+        for (uint64_t g = gtid; g < ngroups; g += gstride) group(g);
+        return;
+    }
+    const uint64_t nrows = (ngroups + gstride - 1) / gstride;
+    const uint64_t srows = nrows - tail_rows;  // the launcher keeps tail_rows < nrows
+    unsigned long long claim = 0;
+    if (tid == 0) claim = atomicAdd(next, 1ull);  // the first tail unit, in flight meanwhile
+    for (uint64_t row = 0; row < srows; ++row) group(row * gstride + gtid);  // full rows
+    if (tid == 0) *slot = claim;
+    __syncthreads();
+    const uint64_t first = srows * gridDim.x, nunits = nrows * gridDim.x;
+    uint64_t u = first + *slot;
+    while (u < nunits) {
+        __syncthreads();  // every lane has read the slot
+        if (tid == 0) claim = atomicAdd(next, 1ull);  // the next unit, during this one
+        const uint64_t g = (u / gridDim.x) * gstride + (u % gridDim.x) * kBlock + tid;
+        if (g < ngroups) group(g);
+        if (tid == 0) *slot = claim;
+        __syncthreads();
+        u = first + *slot;
+    }
+}
+
+// Rows of a launch of `ngroups` groups on `grid` workgroups, and the tail a single-pass
+// launch hands out (about a tenth; none below 16 rows, where the spread is a few us)
+inline uint32_t balanced_tail_rows(uint64_t ngroups, unsigned grid) {
+    const uint64_t per_row = (uint64_t)grid * kBlock;
+    const uint64_t rows = (ngroups + per_row - 1) / per_row;
+    return rows >= 16 ? (uint32_t)std::max<uint64_t>(1, rows / 10) : 0u;
+}
+
 template <bool kHPow2, int kQMode, int kHist, int kQWidth>
 __device__ __forceinline__ void one_tuple(const uint32_t* lut, uint32_t* bins, uint64_t i,
                                           uint32_t col, uint32_t hi, const uint32_t* reta_lds,
@@ -426,39 +473,8 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
             count_queue<kHist>(bins, q2, col, p);
             count_queue<kHist>(bins, q3, col, p);
         };
-        if (p.tail_rows) {
-            // Balanced tail (single-pass launches, DESIGN.md §3 "Balanced tail").  A row is
-            // one grid-stride step of the whole grid (gstride groups).  Rows [0, srows) go
-            // as above, statically; the last tail_rows rows are handed out in order as units
-            // of one workgroup slot (kBlock groups) through the workspace counter ws[Q + 1],
-            // one claim per workgroup in flight (issued one unit ahead), so the XCDs that
-            // stream faster (measured: even XCDs finish ~4 % before odd ones) take more of
-            // the tail and every XCD ends together.  The whole grid still sweeps one window
-            // of the arrays at a time.  The counter is reset by fold_counts' last workgroup.
-            unsigned long long* next = p.ws + 1 + p.Q;
-            unsigned long long* slot = reinterpret_cast<unsigned long long*>(
-                reinterpret_cast<char*>(bins) + p.bal_off);
-            const uint64_t nrows = (ngroups + gstride - 1) / gstride;
-            const uint64_t srows = nrows - p.tail_rows;  // launch_hash: tail_rows < nrows
-            unsigned long long claim = 0;
-            if (tid == 0) claim = atomicAdd(next, 1ull);  // first tail unit, in flight meanwhile
-            for (uint64_t row = 0; row < srows; ++row) group(row * gstride + gtid);
-            if (tid == 0) *slot = claim;
-            __syncthreads();
-            const uint64_t first = srows * gridDim.x, nunits = nrows * gridDim.x;
-            uint64_t u = first + *slot;
-            while (u < nunits) {
-                __syncthreads();  // every lane has read the slot
-                if (tid == 0) claim = atomicAdd(next, 1ull);  // the next unit, during this one
-                const uint64_t g = (u / gridDim.x) * gstride + (u % gridDim.x) * kBlock + tid;
-                if (g < ngroups) group(g);
-                if (tid == 0) *slot = claim;
-                __syncthreads();
-                u = first + *slot;
-            }
-        } else {
-            for (uint64_t g = gtid; g < ngroups; g += gstride) group(g);
-        }
+        walk_rows(group, ngroups, p.tail_rows, p.ws + 1 + p.Q,
+                  reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(bins) + p.bal_off));
         tail_begin = ngroups << 2;
     }
     for (uint64_t i = tail_begin + gtid; i < p.n; i += gstride)
@@ -565,23 +581,35 @@ __global__ __launch_bounds__(kBlock) void rss_queue_hist_wide_kernel(
         }
     };
     constexpr uint32_t kPer = 16 / sizeof(T);  // queues per 16-B load
-    uint64_t tail = 0;
-    if (((uintptr_t)queues & 15) == 0) {
-        const uint4* __restrict__ v = reinterpret_cast<const uint4*>(queues);
-        const uint64_t nv = n / kPer;
-        for (uint64_t i = gtid; i < nv; i += gstride) {
-            const uint4 x = v[i];
-            const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+    auto add16 = [&](const uint4 x) {
+        const uint32_t w[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if constexpr (sizeof(T) == 2) {
-                    add(w[k] & 0xFFFFu);
-                    add(w[k] >> 16);
-                } else {
-                    add(w[k]);
-                }
+        for (int k = 0; k < 4; ++k) {
+            if constexpr (sizeof(T) == 2) {
+                add(w[k] & 0xFFFFu);
+                add(w[k] >> 16);
+            } else {
+                add(w[k]);
             }
         }
+    };
+    uint64_t tail = 0;
+    if (((uintptr_t)queues & 15) == 0) {
+        // four 16-B loads in flight per lane: the adds wait for their returned values (the
+        // guard check), so one load per iteration would leave the stream latency-bound at
+        // one workgroup per CU
+        constexpr int kUnroll = 4;
+        const uint4* __restrict__ v = reinterpret_cast<const uint4*>(queues);
+        const uint64_t nv = n / kPer;
+        uint64_t i = gtid;
+        for (; i + (kUnroll - 1) * gstride < nv; i += kUnroll * gstride) {
+            uint4 x[kUnroll];
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) x[u] = v[i + u * gstride];
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) add16(x[u]);
+        }
+        for (; i < nv; i += gstride) add16(v[i]);
         tail = nv * kPer;
     }
     for (uint64_t i = tail + gtid; i < n; i += gstride) add(queues[i]);
@@ -628,6 +656,8 @@ struct PermParams {
     uint32_t Q;
     uint32_t q_mask;    // QM_MASK
     uint32_t q_m16;     // QM_FAST8
+    uint32_t tail_rows; // balanced tail (walk_rows), with ws only
+    uint32_t bal_off;   // its LDS slot's byte offset in the dynamic LDS
     uint32_t lo[kFields];  // field f: table entries 0..3 (v_perm selector 0..3)
     uint32_t hi[kFields];  //          entries 4..7 (selector 4..7)
 };
@@ -692,7 +722,7 @@ __global__ __launch_bounds__(kBlock, 2) void rss_counts_perm_kernel(const PermPa
     const uint4* __restrict__ src = reinterpret_cast<const uint4*>(p.tuples);
     const uint64_t ngroups = p.n >> 2;
     const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
-    for (uint64_t g = gtid; g < ngroups; g += (uint64_t)gridDim.x * kBlock) {
+    walk_rows([&](uint64_t g) {
         uint32_t w[4 * kWords];  // four tuples = kWords x 16 B, 16-B aligned
 #pragma unroll
         for (int v = 0; v < kWords; ++v) {
@@ -706,7 +736,8 @@ __global__ __launch_bounds__(kBlock, 2) void rss_counts_perm_kernel(const PermPa
 #pragma unroll
         for (int i = 0; i < 4; ++i)
             perm_count(bins, perm_queue<kQMode>((bk >> (8 * i)) & 0xFFu, p), col);
-    }
+    }, ngroups, p.tail_rows, p.ws + 1 + p.Q,
+       reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(bins) + p.bal_off));
     // the last n % 4 tuples: one per lane of the first workgroup, in byte 0
     const uint64_t i = (ngroups << 2) + gtid;
     if (i < p.n) {
@@ -720,7 +751,7 @@ __global__ __launch_bounds__(kBlock, 2) void rss_counts_perm_kernel(const PermPa
         uint32_t s = 0;
         for (uint32_t c = 0; c < kBinCols; ++c) s += bins[q * kBinCols + ((c + q) & (kBinCols - 1))];
         return s;
-    }, p.Q, p.counts, p.ws, p.accumulate, bins);
+    }, p.Q, p.counts, p.ws, p.accumulate, bins, p.tail_rows ? p.ws + 1 + p.Q : nullptr);
 }
 
 // Key search: per-queue counts of the same tuples under many
@@ -1592,12 +1623,19 @@ int launch_counts_perm(const uint32_t* window, const void* tuples, uint64_t n, u
     const uint64_t wgs = wgs_env && wgs_env[0] == '1' ? 1 : 2;
     const uint64_t want = (n + 4 * kBlock - 1) / (4 * kBlock);
     const unsigned grid = (unsigned)(want < wgs * cu_count ? want : wgs * cu_count);
+    uint32_t shmem = bin_bytes;
+    const uint32_t tail = balanced_tail_rows(n / 4, grid);
+    if (ws && tail && balance_enabled()) {  // single-pass: the balanced tail (walk_rows)
+        pp.tail_rows = tail;
+        pp.bal_off = (bin_bytes + 7u) & ~7u;
+        shmem = pp.bal_off + 8;
+    }
     if (qmode == QM_MASK)
         hipLaunchKernelGGL((rss_counts_perm_kernel<QM_MASK, kWords>), dim3(grid), dim3(kBlock),
-                           bin_bytes, stream, pp);
+                           shmem, stream, pp);
     else
         hipLaunchKernelGGL((rss_counts_perm_kernel<QM_FAST8, kWords>), dim3(grid), dim3(kBlock),
-                           bin_bytes, stream, pp);
+                           shmem, stream, pp);
     RSS_HIP_CHECK(hipGetLastError());
     return RSS_OK;
 }
@@ -1807,10 +1845,10 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
     // Balanced tail (single-pass launches: the workspace holds its unit counter and is used
     // by one launch at a time): the last ~1/10 of the grid-stride rows handed out per
     // workgroup slot, so the XCDs finish together.  Needs 8 bytes of LDS beside the bins.
-    const uint64_t rows = (n / 4 + (uint64_t)grid * kBlock - 1) / ((uint64_t)grid * kBlock);
     const uint32_t bal_off = (shmem + 7u) & ~7u;
-    if (single_pass && vec4 && rows >= 16 && bal_off + 8 <= kBinBytesMax && balance_enabled()) {
-        p.tail_rows = (uint32_t)std::max<uint64_t>(1, rows / 10);
+    const uint32_t tail = balanced_tail_rows(n / 4, grid);
+    if (single_pass && vec4 && tail && bal_off + 8 <= kBinBytesMax && balance_enabled()) {
+        p.tail_rows = tail;
         p.bal_off = bal_off;
         shmem = bal_off + 8;
     }

@@ -108,3 +108,44 @@ def test_bench_digest_is_pinned_to_the_oracle(oracle_lib, example_key):
         [int(x) for x in gold["counts"][:2].sum(axis=0)]
     assert bench.golden_counts(gold, 1 << 20, 1 << 27) is None   # not whole chunks
     assert bench.verify_outputs(torch, gold, ht, qt, 5, B)["ok"] is None
+
+
+def check_bench_line(line):
+    """The fields VERDICT r02 asked every bench line to carry (configs[3] block, per-rank
+    timings and placement, the verification of the timed work) are present and coherent."""
+    n = line["n_gpus"]
+    assert line["verified"] is True, line.get("verification")
+    v = line["verification"]
+    assert v["main"]["ok"] is True and v["main"]["counts_ok"] is True
+    c3 = line["configs3"]
+    assert c3["scaling"] == "strong" and c3["global_tuples"] == 1 << 30
+    assert c3["tuples_per_rank_max"] == (1 << 30) // n
+    assert c3["tuples_per_s"] > 0 and c3["ms_per_batch"] > 0
+    assert c3["kernel_ms_max_rank"] <= c3["step_ms_max_rank"] * 1.5
+    assert 0 < c3["roofline"]["frac"] < 1
+    assert v["configs3"]["ok"] is True and v["configs3"]["counts_ok"] is True
+    rows = line["per_rank"]
+    assert [r["rank"] for r in rows] == list(range(n))
+    for r in rows:
+        assert r["kernel_ms"] > 0 and r["chosen_ms"] > 0 and r["first_allocation_ms"] > 0
+        assert r["configs3_kernel_ms"] > 0 and r["verified_main"] is True
+        assert r["verified_configs3"] is True
+    assert line["roofline"]["kernel_ms_max_rank"] == max(r["kernel_ms"] for r in rows)
+    return line
+
+
+def test_committed_bench_lines_carry_the_round3_blocks():
+    """The world-size-1 RCCL run (torchrun --nproc-per-node 1) and the 8-rank gloo rehearsal
+    on one GPU (RSS_BENCH_DEVICE=0), as committed under profiles/r03/."""
+    import glob
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    paths = sorted(glob.glob(os.path.join(root, "profiles", "r03", "bench_lines", "*.json")))
+    assert paths, "no committed round-3 bench lines"
+    seen = set()
+    for p in paths:
+        with open(p) as f:
+            line = check_bench_line(json.loads(f.read().strip().splitlines()[-1]))
+        seen.add((line["n_gpus"], "gloo" if "gloo" in line["config"]["parallelism"] else
+                  ("RCCL" if "RCCL" in line["config"]["parallelism"] else "none")))
+    assert (1, "RCCL") in seen and (8, "gloo") in seen, seen

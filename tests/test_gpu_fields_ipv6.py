@@ -114,7 +114,8 @@ def test_ipv6_narrow_queue_outputs(native, oracle_lib, flag_name, dtype, H, Q):
     flags = getattr(native, flag_name) if flag_name else 0
     for offset in (0, item):
         buf = torch.full((n * item + 64,), 0xAB, dtype=torch.uint8, device=dev)
-        counts = torch.empty(Q, dtype=torch.int64, device=dev)
+        qn = min(H, Q)  # count vectors are min(H, Q) long (_native.queue_modulus)
+        counts = torch.empty(qn, dtype=torch.int64, device=dev)
         native.hash6_device(k6, raw.data_ptr(), n, H, Q, None, buf.data_ptr() + offset,
                             counts.data_ptr(), flags, s)
         torch.cuda.synchronize()
@@ -122,7 +123,7 @@ def test_ipv6_narrow_queue_outputs(native, oracle_lib, flag_name, dtype, H, Q):
         np.testing.assert_array_equal(got[offset:offset + n * item].view(dtype), qo.astype(dtype))
         assert (got[:offset] == 0xAB).all() and (got[offset + n * item:] == 0xAB).all()
         np.testing.assert_array_equal(counts.cpu().numpy().view(np.uint64),
-                                      np.bincount(qo.astype(np.int64), minlength=Q))
+                                      np.bincount(qo.astype(np.int64), minlength=qn))
     from rss_simulator_nvidia_amd.exceptions import DeviceError
     with pytest.raises(DeviceError, match="QUEUE_U8"):
         native.hash6_device(k6, 0, 0, 1024, 257, None, None, None, native.FLAG_QUEUE_U8)

@@ -61,7 +61,11 @@ def test_random_config_matches_oracle(native, oracle_lib, seed):
     hbuf = torch.full((n + guard,), -1, dtype=torch.int32, device=dev)
     qbuf = torch.full((n * qbytes + guard,), 0x5A, dtype=torch.uint8, device=dev)
     base = rng.integers(0, 1000, Q).astype(np.int64)
-    counts = torch.from_numpy(base if c["accumulate"] else np.full(Q, 77, np.int64)).to(dev)
+    # count vectors are min(H, Q) long (_native.queue_modulus): no queue >= H exists; with a
+    # RETA the caller's Q (entries < Q)
+    qn = Q if c["reta"] else native.queue_modulus(H, Q)[1]
+    base = base[:qn]
+    counts = torch.from_numpy(base if c["accumulate"] else np.full(qn, 77, np.int64)).to(dev)
     flags = qflag | (native.FLAG_ACCUMULATE if c["accumulate"] else 0)
     key = native.prepare_key(c["key"])
     h_ptr = hbuf.data_ptr() if c["want_hash"] else None
@@ -75,15 +79,17 @@ def test_random_config_matches_oracle(native, oracle_lib, seed):
         # half the cases as single-pass counts (rss_hash_device_ws; own generator, so the
         # configurations above stay what they were), the workspace followed by guard words
         single_pass = bool(np.random.default_rng(5000 + seed).random() < 0.5)
-        ws = torch.zeros(Q + 1 + 8, dtype=torch.int64, device=dev)
-        ws[Q + 1:] = -7
+        wsn = native.counts_workspace_bytes(H, Q) // 8  # ticket, qn sums, tail counter
+        assert wsn == qn + 2
+        ws = torch.zeros(wsn + 8, dtype=torch.int64, device=dev)
+        ws[wsn:] = -7
         native.hash_device(key, tup_ptr, n, H, Q, h_ptr, q_ptr, counts.data_ptr(), flags, stream,
                            ws.data_ptr() if single_pass else None)
     torch.cuda.synchronize()
     if reta is None:
         wsh = ws.cpu().numpy()
-        assert (wsh[:Q + 1] == 0).all(), "workspace not left zero"
-        assert (wsh[Q + 1:] == -7).all(), "workspace written past Q + 1"
+        assert (wsh[:wsn] == 0).all(), "workspace not left zero"
+        assert (wsh[wsn:] == -7).all(), "workspace written past its size"
 
     eh, eq, ec = oracle_lib.run(c["key"], host, H, Q, threads=8)
     if reta is not None:
@@ -100,7 +106,8 @@ def test_random_config_matches_oracle(native, oracle_lib, seed):
         assert (got_q[n * qbytes:] == 0x5A).all(), "queue store past n"
     else:
         assert (got_q == 0x5A).all()
-    want = ec.astype(np.uint64) + (base.astype(np.uint64) if c["accumulate"] else 0)
+    assert not ec[qn:].any()  # queues >= min(H, Q) never occur
+    want = ec[:qn].astype(np.uint64) + (base.astype(np.uint64) if c["accumulate"] else 0)
     np.testing.assert_array_equal(counts.cpu().numpy().view(np.uint64), want)
 
 
@@ -117,9 +124,12 @@ def test_random_key_search_matches_oracle(native, oracle_lib, seed):
     keys = keysearch.random_keys(nkeys, seed=seed)
     tuples = oracle_lib.generate(seed + 17, 0, n)
     counts = native.HostContext(0).key_search([native.prepare_key(k) for k in keys], tuples, H, Q)
-    assert counts.shape == (nkeys, Q)
+    qn = min(H, Q)  # rows are min(H, Q) long: queues >= H never occur
+    assert counts.shape == (nkeys, qn)
     for k, key in enumerate(keys):
-        np.testing.assert_array_equal(counts[k], oracle_lib.run(key, tuples, H, Q)[2])
+        c = oracle_lib.run(key, tuples, H, Q)[2]
+        assert not c[qn:].any()
+        np.testing.assert_array_equal(counts[k], c[:qn])
 
 
 def test_reta_entries_above_u16_are_refused(native):
@@ -161,8 +171,9 @@ def test_random_ipv6_config_matches_oracle(native, oracle_lib, seed):
     qflag = {"u8": native.FLAG_QUEUE_U8, "u16": native.FLAG_QUEUE_U16, "u32": 0}[width]
     hbuf = torch.full((n + 16,), -1, dtype=torch.int32, device=dev)
     qbuf = torch.full((n * qbytes + 16,), 0x5A, dtype=torch.uint8, device=dev)
-    counts = torch.full((Q,), 3, dtype=torch.int64, device=dev)
     use_reta = H <= 1024 and Q <= 65536 and rng.random() < 0.4
+    qn = Q if use_reta else native.queue_modulus(H, Q)[1]  # min(H, Q) counts without a table
+    counts = torch.full((qn,), 3, dtype=torch.int64, device=dev)
     reta = rng.integers(0, Q, H).astype(np.uint32) if use_reta else None
     if use_reta:
         native.hash6_device_reta(k6, raw.data_ptr() + 4 * off, n, H, reta, Q, hbuf.data_ptr(),
@@ -192,4 +203,5 @@ def test_random_ipv6_config_matches_oracle(native, oracle_lib, seed):
     got_q = qbuf.cpu().numpy()
     np.testing.assert_array_equal(got_q[:n * qbytes].view(qdt), qo.astype(qdt))
     assert (got_q[n * qbytes:] == 0x5A).all()
-    np.testing.assert_array_equal(counts.cpu().numpy().view(np.uint64), co)
+    assert not np.asarray(co)[qn:].any()
+    np.testing.assert_array_equal(counts.cpu().numpy().view(np.uint64), np.asarray(co)[:qn])

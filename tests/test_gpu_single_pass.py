@@ -382,3 +382,34 @@ def test_balanced_tail_stress(native, oracle_lib, example_key):
     for i in range(600):
         np.testing.assert_array_equal(got[i], batches[i % 2][2])
     assert int(ws.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("n", [(1 << 25) + 5, (1 << 26) + 4097])
+def test_balanced_tail_counts_only(native, oracle_lib, example_key, n):
+    """Counts-only single-pass launches (the register-table kernel, two workgroups per CU)
+    take the balanced tail from 16 rows (2^25 tuples) on: counts exact over 40 launches on
+    one workspace, alternating with static ones (RSS_BALANCE=0)."""
+    import os
+    H, Q = 128, 24
+    key = native.prepare_key(example_key)
+    s = torch.cuda.current_stream().cuda_stream
+    host = oracle_lib.generate(43, 0, n)
+    want = oracle_lib.run(example_key, host, H, Q, want_hash=False, want_queue=False,
+                          fn="oracle_run_tables")[2]
+    t = torch.from_numpy(host.view(np.int32).reshape(-1)).to(DEV)
+    ws = _ws(native, H, Q)
+    outs = torch.zeros((40, Q), dtype=torch.int64, device=DEV)
+    try:
+        for i in range(40):
+            if i % 10 == 5:
+                os.environ["RSS_BALANCE"] = "0"
+            elif i % 10 == 8:
+                os.environ.pop("RSS_BALANCE", None)
+            native.hash_device(key, t.data_ptr(), n, H, Q, None, None, outs[i].data_ptr(), 0, s,
+                               ws.data_ptr())
+    finally:
+        os.environ.pop("RSS_BALANCE", None)
+    got = outs.cpu().numpy().view(np.uint64)
+    for i in range(40):
+        np.testing.assert_array_equal(got[i], want)
+    assert int(ws.abs().sum()) == 0

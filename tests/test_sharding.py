@@ -214,3 +214,53 @@ def test_rccl_comm_fails_together_without_a_gpu(tmp_path):
                        nprocs=world, start_method="spawn")
     for r in range(world):
         assert (tmp_path / ("r%d.txt" % r)).read_text().startswith("RcclError"), r
+
+
+def _rccl_stuck_worker(rank, world, port, out_dir):
+    """RcclComm over a fake librccl whose ncclCommInitRank blocks past the timeout."""
+    import time
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import torch
+        from rss_simulator_nvidia_amd import rccl
+
+        class FakeLib:
+            def ncclGetUniqueId(self, uid):
+                return 0
+
+            def ncclCommInitRank(self, comm, world, uid, rank):
+                time.sleep(6)  # a bootstrap that never completes within the timeout
+                return 0
+
+            def ncclGetErrorString(self, rc):
+                return b"fake"
+
+            def ncclCommAbort(self, comm):
+                return 0
+
+            def ncclCommDestroy(self, comm):
+                return 0
+
+        rccl._LIB = FakeLib()
+        torch.cuda.set_device = lambda dev: None  # no GPU here; the fake needs none
+        try:
+            rccl.RcclComm("cpu", timeout_s=1.0)
+            outcome = "constructed"
+        except rccl.RcclError as err:
+            outcome = "stuck=%s %s" % (err.stuck, err)
+        with open(os.path.join(out_dir, "r%d.txt" % rank), "w") as f:
+            f.write(outcome)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_comm_init_timeout_is_stuck(tmp_path):
+    """an init that times out leaves a thread blocked inside RCCL, so every rank
+    raises RcclError(stuck=True) -- the bench exits instead of falling back in-process."""
+    world = 2
+    mp.start_processes(_rccl_stuck_worker, args=(world, _free_port(), str(tmp_path)),
+                       nprocs=world, start_method="spawn")
+    for r in range(world):
+        assert (tmp_path / ("r%d.txt" % r)).read_text().startswith("stuck=True"), r

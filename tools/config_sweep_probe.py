@@ -1,7 +1,9 @@
 """Kernel time across (H, Q) configurations on fixed buffers (tool, not product): full
 output (hash u32 + the narrowest queue width) and counts only, 2^28 tuples, medians of 10
 launches after 5 warm ones, against the same buffers' 12 R + 5 W / 12 R + 6 W / 12 R + 8 W
-byte counts.  Prints one JSON line per configuration."""
+byte counts.  Count vectors are min(H, Q) long (``_native.queue_modulus``): rows with Q >= H
+run the Q <= H kernel.  For Q > 8192 the round-2 narrow range passes (RSS_WIDE_HIST=0) are
+timed beside the wide pass.  Prints one JSON line per configuration."""
 import json
 import os
 import sys
@@ -25,7 +27,7 @@ q = torch.empty(n, dtype=torch.int32, device=dev)
 
 
 def timed(H, Q, outputs, flags, reps=10, warm=5):
-    c = torch.zeros(Q, dtype=torch.int64, device=dev)
+    c = torch.zeros(_native.queue_modulus(H, Q)[1], dtype=torch.int64, device=dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(reps)]
     hp, qp = (h.data_ptr(), q.data_ptr()) if outputs else (None, None)
@@ -42,13 +44,20 @@ def timed(H, Q, outputs, flags, reps=10, warm=5):
 
 
 for H, Q in [(128, 24), (128, 16), (512, 64), (100, 7), (1000, 24), (65536, 24),
+             (128, 129), (128, 20000), (128, 300000), (128, 4 * 10 ** 9),
              (65536, 4096), (1 << 20, 1000), (1 << 20, 8193), (1 << 20, 20000),
              (4294967295, 65536), (1 << 30, 131072), (1 << 30, 131073)]:
-    width = 1 if Q <= 256 else (2 if Q <= 65536 else 4)
+    qn = _native.queue_modulus(H, Q)[1]
+    width = 1 if qn <= 256 else (2 if qn <= 65536 else 4)
     fl = {1: _native.FLAG_QUEUE_U8, 2: _native.FLAG_QUEUE_U16, 4: 0}[width]
     full = timed(H, Q, True, fl)
     co = timed(H, Q, False, 0)
-    print(json.dumps({"H": H, "Q": Q, "queue_bytes": width, "full_ms": full,
-                      "full_GBs": round(n * (16 + width) / (full / 1e3) / 1e9),
-                      "counts_ms": co, "counts_read_GBs": round(n * 12 / (co / 1e3) / 1e9)}),
-          flush=True)
+    rec = {"H": H, "Q": Q, "queues_counted": qn, "queue_bytes": width, "full_ms": full,
+           "full_GBs": round(n * (16 + width) / (full / 1e3) / 1e9),
+           "counts_ms": co, "counts_read_GBs": round(n * 12 / (co / 1e3) / 1e9)}
+    if qn > 8192:  # the round-2 narrow passes beside the wide one
+        os.environ["RSS_WIDE_HIST"] = "0"
+        rec["narrow_full_ms"] = timed(H, Q, True, fl)
+        rec["narrow_counts_ms"] = timed(H, Q, False, 0)
+        os.environ.pop("RSS_WIDE_HIST", None)
+    print(json.dumps(rec), flush=True)

@@ -34,7 +34,8 @@ def main():
                                                                  stream.cuda_stream),
                           stream=stream)
     counts = torch.zeros(Q, dtype=torch.int64, device=dev)
-    modes = {"default": {}, "relaxed": {"RSS_WS_ORDER": "relaxed"}, "static": {"RSS_BALANCE": "0"}}
+    modes = {"default": {}, "relaxed": {"RSS_WS_ORDER": "relaxed"}, "static": {"RSS_BALANCE": "0"},
+             "counts_default": {}, "counts_static": {"RSS_BALANCE": "0"}}
     res = {m: [] for m in modes}
     for _ in range(200):  # clock settle
         batch.hash(counts=counts)
@@ -44,12 +45,13 @@ def main():
             for var in ("RSS_WS_ORDER", "RSS_BALANCE"):
                 os.environ.pop(var, None)
             os.environ.update(modes[mode])
+            outputs = not mode.startswith("counts")  # counts only: the register-table kernel
             for _ in range(10):
-                batch.hash(counts=counts)
+                batch.hash(counts=counts, outputs=outputs)
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(stream)
             for _ in range(50):
-                batch.hash(counts=counts)
+                batch.hash(counts=counts, outputs=outputs)
             b.record(stream)
             torch.cuda.synchronize()
             res[mode].append(a.elapsed_time(b) / 50)
@@ -59,6 +61,8 @@ def main():
     out = {m: {"ms_per_launch": v, "median": statistics.median(v)} for m, v in res.items()}
     out["default_minus_relaxed_us"] = 1e3 * (out["default"]["median"] - out["relaxed"]["median"])
     out["static_minus_default_us"] = 1e3 * (out["static"]["median"] - out["default"]["median"])
+    out["counts_static_minus_default_us"] = 1e3 * (out["counts_static"]["median"] -
+                                                   out["counts_default"]["median"])
     print(json.dumps(out))
 
 
