@@ -567,31 +567,43 @@ __global__ __launch_bounds__(kBlock) void rss_queue_hist_wide_kernel(
     __syncthreads();
     const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
     const uint64_t gstride = (uint64_t)gridDim.x * kBlock;
-    auto add = [&](uint32_t q) {
+    // the add of one queue; returns the bin's previous value (0 when q is out of range)
+    auto add = [&](uint32_t q) -> uint32_t {
         const uint32_t r = q - q_lo;  // wraps for q < q_lo
-        if (r < q_span) {
-            const uint32_t sh = (r & 1u) * 16u;
-            const uint32_t old = __hip_atomic_fetch_add(&bins[r >> 1], 1u << sh, __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (((old >> sh) & 0xFFFFu) == 0x7FFFu) {  // this add set the guard bit
-                __hip_atomic_fetch_sub(&bins[r >> 1], 0x8000u << sh, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_WORKGROUP);
-                atomicAdd(&counts[q], 0x8000ull);
-            }
+        if (r >= q_span) return 0u;
+        const uint32_t sh = (r & 1u) * 16u;
+        return __hip_atomic_fetch_add(&bins[r >> 1], 1u << sh, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    // the guard: the add that returned 0x7FFF (its bin now holds >= 0x8000) moves 2^15 out.
+    // Checked after a group's adds are all issued, so they do not wait for each other; the
+    // adds in flight meanwhile are bounded by the workgroup's lanes, far below 2^15.
+    auto guard = [&](uint32_t q, uint32_t old) {
+        const uint32_t r = q - q_lo;
+        const uint32_t sh = (r & 1u) * 16u;
+        if (r < q_span && ((old >> sh) & 0xFFFFu) == 0x7FFFu) {
+            __hip_atomic_fetch_sub(&bins[r >> 1], 0x8000u << sh, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+            atomicAdd(&counts[q], 0x8000ull);
         }
     };
     constexpr uint32_t kPer = 16 / sizeof(T);  // queues per 16-B load
     auto add16 = [&](const uint4 x) {
         const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+        uint32_t q[kPer], old[kPer];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             if constexpr (sizeof(T) == 2) {
-                add(w[k] & 0xFFFFu);
-                add(w[k] >> 16);
+                q[2 * k] = w[k] & 0xFFFFu;
+                q[2 * k + 1] = w[k] >> 16;
             } else {
-                add(w[k]);
+                q[k] = w[k];
             }
         }
+#pragma unroll
+        for (uint32_t k = 0; k < kPer; ++k) old[k] = add(q[k]);
+#pragma unroll
+        for (uint32_t k = 0; k < kPer; ++k) guard(q[k], old[k]);
     };
     uint64_t tail = 0;
     if (((uintptr_t)queues & 15) == 0) {
@@ -612,7 +624,10 @@ __global__ __launch_bounds__(kBlock) void rss_queue_hist_wide_kernel(
         for (; i < nv; i += gstride) add16(v[i]);
         tail = nv * kPer;
     }
-    for (uint64_t i = tail + gtid; i < n; i += gstride) add(queues[i]);
+    for (uint64_t i = tail + gtid; i < n; i += gstride) {
+        const uint32_t q = queues[i];
+        guard(q, add(q));
+    }
     __syncthreads();
     uint32_t* row = partial + (size_t)blockIdx.x * stride_words;
     for (uint32_t e = tid; e < words; e += kBlock) row[e] = bins[e];
@@ -1623,13 +1638,10 @@ int launch_counts_perm(const uint32_t* window, const void* tuples, uint64_t n, u
     const uint64_t wgs = wgs_env && wgs_env[0] == '1' ? 1 : 2;
     const uint64_t want = (n + 4 * kBlock - 1) / (4 * kBlock);
     const unsigned grid = (unsigned)(want < wgs * cu_count ? want : wgs * cu_count);
-    uint32_t shmem = bin_bytes;
-    const uint32_t tail = balanced_tail_rows(n / 4, grid);
-    if (ws && tail && balance_enabled()) {  // single-pass: the balanced tail (walk_rows)
-        pp.tail_rows = tail;
-        pp.bal_off = (bin_bytes + 7u) & ~7u;
-        shmem = pp.bal_off + 8;
-    }
+    // no balanced tail here (pp.tail_rows = 0, walk_rows' static loop): on this read-only,
+    // two-workgroups-per-CU kernel it measured 5 % SLOWER (0.562 vs 0.536 ms per 2^28
+    // tuples, profiles/r03/c/ab.json), where the full-output kernel gains 3 %
+    const uint32_t shmem = bin_bytes;
     if (qmode == QM_MASK)
         hipLaunchKernelGGL((rss_counts_perm_kernel<QM_MASK, kWords>), dim3(grid), dim3(kBlock),
                            shmem, stream, pp);
