@@ -633,18 +633,52 @@ __global__ __launch_bounds__(kBlock) void rss_queue_hist_wide_kernel(
     for (uint32_t e = tid; e < words; e += kBlock) row[e] = bins[e];
 }
 
-// counts[q_lo + q] += sum over the rows of the u16 partial matrix (column q); one thread per
-// queue, rows read coalesced across the threads.  The wide pass's guard-bit adds have landed
-// already (previous launch on the stream), so a plain read-modify-write suffices.
-__global__ __launch_bounds__(256) void rss_partial_reduce_kernel(const uint16_t* __restrict__ partial,
-                                                                 uint32_t rows, uint32_t stride,
-                                                                 uint32_t q_lo, uint32_t q_span,
-                                                                 unsigned long long* counts) {
-    const uint32_t q = blockIdx.x * 256 + threadIdx.x;
-    if (q >= q_span) return;
-    unsigned long long s = 0;
-    for (uint32_t r = 0; r < rows; ++r) s += partial[(size_t)r * stride + q];
-    if (s) counts[q_lo + q] += s;
+// counts[q_lo + q] += sum over the `rows` rows of the u16 partial matrix (column q).  A
+// workgroup takes a strip of 64 dwords (128 queues) of every row: its 256 threads are 64
+// columns x 4 row groups, each summing its rows' dword (two u16 queues) with eight loads in
+// flight, then the 4 row groups meet in LDS.  (One thread per queue summing all rows ran
+// 60 us per 65536-queue range at 2^28 tuples -- as long as half the wide pass; profiles/r03/
+// mqprof.)  The wide pass's guard-bit adds landed in a previous launch, so a plain
+// read-modify-write of the counts suffices.
+constexpr uint32_t kReduceCols = 64, kReduceGroups = 4;
+__global__ __launch_bounds__(kReduceCols * kReduceGroups) void rss_partial_reduce_kernel(
+        const uint32_t* __restrict__ partial, uint32_t rows, uint32_t stride_words, uint32_t q_lo,
+        uint32_t q_span, unsigned long long* counts) {
+    __shared__ unsigned long long part[kReduceGroups][kReduceCols][2];
+    const uint32_t col = threadIdx.x % kReduceCols, grp = threadIdx.x / kReduceCols;
+    const uint32_t word = blockIdx.x * kReduceCols + col;  // queues 2 * word, 2 * word + 1
+    unsigned long long lo = 0, hi = 0;
+    if (word < stride_words) {
+        constexpr uint32_t kIn = 8;
+        uint32_t r = grp;
+        for (; r + (kIn - 1) * kReduceGroups < rows; r += kIn * kReduceGroups) {
+            uint32_t x[kIn];
+#pragma unroll
+            for (uint32_t k = 0; k < kIn; ++k) x[k] = partial[(size_t)(r + k * kReduceGroups) * stride_words + word];
+#pragma unroll
+            for (uint32_t k = 0; k < kIn; ++k) {
+                lo += x[k] & 0xFFFFu;
+                hi += x[k] >> 16;
+            }
+        }
+        for (; r < rows; r += kReduceGroups) {
+            const uint32_t x = partial[(size_t)r * stride_words + word];
+            lo += x & 0xFFFFu;
+            hi += x >> 16;
+        }
+    }
+    part[grp][col][0] = lo;
+    part[grp][col][1] = hi;
+    __syncthreads();
+    if (grp == 0) {
+        for (uint32_t g = 1; g < kReduceGroups; ++g) {
+            lo += part[g][col][0];
+            hi += part[g][col][1];
+        }
+        const uint32_t q0 = 2 * word;
+        if (q0 < q_span && lo) counts[q_lo + q0] += lo;
+        if (q0 + 1 < q_span && hi) counts[q_lo + q0 + 1] += hi;
+    }
 }
 
 // Counts only, power-of-two H <= 256 (histogram mode, `rss_hash_host` without per-tuple
@@ -1672,7 +1706,10 @@ bool ranged_histogram_ok(uint32_t q_eff, uint32_t span, uint32_t qbytes) {
 int launch_queue_ranges(const void* qcol, int qw, uint64_t n, uint32_t span, uint32_t nqueues,
                         unsigned long long* counts, int cu_count, hipStream_t stream) {
     if (span >= nqueues) return RSS_OK;
-    if (wide_hist_enabled()) {
+    // a wide pass costs about two narrow ones (2^28 tuples: ~0.2 vs ~0.1 ms over a u16
+    // column, profiles/r03/d/config_sweep.jsonl), so it pays from three narrow passes on
+    const uint64_t narrow_passes = ((uint64_t)nqueues - span + span - 1) / span;
+    if (wide_hist_enabled() && narrow_passes >= 3) {
         const uint64_t want = (n + 8ull * kBlock - 1) / (8ull * kBlock);
         const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, cu_count));
         const uint32_t stride_words = kWideSpan / 2;
@@ -1692,9 +1729,12 @@ int launch_queue_ranges(const void* qcol, int qw, uint64_t n, uint32_t span, uin
                                        static_cast<uint32_t*>(partial), stride_words, counts);
                 hipError_t e = hipGetLastError();
                 if (e == hipSuccess) {
-                    hipLaunchKernelGGL(rss_partial_reduce_kernel, dim3((sp + 255) / 256), dim3(256), 0,
-                                       stream, static_cast<const uint16_t*>(partial), grid,
-                                       2 * stride_words, lo, sp, counts);
+                    const uint32_t words = (sp + 1) / 2;
+                    hipLaunchKernelGGL(rss_partial_reduce_kernel,
+                                       dim3((words + kReduceCols - 1) / kReduceCols),
+                                       dim3(kReduceCols * kReduceGroups), 0, stream,
+                                       static_cast<const uint32_t*>(partial), grid, stride_words,
+                                       lo, sp, counts);
                     e = hipGetLastError();
                 }
                 if (e != hipSuccess)

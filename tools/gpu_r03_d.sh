@@ -10,3 +10,8 @@ timeout -k 10 600 python -u -m pytest -v -m gpu --timeout 300 --timeout-method t
 echo "pytest ok"
 timeout -k 10 300 python tools/config_sweep_probe.py > $OUT/config_sweep.jsonl 2> $OUT/config_sweep.err
 echo "sweep ok"
+cd /tmp
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/mqprof -o run -- \
+    python3 $R/tools/many_queues_prof.py > $OUT/mqprof.log 2>&1
+echo "mqprof ok"
