@@ -78,7 +78,11 @@ static_assert(kBlock * 4 == (int)kTableEntries, "LUT build maps 4 entries per th
 
 enum QueueMode { QM_MASK = 0, QM_FAST16 = 1, QM_FAST32 = 2, QM_TABLE = 3, QM_FAST8 = 4 };
 constexpr uint32_t kRetaMax = 1024;  // indirection-table entries carried in the kernarg
-enum HistMode { HIST_PRIVATE = 0, HIST_SHARED = 1, HIST_GLOBAL = 2, HIST_NONE = 3, HIST_RANGE = 4 };
+enum HistMode { HIST_PRIVATE = 0, HIST_SHARED = 1, HIST_GLOBAL = 2, HIST_NONE = 3, HIST_RANGE = 4,
+                HIST_RANGE16 = 5 };
+// HIST_RANGE16 (IPv4 kernel): HIST_RANGE with u16 bins, two per dword, twice the queues in the
+// same LDS -- with the wide pass's guard bit (rss_queue_hist_wide_kernel): the add that
+// returns 0x7FFF moves 2^15 of its bin into the global counts.
 // HIST_RANGE: shared LDS bins for queues [q_lo, q_lo + q_span) only -- one pass of a
 // multi-pass launch for nqueues whose bins do not fit the LDS beside the tables
 // (launch_hash), instead of one global atomic per tuple (13x slower).
@@ -259,6 +263,18 @@ __device__ __forceinline__ void count_queue(uint32_t* bins, uint32_t q, uint32_t
         const uint32_t r = q - p.q_lo;  // wraps for q < q_lo
         if (r < p.q_span)
             __hip_atomic_fetch_add(&bins[r], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else if constexpr (kHist == HIST_RANGE16) {
+        const uint32_t r = q - p.q_lo;
+        if (r < p.q_span) {
+            const uint32_t sh = (r & 1u) * 16u;
+            const uint32_t old = __hip_atomic_fetch_add(&bins[r >> 1], 1u << sh, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (((old >> sh) & 0xFFFFu) == 0x7FFFu) {  // the guard bit: 2^15 out of the bin
+                __hip_atomic_fetch_sub(&bins[r >> 1], 0x8000u << sh, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+                atomicAdd(&p.counts[q], 0x8000ull);
+            }
+        }
     }
 }
 
@@ -428,9 +444,10 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
     const uint32_t tid = threadIdx.x;
 
     build_lut(lut, p.window, tid);
-    const uint32_t nbins = kHist == HIST_PRIVATE ? p.Q * kBinCols
-                         : kHist == HIST_SHARED  ? p.Q
-                         : kHist == HIST_RANGE   ? p.q_span : 0u;
+    const uint32_t nbins = kHist == HIST_PRIVATE   ? p.Q * kBinCols
+                         : kHist == HIST_SHARED    ? p.Q
+                         : kHist == HIST_RANGE     ? p.q_span
+                         : kHist == HIST_RANGE16   ? (p.q_span + 1) / 2 : 0u;  // dwords
     for (uint32_t e = tid; e < nbins; e += kBlock) bins[e] = 0;
     uint32_t* reta_lds = bins + nbins;  // QM_TABLE: H entries after the bins
     if constexpr (kQMode == QM_TABLE)
@@ -497,6 +514,14 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
         __syncthreads();
         for (uint32_t r = tid; r < p.q_span; r += kBlock)
             if (bins[r]) atomicAdd(&p.counts[p.q_lo + r], (unsigned long long)bins[r]);
+    } else if constexpr (kHist == HIST_RANGE16) {
+        __syncthreads();
+        for (uint32_t w = tid; w < nbins; w += kBlock) {
+            const uint32_t x = bins[w], r = 2 * w;
+            if (x & 0xFFFFu) atomicAdd(&p.counts[p.q_lo + r], (unsigned long long)(x & 0xFFFFu));
+            if ((x >> 16) && r + 1 < p.q_span)
+                atomicAdd(&p.counts[p.q_lo + r + 1], (unsigned long long)(x >> 16));
+        }
     }
 }
 
@@ -1415,6 +1440,7 @@ KernelFn pick_hist(int hist, int qwidth, bool vec4) {
         case HIST_SHARED: return pick_width<kHPow2, kQMode, HIST_SHARED>(qwidth, vec4);
         case HIST_GLOBAL: return pick_width<kHPow2, kQMode, HIST_GLOBAL>(qwidth, vec4);
         case HIST_RANGE: return pick_width<kHPow2, kQMode, HIST_RANGE>(qwidth, vec4);
+        case HIST_RANGE16: return pick_width<kHPow2, kQMode, HIST_RANGE16>(qwidth, vec4);
         default: return pick_width<kHPow2, kQMode, HIST_NONE>(qwidth, vec4);
     }
 }
@@ -1852,8 +1878,20 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
     const uint64_t cap = (uint64_t)info.cu_count * kBlocksPerCU;
     const unsigned grid = (unsigned)(want < cap ? want : cap);
     if (hist == HIST_GLOBAL && d_counts) {
-        const uint32_t span = (kBinBytesMax - reta_bytes) / 4;
+        // u16 bins with the guard bit (HIST_RANGE16): twice the queues of u32 bins in the LDS
+        // the tables leave -- up to 16384 queues in the hash pass itself, no queue column
+        const uint32_t span = ((kBinBytesMax - reta_bytes) / 4) * 2;
         const uint32_t qbytes = q_eff <= 65536u ? 2 : 4;
+        if (q_eff <= span) {
+            p.q_lo = 0;
+            p.q_span = q_eff;
+            KernelFn fn = h_pow2 ? pick_queue<true>(qmode, HIST_RANGE16, qwidth, vec4)
+                                 : pick_queue<false>(qmode, HIST_RANGE16, qwidth, vec4);
+            hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), ((q_eff + 1) / 2) * 4 + reta_bytes,
+                               stream, p);
+            RSS_HIP_CHECK(hipGetLastError());
+            return RSS_OK;
+        }
         if (ranged_histogram_ok(q_eff, span, qbytes)) {
             void* qcol = d_queue;
             int qw = qwidth;
@@ -1870,12 +1908,12 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
             if (ranged) {
                 p.queue_out = qcol;
                 p.q_lo = 0;
-                p.q_span = std::min<uint32_t>(span, q_eff);
+                p.q_span = span;  // < q_eff here
                 const bool v4 = vec4 && ((uintptr_t)qcol % (qw == QW_U16 ? 8 : 16)) == 0;
-                KernelFn fn = h_pow2 ? pick_queue<true>(qmode, HIST_RANGE, qw, v4)
-                                     : pick_queue<false>(qmode, HIST_RANGE, qw, v4);
+                KernelFn fn = h_pow2 ? pick_queue<true>(qmode, HIST_RANGE16, qw, v4)
+                                     : pick_queue<false>(qmode, HIST_RANGE16, qw, v4);
                 const unsigned g1 = v4 ? grid : (unsigned)std::min<uint64_t>((n + kBlock - 1) / kBlock, cap);
-                hipLaunchKernelGGL(fn, dim3(g1), dim3(kBlock), span * 4 + reta_bytes, stream, p);
+                hipLaunchKernelGGL(fn, dim3(g1), dim3(kBlock), (span / 2) * 4 + reta_bytes, stream, p);
                 const hipError_t le = hipGetLastError();
                 rc = le == hipSuccess
                          ? launch_queue_ranges(qcol, qw, n, span, q_eff, p.counts, info.cu_count, stream)

@@ -156,16 +156,18 @@ def test_wide_equals_narrow_passes(native, oracle_lib, example_key, H, Q):
             os.environ.pop("RSS_WIDE_HIST", None)
 
 
-@pytest.mark.parametrize("Q", [40000, 100000])
-def test_wide_guard_bit_on_one_hot_queue(native, oracle_lib, example_key, Q):
-    """2^25 identical tuples plus 4099 random ones: every workgroup of the wide pass counts
-    ~2^17 adds into one u16 bin, so the guard bit moves 2^15 out of it again and again; the
-    counts stay exact (the identical tuples' queue gets all 2^25)."""
+@pytest.mark.parametrize("Q,lo,hi", [(100000, 16384, 100000), (40000, 0, 16384),
+                                     (12000, 8192, 12000)])
+def test_wide_guard_bit_on_one_hot_queue(native, oracle_lib, example_key, Q, lo, hi):
+    """2^25 identical tuples plus 4099 random ones, the identical tuples' queue in [lo, hi):
+    every workgroup counts ~2^17 adds into one u16 bin -- of the wide pass (q >= 16384) or of
+    the hash pass's own u16 range (HIST_RANGE16, q < 16384; Q = 12000 is a single pass) -- so
+    the guard bit moves 2^15 out of it again and again; the counts stay exact."""
     n_same, n_rand = 1 << 25, 4099
     H = 1 << 30
     rnd = oracle_lib.generate(28, 0, n_rand)
     _, q_rnd, _ = oracle_lib.run(example_key, rnd, H, Q)
-    pick = int(np.flatnonzero(q_rnd >= 8192)[0])  # a queue past the hash pass's LDS range
+    pick = int(np.flatnonzero((q_rnd >= lo) & (q_rnd < hi))[0])
     one = rnd[pick:pick + 1]
     host = np.concatenate([np.repeat(one, n_same, axis=0), rnd])
     dev = torch.device("cuda:0")

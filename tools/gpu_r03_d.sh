@@ -6,7 +6,7 @@ OUT=$R/gpurun_out/${1:-r03_d}
 mkdir -p $OUT
 cd $R
 timeout -k 10 600 python -u -m pytest -v -m gpu --timeout 300 --timeout-method thread \
-    tests/test_gpu_range_hist.py tests/test_gpu_single_pass.py > $OUT/pytest.log 2>&1
+    tests/test_gpu_range_hist.py tests/test_gpu_single_pass.py tests/test_gpu_random_sweep.py tests/test_gpu_queues_ge_htable.py tests/test_gpu_parity.py > $OUT/pytest.log 2>&1
 echo "pytest ok"
 timeout -k 10 300 python tools/config_sweep_probe.py > $OUT/config_sweep.jsonl 2> $OUT/config_sweep.err
 echo "sweep ok"
