@@ -1,0 +1,28 @@
+#!/bin/bash
+# GPU box: round 3's final validation in one call -- the full -m gpu suite, smoke(), the
+# driver's bench command, a rocprofv3 kernel trace of the same command (+ its timed-launch
+# summary) and the FETCH_SIZE / WRITE_SIZE passes of the bench's step.
+# usage: tools/gpu_validate_r03.sh TAG     (outputs under gpurun_out/TAG/)
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=${1:-r03_final}
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+cd $R
+timeout -k 10 900 python -u -m pytest -q -m gpu --timeout 300 --timeout-method thread tests \
+    > $O/pytest_gpu.log 2>&1
+rc=$?
+tail -3 $O/pytest_gpu.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+set -e
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+tail -2 $O/smoke.log
+timeout -k 10 400 python bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err
+export TMPDIR=/tmp
+cd /tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- \
+    python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/prof.log 2>&1
+python3 $R/tools/prof_timed.py $O/prof/run_kernel_trace.csv $O/prof.log > $O/prof_timed.json
+cat $O/prof_timed.json
+bash $R/tools/pmc_traffic.sh $TAG/pmc > $O/pmc.log 2>&1
+echo "validate done"
