@@ -332,7 +332,7 @@ def gather_rows(torch, dist, row, device, distributed, world):
 
 
 def run_configs3(args, torch, dist, _native, dev, stream, key, comm, rank, world, distributed,
-                 barrier, qw, qflag, probe, gold):
+                 barrier, qw, probe, gold):
     """BASELINE configs[3] as a strong-scaling batch: ``--configs3-tuples`` global tuples of
     the bench stream split over the ranks by ``sharding.shard_range``; one batch = one
     ``rss_hash_device_ws`` launch per rank over its resident shard + ONE all-reduce of the
@@ -744,7 +744,7 @@ def main():
     c3 = None
     if args.configs3_tuples > 0:
         c3 = run_configs3(args, torch, dist, _native, dev, stream, key, comm, rank, world,
-                          distributed, barrier, qw, qflag, probe, gold if verify_ok else None)
+                          distributed, barrier, qw, probe, gold if verify_ok else None)
         verified["configs3"] = c3.pop("verified")
 
     # every rank's timings and placement, gathered for the line (rank 0 prints it)
