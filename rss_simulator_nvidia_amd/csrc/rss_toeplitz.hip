@@ -109,6 +109,8 @@ struct LaunchParams {
     uint32_t q_m16;     // ceil(2^16 / Q): exact b % Q for b < 256 (QM_FAST8, packed search)
     const uint32_t* key_windows;  // key search: nkeys x 96 windows in device memory
     uint32_t q_lo, q_span;        // HIST_RANGE: the queues this pass counts
+    uint32_t* partial;            // HIST_RANGE16: u16 [grid][partial_stride] rows, or NULL
+    uint32_t partial_stride;      //   (atomics into counts); dwords per row
     uint32_t q_stride;            // key search: row stride of the [keys, nqueues] counts (>= Q)
     uint32_t tail_rows;           // balanced tail: rows handed out as units (0 = static grid-stride)
     uint32_t bal_off;             // balanced tail: byte offset of its LDS slot (dynamic LDS)
@@ -208,6 +210,51 @@ __device__ __forceinline__ uint32_t toeplitz_hash(const uint32_t* __restrict__ l
                 lut_term<6>(base, w0, w1, w2, hi) ^ lut_term<7>(base, w0, w1, w2, hi));
 }
 
+// Byte tables (many-queues launches, DESIGN.md §3 "Many queues"): twelve tables of 256
+// entries, table 4k + j indexed by byte j of word k (LSB first, as above) -- 12 KiB instead
+// of 128, so the LDS left for u16 histogram bins grows from 16384 to ~75000 queues, for 12
+// ds_read_b32 per tuple instead of 8.  Entry (t, v) lives at LDS byte t*1024 + v*4.
+constexpr int kByteTables = RSS_INPUT_BITS / 8;                 // 12
+constexpr uint32_t kByteLutDwords = kByteTables * 256;          // 3072
+constexpr uint32_t kByteLutBytes = kByteLutDwords * 4;          // 12 KiB
+__host__ __device__ constexpr int byte_slice_bit(int t, int b) {  // word t/4, bit 8 (t%4) + b
+    return 32 * (t / 4) + 31 - 8 * (t % 4) - b;
+}
+
+__device__ __forceinline__ void build_byte_lut(uint32_t* lut, const uint32_t* __restrict__ window,
+                                               uint32_t tid) {
+    for (uint32_t e = tid; e < kByteLutDwords; e += kBlock) {
+        const int t = (int)(e >> 8);
+        uint32_t v = 0;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) v ^= ((e >> b) & 1u) ? window[byte_slice_bit(t, b)] : 0u;
+        lut[e] = v;
+    }
+}
+
+template <int kT>
+__device__ __forceinline__ uint32_t byte_term(const char* lut, uint32_t w) {
+    constexpr int j = kT & 3;
+    const uint32_t off = j == 0 ? (w << 2) & 0x3FCu : (w >> (8 * j - 2)) & 0x3FCu;
+    return *reinterpret_cast<const uint32_t*>(lut + kT * 1024 + off);
+}
+
+__device__ __forceinline__ uint32_t toeplitz_hash_bytes(const uint32_t* __restrict__ lut, uint32_t w0,
+                                                        uint32_t w1, uint32_t w2) {
+    const char* b = reinterpret_cast<const char*>(lut);
+    return xor3(xor3(xor3(byte_term<0>(b, w0), byte_term<1>(b, w0), byte_term<2>(b, w0)),
+                     xor3(byte_term<3>(b, w0), byte_term<4>(b, w1), byte_term<5>(b, w1)),
+                     xor3(byte_term<6>(b, w1), byte_term<7>(b, w1), byte_term<8>(b, w2))),
+                byte_term<9>(b, w2), byte_term<10>(b, w2) ^ byte_term<11>(b, w2));
+}
+
+template <bool kByteLut>
+__device__ __forceinline__ uint32_t hash_of(const uint32_t* lut, uint32_t w0, uint32_t w1,
+                                            uint32_t w2, uint32_t hi) {
+    if constexpr (kByteLut) return toeplitz_hash_bytes(lut, w0, w1, w2);
+    return toeplitz_hash(lut, w0, w1, w2, hi);
+}
+
 // hash % htable  (simulator.py:97, first modulo)
 template <bool kHPow2>
 __device__ __forceinline__ uint32_t bucket_of(uint32_t h, const LaunchParams& p) {
@@ -249,6 +296,27 @@ __device__ __forceinline__ uint32_t queue_lookup(uint32_t b, const LaunchParams&
     }
 }
 
+// HIST_RANGE16's two halves: the add (returns the dword's previous value, 0 out of range)
+// and the guard bit (the add that returned 0x7FFF moves 2^15 out of its bin).  The 4-tuple
+// body issues its four adds before the four guards, so they do not wait for each other.
+__device__ __forceinline__ uint32_t range16_add(uint32_t* bins, uint32_t q, const LaunchParams& p) {
+    const uint32_t r = q - p.q_lo;  // wraps for q < q_lo
+    if (r >= p.q_span) return 0u;
+    return __hip_atomic_fetch_add(&bins[r >> 1], 1u << ((r & 1u) * 16u), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ void range16_guard(uint32_t* bins, uint32_t q, uint32_t old,
+                                              const LaunchParams& p) {
+    const uint32_t r = q - p.q_lo;
+    const uint32_t sh = (r & 1u) * 16u;
+    if (r < p.q_span && ((old >> sh) & 0xFFFFu) == 0x7FFFu) {
+        __hip_atomic_fetch_sub(&bins[r >> 1], 0x8000u << sh, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+        atomicAdd(&p.counts[q], 0x8000ull);
+    }
+}
+
 template <int kHist>
 __device__ __forceinline__ void count_queue(uint32_t* bins, uint32_t q, uint32_t col,
                                             const LaunchParams& p) {
@@ -264,19 +332,11 @@ __device__ __forceinline__ void count_queue(uint32_t* bins, uint32_t q, uint32_t
         if (r < p.q_span)
             __hip_atomic_fetch_add(&bins[r], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     } else if constexpr (kHist == HIST_RANGE16) {
-        const uint32_t r = q - p.q_lo;
-        if (r < p.q_span) {
-            const uint32_t sh = (r & 1u) * 16u;
-            const uint32_t old = __hip_atomic_fetch_add(&bins[r >> 1], 1u << sh, __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (((old >> sh) & 0xFFFFu) == 0x7FFFu) {  // the guard bit: 2^15 out of the bin
-                __hip_atomic_fetch_sub(&bins[r >> 1], 0x8000u << sh, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_WORKGROUP);
-                atomicAdd(&p.counts[q], 0x8000ull);
-            }
-        }
+        range16_guard(bins, q, range16_add(bins, q, p), p);
     }
 }
+
+
 
 // Streaming outputs are written once and never re-read by this kernel: use
 // nontemporal stores so they do not displace the input stream in L2.
@@ -297,8 +357,8 @@ __device__ __forceinline__ void store_queue1(void* out, uint64_t i, uint32_t q) 
 }
 
 // four consecutive queues of group g (tuples 4g .. 4g+3) as one 4/8/16-byte store
-template <int kQWidth>
-__device__ __forceinline__ void store_queue4(void* out, uint64_t g, uint32_t q0, uint32_t q1,
+template <int kQWidth, typename Idx>
+__device__ __forceinline__ void store_queue4(void* out, Idx g, uint32_t q0, uint32_t q1,
                                              uint32_t q2, uint32_t q3) {
     if constexpr (kQWidth == QW_U8) {
         stream_store(static_cast<uint32_t*>(out) + g, q0 | q1 << 8 | q2 << 16 | q3 << 24);
@@ -425,25 +485,34 @@ inline uint32_t balanced_tail_rows(uint64_t ngroups, unsigned grid) {
     return rows >= 16 ? (uint32_t)std::max<uint64_t>(1, rows / 10) : 0u;
 }
 
-template <bool kHPow2, int kQMode, int kHist, int kQWidth>
+template <bool kHPow2, int kQMode, int kHist, int kQWidth, bool kByteLut>
 __device__ __forceinline__ void one_tuple(const uint32_t* lut, uint32_t* bins, uint64_t i,
                                           uint32_t col, uint32_t hi, const uint32_t* reta_lds,
                                           const LaunchParams& p) {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(p.tuples) + 3 * i;
-    const uint32_t h = toeplitz_hash(lut, src[0], src[1], src[2], hi);
+    const uint32_t h = hash_of<kByteLut>(lut, src[0], src[1], src[2], hi);
     const uint32_t q = queue_lookup<kQMode>(bucket_of<kHPow2>(h, p), p, reta_lds);
     if (p.hash_out) stream_store(p.hash_out + i, h);
     if (p.queue_out) store_queue1<kQWidth>(p.queue_out, i, q);
     count_queue<kHist>(bins, q, col, p);
 }
 
-template <bool kHPow2, int kQMode, int kHist, int kQWidth, bool kVec4>
+// kOff32 (with kVec4): every byte offset of the launch's streams fits 32 bits (12 n < 2^32,
+// e.g. 2^28 tuples), so the loads and stores address the kernel-argument base pointers with
+// a 32-bit per-lane offset (global_load ... v_off, s[base]) instead of 64-bit address pairs.
+// kByteLut: the 12 KiB byte tables instead of the 128 KiB 12-bit ones (many-queues
+// HIST_RANGE16 launches: the rest of the LDS holds up to ~75000 u16 bins).
+template <bool kHPow2, int kQMode, int kHist, int kQWidth, bool kVec4, bool kOff32 = false,
+          bool kByteLut = false>
 __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams p) {
-    __shared__ uint32_t lut[kLutDwords];  // static: table offsets fold into ds_read
+    __shared__ uint32_t lut[kByteLut ? kByteLutDwords : kLutDwords];  // static: table offsets fold into ds_read
     extern __shared__ uint32_t bins[];    // histogram bins, sized at launch
     const uint32_t tid = threadIdx.x;
 
-    build_lut(lut, p.window, tid);
+    if constexpr (kByteLut)
+        build_byte_lut(lut, p.window, tid);
+    else
+        build_lut(lut, p.window, tid);
     const uint32_t nbins = kHist == HIST_PRIVATE   ? p.Q * kBinCols
                          : kHist == HIST_SHARED    ? p.Q
                          : kHist == HIST_RANGE     ? p.q_span
@@ -466,36 +535,61 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
         const uint4* __restrict__ src = reinterpret_cast<const uint4*>(p.tuples);
         const uint64_t ngroups = p.n >> 2;
         auto group = [&](uint64_t g) {
-            const uint4 a = src[3 * g + 0];
-            const uint4 b = src[3 * g + 1];
-            const uint4 c = src[3 * g + 2];
-            const uint32_t h0 = toeplitz_hash(lut, a.x, a.y, a.z, hi);
-            const uint32_t h1 = toeplitz_hash(lut, a.w, b.x, b.y, hi);
-            const uint32_t h2 = toeplitz_hash(lut, b.z, b.w, c.x, hi);
-            const uint32_t h3 = toeplitz_hash(lut, c.y, c.z, c.w, hi);
+            uint4 a, b, c;
+            if constexpr (kOff32) {
+                const char* base = reinterpret_cast<const char*>(p.tuples);
+                const uint32_t off = 48u * (uint32_t)g;
+                a = *reinterpret_cast<const uint4*>(base + off);
+                b = *reinterpret_cast<const uint4*>(base + off + 16u);
+                c = *reinterpret_cast<const uint4*>(base + off + 32u);
+            } else {
+                a = src[3 * g + 0];
+                b = src[3 * g + 1];
+                c = src[3 * g + 2];
+            }
+            const uint32_t h0 = hash_of<kByteLut>(lut, a.x, a.y, a.z, hi);
+            const uint32_t h1 = hash_of<kByteLut>(lut, a.w, b.x, b.y, hi);
+            const uint32_t h2 = hash_of<kByteLut>(lut, b.z, b.w, c.x, hi);
+            const uint32_t h3 = hash_of<kByteLut>(lut, c.y, c.z, c.w, hi);
             const uint32_t q0 = queue_lookup<kQMode>(bucket_of<kHPow2>(h0, p), p, reta_lds);
             const uint32_t q1 = queue_lookup<kQMode>(bucket_of<kHPow2>(h1, p), p, reta_lds);
             const uint32_t q2 = queue_lookup<kQMode>(bucket_of<kHPow2>(h2, p), p, reta_lds);
             const uint32_t q3 = queue_lookup<kQMode>(bucket_of<kHPow2>(h3, p), p, reta_lds);
             if (p.hash_out) {
-                uint32_t* o = p.hash_out + 4 * g;
+                uint32_t* o = kOff32 ? reinterpret_cast<uint32_t*>(
+                                           reinterpret_cast<char*>(p.hash_out) + 16u * (uint32_t)g)
+                                     : p.hash_out + 4 * g;
                 stream_store(o, h0);
                 stream_store(o + 1, h1);
                 stream_store(o + 2, h2);
                 stream_store(o + 3, h3);
             }
-            if (p.queue_out) store_queue4<kQWidth>(p.queue_out, g, q0, q1, q2, q3);
-            count_queue<kHist>(bins, q0, col, p);
-            count_queue<kHist>(bins, q1, col, p);
-            count_queue<kHist>(bins, q2, col, p);
-            count_queue<kHist>(bins, q3, col, p);
+            if (p.queue_out) {
+                if constexpr (kOff32)
+                    store_queue4<kQWidth>(p.queue_out, (uint32_t)g, q0, q1, q2, q3);
+                else
+                    store_queue4<kQWidth>(p.queue_out, g, q0, q1, q2, q3);
+            }
+            if constexpr (kHist == HIST_RANGE16) {
+                const uint32_t o0 = range16_add(bins, q0, p), o1 = range16_add(bins, q1, p);
+                const uint32_t o2 = range16_add(bins, q2, p), o3 = range16_add(bins, q3, p);
+                range16_guard(bins, q0, o0, p);
+                range16_guard(bins, q1, o1, p);
+                range16_guard(bins, q2, o2, p);
+                range16_guard(bins, q3, o3, p);
+            } else {
+                count_queue<kHist>(bins, q0, col, p);
+                count_queue<kHist>(bins, q1, col, p);
+                count_queue<kHist>(bins, q2, col, p);
+                count_queue<kHist>(bins, q3, col, p);
+            }
         };
         walk_rows(group, ngroups, p.tail_rows, p.ws + 1 + p.Q,
                   reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(bins) + p.bal_off));
         tail_begin = ngroups << 2;
     }
     for (uint64_t i = tail_begin + gtid; i < p.n; i += gstride)
-        one_tuple<kHPow2, kQMode, kHist, kQWidth>(lut, bins, i, col, hi, reta_lds, p);
+        one_tuple<kHPow2, kQMode, kHist, kQWidth, kByteLut>(lut, bins, i, col, hi, reta_lds, p);
 
     // Epilogue: fold this workgroup's bins into the global uint64 counts.
     if constexpr (kHist == HIST_PRIVATE || kHist == HIST_SHARED) {
@@ -516,6 +610,11 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
             if (bins[r]) atomicAdd(&p.counts[p.q_lo + r], (unsigned long long)bins[r]);
     } else if constexpr (kHist == HIST_RANGE16) {
         __syncthreads();
+        if (p.partial) {  // one row of the u16 partial matrix (rss_partial_reduce_kernel)
+            uint32_t* row = p.partial + (size_t)blockIdx.x * p.partial_stride;
+            for (uint32_t w = tid; w < nbins; w += kBlock) row[w] = bins[w];
+            return;
+        }
         for (uint32_t w = tid; w < nbins; w += kBlock) {
             const uint32_t x = bins[w], r = 2 * w;
             if (x & 0xFFFFu) atomicAdd(&p.counts[p.q_lo + r], (unsigned long long)(x & 0xFFFFu));
@@ -580,6 +679,7 @@ __global__ __launch_bounds__(kBlock) void rss_queue_hist_kernel(const T* __restr
 // plain coalesced stores -- not Q atomics per workgroup, which would cost more than the pass
 // at Q = 65536 -- and rss_partial_reduce_kernel sums the rows into the counts.
 constexpr uint32_t kWideSpan = 65536;  // 128 KiB of u16 bins: one workgroup per CU
+constexpr uint32_t kNarrowSpan = 16384;  // rss_queue_hist_kernel: u32 bins, two workgroups per CU
 
 template <typename T>
 __global__ __launch_bounds__(kBlock) void rss_queue_hist_wide_kernel(
@@ -1418,14 +1518,24 @@ int device_info(DeviceInfo* out) {
 
 using KernelFn = void (*)(const LaunchParams);
 
+// vec4: 0 = one tuple per lane, 1 = four per lane, 2 = four per lane with 32-bit byte offsets
+// (kOff32; instantiated for the single-pass histogram modes only, the bench's step), 3 = four
+// per lane on the byte tables (kByteLut; HIST_RANGE16 only)
+enum VecMode { VM_SCALAR = 0, VM_VEC4 = 1, VM_OFF32 = 2, VM_BYTE_LUT = 3 };
 template <bool kHPow2, int kQMode, int kHist, int kQWidth>
-KernelFn pick_vec(bool vec4) {
+KernelFn pick_vec(int vec4) {
+    if constexpr (kHist == HIST_PRIVATE || kHist == HIST_SHARED)
+        if (vec4 == VM_OFF32) return rss_toeplitz_kernel<kHPow2, kQMode, kHist, kQWidth, true, true>;
+    if constexpr (kHist == HIST_RANGE16 && kQWidth != QW_U8 && kQMode != QM_FAST8 &&
+                  kQMode != QM_TABLE)  // (H <= 1024 with those: never this many queues)
+        if (vec4 == VM_BYTE_LUT)
+            return rss_toeplitz_kernel<kHPow2, kQMode, kHist, kQWidth, true, false, true>;
     return vec4 ? rss_toeplitz_kernel<kHPow2, kQMode, kHist, kQWidth, true>
                 : rss_toeplitz_kernel<kHPow2, kQMode, kHist, kQWidth, false>;
 }
 
 template <bool kHPow2, int kQMode, int kHist>
-KernelFn pick_width(int qwidth, bool vec4) {
+KernelFn pick_width(int qwidth, int vec4) {
     switch (qwidth) {
         case QW_U8: return pick_vec<kHPow2, kQMode, kHist, QW_U8>(vec4);
         case QW_U16: return pick_vec<kHPow2, kQMode, kHist, QW_U16>(vec4);
@@ -1434,7 +1544,7 @@ KernelFn pick_width(int qwidth, bool vec4) {
 }
 
 template <bool kHPow2, int kQMode>
-KernelFn pick_hist(int hist, int qwidth, bool vec4) {
+KernelFn pick_hist(int hist, int qwidth, int vec4) {
     switch (hist) {
         case HIST_PRIVATE: return pick_width<kHPow2, kQMode, HIST_PRIVATE>(qwidth, vec4);
         case HIST_SHARED: return pick_width<kHPow2, kQMode, HIST_SHARED>(qwidth, vec4);
@@ -1446,7 +1556,7 @@ KernelFn pick_hist(int hist, int qwidth, bool vec4) {
 }
 
 template <bool kHPow2>
-KernelFn pick_queue(int qmode, int hist, int qwidth, bool vec4) {
+KernelFn pick_queue(int qmode, int hist, int qwidth, int vec4) {
     switch (qmode) {
         case QM_MASK: return pick_hist<kHPow2, QM_MASK>(hist, qwidth, vec4);
         case QM_FAST16: return pick_hist<kHPow2, QM_FAST16>(hist, qwidth, vec4);
@@ -1652,6 +1762,12 @@ bool ws_order_acqrel() {
     return !(e && strcmp(e, "relaxed") == 0);
 }
 
+// RSS_OFF32=0: 64-bit addressing even where 32-bit byte offsets fit (A/B, tests)
+bool off32_enabled() {
+    const char* e = getenv("RSS_OFF32");
+    return !(e && e[0] == '0');
+}
+
 // RSS_BALANCE=0: single-pass launches keep the static grid-stride to the end (A/B, tests);
 // read at every launch like RSS_WS_ORDER
 bool balance_enabled() {
@@ -1725,16 +1841,23 @@ bool ranged_histogram_ok(uint32_t q_eff, uint32_t span, uint32_t qbytes) {
     return ((uint64_t)q_eff + span - 1) / span <= (qbytes == 2 ? 64u : 32u);
 }
 
+// The byte tables for a many-queues launch (kByteLut); RSS_BYTE_LUT=0 keeps the 12-bit tables.
+bool byte_lut_enabled() {
+    const char* e = getenv("RSS_BYTE_LUT");
+    return !(e && e[0] == '0');
+}
+
 // Queue ranges [span, nqueues) of a many-queues launch, histogrammed from the queue column
 // (u16 or u32) the first pass wrote: one wide pass (u16 LDS bins, rows of a u16 partial
 // matrix, then a reduce) per kWideSpan queues; RSS_WIDE_HIST=0 (or no memory for the
 // partial matrix) keeps one rss_queue_hist_kernel pass per `span` queues.
-int launch_queue_ranges(const void* qcol, int qw, uint64_t n, uint32_t span, uint32_t nqueues,
+int launch_queue_ranges(const void* qcol, int qw, uint64_t n, uint32_t first, uint32_t nqueues,
                         unsigned long long* counts, int cu_count, hipStream_t stream) {
-    if (span >= nqueues) return RSS_OK;
+    if (first >= nqueues) return RSS_OK;
+    const uint32_t span = kNarrowSpan;
     // a wide pass costs about two narrow ones (2^28 tuples: ~0.2 vs ~0.1 ms over a u16
     // column, profiles/r03/d/config_sweep.jsonl), so it pays from three narrow passes on
-    const uint64_t narrow_passes = ((uint64_t)nqueues - span + span - 1) / span;
+    const uint64_t narrow_passes = ((uint64_t)nqueues - first + span - 1) / span;
     if (wide_hist_enabled() && narrow_passes >= 3) {
         const uint64_t want = (n + 8ull * kBlock - 1) / (8ull * kBlock);
         const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, cu_count));
@@ -1742,7 +1865,7 @@ int launch_queue_ranges(const void* qcol, int qw, uint64_t n, uint32_t span, uin
         void* partial = nullptr;
         if (hipMallocAsync(&partial, (size_t)grid * stride_words * 4, stream) == hipSuccess) {
             int rc = RSS_OK;
-            for (uint32_t lo = span; lo < nqueues && rc == RSS_OK; lo += std::min(kWideSpan, nqueues - lo)) {
+            for (uint32_t lo = first; lo < nqueues && rc == RSS_OK; lo += std::min(kWideSpan, nqueues - lo)) {
                 const uint32_t sp = std::min<uint32_t>(kWideSpan, nqueues - lo);
                 const uint32_t lds = ((sp + 1) / 2) * 4;
                 if (qw == QW_U16)
@@ -1775,7 +1898,7 @@ int launch_queue_ranges(const void* qcol, int qw, uint64_t n, uint32_t span, uin
     }
     const uint64_t qwant = (n + 8ull * kBlock - 1) / (8ull * kBlock);
     const unsigned qgrid = (unsigned)std::min<uint64_t>(qwant, (uint64_t)cu_count * 2);
-    for (uint32_t lo = span; lo < nqueues; lo += span) {
+    for (uint32_t lo = first; lo < nqueues; lo += span) {
         const uint32_t sp = std::min<uint32_t>(span, nqueues - lo);
         if (qw == QW_U16)
             hipLaunchKernelGGL(rss_queue_hist_kernel<uint16_t>, dim3(qgrid), dim3(kBlock), sp * 4,
@@ -1786,6 +1909,42 @@ int launch_queue_ranges(const void* qcol, int qw, uint64_t n, uint32_t span, uin
         RSS_HIP_CHECK(hipGetLastError());
     }
     return RSS_OK;
+}
+
+// A HIST_RANGE16 hash launch over `span` = p.q_span queues.  A wide range's workgroups store
+// their u16 bins as rows of a partial matrix that rss_partial_reduce_kernel sums into the
+// counts (as the wide pass does) -- grid x span u64 atomics instead would cost ~0.2 ms at
+// 65536 queues (256 x 65536 = 16.8M; profiles/r03/e/config_sweep_many.jsonl); a narrow one,
+// or one with no memory for the matrix, folds its bins with atomics.
+constexpr uint32_t kPartialMinSpan = 2048;
+int launch_range16(KernelFn fn, unsigned grid, uint32_t shmem, LaunchParams& p, hipStream_t stream) {
+    const uint32_t words = (p.q_span + 1) / 2;
+    void* partial = nullptr;
+    if (p.q_span >= kPartialMinSpan &&
+        hipMallocAsync(&partial, (size_t)grid * words * 4, stream) != hipSuccess) {
+        (void)hipGetLastError();
+        partial = nullptr;
+    }
+    p.partial = static_cast<uint32_t*>(partial);
+    p.partial_stride = words;
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), shmem, stream, p);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess && partial) {
+        hipLaunchKernelGGL(rss_partial_reduce_kernel, dim3((words + kReduceCols - 1) / kReduceCols),
+                           dim3(kReduceCols * kReduceGroups), 0, stream,
+                           static_cast<const uint32_t*>(partial), grid, words, p.q_lo, p.q_span,
+                           p.counts);
+        e = hipGetLastError();
+    }
+    int rc = e == hipSuccess ? RSS_OK
+                             : set_error(RSS_EIO, "rss_hash_device: launch failed: %s", hipGetErrorString(e));
+    if (partial) {  // stream-ordered after its reader, on every path
+        const hipError_t fe = hipFreeAsync(partial, stream);
+        if (fe != hipSuccess && rc == RSS_OK)
+            rc = set_error(RSS_EIO, "hipFreeAsync failed: %s", hipGetErrorString(fe));
+    }
+    p.partial = nullptr;
+    return rc;
 }
 
 // ws: rss_hash_device_ws's single-pass counts workspace, or NULL (counts zeroed by a
@@ -1879,20 +2038,24 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
     const unsigned grid = (unsigned)(want < cap ? want : cap);
     if (hist == HIST_GLOBAL && d_counts) {
         // u16 bins with the guard bit (HIST_RANGE16): twice the queues of u32 bins in the LDS
-        // the tables leave -- up to 16384 queues in the hash pass itself, no queue column
-        const uint32_t span = ((kBinBytesMax - reta_bytes) / 4) * 2;
+        // the tables leave -- 16384 beside the 12-bit tables, and past that, on the byte
+        // tables (4-tuple body, no indirection table), up to 75776 in the hash pass itself; no
+        // queue column for those.  (Up to 16384 the 12-bit tables' 8 lookups are faster: 0.595
+        // vs 0.68 ms counts only, profiles/r03/e2/config_sweep_many.jsonl.)
+        const uint32_t span12 = ((kBinBytesMax - reta_bytes) / 4) * 2;
+        const bool byte_lut = q_eff > span12 && vec4 && !reta && qwidth != QW_U8 && byte_lut_enabled();
+        const uint32_t lut_bytes = byte_lut ? kByteLutBytes : kLutBytes;
+        const uint32_t span = ((kLdsBytes - lut_bytes - reta_bytes) / 4) * 2;
+        const int vm = byte_lut ? VM_BYTE_LUT : (vec4 ? VM_VEC4 : VM_SCALAR);
         const uint32_t qbytes = q_eff <= 65536u ? 2 : 4;
         if (q_eff <= span) {
             p.q_lo = 0;
             p.q_span = q_eff;
-            KernelFn fn = h_pow2 ? pick_queue<true>(qmode, HIST_RANGE16, qwidth, vec4)
-                                 : pick_queue<false>(qmode, HIST_RANGE16, qwidth, vec4);
-            hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), ((q_eff + 1) / 2) * 4 + reta_bytes,
-                               stream, p);
-            RSS_HIP_CHECK(hipGetLastError());
-            return RSS_OK;
+            KernelFn fn = h_pow2 ? pick_queue<true>(qmode, HIST_RANGE16, qwidth, vm)
+                                 : pick_queue<false>(qmode, HIST_RANGE16, qwidth, vm);
+            return launch_range16(fn, grid, ((q_eff + 1) / 2) * 4 + reta_bytes, p, stream);
         }
-        if (ranged_histogram_ok(q_eff, span, qbytes)) {
+        if (ranged_histogram_ok(q_eff, kNarrowSpan, qbytes)) {
             void* qcol = d_queue;
             int qw = qwidth;
             bool scratch = false, ranged = true;
@@ -1908,17 +2071,19 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
             if (ranged) {
                 p.queue_out = qcol;
                 p.q_lo = 0;
-                p.q_span = span;  // < q_eff here
                 const bool v4 = vec4 && ((uintptr_t)qcol % (qw == QW_U16 ? 8 : 16)) == 0;
-                KernelFn fn = h_pow2 ? pick_queue<true>(qmode, HIST_RANGE16, qw, v4)
-                                     : pick_queue<false>(qmode, HIST_RANGE16, qw, v4);
+                // the first range: the bins the first pass's tables leave (byte tables: 4-tuple
+                // body only; the caller's queue buffer may not be aligned for it)
+                const bool b1 = byte_lut && v4 && qw != QW_U8;
+                const uint32_t span1 = b1 ? span : span12;
+                p.q_span = span1;  // < q_eff here
+                const int vm1 = b1 ? VM_BYTE_LUT : (v4 ? VM_VEC4 : VM_SCALAR);
+                KernelFn fn = h_pow2 ? pick_queue<true>(qmode, HIST_RANGE16, qw, vm1)
+                                     : pick_queue<false>(qmode, HIST_RANGE16, qw, vm1);
                 const unsigned g1 = v4 ? grid : (unsigned)std::min<uint64_t>((n + kBlock - 1) / kBlock, cap);
-                hipLaunchKernelGGL(fn, dim3(g1), dim3(kBlock), (span / 2) * 4 + reta_bytes, stream, p);
-                const hipError_t le = hipGetLastError();
-                rc = le == hipSuccess
-                         ? launch_queue_ranges(qcol, qw, n, span, q_eff, p.counts, info.cu_count, stream)
-                         : set_error(RSS_EIO, "rss_hash_device: range launch failed: %s",
-                                     hipGetErrorString(le));
+                rc = launch_range16(fn, g1, (span1 / 2) * 4 + reta_bytes, p, stream);
+                if (rc == RSS_OK)
+                    rc = launch_queue_ranges(qcol, qw, n, span1, q_eff, p.counts, info.cu_count, stream);
                 // the scratch column goes back on every path (stream-ordered after its readers)
                 if (scratch) {
                     const hipError_t fe = hipFreeAsync(qcol, stream);
@@ -1929,8 +2094,10 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
             }
         }
     }
-    KernelFn fn = h_pow2 ? pick_queue<true>(qmode, hist, qwidth, vec4)
-                         : pick_queue<false>(qmode, hist, qwidth, vec4);
+    // 32-bit byte offsets when every stream's bytes fit them (input 12 n B is the largest)
+    const int vmode = vec4 ? (12ull * n < (1ull << 32) && off32_enabled() ? 2 : 1) : 0;
+    KernelFn fn = h_pow2 ? pick_queue<true>(qmode, hist, qwidth, vmode)
+                         : pick_queue<false>(qmode, hist, qwidth, vmode);
     uint32_t shmem = bin_bytes + reta_bytes;  // dynamic part; the 128 KiB LUT is static
     // Balanced tail (single-pass launches: the workspace holds its unit counter and is used
     // by one launch at a time): the last ~1/10 of the grid-stride rows handed out per

@@ -156,13 +156,14 @@ def test_wide_equals_narrow_passes(native, oracle_lib, example_key, H, Q):
             os.environ.pop("RSS_WIDE_HIST", None)
 
 
-@pytest.mark.parametrize("Q,lo,hi", [(100000, 16384, 100000), (40000, 0, 16384),
-                                     (12000, 8192, 12000)])
+@pytest.mark.parametrize("Q,lo,hi", [(160000, 75776, 160000), (100000, 16384, 75776),
+                                     (40000, 0, 16384), (12000, 8192, 12000)])
 def test_wide_guard_bit_on_one_hot_queue(native, oracle_lib, example_key, Q, lo, hi):
     """2^25 identical tuples plus 4099 random ones, the identical tuples' queue in [lo, hi):
-    every workgroup counts ~2^17 adds into one u16 bin -- of the wide pass (q >= 16384) or of
-    the hash pass's own u16 range (HIST_RANGE16, q < 16384; Q = 12000 is a single pass) -- so
-    the guard bit moves 2^15 out of it again and again; the counts stay exact."""
+    every workgroup counts ~2^17 adds into one u16 bin -- of the wide pass (q >= 75776) or of
+    the hash pass's own u16 range (HIST_RANGE16 on the byte tables, q < 75776; Q = 12000 is a
+    single pass) -- so the guard bit moves 2^15 out of it again and again; the counts stay
+    exact."""
     n_same, n_rand = 1 << 25, 4099
     H = 1 << 30
     rnd = oracle_lib.generate(28, 0, n_rand)
@@ -183,3 +184,65 @@ def test_wide_guard_bit_on_one_hot_queue(native, oracle_lib, example_key, Q, lo,
     got = c.cpu().numpy().view(np.uint64)
     np.testing.assert_array_equal(got, want)
     assert int(got[int(q1[0])]) >= n_same
+
+
+@pytest.mark.parametrize("H,Q", [(1 << 20, 16385), (0xFFFFFFFF, 65536), (1 << 30, 75776),
+                                 (1 << 30, 75777), (1 << 30, 131072), (99991, 50000)])
+def test_byte_tables_equal_12bit_tables(native, oracle_lib, example_key, H, Q):
+    """Many-queues launches hash on the 12 KiB byte tables (kByteLut: up to 75776 queues in
+    the hash pass's u16 bins); RSS_BYTE_LUT=0 keeps the 12-bit tables (16384 queues, then the
+    queue column).  Both give the oracle's hashes, queues and counts on uniform and flow-like
+    input (one address pair, sequential ports), with outputs and counts only."""
+    import os
+    n = (1 << 21) + 5
+    uni = oracle_lib.generate(29, 0, n)
+    flow = uni.copy()
+    flow[:, 0], flow[:, 1] = uni[0, 0], uni[0, 1]
+    flow[:, 2] = (np.arange(n, dtype=np.uint64) % (1 << 32)).astype(np.uint32)
+    dev = torch.device("cuda:0")
+    s = torch.cuda.current_stream(dev).cuda_stream
+    key = native.prepare_key(example_key)
+    u16 = Q <= 65536
+    for host in (uni, flow):
+        tup = torch.from_numpy(host.view(np.int32).reshape(-1)).to(dev)
+        ho, qo, co = oracle_lib.run(example_key, host, H, Q)
+        for lut in ("1", "0"):
+            os.environ["RSS_BYTE_LUT"] = lut
+            try:
+                h = torch.empty(n, dtype=torch.int32, device=dev)
+                q = torch.empty(n, dtype=torch.int16 if u16 else torch.int32, device=dev)
+                c = torch.full((Q,), 9, dtype=torch.int64, device=dev)
+                native.hash_device(key, tup.data_ptr(), n, H, Q, h.data_ptr(), q.data_ptr(),
+                                   c.data_ptr(), native.FLAG_QUEUE_U16 if u16 else 0, s)
+                c2 = torch.full((Q,), 9, dtype=torch.int64, device=dev)
+                native.hash_device(key, tup.data_ptr(), n, H, Q, None, None, c2.data_ptr(), 0, s)
+                torch.cuda.synchronize()
+            finally:
+                os.environ.pop("RSS_BYTE_LUT", None)
+            np.testing.assert_array_equal(h.cpu().numpy().view(np.uint32), ho)
+            qv = q.cpu().numpy().view(np.uint16 if u16 else np.uint32).astype(np.uint32)
+            np.testing.assert_array_equal(qv, qo)
+            np.testing.assert_array_equal(c.cpu().numpy().view(np.uint64), co)
+            np.testing.assert_array_equal(c2.cpu().numpy().view(np.uint64), co)
+
+
+def test_byte_tables_accumulate_and_queue_column_offsets(native, oracle_lib, example_key):
+    """Byte-table launches accumulate (RSS_FLAG_ACCUMULATE); a caller queue column 4 B off
+    the 16-B alignment of four u32 queues makes the first pass fall back to the 12-bit tables
+    and the one-tuple-per-lane body; a 16-B aligned one keeps the byte tables -- same counts."""
+    n, H, Q = (1 << 20) + 3, 1 << 26, 90000
+    host = oracle_lib.generate(30, 0, n)
+    tup = torch.from_numpy(host.view(np.int32).reshape(-1)).to("cuda:0")
+    s = torch.cuda.current_stream().cuda_stream
+    key = native.prepare_key(example_key)
+    _, qo, co = oracle_lib.run(example_key, host, H, Q)
+    for off in (0, 4):
+        qbuf = torch.zeros(n + 4, dtype=torch.int32, device="cuda:0")
+        c = torch.zeros(Q, dtype=torch.int64, device="cuda:0")
+        for _ in range(2):
+            native.hash_device(key, tup.data_ptr(), n, H, Q, None, qbuf.data_ptr() + off,
+                               c.data_ptr(), native.FLAG_ACCUMULATE, s)
+        torch.cuda.synchronize()
+        got_q = qbuf.cpu().numpy().view(np.uint8)[off:off + 4 * n].view(np.uint32)
+        np.testing.assert_array_equal(got_q, qo)
+        np.testing.assert_array_equal(c.cpu().numpy().view(np.uint64), 2 * co)

@@ -25,4 +25,6 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
 python3 $R/tools/prof_timed.py $O/prof/run_kernel_trace.csv $O/prof.log > $O/prof_timed.json
 cat $O/prof_timed.json
 bash $R/tools/pmc_traffic.sh $TAG/pmc > $O/pmc.log 2>&1
+cd $R
+for p in 1 2; do timeout -k 10 200 python tools/ws_order_ab.py 6 > $O/ab_$p.json 2> $O/ab_$p.err; done
 echo "validate done"

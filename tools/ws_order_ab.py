@@ -1,7 +1,7 @@
 """Same-process A/B of single-pass launch variants, alternating in blocks of launches on the
 same buffers: the default (release/acquire hand-off, balanced tail) against
 RSS_WS_ORDER=relaxed (no release ticket / acquire fence; round 2's form) and RSS_BALANCE=0
-(static grid-stride to the end); DESIGN.md §3 "Single-pass counts", "Balanced tail".  The bench's step:
+(static grid-stride to the end) and RSS_OFF32=0 (64-bit addressing); DESIGN.md §3 "Single-pass counts", "Balanced tail".  The bench's step:
 rss_hash_device_ws over 2^28 tuples, H=128, Q=24, u8 queues.
 
     python tools/ws_order_ab.py [rounds]
@@ -35,6 +35,7 @@ def main():
                           stream=stream)
     counts = torch.zeros(Q, dtype=torch.int64, device=dev)
     modes = {"default": {}, "relaxed": {"RSS_WS_ORDER": "relaxed"}, "static": {"RSS_BALANCE": "0"},
+             "off64": {"RSS_OFF32": "0"},
              "counts_default": {}, "counts_static": {"RSS_BALANCE": "0"}}
     res = {m: [] for m in modes}
     for _ in range(200):  # clock settle
@@ -42,7 +43,7 @@ def main():
     for r in range(rounds):
         order = list(modes) if r % 2 == 0 else list(modes)[::-1]
         for mode in order:
-            for var in ("RSS_WS_ORDER", "RSS_BALANCE"):
+            for var in ("RSS_WS_ORDER", "RSS_BALANCE", "RSS_OFF32"):
                 os.environ.pop(var, None)
             os.environ.update(modes[mode])
             outputs = not mode.startswith("counts")  # counts only: the register-table kernel
@@ -56,11 +57,12 @@ def main():
             torch.cuda.synchronize()
             res[mode].append(a.elapsed_time(b) / 50)
             assert int(counts.sum()) == n
-    for var in ("RSS_WS_ORDER", "RSS_BALANCE"):
+    for var in ("RSS_WS_ORDER", "RSS_BALANCE", "RSS_OFF32"):
         os.environ.pop(var, None)
     out = {m: {"ms_per_launch": v, "median": statistics.median(v)} for m, v in res.items()}
     out["default_minus_relaxed_us"] = 1e3 * (out["default"]["median"] - out["relaxed"]["median"])
     out["static_minus_default_us"] = 1e3 * (out["static"]["median"] - out["default"]["median"])
+    out["off64_minus_default_us"] = 1e3 * (out["off64"]["median"] - out["default"]["median"])
     out["counts_static_minus_default_us"] = 1e3 * (out["counts_static"]["median"] -
                                                    out["counts_default"]["median"])
     print(json.dumps(out))
