@@ -86,7 +86,10 @@ enum HistMode { HIST_PRIVATE = 0, HIST_SHARED = 1, HIST_GLOBAL = 2, HIST_NONE = 
 // HIST_RANGE: shared LDS bins for queues [q_lo, q_lo + q_span) only -- one pass of a
 // multi-pass launch for nqueues whose bins do not fit the LDS beside the tables
 // (launch_hash), instead of one global atomic per tuple (13x slower).
-enum QueueWidth { QW_U32 = 0, QW_U16 = 1, QW_U8 = 2 };
+enum QueueWidth { QW_U32 = 0, QW_U16 = 1, QW_U8 = 2, QW_U16R = 3 };
+// QW_U16R: a counts-only many-queues launch's scratch column (launch_hash): u16 q - q_span for
+// the queues past the hash pass's LDS range [0, q_span), 0xFFFF (never counted) for the rest --
+// half the bytes of a u32 column for the wide pass that counts [q_span, q_eff).
 
 // Everything a launch needs, passed by value in the kernarg segment.
 struct LaunchParams {
@@ -345,6 +348,15 @@ __device__ __forceinline__ void stream_store(T* dst, T v) {
     __builtin_nontemporal_store(v, dst);
 }
 
+// the value a queue column of width kQWidth holds for queue q (QW_U16R: see QueueWidth)
+template <int kQWidth>
+__device__ __forceinline__ uint32_t column_queue(uint32_t q, const LaunchParams& p) {
+    if constexpr (kQWidth == QW_U16R) return min(q - p.q_span, 0xFFFFu);  // q < q_span wraps
+    return q;
+}
+template <int kQWidth>
+constexpr int kStoreWidth = kQWidth == QW_U16R ? QW_U16 : kQWidth;
+
 template <int kQWidth>
 __device__ __forceinline__ void store_queue1(void* out, uint64_t i, uint32_t q) {
     if constexpr (kQWidth == QW_U8) {
@@ -493,7 +505,7 @@ __device__ __forceinline__ void one_tuple(const uint32_t* lut, uint32_t* bins, u
     const uint32_t h = hash_of<kByteLut>(lut, src[0], src[1], src[2], hi);
     const uint32_t q = queue_lookup<kQMode>(bucket_of<kHPow2>(h, p), p, reta_lds);
     if (p.hash_out) stream_store(p.hash_out + i, h);
-    if (p.queue_out) store_queue1<kQWidth>(p.queue_out, i, q);
+    if (p.queue_out) store_queue1<kStoreWidth<kQWidth>>(p.queue_out, i, column_queue<kQWidth>(q, p));
     count_queue<kHist>(bins, q, col, p);
 }
 
@@ -565,10 +577,13 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
                 stream_store(o + 3, h3);
             }
             if (p.queue_out) {
+                constexpr int kW = kStoreWidth<kQWidth>;
+                const uint32_t c0 = column_queue<kQWidth>(q0, p), c1 = column_queue<kQWidth>(q1, p);
+                const uint32_t c2 = column_queue<kQWidth>(q2, p), c3 = column_queue<kQWidth>(q3, p);
                 if constexpr (kOff32)
-                    store_queue4<kQWidth>(p.queue_out, (uint32_t)g, q0, q1, q2, q3);
+                    store_queue4<kW>(p.queue_out, (uint32_t)g, c0, c1, c2, c3);
                 else
-                    store_queue4<kQWidth>(p.queue_out, g, q0, q1, q2, q3);
+                    store_queue4<kW>(p.queue_out, g, c0, c1, c2, c3);
             }
             if constexpr (kHist == HIST_RANGE16) {
                 const uint32_t o0 = range16_add(bins, q0, p), o1 = range16_add(bins, q1, p);
@@ -1524,6 +1539,12 @@ using KernelFn = void (*)(const LaunchParams);
 enum VecMode { VM_SCALAR = 0, VM_VEC4 = 1, VM_OFF32 = 2, VM_BYTE_LUT = 3 };
 template <bool kHPow2, int kQMode, int kHist, int kQWidth>
 KernelFn pick_vec(int vec4) {
+    if constexpr (kQWidth == QW_U16R) {  // the byte-table HIST_RANGE16 body only
+        if constexpr (kHist == HIST_RANGE16 && kQMode != QM_FAST8 && kQMode != QM_TABLE)
+            if (vec4 == VM_BYTE_LUT)
+                return rss_toeplitz_kernel<kHPow2, kQMode, kHist, kQWidth, true, false, true>;
+        return nullptr;
+    }
     if constexpr (kHist == HIST_PRIVATE || kHist == HIST_SHARED)
         if (vec4 == VM_OFF32) return rss_toeplitz_kernel<kHPow2, kQMode, kHist, kQWidth, true, true>;
     if constexpr (kHist == HIST_RANGE16 && kQWidth != QW_U8 && kQMode != QM_FAST8 &&
@@ -1539,6 +1560,7 @@ KernelFn pick_width(int qwidth, int vec4) {
     switch (qwidth) {
         case QW_U8: return pick_vec<kHPow2, kQMode, kHist, QW_U8>(vec4);
         case QW_U16: return pick_vec<kHPow2, kQMode, kHist, QW_U16>(vec4);
+        case QW_U16R: return pick_vec<kHPow2, kQMode, kHist, QW_U16R>(vec4);
         default: return pick_vec<kHPow2, kQMode, kHist, QW_U32>(vec4);
     }
 }
@@ -1914,10 +1936,11 @@ int launch_queue_ranges(const void* qcol, int qw, uint64_t n, uint32_t first, ui
 // A HIST_RANGE16 hash launch over `span` = p.q_span queues.  A wide range's workgroups store
 // their u16 bins as rows of a partial matrix that rss_partial_reduce_kernel sums into the
 // counts (as the wide pass does) -- grid x span u64 atomics instead would cost ~0.2 ms at
-// 65536 queues (256 x 65536 = 16.8M; profiles/r03/e/config_sweep_many.jsonl); a narrow one,
+// 65536 queues (256 x 65536 = 16.8M; profiles/r03/many_queues/config_sweep_many_e1.jsonl); a narrow one,
 // or one with no memory for the matrix, folds its bins with atomics.
 constexpr uint32_t kPartialMinSpan = 2048;
 int launch_range16(KernelFn fn, unsigned grid, uint32_t shmem, LaunchParams& p, hipStream_t stream) {
+    if (!fn) return set_error(RSS_EIO, "rss_hash_device: no kernel instance for this launch");
     const uint32_t words = (p.q_span + 1) / 2;
     void* partial = nullptr;
     if (p.q_span >= kPartialMinSpan &&
@@ -2041,7 +2064,7 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
         // the tables leave -- 16384 beside the 12-bit tables, and past that, on the byte
         // tables (4-tuple body, no indirection table), up to 75776 in the hash pass itself; no
         // queue column for those.  (Up to 16384 the 12-bit tables' 8 lookups are faster: 0.595
-        // vs 0.68 ms counts only, profiles/r03/e2/config_sweep_many.jsonl.)
+        // vs 0.68 ms counts only, profiles/r03/many_queues/config_sweep_many_e2.jsonl.)
         const uint32_t span12 = ((kBinBytesMax - reta_bytes) / 4) * 2;
         const bool byte_lut = q_eff > span12 && vec4 && !reta && qwidth != QW_U8 && byte_lut_enabled();
         const uint32_t lut_bytes = byte_lut ? kByteLutBytes : kLutBytes;
@@ -2059,10 +2082,14 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
             void* qcol = d_queue;
             int qw = qwidth;
             bool scratch = false, ranged = true;
+            // counts only past the byte tables' range: a u16 column of q - span (QW_U16R) when
+            // the rest of the queues fit 16 bits, else the queues themselves
+            const bool resid = !d_queue && byte_lut && q_eff - span <= 0xFFFFu;
+            const uint32_t sbytes = resid ? 2 : qbytes;
             if (!qcol || qwidth == QW_U8) {  // (u8 queues always fit the bins: q_eff <= 256)
-                if (hipMallocAsync(&qcol, (size_t)n * qbytes, stream) == hipSuccess) {
+                if (hipMallocAsync(&qcol, (size_t)n * sbytes, stream) == hipSuccess) {
                     scratch = true;
-                    qw = qbytes == 2 ? QW_U16 : QW_U32;
+                    qw = resid ? QW_U16R : (qbytes == 2 ? QW_U16 : QW_U32);
                 } else {
                     (void)hipGetLastError();  // no room for a scratch column: one global
                     ranged = false;           // atomic per tuple below (HIST_GLOBAL) instead
@@ -2071,7 +2098,7 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
             if (ranged) {
                 p.queue_out = qcol;
                 p.q_lo = 0;
-                const bool v4 = vec4 && ((uintptr_t)qcol % (qw == QW_U16 ? 8 : 16)) == 0;
+                const bool v4 = vec4 && ((uintptr_t)qcol % (qw == QW_U32 ? 16 : 8)) == 0;
                 // the first range: the bins the first pass's tables leave (byte tables: 4-tuple
                 // body only; the caller's queue buffer may not be aligned for it)
                 const bool b1 = byte_lut && v4 && qw != QW_U8;
@@ -2082,7 +2109,10 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
                                      : pick_queue<false>(qmode, HIST_RANGE16, qw, vm1);
                 const unsigned g1 = v4 ? grid : (unsigned)std::min<uint64_t>((n + kBlock - 1) / kBlock, cap);
                 rc = launch_range16(fn, g1, (span1 / 2) * 4 + reta_bytes, p, stream);
-                if (rc == RSS_OK)
+                if (rc == RSS_OK && qw == QW_U16R)  // queues [span1, q_eff) as [0, q_eff - span1)
+                    rc = launch_queue_ranges(qcol, QW_U16, n, 0, q_eff - span1, p.counts + span1,
+                                             info.cu_count, stream);
+                else if (rc == RSS_OK)
                     rc = launch_queue_ranges(qcol, qw, n, span1, q_eff, p.counts, info.cu_count, stream);
                 // the scratch column goes back on every path (stream-ordered after its readers)
                 if (scratch) {
@@ -2238,7 +2268,7 @@ int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint
                 p.q_lo = 0;
                 p.q_span = std::min<uint32_t>(span, q_eff);
                 const uint32_t qw = p.qwidth;
-                const bool v4 = vec4 && ((uintptr_t)qcol % (qw == QW_U16 ? 8 : 16)) == 0;
+                const bool v4 = vec4 && ((uintptr_t)qcol % (qw == QW_U32 ? 16 : 8)) == 0;
                 KernelFn6 fn = h_pow2 ? pick6<true>(qmode, HIST_RANGE, v4) : pick6<false>(qmode, HIST_RANGE, v4);
                 const unsigned g1 = v4 ? grid : (unsigned)std::min<uint64_t>((n + kBlock - 1) / kBlock, cap);
                 hipLaunchKernelGGL(fn, dim3(g1), dim3(kBlock), span * 4 + reta_bytes, stream, p);

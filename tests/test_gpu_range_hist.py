@@ -187,11 +187,13 @@ def test_wide_guard_bit_on_one_hot_queue(native, oracle_lib, example_key, Q, lo,
 
 
 @pytest.mark.parametrize("H,Q", [(1 << 20, 16385), (0xFFFFFFFF, 65536), (1 << 30, 75776),
-                                 (1 << 30, 75777), (1 << 30, 131072), (99991, 50000)])
+                                 (1 << 30, 75777), (1 << 30, 131072), (1 << 30, 141311),
+                                 (1 << 30, 141312), (99991, 50000)])
 def test_byte_tables_equal_12bit_tables(native, oracle_lib, example_key, H, Q):
     """Many-queues launches hash on the 12 KiB byte tables (kByteLut: up to 75776 queues in
     the hash pass's u16 bins); RSS_BYTE_LUT=0 keeps the 12-bit tables (16384 queues, then the
-    queue column).  Both give the oracle's hashes, queues and counts on uniform and flow-like
+    queue column).  Counts only past 75776 queues: the scratch column holds q - 75776 as u16
+    up to Q = 141311 (QW_U16R), the queues themselves (u32) from 141312 on.  Both give the oracle's hashes, queues and counts on uniform and flow-like
     input (one address pair, sequential ports), with outputs and counts only."""
     import os
     n = (1 << 21) + 5

@@ -1,7 +1,8 @@
 #!/bin/bash
 # GPU box: round 3's final validation in one call -- the full -m gpu suite, smoke(), the
 # driver's bench command, a rocprofv3 kernel trace of the same command (+ its timed-launch
-# summary) and the FETCH_SIZE / WRITE_SIZE passes of the bench's step.
+# summary), the FETCH_SIZE / WRITE_SIZE passes of the bench's step, the same-buffer A/B of
+# the step's variants and the (H, Q) sweep.
 # usage: tools/gpu_validate_r03.sh TAG     (outputs under gpurun_out/TAG/)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -27,4 +28,5 @@ cat $O/prof_timed.json
 bash $R/tools/pmc_traffic.sh $TAG/pmc > $O/pmc.log 2>&1
 cd $R
 for p in 1 2; do timeout -k 10 200 python tools/ws_order_ab.py 6 > $O/ab_$p.json 2> $O/ab_$p.err; done
+timeout -k 10 600 python tools/config_sweep_probe.py > $O/config_sweep.jsonl 2> $O/sweep.err
 echo "validate done"
