@@ -30,7 +30,7 @@ def main(trace_path, log_path):
     probe = cand["inputs"] * cand["outputs"] * PROBE_LAUNCHES
     w, k = line["warmup"], line["steps"]
     probe += line.get("settle", {}).get("launches", 0)
-    name = "rss_toeplitz_kernel<true, 4, 0, 2, true, true>"  # full output, u8 queues, 32-bit offsets
+    name = "rss_toeplitz_kernel<true, 4, 0, 2, true, true, false>"  # full output, u8 queues, 32-bit offsets
     durs = []
     with open(trace_path) as f:
         for row in csv.DictReader(f):
