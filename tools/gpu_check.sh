@@ -1,5 +1,5 @@
 #!/bin/bash
-# GPU box, round 3: the changed paths' GPU tests, the single-pass variant A/B and one bench
+# GPU box: the changed paths' GPU tests (TESTS, 2nd argument), the single-pass variant A/B and one bench
 # line.  Every step has its own time limit; the first failure ends the script.
 set -eo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}

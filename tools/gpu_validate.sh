@@ -1,6 +1,8 @@
 #!/bin/bash
-# GPU box: the round's validation in one call -- the -m gpu suite, smoke(), the bench and a
-# rocprofv3 kernel-trace of the bench with its timed-launch summary (tools/gpu_bench_prof.sh).
+# GPU box: the round's one final validation, in one call -- the full -m gpu suite, smoke(), the
+# driver's bench command, a rocprofv3 kernel trace of the same command (+ its timed-launch
+# summary), the FETCH_SIZE / WRITE_SIZE passes of the bench's step, the same-buffer A/B of
+# the step's variants and the (H, Q) sweep.
 # usage: tools/gpu_validate.sh TAG     (outputs under gpurun_out/TAG/)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -8,14 +10,23 @@ TAG=${1:-validate}
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd $R
-timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
+timeout -k 10 900 python -u -m pytest -q -m gpu --timeout 300 --timeout-method thread tests \
+    > $O/pytest_gpu.log 2>&1
+rc=$?
 tail -3 $O/pytest_gpu.log
-timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail $O/smoke.log; exit 1; }
-bash $R/tools/gpu_bench_prof.sh $TAG > $O/gbp.log 2>&1 || { tail $O/gbp.log; exit 1; }
-python3 - "$O" <<'PY'
-import json, sys
-d = json.loads(open(sys.argv[1] + "/bench.json").read())
-print(round(d["value"] / 1e9, 1), "G tuples/s, frac", round(d["roofline"]["frac"], 4),
-      "placement", d["placement"]["chosen"], round(d["placement"]["chosen_ms"], 4),
-      "first", round(d["placement"]["first_allocation_ms"], 4))
-PY
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+set -e
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+tail -2 $O/smoke.log
+timeout -k 10 400 python bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err
+export TMPDIR=/tmp
+cd /tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- \
+    python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/prof.log 2>&1
+python3 $R/tools/prof_timed.py $O/prof/run_kernel_trace.csv $O/prof.log > $O/prof_timed.json
+cat $O/prof_timed.json
+mkdir -p $O/pmc && bash $R/tools/pmc_traffic.sh $TAG/pmc > $O/pmc.log 2>&1
+cd $R
+for p in 1 2; do timeout -k 10 200 python tools/ws_order_ab.py 6 > $O/ab_$p.json 2> $O/ab_$p.err; done
+timeout -k 10 600 python tools/config_sweep_probe.py > $O/config_sweep.jsonl 2> $O/sweep.err
+echo "validate done"
