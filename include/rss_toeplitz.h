@@ -125,9 +125,13 @@ int rss_key_select_fields(rss_key* key, uint32_t fields);
  * thread's current device.  Any alignment works; 16-byte aligned tuples/hashes
  * (and 4/8/16-byte aligned u8/u16/u32 queues) take the 4-tuples-per-lane path.
  * Counts-only launches with a power-of-two htable <= 256 run a table-free kernel;
- * with more than ~8192 queues the counts are gathered range by range from the queue
- * column -- d_queue when given, else a stream-ordered scratch column of 2 (nqueues <=
- * 65536) or 4 bytes per tuple (hipMallocAsync / hipFreeAsync on `stream`).
+ * with more than 8192 queues the counts go to u16 LDS bins of the hash pass itself --
+ * up to 16384 queues beside the 12-bit tables, up to 75776 on 12 KiB byte tables (4-tuple
+ * body, no indirection table) -- whose per-workgroup rows a reduce launch sums; the queues
+ * past that are gathered from the queue column (one wide pass per 65536 queues): d_queue
+ * when given, else a stream-ordered scratch column of 2 bytes per tuple (the queue, or for
+ * nqueues <= 141311 the queue minus 75776) or 4 (hipMallocAsync / hipFreeAsync on
+ * `stream`, like the per-workgroup rows).
  */
 int rss_hash_device(const rss_key* key, const rss_tuple4* d_tuples, size_t n,
                     uint32_t htable, uint32_t nqueues, uint32_t* d_hash,
@@ -144,7 +148,7 @@ int rss_hash_device(const rss_key* key, const rss_tuple4* d_tuples, size_t n,
  * aligned device memory (ticket + one sum per queue + the balanced tail's unit counter),
  * zero before its first use (every launch leaves it zero), used
  * by one launch at a time (launches that may run concurrently need their own).  Launches
- * whose counts are not gathered in LDS bins (more than ~8192 queues) leave the workspace
+ * whose counts are not gathered in private/shared LDS bins (more than 8192 queues) leave the workspace
  * untouched and zero d_counts first as rss_hash_device does.  Results are identical to
  * rss_hash_device's.  With d_counts NULL the workspace is not used (may be NULL).
  * Ordering: each workgroup takes its ticket with an agent-scope release and the last one
