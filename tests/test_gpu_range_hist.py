@@ -188,7 +188,8 @@ def test_wide_guard_bit_on_one_hot_queue(native, oracle_lib, example_key, Q, lo,
 
 @pytest.mark.parametrize("H,Q", [(1 << 20, 16385), (0xFFFFFFFF, 65536), (1 << 30, 75776),
                                  (1 << 30, 75777), (1 << 30, 131072), (1 << 30, 141311),
-                                 (1 << 30, 141312), (99991, 50000)])
+                                 (1 << 30, 141312), (99991, 50000), (65536, 20000),
+                                 (60001, 30011)])
 def test_byte_tables_equal_12bit_tables(native, oracle_lib, example_key, H, Q):
     """Many-queues launches hash on the 12 KiB byte tables (kByteLut: up to 75776 queues in
     the hash pass's u16 bins); RSS_BYTE_LUT=0 keeps the 12-bit tables (16384 queues, then the
