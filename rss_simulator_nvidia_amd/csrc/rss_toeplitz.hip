@@ -83,9 +83,9 @@ enum HistMode { HIST_PRIVATE = 0, HIST_SHARED = 1, HIST_GLOBAL = 2, HIST_NONE = 
 // HIST_RANGE16 (IPv4 kernel): HIST_RANGE with u16 bins, two per dword, twice the queues in the
 // same LDS -- with the wide pass's guard bit (rss_queue_hist_wide_kernel): the add that
 // returns 0x7FFF moves 2^15 of its bin into the global counts.
-// HIST_RANGE: shared LDS bins for queues [q_lo, q_lo + q_span) only -- one pass of a
-// multi-pass launch for nqueues whose bins do not fit the LDS beside the tables
-// (launch_hash), instead of one global atomic per tuple (13x slower).
+// HIST_RANGE: shared u32 LDS bins for queues [q_lo, q_lo + q_span) only -- the IPv6 kernel's
+// first range of a multi-pass launch for nqueues whose bins do not fit the LDS beside its
+// tables (launch_hash6), instead of one global atomic per tuple (13x slower).
 enum QueueWidth { QW_U32 = 0, QW_U16 = 1, QW_U8 = 2, QW_U16R = 3 };
 // QW_U16R: a counts-only many-queues launch's scratch column (launch_hash): u16 q - q_span for
 // the queues past the hash pass's LDS range [0, q_span), 0xFFFF (never counted) for the rest --
@@ -1571,9 +1571,9 @@ KernelFn pick_hist(int hist, int qwidth, int vec4) {
         case HIST_PRIVATE: return pick_width<kHPow2, kQMode, HIST_PRIVATE>(qwidth, vec4);
         case HIST_SHARED: return pick_width<kHPow2, kQMode, HIST_SHARED>(qwidth, vec4);
         case HIST_GLOBAL: return pick_width<kHPow2, kQMode, HIST_GLOBAL>(qwidth, vec4);
-        case HIST_RANGE: return pick_width<kHPow2, kQMode, HIST_RANGE>(qwidth, vec4);
         case HIST_RANGE16: return pick_width<kHPow2, kQMode, HIST_RANGE16>(qwidth, vec4);
-        default: return pick_width<kHPow2, kQMode, HIST_NONE>(qwidth, vec4);
+        case HIST_NONE: return pick_width<kHPow2, kQMode, HIST_NONE>(qwidth, vec4);
+        default: return nullptr;  // HIST_RANGE (u32 ranges): the IPv6 kernel's only
     }
 }
 
@@ -2128,6 +2128,7 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
     const int vmode = vec4 ? (12ull * n < (1ull << 32) && off32_enabled() ? 2 : 1) : 0;
     KernelFn fn = h_pow2 ? pick_queue<true>(qmode, hist, qwidth, vmode)
                          : pick_queue<false>(qmode, hist, qwidth, vmode);
+    if (!fn) return set_error(RSS_EIO, "rss_hash_device: no kernel instance for this launch");
     uint32_t shmem = bin_bytes + reta_bytes;  // dynamic part; the 128 KiB LUT is static
     // Balanced tail (single-pass launches: the workspace holds its unit counter and is used
     // by one launch at a time): the last ~1/10 of the grid-stride rows handed out per
