@@ -648,13 +648,16 @@ def main():
     # Clock settle (untimed, rank-local, no collective): the first ~0.4 s of back-to-back
     # launches run ~0.8 % slower than sustained ones, and a box left idle for 0.3 s drops
     # back (tools/drift_probe.py, profiles/r02/drift_probe.jsonl) -- a service hashing batch
-    # after batch runs in the settled state, so the timed steps should too.
+    # after batch runs in the settled state, so the timed steps should too.  The settle
+    # launches carry RSS_FLAG_ADDR64 (same access shape, 64-bit addressing) like the
+    # placement probe's, so a profile's row for the step's 32-bit kernel instance holds the
+    # warmup, timed and spread launches alone.
     settle_launches, t_settle = 0, time.perf_counter()
     while args.settle_ms > 0:
         for _ in range(16):
             _native.hash_device(key, tuples.data_ptr(), n, H, Q, hashes.data_ptr(),
                                 queues.data_ptr(), counts.data_ptr(),
-                                _native.FLAG_ACCUMULATE | qflag, sp)
+                                _native.FLAG_ACCUMULATE | _native.FLAG_ADDR64 | qflag, sp)
         settle_launches += 16
         torch.cuda.synchronize()
         if time.perf_counter() - t_settle >= args.settle_ms / 1e3:
@@ -922,7 +925,7 @@ def main():
                           "note": "untimed launches of the step before the warmup steps "
                                   "(--settle-ms; clock settle, rank-local)"}
         line["placement"] = dict(placement, first_allocation_tuples_per_s_per_gpu=n / (
-            placement["first_allocation_ms"] / 1e3),
+            placement["first_allocation_ms"] / 1e3), probe_addr64=True,
             note="resident buffers chosen among the probed candidate allocations before the "
                  "timed region (ResidentBatch); first_allocation_* = the unplaced allocation's "
                  "kernel-only rate")

@@ -103,6 +103,12 @@ int rss_key_select_fields(rss_key* key, uint32_t fields);
 #define RSS_FLAG_ACCUMULATE 1u  /* add into counts instead of overwriting them      */
 #define RSS_FLAG_QUEUE_U16 2u   /* rss_hash_device: d_queue is uint16_t[n] (Q<=2^16) */
 #define RSS_FLAG_QUEUE_U8 4u    /* rss_hash_device: d_queue is uint8_t[n]  (Q<=256)  */
+/* rss_hash_device: 64-bit addressing even where every stream's byte offsets fit 32 bits
+ * (the instance batches of >= 2^32 / 12 tuples run).  Same results and the same access
+ * shape; it only gives the launch a kernel symbol of its own in traces -- the placement
+ * probe and the clock settle use it, so a profile's row for the 32-bit instance holds the
+ * resident step's launches alone. */
+#define RSS_FLAG_ADDR64 8u
 
 /*
  * Device-resident hot path.  Replaces, for n tuples at once:

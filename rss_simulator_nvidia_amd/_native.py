@@ -23,6 +23,7 @@ ABI_VERSION = 1
 FLAG_ACCUMULATE = 1
 FLAG_QUEUE_U16 = 2
 FLAG_QUEUE_U8 = 4
+FLAG_ADDR64 = 8  # 64-bit addressing where 32-bit offsets fit: own kernel symbol in traces
 FLAG_CSV_COUNTS_ONLY = 1
 KEY_MIN_BYTES = 4
 

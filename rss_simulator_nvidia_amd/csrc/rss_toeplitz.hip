@@ -2125,7 +2125,8 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
         }
     }
     // 32-bit byte offsets when every stream's bytes fit them (input 12 n B is the largest)
-    const int vmode = vec4 ? (12ull * n < (1ull << 32) && off32_enabled() ? 2 : 1) : 0;
+    const int vmode = vec4 ? (12ull * n < (1ull << 32) && off32_enabled() &&
+                              !(flags & RSS_FLAG_ADDR64) ? 2 : 1) : 0;
     KernelFn fn = h_pow2 ? pick_queue<true>(qmode, hist, qwidth, vmode)
                          : pick_queue<false>(qmode, hist, qwidth, vmode);
     if (!fn) return set_error(RSS_EIO, "rss_hash_device: no kernel instance for this launch");

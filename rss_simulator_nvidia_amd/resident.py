@@ -84,8 +84,10 @@ class ResidentBatch:
     def _probe(self, tuples, hashes, queues, events):
         if events is not None:
             events[0].record(self.stream)
+        # RSS_FLAG_ADDR64: the same access shape as the batch's launches under a kernel
+        # symbol of its own, so a profile's row for the step's kernel holds no probe launches
         self._launch(tuples, hashes, queues, self._probe_counts,
-                     QUEUE_FLAGS[self.queue_width] | _native.FLAG_ACCUMULATE)
+                     QUEUE_FLAGS[self.queue_width] | _native.FLAG_ACCUMULATE | _native.FLAG_ADDR64)
         if events is not None:
             events[1].record(self.stream)
 

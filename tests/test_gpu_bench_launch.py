@@ -64,3 +64,20 @@ def test_bench_launch_2p28_elementwise(oracle_lib, example_key):
     v = bench.verify_outputs(torch, gold, batch.hashes, batch.queue_view(), 0, N)
     assert v["ok"] is True and v["blocks"] == N >> 20, v
     assert [int(x) for x in counts.tolist()] == bench.golden_counts(gold, 0, N)
+
+    # RSS_FLAG_ADDR64 (the placement probe's and the clock settle's launches: 64-bit
+    # addressing, a kernel symbol of its own) writes the same bytes, plain and single-pass
+    h32, q32 = batch.hashes.clone(), batch.queues.clone()
+    for ws in (None, pipe.workspace):
+        batch.hashes.zero_()
+        batch.queues.fill_(0xFF)
+        c64 = torch.zeros(Q, dtype=torch.int64, device=dev)
+        _native.hash_device(key, batch.tuples.data_ptr(), N, H, Q, batch.hashes.data_ptr(),
+                            batch.queues.data_ptr(), c64.data_ptr(),
+                            _native.FLAG_QUEUE_U8 | _native.FLAG_ADDR64 |
+                            (_native.FLAG_ACCUMULATE if ws is None else 0), sp,
+                            ws.data_ptr() if ws is not None else None)
+        torch.cuda.synchronize()
+        assert torch.equal(batch.hashes, h32) and torch.equal(batch.queues, q32)
+        np.testing.assert_array_equal(c64.cpu().numpy().view(np.uint64), c)
+    assert int(pipe.workspace.abs().sum()) == 0

@@ -44,6 +44,14 @@ def test_abi_version_matches_header(lib):
     assert lib.rss_abi_version() == int(m.group(1)) == _native.ABI_VERSION
 
 
+def test_flag_constants_match_header():
+    """Every RSS_FLAG_* of the header has the same value in the Python layer."""
+    flags = dict(re.findall(r"#define RSS_FLAG_([A-Z0-9_]+) (\d+)u", open(HEADER).read()))
+    assert {"ACCUMULATE", "QUEUE_U16", "QUEUE_U8", "ADDR64"} <= set(flags)
+    for name, value in flags.items():
+        assert getattr(_native, "FLAG_" + name) == int(value), name
+
+
 def test_struct_layout_matches_c(tmp_path):
     src = tmp_path / "layout.c"
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "rss_toeplitz.h"\n'

@@ -7,7 +7,9 @@ lines.  The bench's ``roofline.kernel_ms`` is the mean over the K timed launches
 comparable profiler figure is the mean duration of exactly those dispatches.  With the bench
 line of the same profiled run (``prof.log``), the full-output kernel's dispatches are, in
 order: the probe (inputs x outputs x (3 warm + 5 timed)), the clock-settle launches
-(``settle.launches``), W warmup steps, K timed steps.
+(``settle.launches``), W warmup steps, K timed steps -- or, since the probe and the settle
+carry RSS_FLAG_ADDR64 (``placement.probe_addr64``), W warmup steps, K timed steps, the K
+event-bracketed spread launches and the flow-like line's launches only.
 
     python tools/prof_timed.py TRACE_CSV PROF_LOG > summary.json
 """
@@ -30,6 +32,10 @@ def main(trace_path, log_path):
     probe = cand["inputs"] * cand["outputs"] * PROBE_LAUNCHES
     w, k = line["warmup"], line["steps"]
     probe += line.get("settle", {}).get("launches", 0)
+    if line["placement"].get("probe_addr64"):
+        # round 3 on: the probe and the settle launch the 64-bit instance (RSS_FLAG_ADDR64),
+        # so this kernel's row starts with the warmup steps
+        probe = 0
     name = "rss_toeplitz_kernel<true, 4, 0, 2, true, true, false>"  # full output, u8 queues, 32-bit offsets
     durs = []
     with open(trace_path) as f:
