@@ -25,7 +25,7 @@ import statistics
 
 def choose_stream_buffers(torch, dev, n, fill_input, probe, n_inputs=2, n_outputs=4,
                           queue_bytes=1, probe_reps=5, probe_warm=3, max_rounds=1,
-                          fast_ratio=0.95):
+                          fast_ratio=0.91):
     """Allocate candidate buffers for an ``n``-tuple stream and return the fastest set.
 
     ``fill_input(tuples)`` writes the resident input into an int32 tensor of ``3 * n``
@@ -42,6 +42,11 @@ def choose_stream_buffers(torch, dev, n, fill_input, probe, n_inputs=2, n_output
     (so they take other memory) and probed with every input, up to ``max_rounds`` rounds
     in all.  On a box with a fast tier one process in six found none in 24 sets
     (``profiles/r02/two_groups_ab.log``, ``one_3``: 0.861 ms against 0.787-0.789).
+    The tiers sit at about 0.785 / 0.81 / 0.865-0.89 ms per 2^28 tuples: every probe that
+    found the fast tier had best / slowest = 0.873-0.904 (28 committed bench lines), every
+    one whose best was the middle tier 0.919-0.97 (e.g. ``profiles/r03/bench_lines/
+    torchrun_w1_rccl.json``: best 0.808 against 0.879) -- hence ``fast_ratio`` 0.91, which
+    keeps probing past a middle-tier best (round 2's 0.95 stopped there).
     """
     if n < 1:
         raise ValueError("choose_stream_buffers: n must be >= 1")

@@ -108,9 +108,16 @@ def _timed_fake(times_of_output):
     (3, 3, 1),      # a fast-tier candidate in the first round: no more rounds
     (15, 3, 2),     # first round all slow, the second finds one
     (None, 3, 3),   # no fast tier on the box: every round probed, the best slow set kept
-    (15, 1, 1)])    # one round requested: no retry
+    (15, 1, 1),     # one round requested: no retry
+    ("mid", 3, 2)])  # first round slow + middle tier (best/slowest 0.92): probe on
 def test_placement_rounds_until_a_faster_tier(fast_at, max_rounds, want_rounds):
     from rss_simulator_nvidia_amd.placement import choose_stream_buffers
+    if fast_at == "mid":  # outputs 0-5 slow, 6-11 middle tier, 12-23 with one fast set (17)
+        fake, probe = _timed_fake(lambda k: 0.879 if k < 6 else (0.785 if k == 17 else 0.808))
+        t, h, q, rep = choose_stream_buffers(fake, "dev", 10, lambda b: None, probe, n_inputs=2,
+                                             n_outputs=12, max_rounds=max_rounds)
+        assert rep["rounds"] == want_rounds and h.ident == 17 and rep["chosen_ms"] == 0.785
+        return
     fake, probe = _timed_fake(lambda k: 0.785 if k == fast_at else 0.865 + 0.001 * (k % 3))
     t, h, q, rep = choose_stream_buffers(fake, "dev", 10, lambda b: None, probe, n_inputs=2,
                                          n_outputs=12, max_rounds=max_rounds)
