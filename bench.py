@@ -605,10 +605,11 @@ def main():
                               allreduce=args.allreduce if distributed else "overlap", comm=comm,
                               bucket=args.allreduce_bucket if distributed else 1)
 
-    def launch(c, workspace=None):
+    def launch(c, workspace=None, extra_flags=0):
         ws = workspace
         _native.hash_device(key, tuples.data_ptr(), n, H, Q, hashes.data_ptr(), queues.data_ptr(),
-                            c.data_ptr(), qflag | (0 if ws is not None else _native.FLAG_ACCUMULATE),
+                            c.data_ptr(), qflag | extra_flags |
+                            (0 if ws is not None else _native.FLAG_ACCUMULATE),
                             torch.cuda.current_stream(dev).cuda_stream,
                             ws.data_ptr() if ws is not None else None)
 
@@ -651,7 +652,7 @@ def main():
     # after batch runs in the settled state, so the timed steps should too.  The settle
     # launches carry RSS_FLAG_ADDR64 (same access shape, 64-bit addressing) like the
     # placement probe's, so a profile's row for the step's 32-bit kernel instance holds the
-    # warmup, timed and spread launches alone.
+    # warmup and timed launches alone.
     settle_launches, t_settle = 0, time.perf_counter()
     while args.settle_ms > 0:
         for _ in range(16):
@@ -713,12 +714,15 @@ def main():
     if total != n * world:
         raise SystemExit("bench: per-queue counts sum to %d, expected %d" % (total, n * world))
     kernel_ms = region[0].elapsed_time(region[1]) / args.steps
-    # per-launch spread: K launches of the same step, each bracketed by its own events
+    # per-launch spread: K launches of the same step, each bracketed by its own events --
+    # with RSS_FLAG_ADDR64 (same access shape, the 64-bit instance) like every untimed
+    # launch of the step, so a profile's row for the step's 32-bit instance holds exactly
+    # the W warmup + K timed launches
     spread_ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                  for _ in range(args.steps)]
     for e in spread_ev:
         e[0].record(stream)
-        launch(counts, workspace=pipeline.workspace)
+        launch(counts, workspace=pipeline.workspace, extra_flags=_native.FLAG_ADDR64)
         e[1].record(stream)
     torch.cuda.synchronize()
     launch_ms = sorted(a.elapsed_time(b) for a, b in spread_ev)
@@ -817,7 +821,8 @@ def main():
         del queues32
         if args.distribution == "uniform":  # same kernel on SURVEY.md 8(d)'s flow-like input
             flow_device(torch, tuples, 0, n, dev)
-            flow_ms = kernel_ms_of(hashes.data_ptr(), queues.data_ptr(), qflag, reps)
+            flow_ms = kernel_ms_of(hashes.data_ptr(), queues.data_ptr(),
+                                   qflag | _native.FLAG_ADDR64, reps)
 
     extras = None
     if rank == 0 and not args.no_extras:
@@ -890,7 +895,9 @@ def main():
                           "events around the %d timed launches (launches + the gaps between "
                           "them), slowest rank (kernel_ms_max_rank); min_max / median / "
                           "events_mean: %d launches each bracketed by HIP events, after the "
-                          "timed region"
+                          "timed region (RSS_FLAG_ADDR64: the 64-bit instance, like the probe, "
+                          "settle and flow-like launches; the step's 32-bit instance runs only "
+                          "the warmup and timed launches)"
                           % (args.steps, args.steps),
             },
             # the HBM-read roofline is the counts-only mode's bound (12 B read

@@ -8,8 +8,8 @@ comparable profiler figure is the mean duration of exactly those dispatches.  Wi
 line of the same profiled run (``prof.log``), the full-output kernel's dispatches are, in
 order: the probe (inputs x outputs x (3 warm + 5 timed)), the clock-settle launches
 (``settle.launches``), W warmup steps, K timed steps -- or, since the probe and the settle
-carry RSS_FLAG_ADDR64 (``placement.probe_addr64``), W warmup steps, K timed steps, the K
-event-bracketed spread launches and the flow-like line's launches only.
+carry RSS_FLAG_ADDR64 (``placement.probe_addr64``; the spread and flow-like launches too),
+W warmup steps and K timed steps only.
 
     python tools/prof_timed.py TRACE_CSV PROF_LOG > summary.json
 """
