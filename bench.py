@@ -458,21 +458,23 @@ def extra_lines(torch, _native, dev, stream, key_bytes):
     """Secondary timings of the row-f kernels on this GPU, after the main measurement
     (DESIGN.md §7-§8): the IPv6 kernel (2^26 uniform 36-byte tuples, u32 hash + u8 queue +
     counts: 36 B read + 5 B written per tuple) and key search (1024 random keys x 2^20 resident
-    tuples, H=128, Q=24, counts only).  Mean of per-launch HIP events after warm launches."""
+    tuples, H=128, Q=24, counts only).  Mean launch time over one HIP event pair around
+    back-to-back launches, after warm launches."""
     from rss_simulator_nvidia_amd import keysearch
     sp = stream.cuda_stream
 
     def timed(fn, warm=10, reps=20):
+        # one pair of HIP events around `reps` back-to-back launches, as the main line's
+        # kernel_ms (a pair around every launch costs ~7 us per launch)
         for _ in range(warm):
             fn()
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(reps)]
-        for a, b in ev:
-            a.record(stream)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for _ in range(reps):
             fn()
-            b.record(stream)
+        b.record(stream)
         torch.cuda.synchronize()
-        return sum(a.elapsed_time(b) for a, b in ev) / reps
+        return a.elapsed_time(b) / reps
 
     out = {}
     n6 = 1 << 26
@@ -481,12 +483,21 @@ def extra_lines(torch, _native, dev, stream, key_bytes):
     q6 = torch.empty(n6, dtype=torch.uint8, device=dev)
     c6 = torch.zeros(24, dtype=torch.int64, device=dev)
     k6 = _native.prepare_key6(key_bytes)
+    ws6 = torch.zeros(_native.counts_workspace_bytes(128, 24) // 8, dtype=torch.int64, device=dev)
+    # the IPv6 step as the IPv4 one: single-pass counts with the balanced tail
+    # (rss_hash6_device_ws); beside it the plain launch (static walk, accumulating counts)
     ms = timed(lambda: _native.hash6_device(k6, words.data_ptr(), n6, 128, 24, h6.data_ptr(),
-                                            q6.data_ptr(), c6.data_ptr(),
-                                            _native.FLAG_QUEUE_U8 | _native.FLAG_ACCUMULATE, sp))
+                                            q6.data_ptr(), c6.data_ptr(), _native.FLAG_QUEUE_U8,
+                                            sp, ws6.data_ptr()))
+    ms_plain = timed(lambda: _native.hash6_device(k6, words.data_ptr(), n6, 128, 24, h6.data_ptr(),
+                                                  q6.data_ptr(), c6.data_ptr(),
+                                                  _native.FLAG_QUEUE_U8 | _native.FLAG_ACCUMULATE,
+                                                  sp))
     out["ipv6_hash"] = {"tuples": n6, "kernel_ms": ms, "tuples_per_s": n6 / (ms / 1e3),
                         "achieved_GBs": n6 * 41 / (ms / 1e3) / 1e9,
-                        "bytes_per_tuple": 41, "outputs": "hash u32 + queue u8 + counts"}
+                        "bytes_per_tuple": 41, "outputs": "hash u32 + queue u8 + counts",
+                        "launch": "rss_hash6_device_ws (single-pass counts, balanced tail)",
+                        "plain_launch_ms": ms_plain}
     del words, h6, q6
     nk, nt = 1024, 1 << 20
     keys = keysearch.random_keys(nk, seed=0)

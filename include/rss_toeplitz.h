@@ -231,6 +231,14 @@ int rss_key6_select_fields(rss_key6* key, uint32_t fields);
 int rss_hash6_device(const rss_key6* key, const rss_tuple6* d_tuples, size_t n,
                      uint32_t htable, uint32_t nqueues, uint32_t* d_hash, void* d_queue,
                      uint64_t* d_counts, uint32_t flags, void* stream);
+/* rss_hash6_device with single-pass counts, as rss_hash_device_ws: d_workspace is a zeroed,
+ * 8-byte aligned device buffer of rss_counts_workspace_bytes(nqueues) bytes used by one launch
+ * at a time (every launch leaves it zero); the kernel's last workgroup writes the counts, so
+ * no zeroing launch runs before it, and launches of >= 2^24 tuples hand their last rows out
+ * per workgroup slot (the balanced tail) -- the IPv6 counterpart of the IPv4 bench step. */
+int rss_hash6_device_ws(const rss_key6* key, const rss_tuple6* d_tuples, size_t n,
+                        uint32_t htable, uint32_t nqueues, uint32_t* d_hash, void* d_queue,
+                        uint64_t* d_counts, uint32_t flags, uint64_t* d_workspace, void* stream);
 
 /* Host-memory convenience path (CSV in -> CSV out): owns device buffers. */
 typedef struct rss_ctx rss_ctx;

@@ -38,7 +38,7 @@ EXPORTED_SYMBOLS = (
     "rss_csv_hash_file", "rss_host_alloc", "rss_host_free", "rss_hash_host_multi",
     "rss_pcap_parse6", "rss_hash6_device_reta", "rss_hash6_host_reta", "rss_csv_parse6",
     "rss_csv_format6_bound", "rss_csv_format6", "rss_csv6_hash_text", "rss_csv6_hash_file",
-    "rss_counts_workspace_bytes", "rss_hash_device_ws",
+    "rss_counts_workspace_bytes", "rss_hash_device_ws", "rss_hash6_device_ws",
 )
 FIELD_SRC_IP, FIELD_DST_IP, FIELD_SRC_PORT, FIELD_DST_PORT = 1, 2, 4, 8
 FIELDS_IP, FIELDS_ALL = 3, 15
@@ -123,6 +123,8 @@ def _bind(lib):
         "rss_key6_prepare": ([ctypes.POINTER(ctypes.c_uint8), sz, ctypes.POINTER(RssKey6)],
                              ctypes.c_int),
         "rss_key6_select_fields": ([ctypes.POINTER(RssKey6), u32], ctypes.c_int),
+        "rss_hash6_device_ws": ([ctypes.POINTER(RssKey6), vp, sz, u32, u32, vp, vp, vp, u32, vp,
+                                 vp], ctypes.c_int),
         "rss_hash6_device": ([ctypes.POINTER(RssKey6), vp, sz, u32, u32, vp, vp, vp, u32, vp],
                              ctypes.c_int),
         "rss_hash6_host": ([vp, ctypes.POINTER(RssKey6), vp, sz, u32, u32, vp, vp, vp, u32],
@@ -579,11 +581,18 @@ def hash_device_reta(key, tuples_ptr, n, htable, reta, nqueues, hash_ptr=None, q
 
 
 def hash6_device(key6, tuples_ptr, n, htable, nqueues, hash_ptr=None, queue_ptr=None,
-                 counts_ptr=None, flags=0, stream=None):
-    """Stream-ordered ``rss_hash6_device`` on raw device pointers (ints)."""
+                 counts_ptr=None, flags=0, stream=None, workspace_ptr=None):
+    """Stream-ordered ``rss_hash6_device`` on raw device pointers (ints); with
+    ``workspace_ptr`` (as :func:`hash_device`) ``rss_hash6_device_ws``: single-pass counts."""
     htable, nqueues = queue_modulus(htable, nqueues)
-    _check(load().rss_hash6_device(ctypes.byref(key6), tuples_ptr, n, htable, nqueues, hash_ptr,
-                                   queue_ptr, counts_ptr, flags, stream), "rss_hash6_device")
+    if workspace_ptr is None:
+        _check(load().rss_hash6_device(ctypes.byref(key6), tuples_ptr, n, htable, nqueues,
+                                       hash_ptr, queue_ptr, counts_ptr, flags, stream),
+               "rss_hash6_device")
+    else:
+        _check(load().rss_hash6_device_ws(ctypes.byref(key6), tuples_ptr, n, htable, nqueues,
+                                          hash_ptr, queue_ptr, counts_ptr, flags, workspace_ptr,
+                                          stream), "rss_hash6_device_ws")
 
 
 def hash6_device_reta(key6, tuples_ptr, n, htable, reta, nqueues, hash_ptr=None, queue_ptr=None,

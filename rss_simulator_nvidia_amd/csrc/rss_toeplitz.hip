@@ -1288,6 +1288,10 @@ struct LaunchParams6 {
     uint32_t q_m16;
     uint64_t q_m64;
     uint32_t q_lo, q_span;    // HIST_RANGE, as LaunchParams
+    unsigned long long* ws;   // single-pass counts workspace (rss_hash6_device_ws) or NULL
+    uint32_t accumulate;      // with ws: fold mode, as LaunchParams
+    uint32_t tail_rows;       // balanced tail rows (0 = static grid-stride), as LaunchParams
+    uint32_t bal_off;         // balanced tail: byte offset of its LDS slot (dynamic LDS)
     uint16_t reta[kRetaMax];  // QM_TABLE: queue of bucket b, as LaunchParams::reta
 };
 
@@ -1412,7 +1416,7 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz6_kernel(const LaunchParam
         // 4 consecutive tuples per lane: 144 B = 9 x dwordx4, 16-B aligned
         const uint4* __restrict__ src = reinterpret_cast<const uint4*>(p6.tuples);
         const uint64_t ngroups = p6.n >> 2;
-        for (uint64_t g = gtid; g < ngroups; g += gstride) {
+        auto group = [&](uint64_t g) {
             uint32_t v[4 * kWords6];
 #pragma unroll
             for (int k = 0; k < kWords6; ++k) {
@@ -1447,7 +1451,11 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz6_kernel(const LaunchParam
             }
 #pragma unroll
             for (int t = 0; t < 4; ++t) count_queue<kHist>(bins, q[t], col, p);
-        }
+        };
+        // single-pass launches hand out the last rows per workgroup slot (walk_rows, the
+        // balanced tail of the IPv4 kernel): the XCDs that stream faster take more of them
+        walk_rows(group, ngroups, p6.tail_rows, p6.ws + 1 + p.Q,
+                  reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(bins) + p6.bal_off));
         tail_begin = ngroups << 2;
     }
     for (uint64_t i = tail_begin + gtid; i < p6.n; i += gstride) {
@@ -1471,17 +1479,17 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz6_kernel(const LaunchParam
     }
     if constexpr (kHist == HIST_PRIVATE || kHist == HIST_SHARED) {
         __syncthreads();
-        for (uint32_t k = tid; k < p.Q; k += kBlock) {
-            uint32_t s;
+        // atomics into the counts, or (single pass) the workspace + the last workgroup's write
+        fold_counts([&](uint32_t k) {
             if constexpr (kHist == HIST_PRIVATE) {
-                s = 0;
+                uint32_t s = 0;  // rotated column order: conflict-free
                 for (uint32_t c = 0; c < kBinCols; ++c)
                     s += bins[k * kBinCols + ((c + k) & (kBinCols - 1))];
+                return s;
             } else {
-                s = bins[k];
+                return bins[k];
             }
-            if (s) atomicAdd(&p.counts[k], (unsigned long long)s);
-        }
+        }, p.Q, p.counts, p6.ws, p6.accumulate, bins, p6.tail_rows ? p6.ws + 1 + p.Q : nullptr);
     } else if constexpr (kHist == HIST_RANGE) {
         __syncthreads();
         for (uint32_t r = tid; r < p.q_span; r += kBlock)
@@ -2178,7 +2186,8 @@ KernelFn6 pick6(int qmode, int hist, bool vec4) {
 
 int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint32_t htable,
                  uint32_t nqueues, uint32_t* d_hash, void* d_queue, uint64_t* d_counts,
-                 uint32_t flags, hipStream_t stream, const uint32_t* reta = nullptr) {
+                 uint32_t flags, hipStream_t stream, const uint32_t* reta = nullptr,
+                 uint64_t* ws = nullptr) {
     if (!key || key->len < RSS_KEY_MIN_BYTES)
         return set_error(RSS_EINVAL, "rss_hash6_device: key NULL or not prepared");
     if (htable < 1 || nqueues < 1)
@@ -2202,9 +2211,6 @@ int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint
                                          "(got %u)", q_eff);
         qwidth = QW_U16;
     }
-    if (d_counts && !(flags & RSS_FLAG_ACCUMULATE))
-        RSS_HIP_CHECK(hipMemsetAsync(d_counts, 0, sizeof(uint64_t) * nqueues, stream));
-    if (n == 0) return RSS_OK;
     LaunchParams tmp;  // reuse the IPv4 mode selection
     memset(&tmp, 0, sizeof tmp);
     int qmode, hist;
@@ -2214,6 +2220,16 @@ int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint
     const bool h_pow2 = setup_modes(&tmp, htable, q_eff, d_counts != nullptr, &qmode, &hist,
                                     &bin_bytes, budget);
     if (reta) qmode = QM_TABLE;
+    // single pass (rss_hash6_device_ws): the kernel's last workgroup writes the counts, as
+    // launch_hash; otherwise zero them first unless accumulating
+    const bool single_pass = ws && d_counts && n > 0 && (hist == HIST_PRIVATE || hist == HIST_SHARED);
+    if (d_counts && !(flags & RSS_FLAG_ACCUMULATE) && !single_pass)
+        RSS_HIP_CHECK(hipMemsetAsync(d_counts, 0, sizeof(uint64_t) * nqueues, stream));
+    else if (single_pass) {
+        const int trc = zero_counts_tail(d_counts, q_eff, nqueues, flags, stream);
+        if (trc) return trc;
+    }
+    if (n == 0) return RSS_OK;
     LaunchParams6 p;
     memset(&p, 0, sizeof p);
     memcpy(p.window, key->window, sizeof p.window);
@@ -2231,6 +2247,11 @@ int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint
     p.q_m16 = tmp.q_m16;
     p.q_m64 = tmp.q_m64;
     p.qwidth = qwidth;
+    if (single_pass) {
+        p.ws = reinterpret_cast<unsigned long long*>(ws);
+        p.accumulate = ((flags & RSS_FLAG_ACCUMULATE) ? kFoldAccumulate : 0u) |
+                       (ws_order_acqrel() ? kFoldOrdered : 0u);
+    }
     if (reta)
         for (uint32_t b = 0; b < htable; ++b) p.reta[b] = (uint16_t)reta[b];
     const uintptr_t qalign = qwidth == QW_U8 ? 4 : (qwidth == QW_U16 ? 8 : 16);
@@ -2244,7 +2265,8 @@ int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint
     if (!d_hash && !d_queue && d_counts && !reta && h_pow2 && htable <= 256u && q_eff <= 256u &&
         (qmode == QM_MASK || qmode == QM_FAST8) && aligned16(d_tuples) && counts_perm_enabled())
         return launch_counts_perm<9>(key->window, d_tuples, n, p.counts, p.h_mask, p.Q, p.q_mask,
-                                     p.q_m16, qmode, q_eff * kBinCols * 4, info.cu_count, stream);
+                                     p.q_m16, qmode, q_eff * kBinCols * 4, info.cu_count, stream,
+                                     p.ws, p.accumulate);
     const uint64_t per_lane = vec4 ? 4 : 1;
     const uint64_t want = (n + per_lane * kBlock - 1) / (per_lane * kBlock);
     const uint64_t cap = (uint64_t)info.cu_count * kBlocksPerCU6;
@@ -2289,7 +2311,16 @@ int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint
         }
     }
     KernelFn6 fn = h_pow2 ? pick6<true>(qmode, hist, vec4) : pick6<false>(qmode, hist, vec4);
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), bin_bytes + reta_bytes, stream, p);
+    uint32_t shmem = bin_bytes + reta_bytes;
+    // the balanced tail of single-pass launches (as launch_hash: 8 bytes of LDS beside the bins)
+    const uint32_t bal_off = (shmem + 7u) & ~7u;
+    const uint32_t tail = balanced_tail_rows(n / 4, grid);
+    if (single_pass && vec4 && tail && bal_off + 8 <= kBinBytesMax6 && balance_enabled()) {
+        p.tail_rows = tail;
+        p.bal_off = bal_off;
+        shmem = bal_off + 8;
+    }
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), shmem, stream, p);
     RSS_HIP_CHECK(hipGetLastError());
     return RSS_OK;
 }
@@ -2382,6 +2413,15 @@ int rss_hash6_device(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, 
                      uint32_t flags, void* stream) {
     return launch_hash6(key, d_tuples, n, htable, nqueues, d_hash, d_queue, d_counts, flags,
                         static_cast<hipStream_t>(stream));
+}
+
+int rss_hash6_device_ws(const rss_key6* key, const rss_tuple6* d_tuples, size_t n,
+                        uint32_t htable, uint32_t nqueues, uint32_t* d_hash, void* d_queue,
+                        uint64_t* d_counts, uint32_t flags, uint64_t* d_workspace, void* stream) {
+    if (d_counts && (!d_workspace || ((uintptr_t)d_workspace & 7u)))
+        return set_error(RSS_EINVAL, "rss_hash6_device_ws: workspace NULL or not 8-byte aligned");
+    return launch_hash6(key, d_tuples, n, htable, nqueues, d_hash, d_queue, d_counts, flags,
+                        static_cast<hipStream_t>(stream), nullptr, d_workspace);
 }
 
 int rss_hash6_device_reta(const rss_key6* key, const rss_tuple6* d_tuples, size_t n,
