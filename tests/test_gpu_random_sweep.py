@@ -1,4 +1,5 @@
-"""Seeded randomised parity sweep of the device API (rss_hash_device / _ws / _reta) against the
+"""Seeded randomised parity sweep of the device API (rss_hash_device / _ws / _reta, and
+rss_hash6_device / _ws / _reta) against the
 C oracle: random sizes (incl. 0 and ragged tails), power-of-two and arbitrary htable /
 nqueues (every modulo and histogram mode), key lengths 16..52, queue widths u8 / u16 /
 u32, NULL outputs, accumulation into non-zero counts and 4-byte-misaligned tuples.
@@ -179,9 +180,20 @@ def test_random_ipv6_config_matches_oracle(native, oracle_lib, seed):
         native.hash6_device_reta(k6, raw.data_ptr() + 4 * off, n, H, reta, Q, hbuf.data_ptr(),
                                  qbuf.data_ptr(), counts.data_ptr(), qflag, stream)
     else:
+        # half the cases as single-pass counts (rss_hash6_device_ws; own generator, as the
+        # IPv4 sweep), the workspace followed by guard words
+        single_pass = bool(np.random.default_rng(6000 + seed).random() < 0.5)
+        wsn = native.counts_workspace_bytes(H, Q) // 8
+        ws = torch.zeros(wsn + 8, dtype=torch.int64, device=dev)
+        ws[wsn:] = -7
         native.hash6_device(k6, raw.data_ptr() + 4 * off, n, H, Q, hbuf.data_ptr(),
-                            qbuf.data_ptr(), counts.data_ptr(), qflag, stream)
+                            qbuf.data_ptr(), counts.data_ptr(), qflag, stream,
+                            ws.data_ptr() if single_pass else None)
     torch.cuda.synchronize()
+    if not use_reta:
+        wsh = ws.cpu().numpy()
+        assert (wsh[:wsn] == 0).all(), "workspace not left zero"
+        assert (wsh[wsn:] == -7).all(), "workspace written past its size"
     if fields == "sdfn":
         want = o.hash_words_np(full, words)
     else:
