@@ -60,9 +60,11 @@ def parse_args():
     p.add_argument("--zero-counts", action="store_true",
                    help="zero each step's counts with a separate launch (counts.zero_() + an "
                         "accumulating rss_hash_device) instead of single-pass counts")
-    p.add_argument("--placement-rounds", type=int, default=3, metavar="R",
+    p.add_argument("--placement-rounds", type=int, default=4, metavar="R",
                    help="up to R rounds of --placement-probe more output candidates while no "
-                        "probed set is clearly faster than the rest (no faster tier found)")
+                        "probed set is clearly faster than the rest (best >= 0.91 x slowest: "
+                        "no faster tier found, or only the middle one); at N > 1 the slowest "
+                        "rank's placement bounds the job")
     p.add_argument("--allreduce", choices=["overlap", "stream", "rccl"], default="rccl",
                    help="per-step count all-reduce (sharding.CountsPipeline): torch.distributed "
                         "async on its own stream (overlap), torch.distributed stream-ordered "

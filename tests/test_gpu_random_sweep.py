@@ -146,7 +146,7 @@ def test_reta_entries_above_u16_are_refused(native):
                                 70000, None, None, counts.data_ptr(), 0, None)
 
 
-@pytest.mark.parametrize("seed", range(24))
+@pytest.mark.parametrize("seed", range(SEED0, SEED0 + max(24, CASES // 2)))
 def test_random_ipv6_config_matches_oracle(native, oracle_lib, seed):
     """IPv6 kernel (36-byte input) under random n / H / Q / field masks / queue widths /
     alignment / indirection tables; the numpy closed form over the oracle's 288 windows
