@@ -488,13 +488,21 @@ def extra_lines(torch, _native, dev, stream, key_bytes):
     ws6 = torch.zeros(_native.counts_workspace_bytes(128, 24) // 8, dtype=torch.int64, device=dev)
     # the IPv6 step as the IPv4 one: single-pass counts with the balanced tail
     # (rss_hash6_device_ws); beside it the plain launch (static walk, accumulating counts)
-    ms = timed(lambda: _native.hash6_device(k6, words.data_ptr(), n6, 128, 24, h6.data_ptr(),
-                                            q6.data_ptr(), c6.data_ptr(), _native.FLAG_QUEUE_U8,
-                                            sp, ws6.data_ptr()))
-    ms_plain = timed(lambda: _native.hash6_device(k6, words.data_ptr(), n6, 128, 24, h6.data_ptr(),
-                                                  q6.data_ptr(), c6.data_ptr(),
-                                                  _native.FLAG_QUEUE_U8 | _native.FLAG_ACCUMULATE,
-                                                  sp))
+    def ipv6_ws():
+        _native.hash6_device(k6, words.data_ptr(), n6, 128, 24, h6.data_ptr(), q6.data_ptr(),
+                             c6.data_ptr(), _native.FLAG_QUEUE_U8, sp, ws6.data_ptr())
+
+    def ipv6_plain():
+        _native.hash6_device(k6, words.data_ptr(), n6, 128, 24, h6.data_ptr(), q6.data_ptr(),
+                             c6.data_ptr(), _native.FLAG_QUEUE_U8 | _native.FLAG_ACCUMULATE, sp)
+
+    # alternating, best of two each: right after the IPv4 launches the first IPv6 launches
+    # run slow while the clocks settle (as counts-only does), which a single
+    # pass would charge to whichever variant went first
+    ms, ms_plain = float("inf"), float("inf")
+    for _ in range(2):
+        ms = min(ms, timed(ipv6_ws, warm=30))
+        ms_plain = min(ms_plain, timed(ipv6_plain, warm=30))
     out["ipv6_hash"] = {"tuples": n6, "kernel_ms": ms, "tuples_per_s": n6 / (ms / 1e3),
                         "achieved_GBs": n6 * 41 / (ms / 1e3) / 1e9,
                         "bytes_per_tuple": 41, "outputs": "hash u32 + queue u8 + counts",
