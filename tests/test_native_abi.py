@@ -87,6 +87,18 @@ def test_key_prepare_rejects_short_keys(lib):
     assert b">= 4 bytes" in lib.rss_last_error()
 
 
+def test_single_pass_workspace_validation(lib, example_key):
+    """rss_hash_device_ws / rss_hash6_device_ws refuse a NULL or misaligned workspace when
+    counts are asked for, before any device work."""
+    key = _native.prepare_key(example_key)
+    k6 = _native.prepare_key6(list(example_key))
+    for ws in (None, 12):
+        with pytest.raises(DeviceError, match="rss_hash_device_ws: workspace"):
+            _native.hash_device(key, 0, 0, 128, 24, None, None, 8, 0, None, ws or 0)
+        with pytest.raises(DeviceError, match="rss_hash6_device_ws: workspace"):
+            _native.hash6_device(k6, 0, 0, 128, 24, None, None, 8, 0, None, ws or 0)
+
+
 def test_argument_validation_before_any_device_work(lib, example_key):
     key = _native.prepare_key(example_key)
     with pytest.raises(DeviceError, match="must be >= 1"):
