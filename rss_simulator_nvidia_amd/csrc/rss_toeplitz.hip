@@ -389,22 +389,43 @@ __device__ __forceinline__ void store_queue4(void* out, Idx g, uint32_t q0, uint
 
 // Fold a workgroup's per-queue totals (`sum_of(q)`, q < Q) into the global uint64 counts.
 // Without a workspace: one atomicAdd per non-zero total (counts zeroed by the caller or by
-// a hipMemsetAsync before the launch).  With one (rss_hash_device_ws, single-pass counts):
-// the totals go into the accumulator ws[1..Q]; the workgroup then takes a ticket (ws[0]),
-// and the last of the gridDim.x workgroups moves the accumulated sums into `counts`
-// (overwriting, or adding when `mode & kFoldAccumulate`) and leaves the workspace zero for
-// the next launch -- so a batch's counts need no zeroing launch before it.  `flag` is one
-// LDS word the caller no longer reads (its bins, after every lane has summed them).
-// Ordering.  Default (`mode & kFoldOrdered`): the ticket is taken with an agent-scope
-// RELEASE and the last workgroup fences with an agent-scope ACQUIRE before reading the sums
-// -- the HIP/AMDGPU memory model's own hand-off between workgroups.  It costs 1.3-1.5 us per
-// 2^28-tuple launch (tools/ws_order_ab.py; a full __threadfence around the ticket cost
-// 90 us).  RSS_WS_ORDER=relaxed drops both: the workspace is touched only by device-scope
-// atomics, which gfx950 performs at one coherence point past the XCDs' L2s, and every lane
-// waits for its adds' return values (the asm use below) before the barrier that precedes the
-// ticket, so on this hardware the last workgroup's exchanges read every add even without
-// release/acquire (stress-tested both ways in tests/test_gpu_single_pass.py).
-constexpr uint32_t kFoldAccumulate = 1u, kFoldOrdered = 2u;
+// a hipMemsetAsync before the launch).  With one (rss_hash_device_ws, single-pass counts) the
+// launch writes the batch's counts itself (overwriting, or adding when `mode &
+// kFoldAccumulate`) and leaves the workspace zero for the next launch -- so a batch's counts
+// need no zeroing launch before it:
+// * arrival fold (default, round 3): each workgroup adds (1 << 44) | total into ws[1 + q] for
+//   every queue; the add whose returned arrival count is gridDim.x - 1 is the queue's last, so
+//   its workgroup writes counts[q] = old sum + its own and resets ws[1 + q].  Every queue is
+//   finalised by one atomic round trip; the sums need no release/acquire (they travel in the
+//   atomics on one location each).  Only the balanced tail's unit counter, reset by queue 0's
+//   finaliser, needs ordering: queue 0's add is an agent-scope RELEASE (after the same
+//   thread's claims) and the finaliser fences with an ACQUIRE before the reset
+//   (`mode & kFoldOrdered`; RSS_WS_ORDER=relaxed drops both).
+// * ticket fold (`mode & kFoldTicket`, RSS_FOLD=ticket; rounds 2-3): the totals go into
+//   ws[1..Q], each workgroup then takes a ticket (ws[0]), and the last of the gridDim.x
+//   workgroups exchanges the sums into the counts -- adds, ticket and exchanges are three
+//   serialised round trips on the last workgroup's path.  Ordered: the ticket is an
+//   agent-scope RELEASE and the last workgroup fences with an ACQUIRE before reading the sums
+//   (+1.3-1.5 us per 2^28-tuple launch over the relaxed form, tools/ws_order_ab.py; a full
+//   __threadfence around the ticket cost 90 us).  Relaxed, it relies on gfx950 performing
+//   device-scope atomics at one coherence point past the XCDs' L2s and on every lane waiting
+//   for its adds' return values before the barrier that precedes the ticket.
+// `flag` is one LDS word the caller no longer reads (its bins, after every lane has summed
+// them); both folds are stress-tested in tests/test_gpu_single_pass.py.
+constexpr uint32_t kFoldAccumulate = 1u, kFoldOrdered = 2u, kFoldTicket = 4u;
+// Arrival fold (default): ws[1 + q] = (arrivals << kArrivalShift) | sum -- every workgroup adds
+// (1 << kArrivalShift) | its total for every queue, and the add that returns arrivals ==
+// gridDim.x - 1 holds the queue's final sum (old + own): one atomic round trip on the last
+// workgroup's path instead of three (adds, ticket, exchanges).  Sums stay below 2^44 (a launch
+// is < 2^44 tuples) and arrivals below 2^20 workgroups.
+constexpr uint32_t kArrivalShift = 44;
+constexpr unsigned long long kArrivalOne = 1ull << kArrivalShift;
+constexpr unsigned long long kSumMask = kArrivalOne - 1;
+// the balanced tail's unit counter: ws[Q + 1]
+__host__ __device__ __forceinline__ unsigned long long* ws_tail_counter(unsigned long long* ws,
+                                                                        uint32_t Q) {
+    return ws + Q + 1;
+}
 
 template <typename SumOf>
 __device__ __forceinline__ void fold_counts(SumOf sum_of, uint32_t Q, unsigned long long* counts,
@@ -418,6 +439,32 @@ __device__ __forceinline__ void fold_counts(SumOf sum_of, uint32_t Q, unsigned l
         }
         return;
     }
+    if (!(mode & kFoldTicket)) {
+        const bool accumulate = (mode & kFoldAccumulate) != 0;
+        const unsigned long long last = (unsigned long long)gridDim.x - 1;
+        for (uint32_t q = tid; q < Q; q += blockDim.x) {
+            const unsigned long long add = kArrivalOne | sum_of(q);
+            // queue 0's add is a RELEASE (ordered mode): it orders this workgroup's balanced-
+            // tail claims (same thread, tid 0) before it, so queue 0's finaliser may reset the
+            // unit counter after an ACQUIRE; the sums themselves travel in the atomics
+            const unsigned long long old =
+                (q == 0 && (mode & kFoldOrdered))
+                    ? __hip_atomic_fetch_add(&ws[1], add, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT)
+                    : atomicAdd(&ws[1 + q], add);
+            if ((old >> kArrivalShift) == last) {  // every other workgroup's add is in `old`
+                const unsigned long long total = (old & kSumMask) + (add & kSumMask);
+                counts[q] = accumulate ? counts[q] + total : total;
+                atomicExch(&ws[1 + q], 0ull);  // after every add of this launch to it
+                if (q == 0 && reset) {
+                    if (mode & kFoldOrdered) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    atomicExch(reset, 0ull);  // every workgroup's last claim precedes its add
+                }
+            }
+        }
+        return;
+    }
+    // Ticket fold (RSS_FOLD=ticket, rounds 2-3): sums into ws[1..Q], a ticket at ws[0], and the
+    // last of the gridDim.x workgroups exchanges the sums into the counts
     for (uint32_t q = tid; q < Q; q += blockDim.x) {
         const uint32_t s = sum_of(q);
         if (s) {
@@ -599,7 +646,7 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
                 count_queue<kHist>(bins, q3, col, p);
             }
         };
-        walk_rows(group, ngroups, p.tail_rows, p.ws + 1 + p.Q,
+        walk_rows(group, ngroups, p.tail_rows, ws_tail_counter(p.ws, p.Q),
                   reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(bins) + p.bal_off));
         tail_begin = ngroups << 2;
     }
@@ -618,7 +665,8 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
             } else {
                 return bins[q];
             }
-        }, p.Q, p.counts, p.ws, p.accumulate, bins, p.tail_rows ? p.ws + 1 + p.Q : nullptr);
+        }, p.Q, p.counts, p.ws, p.accumulate, bins,
+           p.tail_rows ? ws_tail_counter(p.ws, p.Q) : nullptr);
     } else if constexpr (kHist == HIST_RANGE) {
         __syncthreads();
         for (uint32_t r = tid; r < p.q_span; r += kBlock)
@@ -925,7 +973,7 @@ __global__ __launch_bounds__(kBlock, 2) void rss_counts_perm_kernel(const PermPa
 #pragma unroll
         for (int i = 0; i < 4; ++i)
             perm_count(bins, perm_queue<kQMode>((bk >> (8 * i)) & 0xFFu, p), col);
-    }, ngroups, p.tail_rows, p.ws + 1 + p.Q,
+    }, ngroups, p.tail_rows, ws_tail_counter(p.ws, p.Q),
        reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(bins) + p.bal_off));
     // the last n % 4 tuples: one per lane of the first workgroup, in byte 0
     const uint64_t i = (ngroups << 2) + gtid;
@@ -940,7 +988,8 @@ __global__ __launch_bounds__(kBlock, 2) void rss_counts_perm_kernel(const PermPa
         uint32_t s = 0;
         for (uint32_t c = 0; c < kBinCols; ++c) s += bins[q * kBinCols + ((c + q) & (kBinCols - 1))];
         return s;
-    }, p.Q, p.counts, p.ws, p.accumulate, bins, p.tail_rows ? p.ws + 1 + p.Q : nullptr);
+    }, p.Q, p.counts, p.ws, p.accumulate, bins,
+       p.tail_rows ? ws_tail_counter(p.ws, p.Q) : nullptr);
 }
 
 // Key search: per-queue counts of the same tuples under many
@@ -1454,7 +1503,7 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz6_kernel(const LaunchParam
         };
         // single-pass launches hand out the last rows per workgroup slot (walk_rows, the
         // balanced tail of the IPv4 kernel): the XCDs that stream faster take more of them
-        walk_rows(group, ngroups, p6.tail_rows, p6.ws + 1 + p.Q,
+        walk_rows(group, ngroups, p6.tail_rows, ws_tail_counter(p6.ws, p.Q),
                   reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(bins) + p6.bal_off));
         tail_begin = ngroups << 2;
     }
@@ -1489,7 +1538,8 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz6_kernel(const LaunchParam
             } else {
                 return bins[k];
             }
-        }, p.Q, p.counts, p6.ws, p6.accumulate, bins, p6.tail_rows ? p6.ws + 1 + p.Q : nullptr);
+        }, p.Q, p.counts, p6.ws, p6.accumulate, bins,
+           p6.tail_rows ? ws_tail_counter(p6.ws, p.Q) : nullptr);
     } else if constexpr (kHist == HIST_RANGE) {
         __syncthreads();
         for (uint32_t r = tid; r < p.q_span; r += kBlock)
@@ -1792,6 +1842,13 @@ bool ws_order_acqrel() {
     return !(e && strcmp(e, "relaxed") == 0);
 }
 
+// RSS_FOLD=ticket: the single-pass fold of rounds 2-3 (adds, a ticket, the last workgroup's
+// exchanges) instead of the arrival fold (A/B, tests); read at every launch
+bool fold_ticket() {
+    const char* e = getenv("RSS_FOLD");
+    return e && strcmp(e, "ticket") == 0;
+}
+
 // RSS_OFF32=0: 64-bit addressing even where 32-bit byte offsets fit (A/B, tests)
 bool off32_enabled() {
     const char* e = getenv("RSS_OFF32");
@@ -2037,7 +2094,7 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
     if (single_pass) {
         p.ws = reinterpret_cast<unsigned long long*>(ws);
         p.accumulate = ((flags & RSS_FLAG_ACCUMULATE) ? kFoldAccumulate : 0u) |
-                       (ws_order_acqrel() ? kFoldOrdered : 0u);
+                       (ws_order_acqrel() ? kFoldOrdered : 0u) | (fold_ticket() ? kFoldTicket : 0u);
     }
     if (reta) {
         qmode = QM_TABLE;
@@ -2250,7 +2307,7 @@ int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint
     if (single_pass) {
         p.ws = reinterpret_cast<unsigned long long*>(ws);
         p.accumulate = ((flags & RSS_FLAG_ACCUMULATE) ? kFoldAccumulate : 0u) |
-                       (ws_order_acqrel() ? kFoldOrdered : 0u);
+                       (ws_order_acqrel() ? kFoldOrdered : 0u) | (fold_ticket() ? kFoldTicket : 0u);
     }
     if (reta)
         for (uint32_t b = 0; b < htable; ++b) p.reta[b] = (uint16_t)reta[b];
@@ -2528,7 +2585,7 @@ int rss_hash_device(const rss_key* key, const rss_tuple4* d_tuples, size_t n, ui
 int rss_counts_workspace_bytes(uint32_t nqueues, size_t* out) {
     if (!out) return set_error(RSS_EINVAL, "rss_counts_workspace_bytes: NULL argument");
     if (nqueues < 1) return set_error(RSS_EINVAL, "rss_counts_workspace_bytes: nqueues must be >= 1");
-    // ticket + one accumulator per queue + the balanced tail's unit counter
+    // ticket + one accumulator per queue + the balanced tail's unit counter (fold_counts)
     *out = sizeof(uint64_t) * ((size_t)nqueues + 2);
     return RSS_OK;
 }

@@ -81,7 +81,7 @@ def test_random_config_matches_oracle(native, oracle_lib, seed):
         # configurations above stay what they were), the workspace followed by guard words
         single_pass = bool(np.random.default_rng(5000 + seed).random() < 0.5)
         wsn = native.counts_workspace_bytes(H, Q) // 8  # ticket, qn sums, tail counter
-        assert wsn == qn + 2
+        assert wsn >= qn + 2 and wsn % (qn + 2) == 0  # spread 8 << k bytes apart
         ws = torch.zeros(wsn + 8, dtype=torch.int64, device=dev)
         ws[wsn:] = -7
         native.hash_device(key, tup_ptr, n, H, Q, h_ptr, q_ptr, counts.data_ptr(), flags, stream,

@@ -305,21 +305,39 @@ for i in range(300):
 got = outs.cpu().numpy().view(np.uint64)
 assert (got == want[None, :]).all(), "mismatch"
 assert int(ws.abs().sum()) == 0
+# balanced-tail launches (>= 16 rows: the fold also resets the unit counter), outputs on
+n2 = (1 << 24) + 4099
+host2 = lib.generate(8, 0, n2)
+want2 = lib.run(key_bytes, host2, H, Q, want_hash=False, want_queue=False, threads=8,
+               fn="oracle_run_tables")[2]
+t2 = torch.from_numpy(host2.view(np.int32).reshape(-1)).to(dev)
+h2 = torch.empty(n2, dtype=torch.int32, device=dev)
+outs2 = torch.zeros((40, Q), dtype=torch.int64, device=dev)
+for i in range(40):
+    _native.hash_device(key, t2.data_ptr(), n2, H, Q, h2.data_ptr(), None, outs2[i].data_ptr(),
+                        0, s, ws.data_ptr())
+got2 = outs2.cpu().numpy().view(np.uint64)
+assert (got2 == want2[None, :]).all(), "balanced-tail mismatch"
+assert int(ws.abs().sum()) == 0
 print("variant ok")
 """
 
 
-def test_relaxed_ordering_variant(example_key):
-    """RSS_WS_ORDER=relaxed (no release ticket / acquire fence: the hardware-assumption
-    hand-off of round 2; the default is release/acquire since ADVICE r02) gives the same
-    counts launch after launch (in a child process, so the variable never leaks here)."""
+@pytest.mark.parametrize("env", [{"RSS_WS_ORDER": "relaxed"}, {"RSS_FOLD": "ticket"},
+                                 {"RSS_FOLD": "ticket", "RSS_WS_ORDER": "relaxed"}])
+def test_fold_variants(example_key, env):
+    """The other single-pass folds give the same counts launch after launch, static and with
+    the balanced tail: RSS_WS_ORDER=relaxed (no release / acquire: the hardware-assumption
+    hand-off of round 2; the default is release/acquire since ADVICE r02) and RSS_FOLD=ticket
+    (sums + ticket + the last workgroup's exchanges, rounds 2-3; the default is the arrival
+    fold) -- in a child process, so the variables never leak here."""
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     code = VARIANT_SCRIPT % {"root": root, "key": list(example_key)}
     p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240,
-                       env=dict(os.environ, RSS_WS_ORDER="relaxed"))
+                       env=dict(os.environ, **env))
     assert p.returncode == 0 and "variant ok" in p.stdout, p.stdout + p.stderr
 
 
