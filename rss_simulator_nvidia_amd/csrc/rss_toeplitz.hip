@@ -444,11 +444,12 @@ __device__ __forceinline__ void fold_counts(SumOf sum_of, uint32_t Q, unsigned l
         const unsigned long long last = (unsigned long long)gridDim.x - 1;
         for (uint32_t q = tid; q < Q; q += blockDim.x) {
             const unsigned long long add = kArrivalOne | sum_of(q);
-            // queue 0's add is a RELEASE (ordered mode): it orders this workgroup's balanced-
-            // tail claims (same thread, tid 0) before it, so queue 0's finaliser may reset the
-            // unit counter after an ACQUIRE; the sums themselves travel in the atomics
+            // with the balanced tail, queue 0's add is a RELEASE (ordered mode): it orders this
+            // workgroup's tail claims (same thread, tid 0) before it, so queue 0's finaliser may
+            // reset the unit counter after an ACQUIRE; the sums themselves travel in the
+            // atomics, so a launch without the tail needs no ordering at all
             const unsigned long long old =
-                (q == 0 && (mode & kFoldOrdered))
+                (q == 0 && reset && (mode & kFoldOrdered))
                     ? __hip_atomic_fetch_add(&ws[1], add, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT)
                     : atomicAdd(&ws[1 + q], add);
             if ((old >> kArrivalShift) == last) {  // every other workgroup's add is in `old`
