@@ -147,23 +147,25 @@ int rss_hash_device(const rss_key* key, const rss_tuple4* d_tuples, size_t n,
 /*
  * Single-pass counts: rss_hash_device with a caller-owned workspace, so that a batch's
  * counts need no zeroing launch before it (the step of a job that hashes batch after
- * batch into fresh counts, sharding.CountsPipeline).  Every workgroup adds its LDS bins
- * into the workspace's accumulators and takes a ticket; the last one moves the sums into
- * d_counts -- overwriting them, or adding with RSS_FLAG_ACCUMULATE -- and zeroes the
- * workspace again.  d_workspace: rss_counts_workspace_bytes(nqueues) bytes of 8-byte
- * aligned device memory (ticket + one sum per queue + the balanced tail's unit counter),
+ * batch into fresh counts, sharding.CountsPipeline).  Every workgroup adds, for every
+ * queue, its bin total plus one arrival (1 << 44) into the workspace; the add that sees the
+ * last arrival writes that queue's count into d_counts -- overwriting it, or adding with
+ * RSS_FLAG_ACCUMULATE -- and zeroes its word again.  d_workspace: rss_counts_workspace_bytes(nqueues) bytes of 8-byte
+ * aligned device memory (one word per queue + the balanced tail's unit counter + one spare),
  * zero before its first use (every launch leaves it zero), used
  * by one launch at a time (launches that may run concurrently need their own).  Launches
  * whose counts are not gathered in private/shared LDS bins (more than 8192 queues) leave the workspace
  * untouched and zero d_counts first as rss_hash_device does.  Results are identical to
  * rss_hash_device's.  With d_counts NULL the workspace is not used (may be NULL).
- * Ordering: each workgroup takes its ticket with an agent-scope release and the last one
- * fences with an agent-scope acquire before reading the sums (the HIP memory model's
- * hand-off; ~1.5 us per 2^28-tuple launch).  RSS_WS_ORDER=relaxed in the environment drops
- * both and relies on gfx950 performing every device-scope atomic at one coherence point
- * beyond the XCDs' L2s (true on MI355X, stress-tested in tests/test_gpu_single_pass.py,
- * but not promised by the memory model).  Launches of >= 2^24 tuples also take the last
- * tenth of their work from a counter in the workspace (the balanced tail: the XCDs finish
+ * Ordering: a queue's count travels in the atomics on its own word, so it needs no fence;
+ * with the balanced tail (below) queue 0's add is an agent-scope release and its finaliser
+ * fences with an agent-scope acquire before resetting the tail's counter (the HIP memory
+ * model's hand-off).  RSS_WS_ORDER=relaxed in the environment drops both (relying on
+ * gfx950 performing every device-scope atomic at one coherence point beyond the XCDs' L2s);
+ * RSS_FOLD=ticket selects rounds 2-3's fold (sums, a ticket, the last workgroup's
+ * exchanges: two more atomic round trips on the last workgroup's path, ~2 us per launch).
+ * Both are stress-tested in tests/test_gpu_single_pass.py.  Launches of >= 2^24 tuples
+ * also take the last tenth of their work from a counter in the workspace (the balanced tail: the XCDs finish
  * together), so a workspace must never be shared by two launches in flight.
  */
 int rss_counts_workspace_bytes(uint32_t nqueues, size_t* out);
