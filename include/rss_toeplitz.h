@@ -157,14 +157,13 @@ int rss_hash_device(const rss_key* key, const rss_tuple4* d_tuples, size_t n,
  * whose counts are not gathered in private/shared LDS bins (more than 8192 queues) leave the workspace
  * untouched and zero d_counts first as rss_hash_device does.  Results are identical to
  * rss_hash_device's.  With d_counts NULL the workspace is not used (may be NULL).
- * Ordering: a queue's count travels in the atomics on its own word, so it needs no fence;
- * with the balanced tail (below) queue 0's add is an agent-scope release and its finaliser
- * fences with an agent-scope acquire before resetting the tail's counter (the HIP memory
- * model's hand-off).  RSS_WS_ORDER=relaxed in the environment drops both (relying on
- * gfx950 performing every device-scope atomic at one coherence point beyond the XCDs' L2s);
- * RSS_FOLD=ticket selects rounds 2-3's fold (sums, a ticket, the last workgroup's
- * exchanges: two more atomic round trips on the last workgroup's path, ~2 us per launch).
- * Both are stress-tested in tests/test_gpu_single_pass.py.  Launches of >= 2^24 tuples
+ * Ordering: a queue's count travels in the atomics on its own word, and the balanced
+ * tail's counter (below) is reset by the launch's final claim on it, so no fence is needed
+ * (the memory model's single-location coherence).  RSS_FOLD=ticket selects rounds 2-3's
+ * fold (sums, a ticket taken with an agent-scope release, the last workgroup's acquire and
+ * exchanges: two more atomic round trips and the fences on the last workgroup's path);
+ * RSS_WS_ORDER=relaxed drops that fold's release/acquire.  All are stress-tested in
+ * tests/test_gpu_single_pass.py.  Launches of >= 2^24 tuples
  * also take the last tenth of their work from a counter in the workspace (the balanced tail: the XCDs finish
  * together), so a workspace must never be shared by two launches in flight.
  */

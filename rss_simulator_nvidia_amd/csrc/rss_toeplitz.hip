@@ -396,11 +396,9 @@ __device__ __forceinline__ void store_queue4(void* out, Idx g, uint32_t q0, uint
 // * arrival fold (default, round 3): each workgroup adds (1 << 44) | total into ws[1 + q] for
 //   every queue; the add whose returned arrival count is gridDim.x - 1 is the queue's last, so
 //   its workgroup writes counts[q] = old sum + its own and resets ws[1 + q].  Every queue is
-//   finalised by one atomic round trip; the sums need no release/acquire (they travel in the
-//   atomics on one location each).  Only the balanced tail's unit counter, reset by queue 0's
-//   finaliser, needs ordering: queue 0's add is an agent-scope RELEASE (after the same
-//   thread's claims) and the finaliser fences with an ACQUIRE before the reset
-//   (`mode & kFoldOrdered`; RSS_WS_ORDER=relaxed drops both).
+//   finalised by one atomic round trip and needs no release/acquire: its count travels in
+//   the atomics on one location (the balanced tail's unit counter is reset in walk_rows by
+//   the launch's final claim, also one location).
 // * ticket fold (`mode & kFoldTicket`, RSS_FOLD=ticket; rounds 2-3): the totals go into
 //   ws[1..Q], each workgroup then takes a ticket (ws[0]), and the last of the gridDim.x
 //   workgroups exchanges the sums into the counts -- adds, ticket and exchanges are three
@@ -430,7 +428,7 @@ __host__ __device__ __forceinline__ unsigned long long* ws_tail_counter(unsigned
 template <typename SumOf>
 __device__ __forceinline__ void fold_counts(SumOf sum_of, uint32_t Q, unsigned long long* counts,
                                             unsigned long long* ws, uint32_t mode,
-                                            uint32_t* flag, unsigned long long* reset = nullptr) {
+                                            uint32_t* flag) {
     const uint32_t tid = threadIdx.x;
     if (!ws) {
         for (uint32_t q = tid; q < Q; q += blockDim.x) {
@@ -444,22 +442,12 @@ __device__ __forceinline__ void fold_counts(SumOf sum_of, uint32_t Q, unsigned l
         const unsigned long long last = (unsigned long long)gridDim.x - 1;
         for (uint32_t q = tid; q < Q; q += blockDim.x) {
             const unsigned long long add = kArrivalOne | sum_of(q);
-            // with the balanced tail, queue 0's add is a RELEASE (ordered mode): it orders this
-            // workgroup's tail claims (same thread, tid 0) before it, so queue 0's finaliser may
-            // reset the unit counter after an ACQUIRE; the sums themselves travel in the
-            // atomics, so a launch without the tail needs no ordering at all
-            const unsigned long long old =
-                (q == 0 && reset && (mode & kFoldOrdered))
-                    ? __hip_atomic_fetch_add(&ws[1], add, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT)
-                    : atomicAdd(&ws[1 + q], add);
+            // the sums travel in the atomics on one word each: no fence is needed
+            const unsigned long long old = atomicAdd(&ws[1 + q], add);
             if ((old >> kArrivalShift) == last) {  // every other workgroup's add is in `old`
                 const unsigned long long total = (old & kSumMask) + (add & kSumMask);
                 counts[q] = accumulate ? counts[q] + total : total;
                 atomicExch(&ws[1 + q], 0ull);  // after every add of this launch to it
-                if (q == 0 && reset) {
-                    if (mode & kFoldOrdered) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                    atomicExch(reset, 0ull);  // every workgroup's last claim precedes its add
-                }
             }
         }
         return;
@@ -489,12 +477,7 @@ __device__ __forceinline__ void fold_counts(SumOf sum_of, uint32_t Q, unsigned l
             const unsigned long long v = atomicExch(&ws[1 + q], 0ull);  // read + reset
             counts[q] = accumulate ? counts[q] + v : v;
         }
-        if (tid == 0) {
-            atomicExch(&ws[0], 0ull);
-            // the balanced tail's unit counter (ws[Q + 1]): every workgroup made its last
-            // claim before its ticket, so no claim of this launch can follow the reset
-            if (reset) atomicExch(reset, 0ull);
-        }
+        if (tid == 0) atomicExch(&ws[0], 0ull);
     }
 }
 
@@ -506,7 +489,7 @@ __device__ __forceinline__ void fold_counts(SumOf sum_of, uint32_t Q, unsigned l
 // flight (issued one unit ahead, broadcast through the LDS word `slot`), so the workgroups
 // -- the XCDs -- that stream faster (measured: even XCDs finish ~4 % before odd ones) take
 // more of the tail and every XCD ends together, while the whole grid still sweeps one
-// window of the arrays at a time.  `next` is reset by fold_counts' last workgroup.
+// window of the arrays at a time.  `next` is reset by the launch's final claim (below).
 template <typename Group>
 __device__ __forceinline__ void walk_rows(Group group, uint64_t ngroups, uint32_t tail_rows,
                                           unsigned long long* next, unsigned long long* slot) {
@@ -519,10 +502,18 @@ __device__ __forceinline__ void walk_rows(Group group, uint64_t ngroups, uint32_
     }
     const uint64_t nrows = (ngroups + gstride - 1) / gstride;
     const uint64_t srows = nrows - tail_rows;  // the launcher keeps tail_rows < nrows
+    // Every workgroup claims until a claim fails (returns >= the tail's units), so a launch
+    // makes exactly tail units + gridDim.x claims; the one that returns the last of them is the
+    // final RMW of the launch on `next` and resets it -- one location, so no fence is needed.
+    const unsigned long long last_claim = (unsigned long long)tail_rows * gridDim.x + gridDim.x - 1;
+    auto publish = [&](unsigned long long c) {  // tid 0
+        if (c == last_claim) atomicExch(next, 0ull);
+        *slot = c;
+    };
     unsigned long long claim = 0;
     if (tid == 0) claim = atomicAdd(next, 1ull);  // the first tail unit, in flight meanwhile
     for (uint64_t row = 0; row < srows; ++row) group(row * gstride + gtid);  // full rows
-    if (tid == 0) *slot = claim;
+    if (tid == 0) publish(claim);
     __syncthreads();
     const uint64_t first = srows * gridDim.x, nunits = nrows * gridDim.x;
     uint64_t u = first + *slot;
@@ -531,7 +522,7 @@ __device__ __forceinline__ void walk_rows(Group group, uint64_t ngroups, uint32_
         if (tid == 0) claim = atomicAdd(next, 1ull);  // the next unit, during this one
         const uint64_t g = (u / gridDim.x) * gstride + (u % gridDim.x) * kBlock + tid;
         if (g < ngroups) group(g);
-        if (tid == 0) *slot = claim;
+        if (tid == 0) publish(claim);
         __syncthreads();
         u = first + *slot;
     }
@@ -666,8 +657,7 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
             } else {
                 return bins[q];
             }
-        }, p.Q, p.counts, p.ws, p.accumulate, bins,
-           p.tail_rows ? ws_tail_counter(p.ws, p.Q) : nullptr);
+        }, p.Q, p.counts, p.ws, p.accumulate, bins);
     } else if constexpr (kHist == HIST_RANGE) {
         __syncthreads();
         for (uint32_t r = tid; r < p.q_span; r += kBlock)
@@ -989,8 +979,7 @@ __global__ __launch_bounds__(kBlock, 2) void rss_counts_perm_kernel(const PermPa
         uint32_t s = 0;
         for (uint32_t c = 0; c < kBinCols; ++c) s += bins[q * kBinCols + ((c + q) & (kBinCols - 1))];
         return s;
-    }, p.Q, p.counts, p.ws, p.accumulate, bins,
-       p.tail_rows ? ws_tail_counter(p.ws, p.Q) : nullptr);
+    }, p.Q, p.counts, p.ws, p.accumulate, bins);
 }
 
 // Key search: per-queue counts of the same tuples under many
@@ -1539,8 +1528,7 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz6_kernel(const LaunchParam
             } else {
                 return bins[k];
             }
-        }, p.Q, p.counts, p6.ws, p6.accumulate, bins,
-           p6.tail_rows ? ws_tail_counter(p6.ws, p.Q) : nullptr);
+        }, p.Q, p.counts, p6.ws, p6.accumulate, bins);
     } else if constexpr (kHist == HIST_RANGE) {
         __syncthreads();
         for (uint32_t r = tid; r < p.q_span; r += kBlock)
