@@ -1,7 +1,7 @@
 """Single-pass counts and the balanced tail on the IPv6 kernel (``rss_hash6_device_ws``).
 
-The IPv6 counterpart of ``tests/test_gpu_single_pass.py``: the kernel's last workgroup
-writes the counts from a caller-owned workspace that every launch leaves zero, and launches
+The IPv6 counterpart of ``tests/test_gpu_single_pass.py``: the launch writes the counts
+itself from a caller-owned workspace that every launch leaves zero, and launches
 of >= 16 grid rows (2^24 tuples) hand their last rows out per workgroup slot.  Results are
 those of ``rss_hash6_device`` (pinned by the Microsoft IPv6 vectors and the oracle in
 ``tests/test_gpu_fields_ipv6.py``): hash, ``hash % H % Q`` and its ``value_counts``

@@ -80,7 +80,7 @@ def test_random_config_matches_oracle(native, oracle_lib, seed):
         # half the cases as single-pass counts (rss_hash_device_ws; own generator, so the
         # configurations above stay what they were), the workspace followed by guard words
         single_pass = bool(np.random.default_rng(5000 + seed).random() < 0.5)
-        wsn = native.counts_workspace_bytes(H, Q) // 8  # ticket, qn sums, tail counter
+        wsn = native.counts_workspace_bytes(H, Q) // 8  # spare, qn sums, tail counter
         assert wsn >= qn + 2 and wsn % (qn + 2) == 0  # spread 8 << k bytes apart
         ws = torch.zeros(wsn + 8, dtype=torch.int64, device=dev)
         ws[wsn:] = -7

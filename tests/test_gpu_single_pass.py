@@ -1,5 +1,5 @@
-"""Single-pass counts (``rss_hash_device_ws``): the launch's last workgroup writes the
-per-queue counts from a caller-owned workspace, so a batch needs no zeroing launch before
+"""Single-pass counts (``rss_hash_device_ws``): the launch writes the per-queue counts
+itself from a caller-owned workspace (each queue's last arriving add writes its count), so a batch needs no zeroing launch before
 it.  Bar: hash / queue / counts bit-exact to the C oracle (the ``value_counts`` of
 ``simulator.py:107-113``) and to ``rss_hash_device`` on the same inputs, over the kernels
 that take the workspace (LDS-table kernel with private and shared bins, the register-table
@@ -34,7 +34,7 @@ def _dev_tuples(host, offset_bytes=0):
 
 def _ws(native, H, Q):
     nbytes = native.counts_workspace_bytes(H, Q)
-    assert nbytes == 8 * (min(H, Q) + 2)  # ticket, sums, balanced-tail counter
+    assert nbytes == 8 * (min(H, Q) + 2)  # spare (ticket fold), sums, balanced-tail counter
     return torch.zeros(nbytes // 8, dtype=torch.int64, device=DEV)
 
 
@@ -328,7 +328,7 @@ print("variant ok")
 def test_fold_variants(example_key, env):
     """The other single-pass folds give the same counts launch after launch, static and with
     the balanced tail: RSS_WS_ORDER=relaxed (no release / acquire: the hardware-assumption
-    hand-off of round 2; the default is release/acquire since ADVICE r02) and RSS_FOLD=ticket
+    hand-off of round 2; the ticket fold is release/acquire since ADVICE r02) and RSS_FOLD=ticket
     (sums + ticket + the last workgroup's exchanges, rounds 2-3; the default is the arrival
     fold) -- in a child process, so the variables never leak here."""
     import os

@@ -134,7 +134,7 @@ def test_argument_validation_before_any_device_work(lib, example_key):
         _native.hash_device(key, 0x1000, 16, 128, 24, None, None, 0x1000, 0, None, 0x1004)
     with pytest.raises(DeviceError, match="must be >= 1"):
         _native.counts_workspace_bytes(128, 0)
-    assert _native.counts_workspace_bytes(128, 24) == 8 * 26  # ticket, 24 sums, tail counter
+    assert _native.counts_workspace_bytes(128, 24) == 8 * 26  # spare, 24 sums, tail counter
     assert _native.counts_workspace_bytes(2**32 + 1, 24) == 8 * 26  # hash % H % Q rewritten
     fn = lib.rss_hash_host_multi
     with pytest.raises(DeviceError, match="no contexts"):
