@@ -4,9 +4,10 @@ One step = one pass of the hot path (Toeplitz hash -> htable index -> queue
 modulo -> per-queue histogram, all outputs written) over this rank's resident
 shard of synthetic tuples (one ``rss_hash_device_ws`` launch that also writes the step's
 counts from zero -- single-pass counts, no zeroing launch; ``--zero-counts`` = a zeroing launch
-+ an accumulating one; ``--graph`` replays the launch as a captured HIP graph), followed, under a launcher, by the RCCL all-reduce of the
-per-queue count vector, issued async so it overlaps the next step (double-buffered
-counts).  Weak scaling: every rank owns ``--tuples-per-gpu``
++ an accumulating one; ``--graph`` replays the launch as a captured HIP graph), followed, under
+a launcher, by ONE RCCL all-reduce of that batch's per-queue count vector (``ncclAllReduce`` on
+the launch stream; ``--secondary-bucket`` times B batches per collective beside it, labelled).
+Weak scaling: every rank owns ``--tuples-per-gpu``
 tuples (default 2**28, BASELINE configs[2]) of one global splitmix64 stream.
 
     python bench.py [--gpus N --steps K --warmup W]
@@ -70,10 +71,15 @@ def parse_args():
                         "async on its own stream (overlap), torch.distributed stream-ordered "
                         "(stream), or ncclAllReduce through rccl.RcclComm on the launch stream "
                         "(rccl)")
-    p.add_argument("--allreduce-bucket", type=int, default=8, metavar="B",
-                   help="steps per count all-reduce at N > 1: each step's uint64[Q] counts are "
-                        "a row of a [B, Q] bucket reduced by one collective after its B-th "
-                        "step (sharding.CountsPipeline bucket; 1 = one collective per step)")
+    p.add_argument("--allreduce-bucket", type=int, default=1, metavar="B",
+                   help="steps per count all-reduce at N > 1 (default 1: one collective per "
+                        "batch, the reference's unit of work -- one histogram per batch, "
+                        "simulator.py:100-116); B > 1: each step's uint64[Q] counts are a row "
+                        "of a [B, Q] bucket reduced by one collective after its B-th step "
+                        "(sharding.CountsPipeline bucket)")
+    p.add_argument("--secondary-bucket", type=int, default=8, metavar="B",
+                   help="at N > 1, also time the same steps with B steps per collective as the "
+                        "labelled secondary block `bucketed` (0 = skip)")
     p.add_argument("--settle-ms", type=float, default=600,
                    help="untimed launches of the step for this long before the warmup steps "
                         "(clock settle; 0 = none)")
@@ -765,6 +771,40 @@ def main():
             [int(x) & ((1 << 64) - 1) for x in last.tolist()] == want
         verified["main"] = v
 
+    # Labelled secondary block at N > 1: the same steps with B steps' count rows per
+    # collective (CountsPipeline(bucket=B)) -- fewer exchanges than the reference's one
+    # histogram per batch, so never the `value`
+    bucketed = None
+    if distributed and args.secondary_bucket > 1:
+        bpipe = CountsPipeline(Q, dev, single_pass=not args.zero_counts, htable=H,
+                               allreduce=args.allreduce, comm=comm, bucket=args.secondary_bucket)
+        for _ in range(args.warmup):
+            bpipe.step(launch)
+        bpipe.drain()
+        barrier()
+        torch.cuda.synchronize()
+        tb = time.perf_counter()
+        for _ in range(args.steps):
+            bpipe.step(launch)
+        blast = bpipe.drain()
+        torch.cuda.synchronize()
+        barrier()
+        bstats = torch.tensor([time.perf_counter() - tb], dtype=torch.float64, device=dev)
+        dist.all_reduce(bstats, op=dist.ReduceOp.MAX)
+        b_elapsed = float(bstats[0])
+        if int(blast.sum().item()) != n * world:
+            raise SystemExit("bench: bucketed counts sum to %d, expected %d"
+                             % (int(blast.sum().item()), n * world))
+        bucketed = {"steps_per_collective": bpipe.bucket,
+                    "collectives": -(-args.steps // bpipe.bucket),
+                    "value": n * world * args.steps / b_elapsed,
+                    "ms_per_step": b_elapsed * 1e3 / args.steps,
+                    "note": "secondary: the main line's steps with %d steps' count rows per "
+                            "collective (rows of a [%d, %d] bucket; every row is still its own "
+                            "batch's reduced histogram) -- not the reference's one exchange per "
+                            "batch, so not `value`" % (bpipe.bucket, bpipe.bucket, Q)}
+        del bpipe
+
     # BASELINE configs[3]: 2^30 global tuples split over the ranks (sharding.shard_range),
     # one batch = one rss_hash_device_ws launch per rank + ONE all-reduce of its counts
     # (bucket 1) -- the reference's unit of work, one histogram per batch
@@ -881,16 +921,19 @@ def main():
                 "htable": H,
                 "queues": Q,
                 "queue_width": qw,
+                "collectives_per_batch": (1.0 / pipeline.bucket) if distributed else 0,
                 "parallelism": ("tuple-sharded x%d, %s all-reduce of every step's uint64[%d] "
-                                "counts, %d steps per collective (rows of a [%d, %d] bucket) %s"
+                                "counts, %s %s"
                                 % (world, "RCCL" if args.dist_backend == "nccl" else "gloo", Q,
-                                   pipeline.bucket, pipeline.bucket, Q,
+                                   "one collective per batch" if pipeline.bucket == 1 else
+                                   "%d steps per collective (rows of a [%d, %d] bucket)"
+                                   % (pipeline.bucket, pipeline.bucket, Q),
                                    {"overlap": "(torch.distributed async, overlapped with the "
                                                "next step)",
                                     "stream": "(torch.distributed, stream-ordered after the "
-                                              "bucket's last launch)",
+                                              "launch)",
                                     "rccl": "(ncclAllReduce via rccl.RcclComm, stream-ordered "
-                                            "after the bucket's last launch)"}[args.allreduce]))
+                                            "after the launch)"}[args.allreduce]))
                                if distributed else "single process, one GPU (no process group)",
                 "step": ("zero counts + " if args.zero_counts else
                          "single-pass counts (rss_hash_device_ws): ") +
@@ -964,6 +1007,8 @@ def main():
              "configs3_first_allocation_ms": r[6] if c3 else None,
              "verified_main": {1.0: True, 0.0: False}.get(r[7]),
              "verified_configs3": {1.0: True, 0.0: False}.get(r[8])} for r in rows]
+        if bucketed is not None:
+            line["bucketed"] = bucketed
         if c3 is not None:
             c3.pop("kernel_ms_rank", None)
             c3.pop("placement_rank", None)

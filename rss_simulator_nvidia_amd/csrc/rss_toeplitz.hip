@@ -1598,6 +1598,9 @@ KernelFn pick_vec(int vec4) {
                   kQMode != QM_TABLE)  // (H <= 1024 with those: never this many queues)
         if (vec4 == VM_BYTE_LUT)
             return rss_toeplitz_kernel<kHPow2, kQMode, kHist, kQWidth, true, false, true>;
+    // a byte-table request with no byte-table instance must not fall back to the 12-bit
+    // tables: the launcher sized the dynamic LDS for the byte-table span
+    if (vec4 == VM_BYTE_LUT) return nullptr;
     return vec4 ? rss_toeplitz_kernel<kHPow2, kQMode, kHist, kQWidth, true>
                 : rss_toeplitz_kernel<kHPow2, kQMode, kHist, kQWidth, false>;
 }

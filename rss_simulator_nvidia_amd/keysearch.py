@@ -35,9 +35,10 @@ def key_text(key):
     return ":".join("{:02x}".format(b) for b in key)
 
 
-def slot_share(htable, nqueues):
-    """Fraction of the H buckets each queue owns (bucket b -> queue b % Q)."""
-    q = np.arange(nqueues, dtype=np.int64)
+def slot_share(htable, nqueues, width=None):
+    """Fraction of the H buckets each queue owns (bucket b -> queue b % Q), for queues
+    ``[0, width)`` (default: all Q)."""
+    q = np.arange(nqueues if width is None else min(width, nqueues), dtype=np.int64)
     slots = htable // nqueues + (q < htable % nqueues)
     if nqueues > htable:
         slots = (q < htable).astype(np.int64)
@@ -53,7 +54,9 @@ def balance(counts, htable, nqueues):
     """
     counts = np.atleast_2d(np.asarray(counts, dtype=np.float64))
     n = counts.sum(axis=1, keepdims=True)
-    ideal = n * slot_share(htable, nqueues)[None, :]
+    # Count rows are min(H, Q) wide (``_native.queue_modulus``): queues >= H own no bucket,
+    # so the ideal share is cut to the columns present (nothing is lost).
+    ideal = n * slot_share(htable, nqueues, counts.shape[1])[None, :]
     live = ideal[0] > 0
     with np.errstate(divide="ignore", invalid="ignore"):
         rel = np.where(ideal > 0, counts / np.where(ideal > 0, ideal, 1), 0.0)

@@ -86,8 +86,8 @@ class RcclComm:
     group (a MAX all-reduce of [failed, timed out]), and if any rank failed every rank raises
     ``RcclError`` -- so callers fall back together instead of hanging in the bootstrap.  If
     any rank's init timed out the error is ``stuck``: the blocked init cannot be cancelled
-    (a communicator handle that was already returned is ``ncclCommAbort``-ed), so the
-    process must not fall back to RCCL through ``torch.distributed`` -- it should exit.
+    (nor its half-built communicator aborted while the helper thread still runs in it), so
+    the process must not fall back to RCCL through ``torch.distributed`` -- it should exit.
     """
 
     def __init__(self, device, group=None, timeout_s=120.0):
@@ -138,10 +138,12 @@ class RcclComm:
         failed, any_stuck = (int(x) for x in flags.tolist())
         self._comm = comm if why is None else None
         if failed:
+            # A communicator whose blocking init is still running on the helper thread is
+            # left alone: RCCL hands out the handle before that init finishes, so aborting
+            # it here would free memory the helper is still using.  The caller exits the
+            # process instead (``stuck``).
             if self._comm is not None:
                 self.destroy()
-            elif stuck and comm.value:  # a handle exists but init has not returned: abort it
-                lib.ncclCommAbort(comm)
             raise RcclError(why or "ncclCommInitRank failed on another rank", stuck=bool(any_stuck))
 
     def all_reduce_counts(self, counts, stream=None):

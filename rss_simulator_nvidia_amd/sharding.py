@@ -75,7 +75,8 @@ class CountsPipeline:
 
     Two ways to start a step's counts from zero:
 
-    * ``single_pass=True`` (default on a GPU): ``launch(counts, workspace=ws)`` enqueues one
+    * ``single_pass=True`` (default on a GPU when ``htable`` is given; without it the
+      default is ``False``): ``launch(counts, workspace=ws)`` enqueues one
       ``rss_hash_device_ws`` launch that overwrites ``counts`` itself -- the kernel's last
       workgroup writes them from the zero-initialised ``workspace`` (int64 tensor of
       ``_native.counts_workspace_bytes(htable, nqueues) // 8`` -- the library's own size --
@@ -123,8 +124,8 @@ class CountsPipeline:
         if bucket < 1:
             raise ValueError("bucket must be >= 1")
         device = torch.device(device)
-        if single_pass is None:
-            single_pass = device.type == "cuda"
+        if single_pass is None:  # a caller that gives no htable keeps zero + accumulate
+            single_pass = device.type == "cuda" and htable is not None
         if single_pass and htable is None:
             raise ValueError("single_pass counts need htable: the workspace is sized by "
                              "_native.counts_workspace_bytes(htable, nqueues)")

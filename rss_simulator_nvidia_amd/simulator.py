@@ -81,6 +81,7 @@ class Simulator(object):
         self.__ip_df = df
         self.__queues = None
         self.__counts = None
+        self.__count_rows = None
 
     def calc_hash(self):
         """Hash every row on the GPU and add the ``hash_result`` column."""

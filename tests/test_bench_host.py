@@ -134,6 +134,17 @@ def check_bench_line(line):
     return line
 
 
+def test_default_exchange_is_one_collective_per_batch(monkeypatch):
+    """at N > 1 the headline does one all-reduce per batch (the reference's
+    unit of work, one histogram per batch, simulator.py:100-116); bucketing is a labelled
+    secondary block."""
+    import bench
+    monkeypatch.setattr("sys.argv", ["bench.py", "--gpus", "8"])
+    args = bench.parse_args()
+    assert args.allreduce_bucket == 1 and args.secondary_bucket == 8
+    assert args.configs3_tuples == 1 << 30
+
+
 def test_committed_bench_lines_carry_the_round3_blocks():
     """The world-size-1 RCCL run (torchrun --nproc-per-node 1) and the 8-rank gloo rehearsal
     on one GPU (RSS_BENCH_DEVICE=0), as committed under profiles/r03/."""

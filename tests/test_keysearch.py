@@ -50,6 +50,31 @@ def test_search_ranks_by_balance(monkeypatch, oracle_lib):
         np.testing.assert_array_equal(r["counts"], c)
 
 
+@pytest.mark.parametrize("H,Q", [(16, 24), (128, 129), (8, 4 * 10 ** 9)])
+def test_search_with_more_queues_than_buckets(monkeypatch, oracle_lib, H, Q):
+    """the device returns count rows min(H, Q) wide (``queue_modulus``), so
+    ``balance`` must score them against the first min(H, Q) slot shares (queues >= H own
+    no bucket) instead of broadcasting against all Q."""
+    ctx = OracleContext(oracle_lib)
+    width = _native.queue_modulus(H, Q)[1]
+    assert width == min(H, Q)
+
+    class NarrowContext:
+        def key_search(self, keys, tuples, htable, nqueues):
+            return np.stack([ctx.hash(k, tuples, htable, width)[2] for k in keys])
+
+    monkeypatch.setattr(_native, "default_context", lambda: NarrowContext())
+    tuples = oracle_lib.generate(1, 0, 3000)
+    ranked = keysearch.search(tuples, H, Q, n_keys=6, seed=1, top=6)
+    assert len(ranked) == 6
+    for r in ranked:
+        assert r["counts"].shape == (width,) and int(r["counts"].sum()) == 3000
+        assert r["max_load"] >= 1.0 and r["used"] <= width
+    m = keysearch.balance(np.full((1, width), 10, np.uint64), H, Q)
+    np.testing.assert_allclose(m["max_load"], [1.0])  # every bucket its own queue, all equal
+    np.testing.assert_allclose(m["chi2"], [0.0])
+
+
 def test_cli_writes_best_key(monkeypatch, oracle_lib, golden_dir, tmp_path, capsys):
     monkeypatch.setattr(_native, "default_context", lambda: OracleContext(oracle_lib))
     out = tmp_path / "best.txt"
