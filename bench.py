@@ -511,6 +511,8 @@ def extra_lines(torch, _native, dev, stream, key_bytes):
         ms_plain = min(ms_plain, timed(ipv6_plain, warm=30))
     out["ipv6_hash"] = {"tuples": n6, "kernel_ms": ms, "tuples_per_s": n6 / (ms / 1e3),
                         "achieved_GBs": n6 * 41 / (ms / 1e3) / 1e9,
+                        "bound": "hbm", "peak_GBs": HBM_PEAK_GBS,
+                        "frac": n6 * 41 / (ms / 1e3) / 1e9 / HBM_PEAK_GBS,
                         "bytes_per_tuple": 41, "outputs": "hash u32 + queue u8 + counts",
                         "launch": "rss_hash6_device_ws (single-pass counts, balanced tail)",
                         "plain_launch_ms": ms_plain}
@@ -525,9 +527,22 @@ def extra_lines(torch, _native, dev, stream, key_bytes):
     kc = torch.empty((nk, 24), dtype=torch.int64, device=dev)
     ms = timed(lambda: _native.key_search_device(windows.data_ptr(), nk, tup.data_ptr(), nt, 128,
                                                  24, kc.data_ptr(), sp), warm=3, reps=10)
+    rate = nk * nt / (ms / 1e3)
     out["key_search"] = {"keys": nk, "tuples": nt, "kernel_ms": ms,
-                         "key_tuple_evals_per_s": nk * nt / (ms / 1e3), "htable": 128, "queues": 24}
+                         "key_tuple_evals_per_s": rate, "htable": 128, "queues": 24,
+                         "bound": "lds", "peak_evals_per_s": KEYSEARCH_LDS_PEAK,
+                         "frac": rate / KEYSEARCH_LDS_PEAK,
+                         "bound_note": "LDS-array cycles, conflict-free: 9 ds_read_b64 + 8 "
+                                       "ds_add_u32 (2 cycles each) per 64 tuples x 8 keys, 256 CUs "
+                                       "at 2.4 GHz; PMC (profiles/r04/pmc_keysearch/summary.json): "
+                                       "the LDS array is 78 % busy, 55 % of its cycles bank "
+                                       "conflicts of the random table reads; VALU issue 32 %"}
     return out
+
+
+# rss_key_search_packed_kernel's LDS bound: per wave-step of 64 tuples x 8 keys
+# 17 LDS instructions x 2 LDS-array cycles when conflict-free; 256 CUs at 2.4 GHz
+KEYSEARCH_LDS_PEAK = 256 * 2.4e9 / (17 * 2) * 512
 
 
 def main():

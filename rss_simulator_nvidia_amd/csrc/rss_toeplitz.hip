@@ -79,7 +79,10 @@ static_assert(kBlock * 4 == (int)kTableEntries, "LUT build maps 4 entries per th
 enum QueueMode { QM_MASK = 0, QM_FAST16 = 1, QM_FAST32 = 2, QM_TABLE = 3, QM_FAST8 = 4 };
 constexpr uint32_t kRetaMax = 1024;  // indirection-table entries carried in the kernarg
 enum HistMode { HIST_PRIVATE = 0, HIST_SHARED = 1, HIST_GLOBAL = 2, HIST_NONE = 3, HIST_RANGE = 4,
-                HIST_RANGE16 = 5 };
+                HIST_RANGE16 = 5, HIST_RANGE8 = 6 };
+// HIST_RANGE8 (IPv4 byte-table kernel, past the u16 bins' reach): u8 bins, four per dword, a
+// guard at 0x80 and a poison word for a bin that wraps (range8_guard) -- 151552 queues in the
+// LDS beside the byte tables, one pass.
 // HIST_RANGE16 (IPv4 kernel): HIST_RANGE with u16 bins, two per dword, twice the queues in the
 // same LDS -- with the wide pass's guard bit (rss_queue_hist_wide_kernel): the add that
 // returns 0x7FFF moves 2^15 of its bin into the global counts.
@@ -117,6 +120,8 @@ struct LaunchParams {
     uint32_t q_stride;            // key search: row stride of the [keys, nqueues] counts (>= Q)
     uint32_t tail_rows;           // balanced tail: rows handed out as units (0 = static grid-stride)
     uint32_t bal_off;             // balanced tail: byte offset of its LDS slot (dynamic LDS)
+    uint32_t* ovf;                // HIST_RANGE8: u32 [q_span] guard moves (units of 128)
+    uint32_t* poison;             // HIST_RANGE8: set when a u8 bin wrapped (results discarded)
     uint16_t reta[kRetaMax];      // QM_TABLE: queue of bucket b (ethtool -X indirection)
 };
 
@@ -320,6 +325,38 @@ __device__ __forceinline__ void range16_guard(uint32_t* bins, uint32_t q, uint32
     }
 }
 
+// HIST_RANGE8's halves.  u8 bins, four per dword: the add that returns 0x7F (its bin now
+// holds 0x80) subtracts 0x80 from the bin and counts one move of 128 in p.ovf (a u32 per
+// queue, summed by the partial reduce).  Unlike u16 bins, the adds in flight while that
+// subtract is pending are not bounded below the field's headroom: a workgroup can hold 4096
+// adds on one bin (every lane's four tuples in one queue), and a field that passes 0xFF
+// carries into its neighbour.  Exactly the add that takes a field past 0xFF sees 0xFF, so
+// that add raises *p.poison: the launch's bins are then discarded -- the partial reduce is
+// gated on !poison and rss_range8_fallback_kernel (gated on poison) recounts the range with
+// u32 bins.  Uniform and flow-like input stay far from it (a bin meets ~8 adds per workgroup
+// at 131072 queues); a batch of one repeated tuple takes the fallback.
+__device__ __forceinline__ uint32_t range8_add(uint32_t* bins, uint32_t q, const LaunchParams& p) {
+    const uint32_t r = q - p.q_lo;  // wraps for q < q_lo
+    if (r >= p.q_span) return 0u;
+    return __hip_atomic_fetch_add(&bins[r >> 2], 1u << ((r & 3u) * 8u), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ void range8_guard(uint32_t* bins, uint32_t q, uint32_t old,
+                                             const LaunchParams& p) {
+    const uint32_t r = q - p.q_lo;
+    if (r >= p.q_span) return;
+    const uint32_t sh = (r & 3u) * 8u;
+    const uint32_t f = (old >> sh) & 0xFFu;
+    if (f == 0x7Fu) {
+        __hip_atomic_fetch_sub(&bins[r >> 2], 0x80u << sh, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+        atomicAdd(&p.ovf[r], 1u);
+    } else if (f == 0xFFu) {
+        __hip_atomic_store(p.poison, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 template <int kHist>
 __device__ __forceinline__ void count_queue(uint32_t* bins, uint32_t q, uint32_t col,
                                             const LaunchParams& p) {
@@ -336,6 +373,8 @@ __device__ __forceinline__ void count_queue(uint32_t* bins, uint32_t q, uint32_t
             __hip_atomic_fetch_add(&bins[r], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     } else if constexpr (kHist == HIST_RANGE16) {
         range16_guard(bins, q, range16_add(bins, q, p), p);
+    } else if constexpr (kHist == HIST_RANGE8) {
+        range8_guard(bins, q, range8_add(bins, q, p), p);
     }
 }
 
@@ -567,7 +606,8 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
     const uint32_t nbins = kHist == HIST_PRIVATE   ? p.Q * kBinCols
                          : kHist == HIST_SHARED    ? p.Q
                          : kHist == HIST_RANGE     ? p.q_span
-                         : kHist == HIST_RANGE16   ? (p.q_span + 1) / 2 : 0u;  // dwords
+                         : kHist == HIST_RANGE16   ? (p.q_span + 1) / 2
+                         : kHist == HIST_RANGE8    ? (p.q_span + 3) / 4 : 0u;  // dwords
     for (uint32_t e = tid; e < nbins; e += kBlock) bins[e] = 0;
     uint32_t* reta_lds = bins + nbins;  // QM_TABLE: H entries after the bins
     if constexpr (kQMode == QM_TABLE)
@@ -631,6 +671,13 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
                 range16_guard(bins, q1, o1, p);
                 range16_guard(bins, q2, o2, p);
                 range16_guard(bins, q3, o3, p);
+            } else if constexpr (kHist == HIST_RANGE8) {
+                const uint32_t o0 = range8_add(bins, q0, p), o1 = range8_add(bins, q1, p);
+                const uint32_t o2 = range8_add(bins, q2, p), o3 = range8_add(bins, q3, p);
+                range8_guard(bins, q0, o0, p);
+                range8_guard(bins, q1, o1, p);
+                range8_guard(bins, q2, o2, p);
+                range8_guard(bins, q3, o3, p);
             } else {
                 count_queue<kHist>(bins, q0, col, p);
                 count_queue<kHist>(bins, q1, col, p);
@@ -675,6 +722,10 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
             if ((x >> 16) && r + 1 < p.q_span)
                 atomicAdd(&p.counts[p.q_lo + r + 1], (unsigned long long)(x >> 16));
         }
+    } else if constexpr (kHist == HIST_RANGE8) {
+        __syncthreads();  // one row of the u8 partial matrix (the launcher always gives one)
+        uint32_t* row = p.partial + (size_t)blockIdx.x * p.partial_stride;
+        for (uint32_t w = tid; w < nbins; w += kBlock) row[w] = bins[w];
     }
 }
 
@@ -812,21 +863,33 @@ __global__ __launch_bounds__(kBlock) void rss_queue_hist_wide_kernel(
     for (uint32_t e = tid; e < words; e += kBlock) row[e] = bins[e];
 }
 
-// counts[q_lo + q] += sum over the `rows` rows of the u16 partial matrix (column q).  A
-// workgroup takes a strip of 64 dwords (128 queues) of every row: its 256 threads are 64
-// columns x 4 row groups, each summing its rows' dword (two u16 queues) with eight loads in
-// flight, then the 4 row groups meet in LDS.  (One thread per queue summing all rows ran
-// 60 us per 65536-queue range at 2^28 tuples -- as long as half the wide pass; profiles/r03/
-// mqprof.)  The wide pass's guard-bit adds landed in a previous launch, so a plain
-// read-modify-write of the counts suffices.
+// counts[q_lo + q] += sum over the `rows` rows of the u16 (kBits = 16) or u8 (kBits = 8)
+// partial matrix (column q).  A workgroup takes a strip of 64 dwords (128 or 256 queues) of
+// every row: its 256 threads are 64 columns x 4 row groups, each summing its rows' dword with
+// eight loads in flight, then the 4 row groups meet in LDS.  (One thread per queue summing all
+// rows ran 60 us per 65536-queue range at 2^28 tuples -- as long as half the wide pass;
+// profiles/r03/mqprof.)  The guard-bit adds landed in a previous launch, so a plain
+// read-modify-write of the counts suffices.  HIST_RANGE8 passes its guard moves (`ovf`, u32
+// per queue in units of 128) and its poison word: a poisoned launch's rows are discarded here
+// and rss_range8_fallback_kernel recounts the range.
 constexpr uint32_t kReduceCols = 64, kReduceGroups = 4;
+template <int kBits>
 __global__ __launch_bounds__(kReduceCols * kReduceGroups) void rss_partial_reduce_kernel(
         const uint32_t* __restrict__ partial, uint32_t rows, uint32_t stride_words, uint32_t q_lo,
-        uint32_t q_span, unsigned long long* counts) {
-    __shared__ unsigned long long part[kReduceGroups][kReduceCols][2];
+        uint32_t q_span, unsigned long long* counts, const uint32_t* __restrict__ ovf,
+        const uint32_t* __restrict__ poison) {
+    constexpr uint32_t kPer = 32 / kBits, kMask = (1u << kBits) - 1u;
+    if (poison && *poison) return;  // uniform: the fallback recounts this range
+    __shared__ unsigned long long part[kReduceGroups][kReduceCols][kPer];
     const uint32_t col = threadIdx.x % kReduceCols, grp = threadIdx.x / kReduceCols;
-    const uint32_t word = blockIdx.x * kReduceCols + col;  // queues 2 * word, 2 * word + 1
-    unsigned long long lo = 0, hi = 0;
+    const uint32_t word = blockIdx.x * kReduceCols + col;  // queues kPer * word + f
+    unsigned long long acc[kPer];
+#pragma unroll
+    for (uint32_t f = 0; f < kPer; ++f) acc[f] = 0;
+    auto take = [&](uint32_t x) {
+#pragma unroll
+        for (uint32_t f = 0; f < kPer; ++f) acc[f] += (x >> (f * kBits)) & kMask;
+    };
     if (word < stride_words) {
         constexpr uint32_t kIn = 8;
         uint32_t r = grp;
@@ -835,28 +898,64 @@ __global__ __launch_bounds__(kReduceCols * kReduceGroups) void rss_partial_reduc
 #pragma unroll
             for (uint32_t k = 0; k < kIn; ++k) x[k] = partial[(size_t)(r + k * kReduceGroups) * stride_words + word];
 #pragma unroll
-            for (uint32_t k = 0; k < kIn; ++k) {
-                lo += x[k] & 0xFFFFu;
-                hi += x[k] >> 16;
-            }
+            for (uint32_t k = 0; k < kIn; ++k) take(x[k]);
         }
-        for (; r < rows; r += kReduceGroups) {
-            const uint32_t x = partial[(size_t)r * stride_words + word];
-            lo += x & 0xFFFFu;
-            hi += x >> 16;
-        }
+        for (; r < rows; r += kReduceGroups) take(partial[(size_t)r * stride_words + word]);
     }
-    part[grp][col][0] = lo;
-    part[grp][col][1] = hi;
+#pragma unroll
+    for (uint32_t f = 0; f < kPer; ++f) part[grp][col][f] = acc[f];
     __syncthreads();
     if (grp == 0) {
-        for (uint32_t g = 1; g < kReduceGroups; ++g) {
-            lo += part[g][col][0];
-            hi += part[g][col][1];
+#pragma unroll
+        for (uint32_t f = 0; f < kPer; ++f) {
+            for (uint32_t g = 1; g < kReduceGroups; ++g) acc[f] += part[g][col][f];
+            const uint32_t q = kPer * word + f;
+            if (q < q_span) {
+                const unsigned long long v = acc[f] + (ovf ? 128ull * ovf[q] : 0ull);
+                if (v) counts[q_lo + q] += v;
+            }
         }
-        const uint32_t q0 = 2 * word;
-        if (q0 < q_span && lo) counts[q_lo + q0] += lo;
-        if (q0 + 1 < q_span && hi) counts[q_lo + q0 + 1] += hi;
+    }
+}
+
+// HIST_RANGE8's recount (see range8_guard), launched after every u8 pass: returns at once
+// unless the pass raised its poison word.  Then every workgroup counts the range in slices
+// of kFallbackSpan queues with u32 LDS bins (no guard needed: a bin holds one workgroup's
+// share of the batch) -- from the queue column when the pass wrote one with the queues
+// themselves (u32), else by hashing the tuples again on the byte tables -- and folds each
+// slice with atomics into the counts.  Slow (a pass over the batch per slice), exact, and
+// only ever run on inputs that pile thousands of tuples into one bin at once.
+constexpr uint32_t kFallbackSpan = 36864;  // 144 KiB of u32 bins beside the 12 KiB byte tables
+template <bool kHPow2, int kQMode>
+__global__ __launch_bounds__(kBlock) void rss_range8_fallback_kernel(const LaunchParams p,
+                                                                    const uint32_t* __restrict__ qcol) {
+    if (!*p.poison) return;  // uniform across the grid: no wave is left behind
+    __shared__ uint32_t lut[kByteLutDwords];
+    extern __shared__ uint32_t bins[];
+    const uint32_t tid = threadIdx.x;
+    if (!qcol) build_byte_lut(lut, p.window, tid);
+    const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
+    const uint64_t gstride = (uint64_t)gridDim.x * kBlock;
+    for (uint32_t lo = 0; lo < p.q_span; lo += kFallbackSpan) {
+        const uint32_t span = min(kFallbackSpan, p.q_span - lo);
+        for (uint32_t e = tid; e < span; e += kBlock) bins[e] = 0;
+        __syncthreads();
+        for (uint64_t i = gtid; i < p.n; i += gstride) {
+            uint32_t q;
+            if (qcol) {
+                q = qcol[i];
+            } else {
+                const uint32_t* src = reinterpret_cast<const uint32_t*>(p.tuples) + 3 * i;
+                q = queue_of<kQMode>(bucket_of<kHPow2>(toeplitz_hash_bytes(lut, src[0], src[1], src[2]), p), p);
+            }
+            const uint32_t r = q - p.q_lo - lo;  // wraps below the slice
+            if (r < span)
+                __hip_atomic_fetch_add(&bins[r], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        __syncthreads();
+        for (uint32_t e = tid; e < span; e += kBlock)
+            if (bins[e]) atomicAdd(&p.counts[p.q_lo + lo + e], (unsigned long long)bins[e]);
+        __syncthreads();
     }
 }
 
@@ -1586,6 +1685,13 @@ using KernelFn = void (*)(const LaunchParams);
 enum VecMode { VM_SCALAR = 0, VM_VEC4 = 1, VM_OFF32 = 2, VM_BYTE_LUT = 3 };
 template <bool kHPow2, int kQMode, int kHist, int kQWidth>
 KernelFn pick_vec(int vec4) {
+    if constexpr (kHist == HIST_RANGE8) {  // byte tables, u32 / u16-residual columns only
+        if constexpr ((kQWidth == QW_U32 || kQWidth == QW_U16R) && kQMode != QM_FAST8 &&
+                      kQMode != QM_TABLE)
+            if (vec4 == VM_BYTE_LUT)
+                return rss_toeplitz_kernel<kHPow2, kQMode, kHist, kQWidth, true, false, true>;
+        return nullptr;
+    }
     if constexpr (kQWidth == QW_U16R) {  // the byte-table HIST_RANGE16 body only
         if constexpr (kHist == HIST_RANGE16 && kQMode != QM_FAST8 && kQMode != QM_TABLE)
             if (vec4 == VM_BYTE_LUT)
@@ -1622,6 +1728,7 @@ KernelFn pick_hist(int hist, int qwidth, int vec4) {
         case HIST_SHARED: return pick_width<kHPow2, kQMode, HIST_SHARED>(qwidth, vec4);
         case HIST_GLOBAL: return pick_width<kHPow2, kQMode, HIST_GLOBAL>(qwidth, vec4);
         case HIST_RANGE16: return pick_width<kHPow2, kQMode, HIST_RANGE16>(qwidth, vec4);
+        case HIST_RANGE8: return pick_width<kHPow2, kQMode, HIST_RANGE8>(qwidth, vec4);
         case HIST_NONE: return pick_width<kHPow2, kQMode, HIST_NONE>(qwidth, vec4);
         default: return nullptr;  // HIST_RANGE (u32 ranges): the IPv6 kernel's only
     }
@@ -1958,11 +2065,12 @@ int launch_queue_ranges(const void* qcol, int qw, uint64_t n, uint32_t first, ui
                 hipError_t e = hipGetLastError();
                 if (e == hipSuccess) {
                     const uint32_t words = (sp + 1) / 2;
-                    hipLaunchKernelGGL(rss_partial_reduce_kernel,
+                    hipLaunchKernelGGL(rss_partial_reduce_kernel<16>,
                                        dim3((words + kReduceCols - 1) / kReduceCols),
                                        dim3(kReduceCols * kReduceGroups), 0, stream,
                                        static_cast<const uint32_t*>(partial), grid, stride_words,
-                                       lo, sp, counts);
+                                       lo, sp, counts, (const uint32_t*)nullptr,
+                                       (const uint32_t*)nullptr);
                     e = hipGetLastError();
                 }
                 if (e != hipSuccess)
@@ -2010,10 +2118,10 @@ int launch_range16(KernelFn fn, unsigned grid, uint32_t shmem, LaunchParams& p, 
     hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), shmem, stream, p);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && partial) {
-        hipLaunchKernelGGL(rss_partial_reduce_kernel, dim3((words + kReduceCols - 1) / kReduceCols),
+        hipLaunchKernelGGL(rss_partial_reduce_kernel<16>, dim3((words + kReduceCols - 1) / kReduceCols),
                            dim3(kReduceCols * kReduceGroups), 0, stream,
                            static_cast<const uint32_t*>(partial), grid, words, p.q_lo, p.q_span,
-                           p.counts);
+                           p.counts, (const uint32_t*)nullptr, (const uint32_t*)nullptr);
         e = hipGetLastError();
     }
     int rc = e == hipSuccess ? RSS_OK
@@ -2024,6 +2132,95 @@ int launch_range16(KernelFn fn, unsigned grid, uint32_t shmem, LaunchParams& p, 
             rc = set_error(RSS_EIO, "hipFreeAsync failed: %s", hipGetErrorString(fe));
     }
     p.partial = nullptr;
+    return rc;
+}
+
+// RSS_RANGE8=0 keeps u16 bins (+ queue-column passes) past 75776 queues (A/B, tests)
+bool range8_enabled() {
+    const char* e = getenv("RSS_RANGE8");
+    return !(e && e[0] == '0');
+}
+
+// Tests only: RSS_RANGE8_DEBUG=force sets the poison word before the pass (the fallback then
+// recounts every launch); =nofallback drops the gate and the fallback (a wrap would then show
+// as wrong counts -- proves a launch's counts came from the u8 bins and their guard moves)
+int range8_debug() {
+    const char* e = getenv("RSS_RANGE8_DEBUG");
+    if (!e) return 0;
+    return strcmp(e, "force") == 0 ? 1 : (strcmp(e, "nofallback") == 0 ? 2 : 0);
+}
+
+using FallbackFn = void (*)(const LaunchParams, const uint32_t*);
+template <bool kHPow2>
+FallbackFn pick_fallback(int qmode) {
+    switch (qmode) {
+        case QM_MASK: return rss_range8_fallback_kernel<kHPow2, QM_MASK>;
+        case QM_FAST16: return rss_range8_fallback_kernel<kHPow2, QM_FAST16>;
+        case QM_FAST32: return rss_range8_fallback_kernel<kHPow2, QM_FAST32>;
+        default: return nullptr;  // (FAST8 / TABLE: H <= 1024, never this many queues)
+    }
+}
+
+// A HIST_RANGE8 hash launch's scratch block: the u8 partial matrix (a row per workgroup),
+// the guard moves (u32 per queue) and the poison word.  NULL when it cannot be allocated (the
+// caller then keeps the u16 path).
+size_t range8_rows_bytes(unsigned grid, uint32_t q_span) { return (size_t)grid * ((q_span + 3) / 4) * 4; }
+size_t range8_tail_bytes(uint32_t q_span) { return ((size_t)q_span + 4) * 4; }  // ovf + poison + pad
+void* alloc_range8(unsigned grid, uint32_t q_span, hipStream_t stream) {
+    void* buf = nullptr;
+    if (hipMallocAsync(&buf, range8_rows_bytes(grid, q_span) + range8_tail_bytes(q_span), stream) !=
+        hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return buf;
+}
+
+// A HIST_RANGE8 hash launch over [p.q_lo, p.q_lo + p.q_span) on the block `buf` (alloc_range8,
+// freed here on every path): the guard moves and the poison word are zeroed, then the pass,
+// the reduce (gated on !poison) and the fallback (gated on poison; `qcol` = a u32 column of
+// the queues the pass writes, else it rehashes).
+int launch_range8(KernelFn fn, FallbackFn fallback, unsigned grid, int cu_count, LaunchParams& p,
+                  const uint32_t* qcol, void* buf, hipStream_t stream) {
+    const uint32_t words = (p.q_span + 3) / 4;
+    const size_t rows_bytes = range8_rows_bytes(grid, p.q_span);
+    const size_t tail_bytes = range8_tail_bytes(p.q_span);
+    if (!fn || !fallback) {
+        (void)hipFreeAsync(buf, stream);
+        return set_error(RSS_EIO, "rss_hash_device: no kernel instance for this launch");
+    }
+    uint32_t* tail = reinterpret_cast<uint32_t*>(static_cast<char*>(buf) + rows_bytes);
+    p.partial = static_cast<uint32_t*>(buf);
+    p.partial_stride = words;
+    p.ovf = tail;
+    p.poison = tail + p.q_span;
+    const int debug = range8_debug();
+    hipError_t e = hipMemsetAsync(tail, 0, tail_bytes, stream);
+    if (e == hipSuccess && debug == 1) e = hipMemsetD32Async(p.poison, 1, 1, stream);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), words * 4, stream, p);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(rss_partial_reduce_kernel<8>, dim3((words + kReduceCols - 1) / kReduceCols),
+                           dim3(kReduceCols * kReduceGroups), 0, stream,
+                           static_cast<const uint32_t*>(p.partial), grid, words, p.q_lo, p.q_span,
+                           p.counts, static_cast<const uint32_t*>(p.ovf),
+                           debug == 2 ? nullptr : static_cast<const uint32_t*>(p.poison));
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess && debug != 2) {
+        hipLaunchKernelGGL(fallback, dim3(cu_count), dim3(kBlock),
+                           std::min(kFallbackSpan, p.q_span) * 4, stream, p, qcol);
+        e = hipGetLastError();
+    }
+    int rc = e == hipSuccess ? RSS_OK
+                             : set_error(RSS_EIO, "rss_hash_device: launch failed: %s", hipGetErrorString(e));
+    const hipError_t fe = hipFreeAsync(buf, stream);  // stream-ordered after its readers
+    if (fe != hipSuccess && rc == RSS_OK)
+        rc = set_error(RSS_EIO, "hipFreeAsync failed: %s", hipGetErrorString(fe));
+    p.partial = nullptr;
+    p.ovf = p.poison = nullptr;
     return rc;
 }
 
@@ -2135,13 +2332,31 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
                                  : pick_queue<false>(qmode, HIST_RANGE16, qwidth, vm);
             return launch_range16(fn, grid, ((q_eff + 1) / 2) * 4 + reta_bytes, p, stream);
         }
+        // Past the u16 bins' reach: u8 bins (HIST_RANGE8, a guard at 0x80 and a poison-gated
+        // recount, range8_guard) hold span8 = 151552 queues beside the byte tables -- one pass
+        // up to there, and the first range of a queue-column launch beyond.
+        const uint32_t span8 = kLdsBytes - kByteLutBytes;
+        FallbackFn fb8 = h_pow2 ? pick_fallback<true>(qmode) : pick_fallback<false>(qmode);
+        void* r8buf = nullptr;  // the u8 pass's scratch block, when it runs
+        if (byte_lut && range8_enabled() && fb8)
+            r8buf = alloc_range8(grid, std::min(q_eff, span8), stream);
+        if (r8buf && q_eff <= span8) {
+            p.q_lo = 0;
+            p.q_span = q_eff;
+            KernelFn fn = h_pow2 ? pick_queue<true>(qmode, HIST_RANGE8, qwidth, VM_BYTE_LUT)
+                                 : pick_queue<false>(qmode, HIST_RANGE8, qwidth, VM_BYTE_LUT);
+            // the caller's u32 column holds the queues (exact even when the bins are poisoned)
+            const uint32_t* col = d_queue ? static_cast<const uint32_t*>(d_queue) : nullptr;
+            return launch_range8(fn, fb8, grid, info.cu_count, p, col, r8buf, stream);
+        }
         if (ranged_histogram_ok(q_eff, kNarrowSpan, qbytes)) {
             void* qcol = d_queue;
             int qw = qwidth;
             bool scratch = false, ranged = true;
             // counts only past the byte tables' range: a u16 column of q - span (QW_U16R) when
             // the rest of the queues fit 16 bits, else the queues themselves
-            const bool resid = !d_queue && byte_lut && q_eff - span <= 0xFFFFu;
+            const uint32_t first_span = r8buf ? span8 : span;
+            const bool resid = !d_queue && byte_lut && q_eff - first_span <= 0xFFFFu;
             const uint32_t sbytes = resid ? 2 : qbytes;
             if (!qcol || qwidth == QW_U8) {  // (u8 queues always fit the bins: q_eff <= 256)
                 if (hipMallocAsync(&qcol, (size_t)n * sbytes, stream) == hipSuccess) {
@@ -2159,13 +2374,26 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
                 // the first range: the bins the first pass's tables leave (byte tables: 4-tuple
                 // body only; the caller's queue buffer may not be aligned for it)
                 const bool b1 = byte_lut && v4 && qw != QW_U8;
-                const uint32_t span1 = b1 ? span : span12;
+                const bool r8 = b1 && r8buf;  // (a caller's u32 column: b1 == byte_lut)
+                if (!r8 && r8buf) {
+                    (void)hipFreeAsync(r8buf, stream);
+                    r8buf = nullptr;
+                }
+                const uint32_t span1 = b1 ? (r8 ? span8 : span) : span12;
                 p.q_span = span1;  // < q_eff here
                 const int vm1 = b1 ? VM_BYTE_LUT : (v4 ? VM_VEC4 : VM_SCALAR);
-                KernelFn fn = h_pow2 ? pick_queue<true>(qmode, HIST_RANGE16, qw, vm1)
-                                     : pick_queue<false>(qmode, HIST_RANGE16, qw, vm1);
+                const int hist1 = r8 ? HIST_RANGE8 : HIST_RANGE16;
+                KernelFn fn = h_pow2 ? pick_queue<true>(qmode, hist1, qw, vm1)
+                                     : pick_queue<false>(qmode, hist1, qw, vm1);
                 const unsigned g1 = v4 ? grid : (unsigned)std::min<uint64_t>((n + kBlock - 1) / kBlock, cap);
-                rc = launch_range16(fn, g1, (span1 / 2) * 4 + reta_bytes, p, stream);
+                if (r8) {  // the fallback reads the column when it holds the queues themselves
+                    rc = launch_range8(fn, fb8, g1, info.cu_count, p,
+                                       qw == QW_U32 ? static_cast<const uint32_t*>(qcol) : nullptr,
+                                       r8buf, stream);
+                    r8buf = nullptr;
+                } else {
+                    rc = launch_range16(fn, g1, (span1 / 2) * 4 + reta_bytes, p, stream);
+                }
                 if (rc == RSS_OK && qw == QW_U16R)  // queues [span1, q_eff) as [0, q_eff - span1)
                     rc = launch_queue_ranges(qcol, QW_U16, n, 0, q_eff - span1, p.counts + span1,
                                              info.cu_count, stream);
@@ -2180,6 +2408,7 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
                 return rc;
             }
         }
+        if (r8buf) (void)hipFreeAsync(r8buf, stream);  // unused: global atomics below
     }
     // 32-bit byte offsets when every stream's bytes fit them (input 12 n B is the largest)
     const int vmode = vec4 ? (12ull * n < (1ull << 32) && off32_enabled() &&

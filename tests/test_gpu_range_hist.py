@@ -249,3 +249,111 @@ def test_byte_tables_accumulate_and_queue_column_offsets(native, oracle_lib, exa
         got_q = qbuf.cpu().numpy().view(np.uint8)[off:off + 4 * n].view(np.uint32)
         np.testing.assert_array_equal(got_q, qo)
         np.testing.assert_array_equal(c.cpu().numpy().view(np.uint64), 2 * co)
+
+
+def _launch(native, key, tup, n, H, Q, outputs, counts_fill=0, flags=0):
+    dev = tup.device
+    s = torch.cuda.current_stream(dev).cuda_stream
+    h = torch.empty(n, dtype=torch.int32, device=dev) if outputs else None
+    q = torch.empty(n, dtype=torch.int32, device=dev) if outputs else None
+    c = torch.full((Q,), counts_fill, dtype=torch.int64, device=dev)
+    native.hash_device(key, tup.data_ptr(), n, H, Q, h.data_ptr() if outputs else None,
+                       q.data_ptr() if outputs else None, c.data_ptr(), flags, s)
+    torch.cuda.synchronize()
+    return h, q, c
+
+
+def _with_env(name, value, fn):
+    import os
+    old = os.environ.get(name)
+    os.environ[name] = value
+    try:
+        return fn()
+    finally:
+        if old is None:
+            os.environ.pop(name, None)
+        else:
+            os.environ[name] = old
+
+
+@pytest.mark.parametrize("Q", [75777, 131072, 151552, 151553, 217087, 262144, 10 ** 6])
+def test_range8_u8_bins_equal_oracle(native, oracle_lib, example_key, Q):
+    """Past 75776 queues the byte-table pass counts up to 151552 of them in u8 LDS bins
+    (HIST_RANGE8: guard at 0x80, moves into a u32 per queue, poison-gated recount); past
+    151552 it is the first range of a queue-column launch (counts only: a u16 column of
+    q - 151552 up to Q = 217087, u32 beyond).  On uniform input the u8 path alone
+    (RSS_RANGE8_DEBUG=nofallback: no gate, no recount), the recount alone
+    (RSS_RANGE8_DEBUG=force), the default and the u16 path (RSS_RANGE8=0) all give the
+    oracle's hashes, queues and counts, with and without per-tuple outputs."""
+    n, H = (1 << 21) + 5, 1 << 30
+    host = oracle_lib.generate(31, 0, n)
+    tup = torch.from_numpy(host.view(np.int32).reshape(-1)).to("cuda:0")
+    key = native.prepare_key(example_key)
+    ho, qo, co = oracle_lib.run(example_key, host, H, Q)
+    runs = [("RSS_RANGE8_DEBUG", "nofallback"), ("RSS_RANGE8_DEBUG", "force"),
+            ("RSS_RANGE8", "1"), ("RSS_RANGE8", "0")]
+    for name, value in runs:
+        for outputs in (True, False):
+            h, q, c = _with_env(name, value,
+                                lambda: _launch(native, key, tup, n, H, Q, outputs, counts_fill=7))
+            np.testing.assert_array_equal(c.cpu().numpy().view(np.uint64), co,
+                                          err_msg="%s=%s outputs=%s" % (name, value, outputs))
+            if outputs:
+                np.testing.assert_array_equal(h.cpu().numpy().view(np.uint32), ho)
+                np.testing.assert_array_equal(q.cpu().numpy().view(np.uint32), qo)
+
+
+@pytest.mark.parametrize("Q", [131072, 200000])
+def test_range8_guard_moves(native, oracle_lib, example_key, Q):
+    """1024 distinct tuples repeated over 2^26 tuples: every workgroup adds ~256 times into
+    each of their u8 bins, a few at a time, so the 0x80 guard moves 128 out of a bin into its
+    u32 again and again without a bin ever wrapping.  With the gate and the recount switched
+    off (RSS_RANGE8_DEBUG=nofallback) the counts come from the u8 bins and the guard moves
+    alone -- and equal the oracle's; the default launch agrees."""
+    n, H, base_n = 1 << 26, 1 << 30, 1024
+    base = oracle_lib.generate(32, 0, base_n)
+    host = np.tile(base, (n // base_n, 1))
+    tup = torch.from_numpy(host.view(np.int32).reshape(-1)).to("cuda:0")
+    _, qb, _ = oracle_lib.run(example_key, base, H, Q)
+    want = np.bincount(qb.astype(np.int64), minlength=Q).astype(np.uint64) * np.uint64(n // base_n)
+    key = native.prepare_key(example_key)
+    for value in ("nofallback", "default"):
+        for outputs in (True, False):
+            _, q, c = _with_env("RSS_RANGE8_DEBUG", value,
+                                lambda: _launch(native, key, tup, n, H, Q, outputs))
+            np.testing.assert_array_equal(c.cpu().numpy().view(np.uint64), want,
+                                          err_msg="%s outputs=%s" % (value, outputs))
+            if outputs:
+                got = q[:base_n].cpu().numpy().view(np.uint32)
+                np.testing.assert_array_equal(got, qb)
+
+
+@pytest.mark.parametrize("Q,outputs", [(131072, True), (131072, False), (200000, True),
+                                       (200000, False)])
+def test_range8_poisoned_pass_recounts(native, oracle_lib, example_key, Q, outputs):
+    """2^22 copies of one tuple whose queue lies in the u8 bins' range, plus 4099 random
+    tuples: every workgroup piles thousands of in-flight adds onto one u8 bin, which wraps;
+    the add that wraps it raises the poison word, the reduce skips the pass's rows and the
+    recount (from the caller's u32 queue column, or by rehashing for counts only) gives the
+    exact counts -- also when accumulating onto the caller's counts."""
+    n_same, n_rand, H = 1 << 22, 4099, 1 << 30
+    rnd = oracle_lib.generate(33, 0, n_rand)
+    _, q_rnd, _ = oracle_lib.run(example_key, rnd, H, Q)
+    pick = int(np.flatnonzero(q_rnd < 151552)[0])
+    one = rnd[pick:pick + 1]
+    host = np.concatenate([rnd[:2000], np.repeat(one, n_same, axis=0), rnd[2000:]])
+    n = len(host)
+    tup = torch.from_numpy(host.view(np.int32).reshape(-1)).to("cuda:0")
+    want = oracle_lib.run(example_key, rnd, H, Q, want_hash=False, want_queue=False)[2]
+    want[int(q_rnd[pick])] += n_same
+    key = native.prepare_key(example_key)
+    _, q, c = _launch(native, key, tup, n, H, Q, outputs, counts_fill=11,
+                      flags=native.FLAG_ACCUMULATE)
+    np.testing.assert_array_equal(c.cpu().numpy().view(np.uint64), want + np.uint64(11))
+    if outputs:
+        got = q.cpu().numpy().view(np.uint32)
+        assert np.all(got[2000:2000 + n_same] == q_rnd[pick])
+    # the u8 bins alone are wrong here: proof that the poison gate is what kept them out
+    _, _, bad = _with_env("RSS_RANGE8_DEBUG", "nofallback",
+                          lambda: _launch(native, key, tup, n, H, Q, outputs))
+    assert not np.array_equal(bad.cpu().numpy().view(np.uint64), want)
