@@ -784,15 +784,22 @@ __global__ __launch_bounds__(kBlock) void rss_queue_hist_kernel(const T* __restr
 // plain coalesced stores -- not Q atomics per workgroup, which would cost more than the pass
 // at Q = 65536 -- and rss_partial_reduce_kernel sums the rows into the counts.
 constexpr uint32_t kWideSpan = 65536;  // 128 KiB of u16 bins: one workgroup per CU
+constexpr uint32_t kWideSpan8 = 163840;  // u8 bins (kBits = 8): the whole 160 KiB LDS
 constexpr uint32_t kNarrowSpan = 16384;  // rss_queue_hist_kernel: u32 bins, two workgroups per CU
 
-template <typename T>
+// kBits = 8: u8 bins, four per dword, with HIST_RANGE8's guard (0x7F -> a move of 128 into
+// ovf[r]) and poison word (a field that wrapped; the reduce is gated on it and
+// rss_range8_fallback_col_kernel recounts the range) -- 163840 queues per read of the column.
+template <typename T, int kBits = 16>
 __global__ __launch_bounds__(kBlock) void rss_queue_hist_wide_kernel(
         const T* __restrict__ queues, uint64_t n, uint32_t q_lo, uint32_t q_span,
-        uint32_t* __restrict__ partial, uint32_t stride_words, unsigned long long* counts) {
+        uint32_t* __restrict__ partial, uint32_t stride_words, unsigned long long* counts,
+        uint32_t* __restrict__ ovf, uint32_t* __restrict__ poison) {
+    constexpr uint32_t kPerWord = 32 / kBits, kField = (1u << kBits) - 1u;
+    constexpr uint32_t kHalf = 1u << (kBits - 1);  // the guard's move
     extern __shared__ uint32_t bins[];
     const uint32_t tid = threadIdx.x;
-    const uint32_t words = (q_span + 1) / 2;
+    const uint32_t words = (q_span + kPerWord - 1) / kPerWord;
     for (uint32_t e = tid; e < words; e += kBlock) bins[e] = 0;
     __syncthreads();
     const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
@@ -801,20 +808,28 @@ __global__ __launch_bounds__(kBlock) void rss_queue_hist_wide_kernel(
     auto add = [&](uint32_t q) -> uint32_t {
         const uint32_t r = q - q_lo;  // wraps for q < q_lo
         if (r >= q_span) return 0u;
-        const uint32_t sh = (r & 1u) * 16u;
-        return __hip_atomic_fetch_add(&bins[r >> 1], 1u << sh, __ATOMIC_RELAXED,
+        const uint32_t sh = (r % kPerWord) * kBits;
+        return __hip_atomic_fetch_add(&bins[r / kPerWord], 1u << sh, __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_WORKGROUP);
     };
-    // the guard: the add that returned 0x7FFF (its bin now holds >= 0x8000) moves 2^15 out.
-    // Checked after a group's adds are all issued, so they do not wait for each other; the
-    // adds in flight meanwhile are bounded by the workgroup's lanes, far below 2^15.
+    // the guard: the add that returned kHalf - 1 (its bin now holds kHalf) moves kHalf out.
+    // Checked after a group's adds are all issued, so they do not wait for each other.  u16:
+    // the adds in flight meanwhile are bounded by the workgroup's lanes, far below 2^15; u8:
+    // not bounded below 128, so the add that sees 0xFF (a wrap) poisons the pass.
     auto guard = [&](uint32_t q, uint32_t old) {
         const uint32_t r = q - q_lo;
-        const uint32_t sh = (r & 1u) * 16u;
-        if (r < q_span && ((old >> sh) & 0xFFFFu) == 0x7FFFu) {
-            __hip_atomic_fetch_sub(&bins[r >> 1], 0x8000u << sh, __ATOMIC_RELAXED,
+        if (r >= q_span) return;
+        const uint32_t sh = (r % kPerWord) * kBits;
+        const uint32_t f = (old >> sh) & kField;
+        if (f == kHalf - 1u) {
+            __hip_atomic_fetch_sub(&bins[r / kPerWord], kHalf << sh, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_WORKGROUP);
-            atomicAdd(&counts[q], 0x8000ull);
+            if constexpr (kBits == 8)
+                atomicAdd(&ovf[r], 1u);
+            else
+                atomicAdd(&counts[q], (unsigned long long)kHalf);
+        } else if constexpr (kBits == 8) {
+            if (f == kField) __hip_atomic_store(poison, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     };
     constexpr uint32_t kPer = 16 / sizeof(T);  // queues per 16-B load
@@ -920,20 +935,21 @@ __global__ __launch_bounds__(kReduceCols * kReduceGroups) void rss_partial_reduc
 
 // HIST_RANGE8's recount (see range8_guard), launched after every u8 pass: returns at once
 // unless the pass raised its poison word.  Then every workgroup counts the range in slices
-// of kFallbackSpan queues with u32 LDS bins (no guard needed: a bin holds one workgroup's
-// share of the batch) -- from the queue column when the pass wrote one with the queues
-// themselves (u32), else by hashing the tuples again on the byte tables -- and folds each
-// slice with atomics into the counts.  Slow (a pass over the batch per slice), exact, and
-// only ever run on inputs that pile thousands of tuples into one bin at once.
-constexpr uint32_t kFallbackSpan = 36864;  // 144 KiB of u32 bins beside the 12 KiB byte tables
+// with u32 LDS bins (no guard needed: a bin holds one workgroup's share of the batch) and
+// folds each slice with atomics into the counts.  Slow (a pass over the batch per slice),
+// exact, and only ever run on inputs that pile thousands of tuples into one bin at once.
+// Two forms: this one hashes the tuples again on the byte tables (a counts-only hash pass);
+// rss_range8_fallback_col_kernel reads a queue column (a wide pass, or a hash pass whose
+// caller's u32 column holds the queues).
+constexpr uint32_t kFallbackSpan = 36864;     // 144 KiB of u32 bins beside the 12 KiB byte tables
+constexpr uint32_t kFallbackColSpan = 40960;  // 160 KiB of u32 bins
 template <bool kHPow2, int kQMode>
-__global__ __launch_bounds__(kBlock) void rss_range8_fallback_kernel(const LaunchParams p,
-                                                                    const uint32_t* __restrict__ qcol) {
+__global__ __launch_bounds__(kBlock) void rss_range8_fallback_kernel(const LaunchParams p) {
     if (!*p.poison) return;  // uniform across the grid: no wave is left behind
     __shared__ uint32_t lut[kByteLutDwords];
     extern __shared__ uint32_t bins[];
     const uint32_t tid = threadIdx.x;
-    if (!qcol) build_byte_lut(lut, p.window, tid);
+    build_byte_lut(lut, p.window, tid);
     const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
     const uint64_t gstride = (uint64_t)gridDim.x * kBlock;
     for (uint32_t lo = 0; lo < p.q_span; lo += kFallbackSpan) {
@@ -941,20 +957,40 @@ __global__ __launch_bounds__(kBlock) void rss_range8_fallback_kernel(const Launc
         for (uint32_t e = tid; e < span; e += kBlock) bins[e] = 0;
         __syncthreads();
         for (uint64_t i = gtid; i < p.n; i += gstride) {
-            uint32_t q;
-            if (qcol) {
-                q = qcol[i];
-            } else {
-                const uint32_t* src = reinterpret_cast<const uint32_t*>(p.tuples) + 3 * i;
-                q = queue_of<kQMode>(bucket_of<kHPow2>(toeplitz_hash_bytes(lut, src[0], src[1], src[2]), p), p);
-            }
-            const uint32_t r = q - p.q_lo - lo;  // wraps below the slice
-            if (r < span)
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(p.tuples) + 3 * i;
+            const uint32_t h = toeplitz_hash_bytes(lut, src[0], src[1], src[2]);
+            const uint32_t r = queue_of<kQMode>(bucket_of<kHPow2>(h, p), p) - p.q_lo - lo;
+            if (r < span)  // (wraps below the slice)
                 __hip_atomic_fetch_add(&bins[r], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         __syncthreads();
         for (uint32_t e = tid; e < span; e += kBlock)
             if (bins[e]) atomicAdd(&p.counts[p.q_lo + lo + e], (unsigned long long)bins[e]);
+        __syncthreads();
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void rss_range8_fallback_col_kernel(
+        const T* __restrict__ col, uint64_t n, uint32_t q_lo, uint32_t q_span,
+        unsigned long long* counts, const uint32_t* __restrict__ poison) {
+    if (!*poison) return;  // uniform across the grid
+    extern __shared__ uint32_t bins[];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
+    const uint64_t gstride = (uint64_t)gridDim.x * kBlock;
+    for (uint32_t lo = 0; lo < q_span; lo += kFallbackColSpan) {
+        const uint32_t span = min(kFallbackColSpan, q_span - lo);
+        for (uint32_t e = tid; e < span; e += kBlock) bins[e] = 0;
+        __syncthreads();
+        for (uint64_t i = gtid; i < n; i += gstride) {
+            const uint32_t r = (uint32_t)col[i] - q_lo - lo;  // wraps below the slice
+            if (r < span)
+                __hip_atomic_fetch_add(&bins[r], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        __syncthreads();
+        for (uint32_t e = tid; e < span; e += kBlock)
+            if (bins[e]) atomicAdd(&counts[q_lo + lo + e], (unsigned long long)bins[e]);
         __syncthreads();
     }
 }
@@ -2033,6 +2069,68 @@ bool byte_lut_enabled() {
     return !(e && e[0] == '0');
 }
 
+// RSS_RANGE8=0 keeps u16 bins (+ queue-column passes) past 75776 queues (A/B, tests)
+bool range8_enabled() {
+    const char* e = getenv("RSS_RANGE8");
+    return !(e && e[0] == '0');
+}
+
+// Tests only: RSS_RANGE8_DEBUG=force sets the poison word before the pass (the fallback then
+// recounts every launch); =nofallback drops the gate and the fallback (a wrap would then show
+// as wrong counts -- proves a launch's counts came from the u8 bins and their guard moves)
+int range8_debug() {
+    const char* e = getenv("RSS_RANGE8_DEBUG");
+    if (!e) return 0;
+    return strcmp(e, "force") == 0 ? 1 : (strcmp(e, "nofallback") == 0 ? 2 : 0);
+}
+
+// One u8 wide pass over [lo, lo + sp) of a queue column (rss_queue_hist_wide_kernel<T, 8>):
+// a scratch block of the u8 partial matrix, the guard moves and the poison word (zeroed),
+// the pass, the reduce (gated on !poison) and the column recount (gated on poison).  Returns
+// RSS_ENOMEM without launching anything when the block cannot be allocated.
+template <typename T>
+int launch_wide8(const T* qcol, uint64_t n, uint32_t lo, uint32_t sp, unsigned long long* counts,
+                 unsigned grid, int cu_count, hipStream_t stream) {
+    const uint32_t words = (sp + 3) / 4;
+    const size_t rows_bytes = (size_t)grid * words * 4, tail_bytes = ((size_t)sp + 4) * 4;
+    void* buf = nullptr;
+    if (hipMallocAsync(&buf, rows_bytes + tail_bytes, stream) != hipSuccess) {
+        (void)hipGetLastError();
+        return RSS_ENOMEM;
+    }
+    uint32_t* partial = static_cast<uint32_t*>(buf);
+    uint32_t* ovf = reinterpret_cast<uint32_t*>(static_cast<char*>(buf) + rows_bytes);
+    uint32_t* poison = ovf + sp;
+    const int debug = range8_debug();
+    hipError_t e = hipMemsetAsync(ovf, 0, tail_bytes, stream);
+    if (e == hipSuccess && debug == 1) e = hipMemsetD32Async(poison, 1, 1, stream);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL((rss_queue_hist_wide_kernel<T, 8>), dim3(grid), dim3(kBlock), words * 4,
+                           stream, qcol, n, lo, sp, partial, words, counts, ovf, poison);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(rss_partial_reduce_kernel<8>, dim3((words + kReduceCols - 1) / kReduceCols),
+                           dim3(kReduceCols * kReduceGroups), 0, stream,
+                           static_cast<const uint32_t*>(partial), grid, words, lo, sp, counts,
+                           static_cast<const uint32_t*>(ovf),
+                           debug == 2 ? nullptr : static_cast<const uint32_t*>(poison));
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess && debug != 2) {
+        hipLaunchKernelGGL(rss_range8_fallback_col_kernel<T>, dim3(cu_count), dim3(kBlock),
+                           std::min(kFallbackColSpan, sp) * 4, stream, qcol, n, lo, sp, counts,
+                           static_cast<const uint32_t*>(poison));
+        e = hipGetLastError();
+    }
+    int rc = e == hipSuccess ? RSS_OK
+                             : set_error(RSS_EIO, "wide queue histogram launch failed: %s", hipGetErrorString(e));
+    const hipError_t fe = hipFreeAsync(buf, stream);  // stream-ordered after its readers
+    if (fe != hipSuccess && rc == RSS_OK)
+        rc = set_error(RSS_EIO, "hipFreeAsync failed: %s", hipGetErrorString(fe));
+    return rc;
+}
+
 // Queue ranges [span, nqueues) of a many-queues launch, histogrammed from the queue column
 // (u16 or u32) the first pass wrote: one wide pass (u16 LDS bins, rows of a u16 partial
 // matrix, then a reduce) per kWideSpan queues; RSS_WIDE_HIST=0 (or no memory for the
@@ -2051,17 +2149,33 @@ int launch_queue_ranges(const void* qcol, int qw, uint64_t n, uint32_t first, ui
         void* partial = nullptr;
         if (hipMallocAsync(&partial, (size_t)grid * stride_words * 4, stream) == hipSuccess) {
             int rc = RSS_OK;
-            for (uint32_t lo = first; lo < nqueues && rc == RSS_OK; lo += std::min(kWideSpan, nqueues - lo)) {
+            for (uint32_t lo = first; lo < nqueues && rc == RSS_OK;) {
+                // more queues left than one u16 pass holds: a u8 pass (163840 queues, poison-
+                // gated recount) -- 2.5 times the queues per read of the column
+                if (range8_enabled() && nqueues - lo > kWideSpan) {
+                    const uint32_t sp8 = std::min<uint32_t>(kWideSpan8, nqueues - lo);
+                    rc = qw == QW_U16
+                             ? launch_wide8(static_cast<const uint16_t*>(qcol), n, lo, sp8, counts, grid, cu_count, stream)
+                             : launch_wide8(static_cast<const uint32_t*>(qcol), n, lo, sp8, counts, grid, cu_count, stream);
+                    if (rc == RSS_OK) {
+                        lo += sp8;
+                        continue;
+                    }
+                    if (rc != RSS_ENOMEM) break;
+                    rc = RSS_OK;  // no room for its scratch block: the u16 pass below
+                }
                 const uint32_t sp = std::min<uint32_t>(kWideSpan, nqueues - lo);
                 const uint32_t lds = ((sp + 1) / 2) * 4;
                 if (qw == QW_U16)
                     hipLaunchKernelGGL(rss_queue_hist_wide_kernel<uint16_t>, dim3(grid), dim3(kBlock), lds,
                                        stream, static_cast<const uint16_t*>(qcol), n, lo, sp,
-                                       static_cast<uint32_t*>(partial), stride_words, counts);
+                                       static_cast<uint32_t*>(partial), stride_words, counts,
+                                       (uint32_t*)nullptr, (uint32_t*)nullptr);
                 else
                     hipLaunchKernelGGL(rss_queue_hist_wide_kernel<uint32_t>, dim3(grid), dim3(kBlock), lds,
                                        stream, static_cast<const uint32_t*>(qcol), n, lo, sp,
-                                       static_cast<uint32_t*>(partial), stride_words, counts);
+                                       static_cast<uint32_t*>(partial), stride_words, counts,
+                                       (uint32_t*)nullptr, (uint32_t*)nullptr);
                 hipError_t e = hipGetLastError();
                 if (e == hipSuccess) {
                     const uint32_t words = (sp + 1) / 2;
@@ -2075,6 +2189,7 @@ int launch_queue_ranges(const void* qcol, int qw, uint64_t n, uint32_t first, ui
                 }
                 if (e != hipSuccess)
                     rc = set_error(RSS_EIO, "wide queue histogram launch failed: %s", hipGetErrorString(e));
+                lo += sp;
             }
             const hipError_t fe = hipFreeAsync(partial, stream);
             if (fe != hipSuccess && rc == RSS_OK)
@@ -2135,22 +2250,7 @@ int launch_range16(KernelFn fn, unsigned grid, uint32_t shmem, LaunchParams& p, 
     return rc;
 }
 
-// RSS_RANGE8=0 keeps u16 bins (+ queue-column passes) past 75776 queues (A/B, tests)
-bool range8_enabled() {
-    const char* e = getenv("RSS_RANGE8");
-    return !(e && e[0] == '0');
-}
-
-// Tests only: RSS_RANGE8_DEBUG=force sets the poison word before the pass (the fallback then
-// recounts every launch); =nofallback drops the gate and the fallback (a wrap would then show
-// as wrong counts -- proves a launch's counts came from the u8 bins and their guard moves)
-int range8_debug() {
-    const char* e = getenv("RSS_RANGE8_DEBUG");
-    if (!e) return 0;
-    return strcmp(e, "force") == 0 ? 1 : (strcmp(e, "nofallback") == 0 ? 2 : 0);
-}
-
-using FallbackFn = void (*)(const LaunchParams, const uint32_t*);
+using FallbackFn = void (*)(const LaunchParams);
 template <bool kHPow2>
 FallbackFn pick_fallback(int qmode) {
     switch (qmode) {
@@ -2210,8 +2310,13 @@ int launch_range8(KernelFn fn, FallbackFn fallback, unsigned grid, int cu_count,
         e = hipGetLastError();
     }
     if (e == hipSuccess && debug != 2) {
-        hipLaunchKernelGGL(fallback, dim3(cu_count), dim3(kBlock),
-                           std::min(kFallbackSpan, p.q_span) * 4, stream, p, qcol);
+        if (qcol)
+            hipLaunchKernelGGL(rss_range8_fallback_col_kernel<uint32_t>, dim3(cu_count), dim3(kBlock),
+                               std::min(kFallbackColSpan, p.q_span) * 4, stream, qcol, p.n, p.q_lo,
+                               p.q_span, p.counts, static_cast<const uint32_t*>(p.poison));
+        else
+            hipLaunchKernelGGL(fallback, dim3(cu_count), dim3(kBlock),
+                               std::min(kFallbackSpan, p.q_span) * 4, stream, p);
         e = hipGetLastError();
     }
     int rc = e == hipSuccess ? RSS_OK

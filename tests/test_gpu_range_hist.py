@@ -276,12 +276,14 @@ def _with_env(name, value, fn):
             os.environ[name] = old
 
 
-@pytest.mark.parametrize("Q", [75777, 131072, 151552, 151553, 217087, 262144, 10 ** 6])
+@pytest.mark.parametrize("Q", [75777, 131072, 151552, 151553, 217087, 217088, 262144,
+                               151552 + 65536 + 163840 + 1, 10 ** 6])
 def test_range8_u8_bins_equal_oracle(native, oracle_lib, example_key, Q):
     """Past 75776 queues the byte-table pass counts up to 151552 of them in u8 LDS bins
     (HIST_RANGE8: guard at 0x80, moves into a u32 per queue, poison-gated recount); past
     151552 it is the first range of a queue-column launch (counts only: a u16 column of
-    q - 151552 up to Q = 217087, u32 beyond).  On uniform input the u8 path alone
+    q - 151552 up to Q = 217087, u32 beyond), whose passes over the column take 163840
+    queues each in u8 bins while more than 65536 are left (one u16 pass for the rest).  On uniform input the u8 path alone
     (RSS_RANGE8_DEBUG=nofallback: no gate, no recount), the recount alone
     (RSS_RANGE8_DEBUG=force), the default and the u16 path (RSS_RANGE8=0) all give the
     oracle's hashes, queues and counts, with and without per-tuple outputs."""
@@ -328,18 +330,21 @@ def test_range8_guard_moves(native, oracle_lib, example_key, Q):
                 np.testing.assert_array_equal(got, qb)
 
 
-@pytest.mark.parametrize("Q,outputs", [(131072, True), (131072, False), (200000, True),
-                                       (200000, False)])
-def test_range8_poisoned_pass_recounts(native, oracle_lib, example_key, Q, outputs):
-    """2^22 copies of one tuple whose queue lies in the u8 bins' range, plus 4099 random
-    tuples: every workgroup piles thousands of in-flight adds onto one u8 bin, which wraps;
-    the add that wraps it raises the poison word, the reduce skips the pass's rows and the
-    recount (from the caller's u32 queue column, or by rehashing for counts only) gives the
-    exact counts -- also when accumulating onto the caller's counts."""
+@pytest.mark.parametrize("Q,outputs,lo,hi", [(131072, True, 0, 151552), (131072, False, 0, 151552),
+                                             (200000, True, 0, 151552), (200000, False, 0, 151552),
+                                             (400000, True, 151552, 315392),
+                                             (400000, False, 151552, 315392)])
+def test_range8_poisoned_pass_recounts(native, oracle_lib, example_key, Q, outputs, lo, hi):
+    """2^22 copies of one tuple whose queue lies in a u8 range -- the hash pass's [0, 151552),
+    or (Q = 400000) the first u8 wide pass's [151552, 315392) over the queue column -- plus
+    4099 random tuples: every workgroup piles thousands of in-flight adds onto one u8 bin,
+    which wraps; the add that wraps it raises the poison word, the reduce skips the pass's
+    rows and the recount (from the u32 queue column, or by rehashing for a counts-only hash
+    pass) gives the exact counts -- also when accumulating onto the caller's counts."""
     n_same, n_rand, H = 1 << 22, 4099, 1 << 30
     rnd = oracle_lib.generate(33, 0, n_rand)
     _, q_rnd, _ = oracle_lib.run(example_key, rnd, H, Q)
-    pick = int(np.flatnonzero(q_rnd < 151552)[0])
+    pick = int(np.flatnonzero((q_rnd >= lo) & (q_rnd < hi))[0])
     one = rnd[pick:pick + 1]
     host = np.concatenate([rnd[:2000], np.repeat(one, n_same, axis=0), rnd[2000:]])
     n = len(host)
