@@ -145,18 +145,28 @@ def test_default_exchange_is_one_collective_per_batch(monkeypatch):
     assert args.configs3_tuples == 1 << 30
 
 
-def test_committed_bench_lines_carry_the_round3_blocks():
+def test_committed_bench_lines_do_one_exchange_per_batch():
     """The world-size-1 RCCL run (torchrun --nproc-per-node 1) and the 8-rank gloo rehearsal
-    on one GPU (RSS_BENCH_DEVICE=0), as committed under profiles/r03/."""
+    on one GPU (RSS_BENCH_DEVICE=0), as committed under profiles/r04/: the configs[3] and
+    per-rank blocks, ONE all-reduce per batch in the main line (VERDICT r03 item 2:
+    simulator.py:100-116 makes one histogram per batch) and the 8-steps-per-collective form
+    only as the labelled `bucketed` block."""
     import glob
     import os
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    paths = sorted(glob.glob(os.path.join(root, "profiles", "r03", "bench_lines", "*.json")))
-    assert paths, "no committed round-3 bench lines"
+    paths = sorted(glob.glob(os.path.join(root, "profiles", "r04", "bench_lines", "*.json")))
+    assert paths, "no committed round-4 bench lines"
     seen = set()
     for p in paths:
         with open(p) as f:
             line = check_bench_line(json.loads(f.read().strip().splitlines()[-1]))
-        seen.add((line["n_gpus"], "gloo" if "gloo" in line["config"]["parallelism"] else
-                  ("RCCL" if "RCCL" in line["config"]["parallelism"] else "none")))
+        cfg = line["config"]
+        assert cfg["collectives_per_batch"] == 1.0, p
+        assert "one collective per batch" in cfg["parallelism"], p
+        b = line["bucketed"]
+        assert b["steps_per_collective"] == 8 and b["value"] > 0
+        assert b["collectives"] == -(-line["steps"] // 8)
+        assert line["configs3"]["scaling"] == "strong"
+        seen.add((line["n_gpus"], "gloo" if "gloo" in cfg["parallelism"] else
+                  ("RCCL" if "RCCL" in cfg["parallelism"] else "none")))
     assert (1, "RCCL") in seen and (8, "gloo") in seen, seen
