@@ -122,6 +122,7 @@ struct LaunchParams {
     uint32_t bal_off;             // balanced tail: byte offset of its LDS slot (dynamic LDS)
     uint32_t* ovf;                // HIST_RANGE8: u32 [q_span] guard moves (units of 128)
     uint32_t* poison;             // HIST_RANGE8: set when a u8 bin wrapped (results discarded)
+    uint32_t prefetch;            // byte-table passes: next group's loads before this group's LDS work
     uint16_t reta[kRetaMax];      // QM_TABLE: queue of bucket b (ethtool -X indirection)
 };
 
@@ -625,8 +626,7 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
         // 4 consecutive tuples per lane: 48 B = 3 x dwordx4, 16-B aligned.
         const uint4* __restrict__ src = reinterpret_cast<const uint4*>(p.tuples);
         const uint64_t ngroups = p.n >> 2;
-        auto group = [&](uint64_t g) {
-            uint4 a, b, c;
+        auto load = [&](uint64_t g, uint4& a, uint4& b, uint4& c) {
             if constexpr (kOff32) {
                 const char* base = reinterpret_cast<const char*>(p.tuples);
                 const uint32_t off = 48u * (uint32_t)g;
@@ -638,6 +638,8 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
                 b = src[3 * g + 1];
                 c = src[3 * g + 2];
             }
+        };
+        auto body = [&](uint64_t g, const uint4 a, const uint4 b, const uint4 c) {
             const uint32_t h0 = hash_of<kByteLut>(lut, a.x, a.y, a.z, hi);
             const uint32_t h1 = hash_of<kByteLut>(lut, a.w, b.x, b.y, hi);
             const uint32_t h2 = hash_of<kByteLut>(lut, b.z, b.w, c.x, hi);
@@ -685,8 +687,35 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
                 count_queue<kHist>(bins, q3, col, p);
             }
         };
-        walk_rows(group, ngroups, p.tail_rows, ws_tail_counter(p.ws, p.Q),
-                  reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(bins) + p.bal_off));
+        auto group = [&](uint64_t g) {
+            uint4 a, b, c;
+            load(g, a, b, c);
+            body(g, a, b, c);
+        };
+        bool walked = false;
+        if constexpr (kByteLut) {
+            // many-queues passes (LDS-heavy: 12 table reads and a returning atomic per tuple):
+            // the next group's loads are issued before this group's LDS work (p.prefetch)
+            if (p.prefetch && !p.tail_rows) {
+                uint64_t g = gtid;
+                uint4 a, b, c;
+                if (g < ngroups) load(g, a, b, c);
+                while (g < ngroups) {
+                    const uint64_t gn = g + gstride;
+                    uint4 an = a, bn = b, cn = c;
+                    if (gn < ngroups) load(gn, an, bn, cn);
+                    body(g, a, b, c);
+                    a = an;
+                    b = bn;
+                    c = cn;
+                    g = gn;
+                }
+                walked = true;
+            }
+        }
+        if (!walked)
+            walk_rows(group, ngroups, p.tail_rows, ws_tail_counter(p.ws, p.Q),
+                      reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(bins) + p.bal_off));
         tail_begin = ngroups << 2;
     }
     for (uint64_t i = tail_begin + gtid; i < p.n; i += gstride)
@@ -1984,6 +2013,13 @@ bool fold_ticket() {
     return e && strcmp(e, "ticket") == 0;
 }
 
+// RSS_PREFETCH=1: byte-table passes issue the next group's loads before this group's LDS
+// work (A/B; read at every launch)
+bool prefetch_enabled() {
+    const char* e = getenv("RSS_PREFETCH");
+    return e && e[0] == '1';
+}
+
 // RSS_OFF32=0: 64-bit addressing even where 32-bit byte offsets fit (A/B, tests)
 bool off32_enabled() {
     const char* e = getenv("RSS_OFF32");
@@ -2382,6 +2418,7 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
     p.tuples = d_tuples;
     p.hash_out = d_hash;
     p.queue_out = d_queue;
+    p.prefetch = prefetch_enabled();
 
     p.counts = reinterpret_cast<unsigned long long*>(d_counts);
     p.n = n;

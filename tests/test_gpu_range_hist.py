@@ -362,3 +362,23 @@ def test_range8_poisoned_pass_recounts(native, oracle_lib, example_key, Q, outpu
     _, _, bad = _with_env("RSS_RANGE8_DEBUG", "nofallback",
                           lambda: _launch(native, key, tup, n, H, Q, outputs))
     assert not np.array_equal(bad.cpu().numpy().view(np.uint64), want)
+
+
+@pytest.mark.parametrize("Q,outputs", [(131072, True), (131072, False), (400000, False)])
+def test_range8_zipf_flows_equal_oracle(native, oracle_lib, example_key, Q, outputs):
+    """Skewed traffic: 2^22 tuples drawn Zipf(1.3) from 50000 distinct flows, shuffled -- a
+    few flows hold tens of thousands of tuples spread over the batch, most hold a handful.
+    Whether or not some workgroup's u8 bin wraps (the recount then takes the launch), the
+    counts, and the queues, equal the oracle's."""
+    n, H, flows = 1 << 22, 1 << 30, 50000
+    base = oracle_lib.generate(34, 0, flows)
+    rng = np.random.default_rng(34)
+    pick = np.minimum(rng.zipf(1.3, n) - 1, flows - 1)
+    host = np.ascontiguousarray(base[pick])
+    tup = torch.from_numpy(host.view(np.int32).reshape(-1)).to("cuda:0")
+    _, qb, _ = oracle_lib.run(example_key, base, H, Q)
+    want = np.bincount(qb[pick].astype(np.int64), minlength=Q).astype(np.uint64)
+    _, q, c = _launch(native, native.prepare_key(example_key), tup, n, H, Q, outputs)
+    np.testing.assert_array_equal(c.cpu().numpy().view(np.uint64), want)
+    if outputs:
+        np.testing.assert_array_equal(q.cpu().numpy().view(np.uint32), qb[pick])
