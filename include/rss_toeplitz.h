@@ -131,13 +131,14 @@ int rss_key_select_fields(rss_key* key, uint32_t fields);
  * thread's current device.  Any alignment works; 16-byte aligned tuples/hashes
  * (and 4/8/16-byte aligned u8/u16/u32 queues) take the 4-tuples-per-lane path.
  * Counts-only launches with a power-of-two htable <= 256 run a table-free kernel;
- * with more than 8192 queues the counts go to u16 LDS bins of the hash pass itself --
- * up to 16384 queues beside the 12-bit tables, up to 75776 on 12 KiB byte tables (4-tuple
- * body, no indirection table) -- whose per-workgroup rows a reduce launch sums; the queues
- * past that are gathered from the queue column (one wide pass per 65536 queues): d_queue
- * when given, else a stream-ordered scratch column of 2 bytes per tuple (the queue, or for
- * nqueues <= 141311 the queue minus 75776) or 4 (hipMallocAsync / hipFreeAsync on
- * `stream`, like the per-workgroup rows).
+ * with more than 8192 queues the counts go to LDS bins of the hash pass itself -- u16 bins
+ * for up to 16384 queues beside the 12-bit tables and up to 80572 beside the 2.6 KiB
+ * small tables (4-tuple body, no indirection table), u8 bins for up to 161144 (a bin that
+ * wraps poisons the pass and a gated recount replaces its counts) -- whose per-workgroup
+ * rows a reduce launch sums; the queues past that are gathered from the queue column (one
+ * wide pass per 163840 queues in u8 bins, 65536 in u16): d_queue when given, else a
+ * stream-ordered scratch column of 2 bytes per tuple (for nqueues <= 226679 the queue minus
+ * 161144) or 4 (hipMallocAsync / hipFreeAsync on `stream`, like the per-workgroup rows).
  */
 int rss_hash_device(const rss_key* key, const rss_tuple4* d_tuples, size_t n,
                     uint32_t htable, uint32_t nqueues, uint32_t* d_hash,

@@ -80,9 +80,9 @@ enum QueueMode { QM_MASK = 0, QM_FAST16 = 1, QM_FAST32 = 2, QM_TABLE = 3, QM_FAS
 constexpr uint32_t kRetaMax = 1024;  // indirection-table entries carried in the kernarg
 enum HistMode { HIST_PRIVATE = 0, HIST_SHARED = 1, HIST_GLOBAL = 2, HIST_NONE = 3, HIST_RANGE = 4,
                 HIST_RANGE16 = 5, HIST_RANGE8 = 6 };
-// HIST_RANGE8 (IPv4 byte-table kernel, past the u16 bins' reach): u8 bins, four per dword, a
-// guard at 0x80 and a poison word for a bin that wraps (range8_guard) -- 151552 queues in the
-// LDS beside the byte tables, one pass.
+// HIST_RANGE8 (IPv4 small-table kernel, past the u16 bins' reach): u8 bins, four per dword, a
+// guard at 0x80 and a poison word for a bin that wraps (range8_guard) -- 161144 queues in the
+// LDS beside the small tables, one pass.
 // HIST_RANGE16 (IPv4 kernel): HIST_RANGE with u16 bins, two per dword, twice the queues in the
 // same LDS -- with the wide pass's guard bit (rss_queue_hist_wide_kernel): the add that
 // returns 0x7FFF moves 2^15 of its bin into the global counts.
@@ -122,7 +122,8 @@ struct LaunchParams {
     uint32_t bal_off;             // balanced tail: byte offset of its LDS slot (dynamic LDS)
     uint32_t* ovf;                // HIST_RANGE8: u32 [q_span] guard moves (units of 128)
     uint32_t* poison;             // HIST_RANGE8: set when a u8 bin wrapped (results discarded)
-    uint32_t prefetch;            // byte-table passes: next group's loads before this group's LDS work
+    uint32_t prefetch;            // small-table passes: next group's loads before this group's LDS work
+    unsigned long long* tail_ctr; // balanced tail's unit counter when the launch has no ws (HIST_RANGE8)
     uint16_t reta[kRetaMax];      // QM_TABLE: queue of bucket b (ethtool -X indirection)
 };
 
@@ -219,48 +220,74 @@ __device__ __forceinline__ uint32_t toeplitz_hash(const uint32_t* __restrict__ l
                 lut_term<6>(base, w0, w1, w2, hi) ^ lut_term<7>(base, w0, w1, w2, hi));
 }
 
-// Byte tables (many-queues launches, DESIGN.md §3 "Many queues"): twelve tables of 256
-// entries, table 4k + j indexed by byte j of word k (LSB first, as above) -- 12 KiB instead
-// of 128, so the LDS left for u16 histogram bins grows from 16384 to ~75000 queues, for 12
-// ds_read_b32 per tuple instead of 8.  Entry (t, v) lives at LDS byte t*1024 + v*4.
-constexpr int kByteTables = RSS_INPUT_BITS / 8;                 // 12
-constexpr uint32_t kByteLutDwords = kByteTables * 256;          // 3072
-constexpr uint32_t kByteLutBytes = kByteLutDwords * 4;          // 12 KiB
-__host__ __device__ constexpr int byte_slice_bit(int t, int b) {  // word t/4, bit 8 (t%4) + b
-    return 32 * (t / 4) + 31 - 8 * (t % 4) - b;
+// Small tables (many-queues launches, DESIGN.md §3 "Many queues"): 21 tables of at most 32
+// entries -- word k (w0, w1, w2) cut LSB first into fields of 5, 5, 5, 5, 5, 5 and 2 bits,
+// table 7k + j indexed by field j -- 2688 bytes instead of the 12-bit tables' 128 KiB, so the
+// LDS left for histogram bins grows from 16384 u16 queues to 80572 u16 / 161144 u8 queues.
+// Each table starts on a 128-byte (32-bank) boundary and has at most 32 entries, so entry v
+// is alone on bank v: lanes that hit one bank read one address and broadcast -- a random
+// index can never conflict.  21 conflict-free ds_read_b32 (2 LDS cycles each) per tuple
+// replace 8 random 12-bit reads (2 + ~4.5 conflict cycles each on uniform input) or 12
+// random byte-table reads (the round-3 form, ~7 cycles each).  Entry (t, v) lives at LDS
+// byte t*128 + v*4.
+constexpr int kSmallFields = 7;                                  // per 32-bit word
+constexpr int kSmallTables = 3 * kSmallFields;                   // 21
+constexpr uint32_t kSmallLutDwords = kSmallTables * 32;          // 672
+constexpr uint32_t kSmallLutBytes = kSmallLutDwords * 4;         // 2688
+constexpr uint32_t kSmallStaticBytes = kSmallLutBytes + 8;      // + the balanced tail's LDS slot
+__host__ __device__ constexpr int small_width(int j) { return j < 6 ? 5 : 2; }
+// input bit (toeplitz.py:65-68 order) of bit b of table t's index: word t/7, bit 5 (t%7) + b
+__host__ __device__ constexpr int small_slice_bit(int t, int b) {
+    return 32 * (t / kSmallFields) + 31 - 5 * (t % kSmallFields) - b;
 }
 
-__device__ __forceinline__ void build_byte_lut(uint32_t* lut, const uint32_t* __restrict__ window,
-                                               uint32_t tid) {
-    for (uint32_t e = tid; e < kByteLutDwords; e += kBlock) {
-        const int t = (int)(e >> 8);
-        uint32_t v = 0;
+__device__ __forceinline__ void build_small_lut(uint32_t* lut, const uint32_t* __restrict__ window,
+                                                uint32_t tid) {
+    for (uint32_t e = tid; e < kSmallLutDwords; e += kBlock) {
+        const int t = (int)(e >> 5);
+        const uint32_t v = e & 31u;
+        const int width = small_width(t % kSmallFields);
+        uint32_t x = 0;
 #pragma unroll
-        for (int b = 0; b < 8; ++b) v ^= ((e >> b) & 1u) ? window[byte_slice_bit(t, b)] : 0u;
-        lut[e] = v;
+        for (int b = 0; b < 5; ++b)
+            x ^= (b < width && ((v >> b) & 1u)) ? window[small_slice_bit(t, b)] : 0u;
+        lut[e] = (v >> width) ? 0u : x;  // entries past a 2-bit table's 4 are never read
     }
 }
 
+// table 7k + j's term for word w (= word k): the field moved to byte offset 4 * field
 template <int kT>
-__device__ __forceinline__ uint32_t byte_term(const char* lut, uint32_t w) {
-    constexpr int j = kT & 3;
-    const uint32_t off = j == 0 ? (w << 2) & 0x3FCu : (w >> (8 * j - 2)) & 0x3FCu;
-    return *reinterpret_cast<const uint32_t*>(lut + kT * 1024 + off);
+__device__ __forceinline__ uint32_t small_term(const char* lut, uint32_t w) {
+    constexpr int j = kT % kSmallFields, o = 5 * j;
+    uint32_t off;
+    if constexpr (j == 0)
+        off = (w << 2) & 0x7Cu;
+    else if constexpr (j == 6)
+        off = (w >> 28) & 0x0Cu;
+    else
+        off = (w >> (o - 2)) & 0x7Cu;
+    return *reinterpret_cast<const uint32_t*>(lut + kT * 128 + off);
 }
 
-__device__ __forceinline__ uint32_t toeplitz_hash_bytes(const uint32_t* __restrict__ lut, uint32_t w0,
+template <int kBase>
+__device__ __forceinline__ uint32_t small_word(const char* lut, uint32_t w) {  // 7 terms
+    return xor3(xor3(small_term<kBase + 0>(lut, w), small_term<kBase + 1>(lut, w),
+                     small_term<kBase + 2>(lut, w)),
+                xor3(small_term<kBase + 3>(lut, w), small_term<kBase + 4>(lut, w),
+                     small_term<kBase + 5>(lut, w)),
+                small_term<kBase + 6>(lut, w));
+}
+
+__device__ __forceinline__ uint32_t toeplitz_hash_small(const uint32_t* __restrict__ lut, uint32_t w0,
                                                         uint32_t w1, uint32_t w2) {
     const char* b = reinterpret_cast<const char*>(lut);
-    return xor3(xor3(xor3(byte_term<0>(b, w0), byte_term<1>(b, w0), byte_term<2>(b, w0)),
-                     xor3(byte_term<3>(b, w0), byte_term<4>(b, w1), byte_term<5>(b, w1)),
-                     xor3(byte_term<6>(b, w1), byte_term<7>(b, w1), byte_term<8>(b, w2))),
-                byte_term<9>(b, w2), byte_term<10>(b, w2) ^ byte_term<11>(b, w2));
+    return xor3(small_word<0>(b, w0), small_word<7>(b, w1), small_word<14>(b, w2));
 }
 
-template <bool kByteLut>
+template <bool kSmallLut>
 __device__ __forceinline__ uint32_t hash_of(const uint32_t* lut, uint32_t w0, uint32_t w1,
                                             uint32_t w2, uint32_t hi) {
-    if constexpr (kByteLut) return toeplitz_hash_bytes(lut, w0, w1, w2);
+    if constexpr (kSmallLut) return toeplitz_hash_small(lut, w0, w1, w2);
     return toeplitz_hash(lut, w0, w1, w2, hi);
 }
 
@@ -576,12 +603,12 @@ inline uint32_t balanced_tail_rows(uint64_t ngroups, unsigned grid) {
     return rows >= 16 ? (uint32_t)std::max<uint64_t>(1, rows / 10) : 0u;
 }
 
-template <bool kHPow2, int kQMode, int kHist, int kQWidth, bool kByteLut>
+template <bool kHPow2, int kQMode, int kHist, int kQWidth, bool kSmallLut>
 __device__ __forceinline__ void one_tuple(const uint32_t* lut, uint32_t* bins, uint64_t i,
                                           uint32_t col, uint32_t hi, const uint32_t* reta_lds,
                                           const LaunchParams& p) {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(p.tuples) + 3 * i;
-    const uint32_t h = hash_of<kByteLut>(lut, src[0], src[1], src[2], hi);
+    const uint32_t h = hash_of<kSmallLut>(lut, src[0], src[1], src[2], hi);
     const uint32_t q = queue_lookup<kQMode>(bucket_of<kHPow2>(h, p), p, reta_lds);
     if (p.hash_out) stream_store(p.hash_out + i, h);
     if (p.queue_out) store_queue1<kStoreWidth<kQWidth>>(p.queue_out, i, column_queue<kQWidth>(q, p));
@@ -591,17 +618,19 @@ __device__ __forceinline__ void one_tuple(const uint32_t* lut, uint32_t* bins, u
 // kOff32 (with kVec4): every byte offset of the launch's streams fits 32 bits (12 n < 2^32,
 // e.g. 2^28 tuples), so the loads and stores address the kernel-argument base pointers with
 // a 32-bit per-lane offset (global_load ... v_off, s[base]) instead of 64-bit address pairs.
-// kByteLut: the 12 KiB byte tables instead of the 128 KiB 12-bit ones (many-queues
+// kSmallLut: the 2.6 KiB conflict-free small tables instead of the 128 KiB 12-bit ones (many-queues
 // HIST_RANGE16 launches: the rest of the LDS holds up to ~75000 u16 bins).
 template <bool kHPow2, int kQMode, int kHist, int kQWidth, bool kVec4, bool kOff32 = false,
-          bool kByteLut = false>
+          bool kSmallLut = false>
 __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams p) {
-    __shared__ uint32_t lut[kByteLut ? kByteLutDwords : kLutDwords];  // static: table offsets fold into ds_read
+    // static: table offsets fold into ds_read; the small tables keep two more dwords for the
+    // balanced tail's LDS slot (their launches' bins fill the rest of the LDS)
+    __shared__ __attribute__((aligned(16))) uint32_t lut[kSmallLut ? kSmallLutDwords + 2 : kLutDwords];
     extern __shared__ uint32_t bins[];    // histogram bins, sized at launch
     const uint32_t tid = threadIdx.x;
 
-    if constexpr (kByteLut)
-        build_byte_lut(lut, p.window, tid);
+    if constexpr (kSmallLut)
+        build_small_lut(lut, p.window, tid);
     else
         build_lut(lut, p.window, tid);
     const uint32_t nbins = kHist == HIST_PRIVATE   ? p.Q * kBinCols
@@ -640,10 +669,10 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
             }
         };
         auto body = [&](uint64_t g, const uint4 a, const uint4 b, const uint4 c) {
-            const uint32_t h0 = hash_of<kByteLut>(lut, a.x, a.y, a.z, hi);
-            const uint32_t h1 = hash_of<kByteLut>(lut, a.w, b.x, b.y, hi);
-            const uint32_t h2 = hash_of<kByteLut>(lut, b.z, b.w, c.x, hi);
-            const uint32_t h3 = hash_of<kByteLut>(lut, c.y, c.z, c.w, hi);
+            const uint32_t h0 = hash_of<kSmallLut>(lut, a.x, a.y, a.z, hi);
+            const uint32_t h1 = hash_of<kSmallLut>(lut, a.w, b.x, b.y, hi);
+            const uint32_t h2 = hash_of<kSmallLut>(lut, b.z, b.w, c.x, hi);
+            const uint32_t h3 = hash_of<kSmallLut>(lut, c.y, c.z, c.w, hi);
             const uint32_t q0 = queue_lookup<kQMode>(bucket_of<kHPow2>(h0, p), p, reta_lds);
             const uint32_t q1 = queue_lookup<kQMode>(bucket_of<kHPow2>(h1, p), p, reta_lds);
             const uint32_t q2 = queue_lookup<kQMode>(bucket_of<kHPow2>(h2, p), p, reta_lds);
@@ -693,7 +722,7 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
             body(g, a, b, c);
         };
         bool walked = false;
-        if constexpr (kByteLut) {
+        if constexpr (kSmallLut) {
             // many-queues passes (LDS-heavy: 12 table reads and a returning atomic per tuple):
             // the next group's loads are issued before this group's LDS work (p.prefetch)
             if (p.prefetch && !p.tail_rows) {
@@ -714,12 +743,14 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
             }
         }
         if (!walked)
-            walk_rows(group, ngroups, p.tail_rows, ws_tail_counter(p.ws, p.Q),
-                      reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(bins) + p.bal_off));
+            walk_rows(group, ngroups, p.tail_rows,
+                      p.tail_ctr ? p.tail_ctr : ws_tail_counter(p.ws, p.Q),
+                      kSmallLut ? reinterpret_cast<unsigned long long*>(lut + kSmallLutDwords)
+                                : reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(bins) + p.bal_off));
         tail_begin = ngroups << 2;
     }
     for (uint64_t i = tail_begin + gtid; i < p.n; i += gstride)
-        one_tuple<kHPow2, kQMode, kHist, kQWidth, kByteLut>(lut, bins, i, col, hi, reta_lds, p);
+        one_tuple<kHPow2, kQMode, kHist, kQWidth, kSmallLut>(lut, bins, i, col, hi, reta_lds, p);
 
     // Epilogue: fold this workgroup's bins into the global uint64 counts.
     if constexpr (kHist == HIST_PRIVATE || kHist == HIST_SHARED) {
@@ -967,18 +998,18 @@ __global__ __launch_bounds__(kReduceCols * kReduceGroups) void rss_partial_reduc
 // with u32 LDS bins (no guard needed: a bin holds one workgroup's share of the batch) and
 // folds each slice with atomics into the counts.  Slow (a pass over the batch per slice),
 // exact, and only ever run on inputs that pile thousands of tuples into one bin at once.
-// Two forms: this one hashes the tuples again on the byte tables (a counts-only hash pass);
+// Two forms: this one hashes the tuples again on the small tables (a counts-only hash pass);
 // rss_range8_fallback_col_kernel reads a queue column (a wide pass, or a hash pass whose
 // caller's u32 column holds the queues).
-constexpr uint32_t kFallbackSpan = 36864;     // 144 KiB of u32 bins beside the 12 KiB byte tables
+constexpr uint32_t kFallbackSpan = 40192;     // 157 KiB of u32 bins beside the small tables
 constexpr uint32_t kFallbackColSpan = 40960;  // 160 KiB of u32 bins
 template <bool kHPow2, int kQMode>
 __global__ __launch_bounds__(kBlock) void rss_range8_fallback_kernel(const LaunchParams p) {
     if (!*p.poison) return;  // uniform across the grid: no wave is left behind
-    __shared__ uint32_t lut[kByteLutDwords];
+    __shared__ uint32_t lut[kSmallLutDwords];
     extern __shared__ uint32_t bins[];
     const uint32_t tid = threadIdx.x;
-    build_byte_lut(lut, p.window, tid);
+    build_small_lut(lut, p.window, tid);
     const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
     const uint64_t gstride = (uint64_t)gridDim.x * kBlock;
     for (uint32_t lo = 0; lo < p.q_span; lo += kFallbackSpan) {
@@ -987,7 +1018,7 @@ __global__ __launch_bounds__(kBlock) void rss_range8_fallback_kernel(const Launc
         __syncthreads();
         for (uint64_t i = gtid; i < p.n; i += gstride) {
             const uint32_t* src = reinterpret_cast<const uint32_t*>(p.tuples) + 3 * i;
-            const uint32_t h = toeplitz_hash_bytes(lut, src[0], src[1], src[2]);
+            const uint32_t h = toeplitz_hash_small(lut, src[0], src[1], src[2]);
             const uint32_t r = queue_of<kQMode>(bucket_of<kHPow2>(h, p), p) - p.q_lo - lo;
             if (r < span)  // (wraps below the slice)
                 __hip_atomic_fetch_add(&bins[r], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1147,84 +1178,73 @@ __global__ __launch_bounds__(kBlock, 2) void rss_counts_perm_kernel(const PermPa
 }
 
 // Key search: per-queue counts of the same tuples under many
-// keys.  A table index depends only on the tuple, so one table can serve two keys:
-// entry v holds (key A's XOR of windows, key B's) as 8 bytes and ONE ds_read_b64 --
-// 64 banks, 256 B/clk (twice ds_read_b32's rate) -- fetches both keys' terms.  Nine
-// tables of 2048 / 1024 entries (11 / 10 input bits, field LSBs first as in the hash
-// kernel's partition):
-//   t0 w0[10:0]  t1 w0[21:11]  t2 w1[10:0]  t3 w2[15:11] | w2[31:27] << 5  t4 w0[31:22]
-//   t5 w1[21:11] t6 w2[10:0]   t7 w2[26:16] t8 w1[31:22]
-// = 6 x 16 + 3 x 8 KiB = 120 KiB.  Per tuple: 20 VALU of addresses and 9 LDS reads shared
-// by the pair, then XOR / modulo / histogram per key.  blockIdx.y selects the pair; each
-// workgroup histograms its grid-stride share of the tuples into counts rows 2y, 2y+1.
-// With the tuples resident in the 256 MiB Infinity Cache the re-reads stay on die.
-constexpr uint32_t kPairLutBytes = 6 * 16384 + 3 * 8192;   // 122880
-constexpr uint32_t kPairBinBytesMax = kLdsBytes - kPairLutBytes;  // 40 KiB for 2 x Q bins
+// keys.  A table index depends only on the tuple, so one table can serve two keys: entry
+// v holds (key A's XOR of windows, key B's) as 8 bytes and ONE ds_read_b64 -- 64 banks,
+// 256 B/clk (twice ds_read_b32's rate) -- fetches both keys' terms.  The tables are the
+// small tables' 21 fields (5, 5, 5, 5, 5, 5, 2 bits of each word, LSB first; kSmallLut) with
+// 8-byte entries: 32 entries x 8 B = 256 B cover the 64 banks exactly once, so every entry
+// sits on its own bank pair and a random index never conflicts -- 21 conflict-free reads
+// (2 LDS cycles each) per tuple where the round-1..3 tables (nine of 11 / 10 input bits,
+// 120 KiB) took 9 random reads at ~7 cycles each (PMC: 44 of the 80 LDS cycles per 64
+// tuples x 8 keys were bank conflicts, profiles/r04/pmc_keysearch/).  5.25 KiB of tables
+// also leave ~155 KiB of the LDS to the bins.  blockIdx.y selects the pair; each workgroup
+// histograms its grid-stride share of the tuples into counts rows 2y, 2y+1.  With the
+// tuples resident in the 256 MiB Infinity Cache the re-reads stay on die.
+constexpr uint32_t kPairLutBytes = kSmallTables * 256;            // 5376
+constexpr uint32_t kPairBinBytesMax = kLdsBytes - kPairLutBytes;  // 154.75 KiB for the bins
 
-__host__ __device__ constexpr int pair_width(int t) {
-    return (t == 3 || t == 4 || t == 8) ? 10 : 11;
-}
-__host__ __device__ constexpr uint32_t pair_table(int t) {  // byte offset
-    return t == 0 ? 0u : t == 1 ? 16384u : t == 2 ? 32768u : t == 3 ? 49152u : t == 4 ? 57344u
-         : t == 5 ? 65536u : t == 6 ? 81920u : t == 7 ? 98304u : 114688u;
-}
-// input bit (0 = MSB of the source ip) feeding bit b of table t's index
-__host__ __device__ constexpr int pair_bit(int t, int b) {
-    return t == 0 ? 31 - b : t == 1 ? 20 - b : t == 2 ? 63 - b
-         : t == 3 ? (b < 5 ? 84 - b : 73 - b)
-         : t == 4 ? 9 - b : t == 5 ? 52 - b : t == 6 ? 95 - b : t == 7 ? 79 - b : 41 - b;
-}
-
-template <int kT>
-__device__ __forceinline__ void build_pair_table(uint2* lut, const uint32_t* __restrict__ wa,
-                                                 const uint32_t* __restrict__ wb, uint32_t tid) {
-    uint32_t a = 0, b = 0;
+// entry e = 32 t + v of the 21 pair tables: (XOR of key A's windows, of key B's) over the
+// input bits set in v; `win(i)` gives the two keys' window i as a uint2
+template <typename Win>
+__device__ __forceinline__ void build_small_pair_lut(uint2* lut, Win win, uint32_t tid) {
+    for (uint32_t e = tid; e < kSmallLutDwords; e += kBlock) {
+        const int t = (int)(e >> 5);
+        const uint32_t v = e & 31u;
+        const int width = small_width(t % kSmallFields);
+        uint32_t a = 0, b = 0;
 #pragma unroll
-    for (int j = 0; j < 10; ++j) {
-        const bool set = (tid >> j) & 1u;
-        a ^= set ? wa[pair_bit(kT, j)] : 0u;
-        b ^= set ? wb[pair_bit(kT, j)] : 0u;
+        for (int j = 0; j < 5; ++j) {
+            if (j < width && ((v >> j) & 1u)) {
+                const uint2 w = win(small_slice_bit(t, j));
+                a ^= w.x;
+                b ^= w.y;
+            }
+        }
+        lut[e] = (v >> width) ? make_uint2(0u, 0u) : make_uint2(a, b);
     }
-    uint2* dst = lut + pair_table(kT) / 8;
-    dst[tid] = make_uint2(a, b);
-    if constexpr (pair_width(kT) == 11)
-        dst[tid + 1024] = make_uint2(a ^ wa[pair_bit(kT, 10)], b ^ wb[pair_bit(kT, 10)]);
 }
 
-// byte address of table t's entry: 2 VALU (4 for the two-field t3); tables 5..8 take
-// their 64 KiB base from the opaque register `hi`
+// table 7k + j's 8-byte term for word w (= word k): the field moved to byte offset 8 * field
 template <int kT>
-__device__ __forceinline__ uint32_t pair_offset(uint32_t w0, uint32_t w1, uint32_t w2,
-                                                uint32_t hi) {
-    if constexpr (kT == 0) return (w0 << 3) & 0x3FF8u;
-    if constexpr (kT == 1) return (w0 >> 8) & 0x3FF8u;
-    if constexpr (kT == 2) return (w1 << 3) & 0x3FF8u;
-    if constexpr (kT == 3) return ((w2 >> 8) & 0xF8u) | ((w2 >> 19) & 0x1F00u);
-    if constexpr (kT == 4) return (w0 >> 19) & 0x1FF8u;
-    if constexpr (kT == 5) return ((w1 >> 8) & 0x3FF8u) | hi;
-    if constexpr (kT == 6) return ((w2 << 3) & 0x3FF8u) | hi;
-    if constexpr (kT == 7) return ((w2 >> 13) & 0x3FF8u) | hi;
-    return ((w1 >> 19) & 0x1FF8u) | hi;
+__device__ __forceinline__ uint2 small_pair_term(const char* lut, uint32_t w) {
+    constexpr int j = kT % kSmallFields, o = 5 * j;
+    uint32_t off;
+    if constexpr (j == 0)
+        off = (w << 3) & 0xF8u;
+    else if constexpr (j == 6)
+        off = (w >> 27) & 0x18u;
+    else
+        off = (w >> (o - 3)) & 0xF8u;
+    return *reinterpret_cast<const uint2*>(lut + kT * 256 + off);
 }
 
-template <int kT>
-__device__ __forceinline__ uint2 pair_term(const char* lut, uint32_t w0, uint32_t w1, uint32_t w2,
-                                           uint32_t hi) {
-    constexpr uint32_t kImm = pair_table(kT) & 0xFFFFu;
-    return *reinterpret_cast<const uint2*>(lut + kImm + pair_offset<kT>(w0, w1, w2, hi));
+template <int kBase>
+__device__ __forceinline__ uint2 small_pair_word(const char* lut, uint32_t w) {  // 7 terms
+    const uint2 t0 = small_pair_term<kBase + 0>(lut, w), t1 = small_pair_term<kBase + 1>(lut, w);
+    const uint2 t2 = small_pair_term<kBase + 2>(lut, w), t3 = small_pair_term<kBase + 3>(lut, w);
+    const uint2 t4 = small_pair_term<kBase + 4>(lut, w), t5 = small_pair_term<kBase + 5>(lut, w);
+    const uint2 t6 = small_pair_term<kBase + 6>(lut, w);
+    return make_uint2(xor3(xor3(t0.x, t1.x, t2.x), xor3(t3.x, t4.x, t5.x), t6.x),
+                      xor3(xor3(t0.y, t1.y, t2.y), xor3(t3.y, t4.y, t5.y), t6.y));
 }
 
-// (hash under key A, hash under key B) of one tuple
+// (hash under key A, hash under key B) of one tuple (packed kernel: 8 / 4 keys' low bits)
 __device__ __forceinline__ uint2 toeplitz_hash_pair(const uint2* __restrict__ lut, uint32_t w0,
-                                                    uint32_t w1, uint32_t w2, uint32_t hi) {
+                                                    uint32_t w1, uint32_t w2) {
     const char* base = reinterpret_cast<const char*>(lut);
-    const uint2 t0 = pair_term<0>(base, w0, w1, w2, hi), t1 = pair_term<1>(base, w0, w1, w2, hi);
-    const uint2 t2 = pair_term<2>(base, w0, w1, w2, hi), t3 = pair_term<3>(base, w0, w1, w2, hi);
-    const uint2 t4 = pair_term<4>(base, w0, w1, w2, hi), t5 = pair_term<5>(base, w0, w1, w2, hi);
-    const uint2 t6 = pair_term<6>(base, w0, w1, w2, hi), t7 = pair_term<7>(base, w0, w1, w2, hi);
-    const uint2 t8 = pair_term<8>(base, w0, w1, w2, hi);
-    return make_uint2(xor3(xor3(t0.x, t1.x, t2.x), xor3(t3.x, t4.x, t5.x), xor3(t6.x, t7.x, t8.x)),
-                      xor3(xor3(t0.y, t1.y, t2.y), xor3(t3.y, t4.y, t5.y), xor3(t6.y, t7.y, t8.y)));
+    const uint2 a = small_pair_word<0>(base, w0), b = small_pair_word<7>(base, w1);
+    const uint2 c = small_pair_word<14>(base, w2);
+    return make_uint2(xor3(a.x, b.x, c.x), xor3(a.y, b.y, c.y));
 }
 
 template <bool kHPow2, int kQMode, int kHist>
@@ -1261,15 +1281,7 @@ __global__ __launch_bounds__(kBlock) void rss_key_search_kernel(const LaunchPara
     const uint32_t key_b = has_b ? key_a + 1 : key_a;
     const uint32_t* wa = p.key_windows + (size_t)RSS_INPUT_BITS * key_a;
     const uint32_t* wb = p.key_windows + (size_t)RSS_INPUT_BITS * key_b;
-    build_pair_table<0>(lut, wa, wb, tid);
-    build_pair_table<1>(lut, wa, wb, tid);
-    build_pair_table<2>(lut, wa, wb, tid);
-    build_pair_table<3>(lut, wa, wb, tid);
-    build_pair_table<4>(lut, wa, wb, tid);
-    build_pair_table<5>(lut, wa, wb, tid);
-    build_pair_table<6>(lut, wa, wb, tid);
-    build_pair_table<7>(lut, wa, wb, tid);
-    build_pair_table<8>(lut, wa, wb, tid);
+    build_small_pair_lut(lut, [&](int i) { return make_uint2(wa[i], wb[i]); }, tid);
     const uint32_t per_key =
         kHist == HIST_PRIVATE ? p.Q * kBinCols : (kHist == HIST_SHARED ? p.Q : 0u);
     for (uint32_t e = tid; e < 2 * per_key; e += kBlock) bins[e] = 0;
@@ -1281,8 +1293,6 @@ __global__ __launch_bounds__(kBlock) void rss_key_search_kernel(const LaunchPara
     uint32_t* bins_a = bins;
     uint32_t* bins_b = bins + per_key;
     const uint32_t col = tid & (kBinCols - 1);
-    uint32_t hi = 65536u;
-    asm volatile("" : "+v"(hi));
     const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
     const uint64_t gstride = (uint64_t)gridDim.x * kBlock;
     uint64_t tail_begin = 0;
@@ -1293,16 +1303,16 @@ __global__ __launch_bounds__(kBlock) void rss_key_search_kernel(const LaunchPara
             const uint4 a = src[3 * g + 0];
             const uint4 b = src[3 * g + 1];
             const uint4 c = src[3 * g + 2];
-            count_pair<kHPow2, kQMode, kHist>(bins_a, bins_b, toeplitz_hash_pair(lut, a.x, a.y, a.z, hi), col, qa, qb);
-            count_pair<kHPow2, kQMode, kHist>(bins_a, bins_b, toeplitz_hash_pair(lut, a.w, b.x, b.y, hi), col, qa, qb);
-            count_pair<kHPow2, kQMode, kHist>(bins_a, bins_b, toeplitz_hash_pair(lut, b.z, b.w, c.x, hi), col, qa, qb);
-            count_pair<kHPow2, kQMode, kHist>(bins_a, bins_b, toeplitz_hash_pair(lut, c.y, c.z, c.w, hi), col, qa, qb);
+            count_pair<kHPow2, kQMode, kHist>(bins_a, bins_b, toeplitz_hash_pair(lut, a.x, a.y, a.z), col, qa, qb);
+            count_pair<kHPow2, kQMode, kHist>(bins_a, bins_b, toeplitz_hash_pair(lut, a.w, b.x, b.y), col, qa, qb);
+            count_pair<kHPow2, kQMode, kHist>(bins_a, bins_b, toeplitz_hash_pair(lut, b.z, b.w, c.x), col, qa, qb);
+            count_pair<kHPow2, kQMode, kHist>(bins_a, bins_b, toeplitz_hash_pair(lut, c.y, c.z, c.w), col, qa, qb);
         }
         tail_begin = ngroups << 2;
     }
     for (uint64_t i = tail_begin + gtid; i < p.n; i += gstride) {
         const uint32_t* t = reinterpret_cast<const uint32_t*>(p.tuples) + 3 * i;
-        count_pair<kHPow2, kQMode, kHist>(bins_a, bins_b, toeplitz_hash_pair(lut, t[0], t[1], t[2], hi), col, qa, qb);
+        count_pair<kHPow2, kQMode, kHist>(bins_a, bins_b, toeplitz_hash_pair(lut, t[0], t[1], t[2]), col, qa, qb);
     }
     if constexpr (kHist == HIST_PRIVATE || kHist == HIST_SHARED) {
         __syncthreads();
@@ -1315,30 +1325,12 @@ __global__ __launch_bounds__(kBlock) void rss_key_search_kernel(const LaunchPara
 // `hash % htable`) is the low log2(H) bits of the hash, and the low bits of a XOR are
 // the XOR of the low bits: a table term needs only those bits of each key.  With
 // H <= 256 an 8-byte entry holds the low BYTE of 8 keys' terms (H <= 65536: the low
-// half-word of 4 keys'), so the same nine ds_read_b64 of the pair kernel serve 8 (4)
-// keys and the per-key work is a bit-field extract, the queue step and one LDS add.
+// half-word of 4 keys'), so the same 21 conflict-free ds_read_b64 of the pair kernel
+// serve 8 (4) keys and the per-key work is a bit-field extract, the queue step and one
+// LDS add.
 // Bins are [q][key][lane column]: the key's offset is a ds_add immediate and every
 // half-wave's adds stay conflict-free.
 constexpr uint32_t kPackedPrepBytes = RSS_INPUT_BITS * 8;  // packed windows, before the bins
-
-// table t entry v (and v + 1024) of the packed kernel: XOR of the packed windows
-template <int kT>
-__device__ __forceinline__ void build_packed_table(uint2* lut, const uint2* packed, uint32_t tid) {
-    uint32_t a = 0, b = 0;
-#pragma unroll
-    for (int j = 0; j < 10; ++j) {
-        const bool set = (tid >> j) & 1u;
-        const uint2 w = packed[pair_bit(kT, j)];
-        a ^= set ? w.x : 0u;
-        b ^= set ? w.y : 0u;
-    }
-    uint2* dst = lut + pair_table(kT) / 8;
-    dst[tid] = make_uint2(a, b);
-    if constexpr (pair_width(kT) == 11) {
-        const uint2 w = packed[pair_bit(kT, 10)];
-        dst[tid + 1024] = make_uint2(a ^ w.x, b ^ w.y);
-    }
-}
 
 template <int kLaneBits, int kQMode, bool kVec4>
 __global__ __launch_bounds__(kBlock) void rss_key_search_packed_kernel(const LaunchParams p) {
@@ -1365,15 +1357,7 @@ __global__ __launch_bounds__(kBlock) void rss_key_search_packed_kernel(const Lau
         packed[tid] = make_uint2(lo, hi);
     }
     __syncthreads();
-    build_packed_table<0>(lut, packed, tid);
-    build_packed_table<1>(lut, packed, tid);
-    build_packed_table<2>(lut, packed, tid);
-    build_packed_table<3>(lut, packed, tid);
-    build_packed_table<4>(lut, packed, tid);
-    build_packed_table<5>(lut, packed, tid);
-    build_packed_table<6>(lut, packed, tid);
-    build_packed_table<7>(lut, packed, tid);
-    build_packed_table<8>(lut, packed, tid);
+    build_small_pair_lut(lut, [&](int i) { return packed[i]; }, tid);
     __syncthreads();  // packed windows are dead: the region becomes bins
     const uint32_t nbins = p.Q * kKeys * kBinCols;
     for (uint32_t e = tid; e < nbins; e += kBlock) bins[e] = 0;
@@ -1387,8 +1371,6 @@ __global__ __launch_bounds__(kBlock) void rss_key_search_packed_kernel(const Lau
     // (b << kRowShift) - d * (Q << kRowShift), d = floor(b / Q) (as QM_FAST8): two
     // full-rate 24-bit multiplies, the second a v_mad_i32_i24
     const int neg_q_row = -(int)(p.Q << kRowShift);
-    uint32_t hi = 65536u;
-    asm volatile("" : "+v"(hi));
     // byte lanes: mask every lane to the bucket bits at once, then each key's bucket is
     // a plain byte select (which the multiplies and shifts take as an SDWA operand)
     const uint32_t lane_mask4 = (p.H - 1) * 0x01010101u;
@@ -1423,16 +1405,16 @@ __global__ __launch_bounds__(kBlock) void rss_key_search_packed_kernel(const Lau
             const uint4 a = src[3 * g + 0];
             const uint4 b = src[3 * g + 1];
             const uint4 c = src[3 * g + 2];
-            count(toeplitz_hash_pair(lut, a.x, a.y, a.z, hi));
-            count(toeplitz_hash_pair(lut, a.w, b.x, b.y, hi));
-            count(toeplitz_hash_pair(lut, b.z, b.w, c.x, hi));
-            count(toeplitz_hash_pair(lut, c.y, c.z, c.w, hi));
+            count(toeplitz_hash_pair(lut, a.x, a.y, a.z));
+            count(toeplitz_hash_pair(lut, a.w, b.x, b.y));
+            count(toeplitz_hash_pair(lut, b.z, b.w, c.x));
+            count(toeplitz_hash_pair(lut, c.y, c.z, c.w));
         }
         tail_begin = ngroups << 2;
     }
     for (uint64_t i = tail_begin + gtid; i < p.n; i += gstride) {
         const uint32_t* t = reinterpret_cast<const uint32_t*>(p.tuples) + 3 * i;
-        count(toeplitz_hash_pair(lut, t[0], t[1], t[2], hi));
+        count(toeplitz_hash_pair(lut, t[0], t[1], t[2]));
     }
     __syncthreads();
     for (uint32_t e = tid; e < p.Q * kKeys; e += kBlock) {
@@ -1746,20 +1728,20 @@ using KernelFn = void (*)(const LaunchParams);
 
 // vec4: 0 = one tuple per lane, 1 = four per lane, 2 = four per lane with 32-bit byte offsets
 // (kOff32; instantiated for the single-pass histogram modes only, the bench's step), 3 = four
-// per lane on the byte tables (kByteLut; HIST_RANGE16 only)
-enum VecMode { VM_SCALAR = 0, VM_VEC4 = 1, VM_OFF32 = 2, VM_BYTE_LUT = 3 };
+// per lane on the small tables (kSmallLut; HIST_RANGE16 / HIST_RANGE8 only)
+enum VecMode { VM_SCALAR = 0, VM_VEC4 = 1, VM_OFF32 = 2, VM_SMALL_LUT = 3 };
 template <bool kHPow2, int kQMode, int kHist, int kQWidth>
 KernelFn pick_vec(int vec4) {
-    if constexpr (kHist == HIST_RANGE8) {  // byte tables, u32 / u16-residual columns only
+    if constexpr (kHist == HIST_RANGE8) {  // small tables, u32 / u16-residual columns only
         if constexpr ((kQWidth == QW_U32 || kQWidth == QW_U16R) && kQMode != QM_FAST8 &&
                       kQMode != QM_TABLE)
-            if (vec4 == VM_BYTE_LUT)
+            if (vec4 == VM_SMALL_LUT)
                 return rss_toeplitz_kernel<kHPow2, kQMode, kHist, kQWidth, true, false, true>;
         return nullptr;
     }
-    if constexpr (kQWidth == QW_U16R) {  // the byte-table HIST_RANGE16 body only
+    if constexpr (kQWidth == QW_U16R) {  // the small-table HIST_RANGE16 / RANGE8 bodies only
         if constexpr (kHist == HIST_RANGE16 && kQMode != QM_FAST8 && kQMode != QM_TABLE)
-            if (vec4 == VM_BYTE_LUT)
+            if (vec4 == VM_SMALL_LUT)
                 return rss_toeplitz_kernel<kHPow2, kQMode, kHist, kQWidth, true, false, true>;
         return nullptr;
     }
@@ -1767,11 +1749,11 @@ KernelFn pick_vec(int vec4) {
         if (vec4 == VM_OFF32) return rss_toeplitz_kernel<kHPow2, kQMode, kHist, kQWidth, true, true>;
     if constexpr (kHist == HIST_RANGE16 && kQWidth != QW_U8 && kQMode != QM_FAST8 &&
                   kQMode != QM_TABLE)  // (H <= 1024 with those: never this many queues)
-        if (vec4 == VM_BYTE_LUT)
+        if (vec4 == VM_SMALL_LUT)
             return rss_toeplitz_kernel<kHPow2, kQMode, kHist, kQWidth, true, false, true>;
-    // a byte-table request with no byte-table instance must not fall back to the 12-bit
-    // tables: the launcher sized the dynamic LDS for the byte-table span
-    if (vec4 == VM_BYTE_LUT) return nullptr;
+    // a small-table request with no small-table instance must not fall back to the 12-bit
+    // tables: the launcher sized the dynamic LDS for the small-table span
+    if (vec4 == VM_SMALL_LUT) return nullptr;
     return vec4 ? rss_toeplitz_kernel<kHPow2, kQMode, kHist, kQWidth, true>
                 : rss_toeplitz_kernel<kHPow2, kQMode, kHist, kQWidth, false>;
 }
@@ -1947,7 +1929,7 @@ int launch_search(const uint32_t* d_windows, size_t nkeys, const rss_tuple4* d_t
     int rc = device_info(&info);
     if (rc) return rc;
     // packed buckets (8 keys per table entry for H <= 256, 4 for H <= 65536) whenever
-    // their private bins fit (8 keys: Q <= 40, 4 keys: Q <= 80); else pairs of full hashes
+    // their private bins fit (8 keys: Q <= 154, 4 keys: Q <= 309); else pairs of full hashes
     const bool bytes_fit = (uint64_t)q_eff * 8 * kBinCols * 4 <= kPairBinBytesMax;
     const int lane_bits = htable <= 256u && bytes_fit ? 8 : 16;
     const uint32_t keys_per_wg = 64 / lane_bits;
@@ -2013,7 +1995,7 @@ bool fold_ticket() {
     return e && strcmp(e, "ticket") == 0;
 }
 
-// RSS_PREFETCH=1: byte-table passes issue the next group's loads before this group's LDS
+// RSS_PREFETCH=1: small-table passes issue the next group's loads before this group's LDS
 // work (A/B; read at every launch)
 bool prefetch_enabled() {
     const char* e = getenv("RSS_PREFETCH");
@@ -2099,13 +2081,13 @@ bool ranged_histogram_ok(uint32_t q_eff, uint32_t span, uint32_t qbytes) {
     return ((uint64_t)q_eff + span - 1) / span <= (qbytes == 2 ? 64u : 32u);
 }
 
-// The byte tables for a many-queues launch (kByteLut); RSS_BYTE_LUT=0 keeps the 12-bit tables.
-bool byte_lut_enabled() {
-    const char* e = getenv("RSS_BYTE_LUT");
+// The small tables for a many-queues launch (kSmallLut); RSS_SMALL_LUT=0 keeps the 12-bit tables.
+bool small_lut_enabled() {
+    const char* e = getenv("RSS_SMALL_LUT");
     return !(e && e[0] == '0');
 }
 
-// RSS_RANGE8=0 keeps u16 bins (+ queue-column passes) past 75776 queues (A/B, tests)
+// RSS_RANGE8=0 keeps u16 bins (+ queue-column passes) past 80572 queues (A/B, tests)
 bool range8_enabled() {
     const char* e = getenv("RSS_RANGE8");
     return !(e && e[0] == '0');
@@ -2300,8 +2282,12 @@ FallbackFn pick_fallback(int qmode) {
 // A HIST_RANGE8 hash launch's scratch block: the u8 partial matrix (a row per workgroup),
 // the guard moves (u32 per queue) and the poison word.  NULL when it cannot be allocated (the
 // caller then keeps the u16 path).
-size_t range8_rows_bytes(unsigned grid, uint32_t q_span) { return (size_t)grid * ((q_span + 3) / 4) * 4; }
-size_t range8_tail_bytes(uint32_t q_span) { return ((size_t)q_span + 4) * 4; }  // ovf + poison + pad
+// layout: the rows (rounded to 16 B) | ovf[q_span] | poison | pad | the balanced tail's counter
+size_t range8_rows_bytes(unsigned grid, uint32_t q_span) {
+    return ((size_t)grid * ((q_span + 3) / 4) * 4 + 15) & ~(size_t)15;
+}
+size_t range8_ctr_offset(uint32_t q_span) { return (((size_t)q_span + 1) * 4 + 7) & ~(size_t)7; }
+size_t range8_tail_bytes(uint32_t q_span) { return range8_ctr_offset(q_span) + 8; }
 void* alloc_range8(unsigned grid, uint32_t q_span, hipStream_t stream) {
     void* buf = nullptr;
     if (hipMallocAsync(&buf, range8_rows_bytes(grid, q_span) + range8_tail_bytes(q_span), stream) !=
@@ -2330,6 +2316,14 @@ int launch_range8(KernelFn fn, FallbackFn fallback, unsigned grid, int cu_count,
     p.partial_stride = words;
     p.ovf = tail;
     p.poison = tail + p.q_span;
+    // balanced tail (walk_rows): its unit counter in the zeroed block, its LDS slot past the
+    // small tables; the last tenth of the rows goes out per workgroup slot
+    const uint32_t tail_rows = balanced_tail_rows(p.n / 4, grid);
+    if (tail_rows && balance_enabled()) {
+        p.tail_rows = tail_rows;
+        p.tail_ctr = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(tail) +
+                                                           range8_ctr_offset(p.q_span));
+    }
     const int debug = range8_debug();
     hipError_t e = hipMemsetAsync(tail, 0, tail_bytes, stream);
     if (e == hipSuccess && debug == 1) e = hipMemsetD32Async(p.poison, 1, 1, stream);
@@ -2362,6 +2356,8 @@ int launch_range8(KernelFn fn, FallbackFn fallback, unsigned grid, int cu_count,
         rc = set_error(RSS_EIO, "hipFreeAsync failed: %s", hipGetErrorString(fe));
     p.partial = nullptr;
     p.ovf = p.poison = nullptr;
+    p.tail_ctr = nullptr;
+    p.tail_rows = 0;
     return rc;
 }
 
@@ -2457,15 +2453,15 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
     const unsigned grid = (unsigned)(want < cap ? want : cap);
     if (hist == HIST_GLOBAL && d_counts) {
         // u16 bins with the guard bit (HIST_RANGE16): twice the queues of u32 bins in the LDS
-        // the tables leave -- 16384 beside the 12-bit tables, and past that, on the byte
-        // tables (4-tuple body, no indirection table), up to 75776 in the hash pass itself; no
-        // queue column for those.  (Up to 16384 the 12-bit tables' 8 lookups are faster: 0.595
-        // vs 0.68 ms counts only, profiles/r03/many_queues/config_sweep_many_e2.jsonl.)
+        // the tables leave -- 16384 beside the 12-bit tables, and past that, on the small
+        // tables (4-tuple body, no indirection table), up to 80576 in the hash pass itself; no
+        // queue column for those.  Up to 16384 the 12-bit tables stay: 8 lookups and 3 VALU
+        // per lookup fewer than the small tables' 21 when the bins fit beside them.
         const uint32_t span12 = ((kBinBytesMax - reta_bytes) / 4) * 2;
-        const bool byte_lut = q_eff > span12 && vec4 && !reta && qwidth != QW_U8 && byte_lut_enabled();
-        const uint32_t lut_bytes = byte_lut ? kByteLutBytes : kLutBytes;
+        const bool small_lut = q_eff > span12 && vec4 && !reta && qwidth != QW_U8 && small_lut_enabled();
+        const uint32_t lut_bytes = small_lut ? kSmallStaticBytes : kLutBytes;
         const uint32_t span = ((kLdsBytes - lut_bytes - reta_bytes) / 4) * 2;
-        const int vm = byte_lut ? VM_BYTE_LUT : (vec4 ? VM_VEC4 : VM_SCALAR);
+        const int vm = small_lut ? VM_SMALL_LUT : (vec4 ? VM_VEC4 : VM_SCALAR);
         const uint32_t qbytes = q_eff <= 65536u ? 2 : 4;
         if (q_eff <= span) {
             p.q_lo = 0;
@@ -2475,18 +2471,18 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
             return launch_range16(fn, grid, ((q_eff + 1) / 2) * 4 + reta_bytes, p, stream);
         }
         // Past the u16 bins' reach: u8 bins (HIST_RANGE8, a guard at 0x80 and a poison-gated
-        // recount, range8_guard) hold span8 = 151552 queues beside the byte tables -- one pass
+        // recount, range8_guard) hold span8 = 161144 queues beside the small tables -- one pass
         // up to there, and the first range of a queue-column launch beyond.
-        const uint32_t span8 = kLdsBytes - kByteLutBytes;
+        const uint32_t span8 = kLdsBytes - kSmallStaticBytes;
         FallbackFn fb8 = h_pow2 ? pick_fallback<true>(qmode) : pick_fallback<false>(qmode);
         void* r8buf = nullptr;  // the u8 pass's scratch block, when it runs
-        if (byte_lut && range8_enabled() && fb8)
+        if (small_lut && range8_enabled() && fb8)
             r8buf = alloc_range8(grid, std::min(q_eff, span8), stream);
         if (r8buf && q_eff <= span8) {
             p.q_lo = 0;
             p.q_span = q_eff;
-            KernelFn fn = h_pow2 ? pick_queue<true>(qmode, HIST_RANGE8, qwidth, VM_BYTE_LUT)
-                                 : pick_queue<false>(qmode, HIST_RANGE8, qwidth, VM_BYTE_LUT);
+            KernelFn fn = h_pow2 ? pick_queue<true>(qmode, HIST_RANGE8, qwidth, VM_SMALL_LUT)
+                                 : pick_queue<false>(qmode, HIST_RANGE8, qwidth, VM_SMALL_LUT);
             // the caller's u32 column holds the queues (exact even when the bins are poisoned)
             const uint32_t* col = d_queue ? static_cast<const uint32_t*>(d_queue) : nullptr;
             return launch_range8(fn, fb8, grid, info.cu_count, p, col, r8buf, stream);
@@ -2495,10 +2491,10 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
             void* qcol = d_queue;
             int qw = qwidth;
             bool scratch = false, ranged = true;
-            // counts only past the byte tables' range: a u16 column of q - span (QW_U16R) when
+            // counts only past the small tables' range: a u16 column of q - span (QW_U16R) when
             // the rest of the queues fit 16 bits, else the queues themselves
             const uint32_t first_span = r8buf ? span8 : span;
-            const bool resid = !d_queue && byte_lut && q_eff - first_span <= 0xFFFFu;
+            const bool resid = !d_queue && small_lut && q_eff - first_span <= 0xFFFFu;
             const uint32_t sbytes = resid ? 2 : qbytes;
             if (!qcol || qwidth == QW_U8) {  // (u8 queues always fit the bins: q_eff <= 256)
                 if (hipMallocAsync(&qcol, (size_t)n * sbytes, stream) == hipSuccess) {
@@ -2513,17 +2509,17 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
                 p.queue_out = qcol;
                 p.q_lo = 0;
                 const bool v4 = vec4 && ((uintptr_t)qcol % (qw == QW_U32 ? 16 : 8)) == 0;
-                // the first range: the bins the first pass's tables leave (byte tables: 4-tuple
+                // the first range: the bins the first pass's tables leave (small tables: 4-tuple
                 // body only; the caller's queue buffer may not be aligned for it)
-                const bool b1 = byte_lut && v4 && qw != QW_U8;
-                const bool r8 = b1 && r8buf;  // (a caller's u32 column: b1 == byte_lut)
+                const bool b1 = small_lut && v4 && qw != QW_U8;
+                const bool r8 = b1 && r8buf;  // (a caller's u32 column: b1 == small_lut)
                 if (!r8 && r8buf) {
                     (void)hipFreeAsync(r8buf, stream);
                     r8buf = nullptr;
                 }
                 const uint32_t span1 = b1 ? (r8 ? span8 : span) : span12;
                 p.q_span = span1;  // < q_eff here
-                const int vm1 = b1 ? VM_BYTE_LUT : (v4 ? VM_VEC4 : VM_SCALAR);
+                const int vm1 = b1 ? VM_SMALL_LUT : (v4 ? VM_VEC4 : VM_SCALAR);
                 const int hist1 = r8 ? HIST_RANGE8 : HIST_RANGE16;
                 KernelFn fn = h_pow2 ? pick_queue<true>(qmode, hist1, qw, vm1)
                                      : pick_queue<false>(qmode, hist1, qw, vm1);

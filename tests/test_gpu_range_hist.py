@@ -13,6 +13,10 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
+# queues counted in the hash pass beside the 2688-byte small tables: u16 bins / u8 bins; u8
+# bins per wide pass over the queue column
+SPAN16, SPAN8, WIDE8 = 80572, 161144, 163840
+
 
 @pytest.fixture(scope="module")
 def native():
@@ -156,12 +160,13 @@ def test_wide_equals_narrow_passes(native, oracle_lib, example_key, H, Q):
             os.environ.pop("RSS_WIDE_HIST", None)
 
 
-@pytest.mark.parametrize("Q,lo,hi", [(160000, 75776, 160000), (100000, 16384, 75776),
+@pytest.mark.parametrize("Q,lo,hi", [(170000, SPAN8, 170000), (60000, 16384, 60000),
                                      (40000, 0, 16384), (12000, 8192, 12000)])
 def test_wide_guard_bit_on_one_hot_queue(native, oracle_lib, example_key, Q, lo, hi):
     """2^25 identical tuples plus 4099 random ones, the identical tuples' queue in [lo, hi):
-    every workgroup counts ~2^17 adds into one u16 bin -- of the wide pass (q >= 75776) or of
-    the hash pass's own u16 range (HIST_RANGE16 on the byte tables, q < 75776; Q = 12000 is a
+    every workgroup counts ~2^17 adds into one u16 bin -- of the u16 wide pass after the u8
+    hash pass (q >= 161144) or of the hash pass's own u16 range (HIST_RANGE16 on the small
+    tables, Q <= 80572; Q = 12000 is a
     single pass) -- so the guard bit moves 2^15 out of it again and again; the counts stay
     exact."""
     n_same, n_rand = 1 << 25, 4099
@@ -186,15 +191,16 @@ def test_wide_guard_bit_on_one_hot_queue(native, oracle_lib, example_key, Q, lo,
     assert int(got[int(q1[0])]) >= n_same
 
 
-@pytest.mark.parametrize("H,Q", [(1 << 20, 16385), (0xFFFFFFFF, 65536), (1 << 30, 75776),
-                                 (1 << 30, 75777), (1 << 30, 131072), (1 << 30, 141311),
-                                 (1 << 30, 141312), (99991, 50000), (65536, 20000),
+@pytest.mark.parametrize("H,Q", [(1 << 20, 16385), (0xFFFFFFFF, 65536), (1 << 30, SPAN16),
+                                 (1 << 30, SPAN16 + 1), (1 << 30, 131072), (1 << 30, SPAN8 + 65535),
+                                 (1 << 30, SPAN8 + 65536), (99991, 50000), (65536, 20000),
                                  (60001, 30011)])
 def test_byte_tables_equal_12bit_tables(native, oracle_lib, example_key, H, Q):
-    """Many-queues launches hash on the 12 KiB byte tables (kByteLut: up to 75776 queues in
-    the hash pass's u16 bins); RSS_BYTE_LUT=0 keeps the 12-bit tables (16384 queues, then the
-    queue column).  Counts only past 75776 queues: the scratch column holds q - 75776 as u16
-    up to Q = 141311 (QW_U16R), the queues themselves (u32) from 141312 on.  Both give the oracle's hashes, queues and counts on uniform and flow-like
+    """Many-queues launches hash on the 21 conflict-free 5-bit small tables (kSmallLut: up to
+    80572 queues in the hash pass's u16 bins, 161144 in u8 bins); RSS_SMALL_LUT=0 keeps the
+    12-bit tables (16384 queues, then the queue column).  Counts only past 161144 queues: the
+    scratch column holds q - 161144 as u16 up to Q = 226679 (QW_U16R), the queues themselves
+    (u32) from 226680 on.  Both give the oracle's hashes, queues and counts on uniform and flow-like
     input (one address pair, sequential ports), with outputs and counts only."""
     import os
     n = (1 << 21) + 5
@@ -210,7 +216,7 @@ def test_byte_tables_equal_12bit_tables(native, oracle_lib, example_key, H, Q):
         tup = torch.from_numpy(host.view(np.int32).reshape(-1)).to(dev)
         ho, qo, co = oracle_lib.run(example_key, host, H, Q)
         for lut in ("1", "0"):
-            os.environ["RSS_BYTE_LUT"] = lut
+            os.environ["RSS_SMALL_LUT"] = lut
             try:
                 h = torch.empty(n, dtype=torch.int32, device=dev)
                 q = torch.empty(n, dtype=torch.int16 if u16 else torch.int32, device=dev)
@@ -221,7 +227,7 @@ def test_byte_tables_equal_12bit_tables(native, oracle_lib, example_key, H, Q):
                 native.hash_device(key, tup.data_ptr(), n, H, Q, None, None, c2.data_ptr(), 0, s)
                 torch.cuda.synchronize()
             finally:
-                os.environ.pop("RSS_BYTE_LUT", None)
+                os.environ.pop("RSS_SMALL_LUT", None)
             np.testing.assert_array_equal(h.cpu().numpy().view(np.uint32), ho)
             qv = q.cpu().numpy().view(np.uint16 if u16 else np.uint32).astype(np.uint32)
             np.testing.assert_array_equal(qv, qo)
@@ -232,7 +238,7 @@ def test_byte_tables_equal_12bit_tables(native, oracle_lib, example_key, H, Q):
 def test_byte_tables_accumulate_and_queue_column_offsets(native, oracle_lib, example_key):
     """Byte-table launches accumulate (RSS_FLAG_ACCUMULATE); a caller queue column 4 B off
     the 16-B alignment of four u32 queues makes the first pass fall back to the 12-bit tables
-    and the one-tuple-per-lane body; a 16-B aligned one keeps the byte tables -- same counts."""
+    and the one-tuple-per-lane body; a 16-B aligned one keeps the small tables -- same counts."""
     n, H, Q = (1 << 20) + 3, 1 << 26, 90000
     host = oracle_lib.generate(30, 0, n)
     tup = torch.from_numpy(host.view(np.int32).reshape(-1)).to("cuda:0")
@@ -276,13 +282,13 @@ def _with_env(name, value, fn):
             os.environ[name] = old
 
 
-@pytest.mark.parametrize("Q", [75777, 131072, 151552, 151553, 217087, 217088, 262144,
-                               151552 + 65536 + 163840 + 1, 10 ** 6])
+@pytest.mark.parametrize("Q", [SPAN16 + 1, 131072, SPAN8, SPAN8 + 1, SPAN8 + 65535, SPAN8 + 65536,
+                               262144, SPAN8 + 65536 + WIDE8 + 1, 10 ** 6])
 def test_range8_u8_bins_equal_oracle(native, oracle_lib, example_key, Q):
-    """Past 75776 queues the byte-table pass counts up to 151552 of them in u8 LDS bins
+    """Past 80572 queues the small-table pass counts up to 161144 of them in u8 LDS bins
     (HIST_RANGE8: guard at 0x80, moves into a u32 per queue, poison-gated recount); past
-    151552 it is the first range of a queue-column launch (counts only: a u16 column of
-    q - 151552 up to Q = 217087, u32 beyond), whose passes over the column take 163840
+    161144 it is the first range of a queue-column launch (counts only: a u16 column of
+    q - 161144 up to Q = 226679, u32 beyond), whose passes over the column take 163840
     queues each in u8 bins while more than 65536 are left (one u16 pass for the rest).  On uniform input the u8 path alone
     (RSS_RANGE8_DEBUG=nofallback: no gate, no recount), the recount alone
     (RSS_RANGE8_DEBUG=force), the default and the u16 path (RSS_RANGE8=0) all give the
@@ -330,13 +336,13 @@ def test_range8_guard_moves(native, oracle_lib, example_key, Q):
                 np.testing.assert_array_equal(got, qb)
 
 
-@pytest.mark.parametrize("Q,outputs,lo,hi", [(131072, True, 0, 151552), (131072, False, 0, 151552),
-                                             (200000, True, 0, 151552), (200000, False, 0, 151552),
-                                             (400000, True, 151552, 315392),
-                                             (400000, False, 151552, 315392)])
+@pytest.mark.parametrize("Q,outputs,lo,hi", [(131072, True, 0, SPAN8), (131072, False, 0, SPAN8),
+                                             (200000, True, 0, SPAN8), (200000, False, 0, SPAN8),
+                                             (400000, True, SPAN8, SPAN8 + WIDE8),
+                                             (400000, False, SPAN8, SPAN8 + WIDE8)])
 def test_range8_poisoned_pass_recounts(native, oracle_lib, example_key, Q, outputs, lo, hi):
-    """2^22 copies of one tuple whose queue lies in a u8 range -- the hash pass's [0, 151552),
-    or (Q = 400000) the first u8 wide pass's [151552, 315392) over the queue column -- plus
+    """2^22 copies of one tuple whose queue lies in a u8 range -- the hash pass's [0, 161144),
+    or (Q = 400000) the first u8 wide pass's [161144, 324984) over the queue column -- plus
     4099 random tuples: every workgroup piles thousands of in-flight adds onto one u8 bin,
     which wraps; the add that wraps it raises the poison word, the reduce skips the pass's
     rows and the recount (from the u32 queue column, or by rehashing for a counts-only hash

@@ -3,8 +3,8 @@ output (hash u32 + the narrowest queue width) and counts only, 2^28 tuples, medi
 launches after 5 warm ones, against the same buffers' 12 R + 5 W / 12 R + 6 W / 12 R + 8 W
 byte counts.  Count vectors are min(H, Q) long (``_native.queue_modulus``): rows with Q >= H
 run the Q <= H kernel.  For Q > 8192 the round-2 narrow range passes (RSS_WIDE_HIST=0) are
-timed beside the wide pass; the 12-bit tables (RSS_BYTE_LUT=0: 16384 queues in the
-hash pass) beside the byte tables (up to 75776) for Q > 8192.  ``many`` as the argument: the Q > 8192 rows
+timed beside the wide pass; the 12-bit tables (RSS_SMALL_LUT=0: 16384 queues in the
+hash pass) beside the small tables (up to 80572 in u16 bins, 161144 in u8) for Q > 8192.  ``many`` as the argument: the Q > 8192 rows
 only.  Prints one JSON line per configuration."""
 import json
 import os
@@ -49,7 +49,7 @@ ROWS = [(128, 24), (128, 16), (512, 64), (100, 7), (1000, 24), (65536, 24),
         (128, 129), (128, 20000), (128, 300000), (128, 4 * 10 ** 9),
         (65536, 4096), (1 << 20, 1000), (1 << 20, 8193), (1 << 20, 16384), (1 << 20, 20000),
         (1 << 20, 40000),
-        (4294967295, 65536), (1 << 30, 75776), (1 << 30, 131072), (1 << 30, 131073),
+        (4294967295, 65536), (1 << 30, 80572), (1 << 30, 131072), (1 << 30, 131073),
         (1 << 30, 262144)]
 many = sys.argv[1:] == ["many"]
 for H, Q in ROWS:
@@ -69,8 +69,8 @@ for H, Q in ROWS:
         rec["narrow_counts_ms"] = timed(H, Q, False, 0)
         os.environ.pop("RSS_WIDE_HIST", None)
     if qn > 8192:  # the 12-bit tables: 16384 queues in the hash pass, the rest from the column
-        os.environ["RSS_BYTE_LUT"] = "0"
+        os.environ["RSS_SMALL_LUT"] = "0"
         rec["tables12_full_ms"] = timed(H, Q, True, fl)
         rec["tables12_counts_ms"] = timed(H, Q, False, 0)
-        os.environ.pop("RSS_BYTE_LUT", None)
+        os.environ.pop("RSS_SMALL_LUT", None)
     print(json.dumps(rec), flush=True)

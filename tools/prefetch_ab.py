@@ -1,5 +1,6 @@
-"""Same-buffer A/B of the byte-table passes' load prefetch (RSS_PREFETCH=1: the next group's
-three 16-B loads issued before this group's LDS work) against the plain walk (tool, not
+"""Same-buffer A/B/C of the small-table passes' walk: static grid-stride (RSS_BALANCE=0), the
+same with a load prefetch (RSS_PREFETCH=1: the next group's three 16-B loads issued before
+this group's LDS work) and the balanced tail (the default; HIST_RANGE8 launches) (tool, not
 product): 2^28 uniform tuples, H = 2^30, full outputs (hash u32 + queue u32) and counts only,
 three alternating rounds, medians of 10 launches after 5 warm ones.  One JSON line per Q.
 
@@ -26,8 +27,13 @@ h = torch.empty(n, dtype=torch.int32, device=dev)
 q = torch.empty(n, dtype=torch.int32, device=dev)
 
 
-def timed(Q, outputs, prefetch, reps=10, warm=5):
-    os.environ["RSS_PREFETCH"] = prefetch
+VARIANTS = {"static": {"RSS_BALANCE": "0", "RSS_PREFETCH": "0"},
+            "prefetch": {"RSS_BALANCE": "0", "RSS_PREFETCH": "1"},
+            "tail": {"RSS_BALANCE": "1", "RSS_PREFETCH": "0"}}
+
+
+def timed(Q, outputs, variant, reps=10, warm=5):
+    os.environ.update(VARIANTS[variant])
     c = torch.zeros(Q, dtype=torch.int64, device=dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(reps)]
@@ -44,14 +50,15 @@ def timed(Q, outputs, prefetch, reps=10, warm=5):
     return x[len(x) // 2]
 
 
-for Q in [int(x) for x in sys.argv[1:]] or [20000, 65536, 131072, 151552]:
+for Q in [int(x) for x in sys.argv[1:]] or [20000, 65536, 131072, 161144]:
     rec = {"Q": Q, "tuples": n}
     for rnd in range(3):
-        for pf in ("0", "1"):
+        for v in VARIANTS:
             for outputs in (True, False):
-                k = "pf%s_%s_ms" % (pf, "full" if outputs else "counts")
-                rec.setdefault(k, []).append(round(timed(Q, outputs, pf), 4))
+                k = "%s_%s_ms" % (v, "full" if outputs else "counts")
+                rec.setdefault(k, []).append(round(timed(Q, outputs, v), 4))
     os.environ.pop("RSS_PREFETCH", None)
+    os.environ.pop("RSS_BALANCE", None)
     for k in [k for k in rec if k.endswith("_ms")]:
         rec[k + "_best"] = min(rec[k])
     print(json.dumps(rec), flush=True)

@@ -52,7 +52,7 @@ def timed(Q, outputs, env, reps=10, warm=5):
             os.environ.pop(k, None)
 
 
-qs = [int(x) for x in sys.argv[1:]] or [65536, 75777, 100000, 131072, 151552, 200000, 262144,
+qs = [int(x) for x in sys.argv[1:]] or [65536, 80577, 100000, 131072, 161144, 200000, 262144,
                                         1000000]
 # the bench's step shape on the same input for scale: H=128, Q=24, u8 queues, counts
 c24 = torch.zeros(24, dtype=torch.int64, device=dev)
