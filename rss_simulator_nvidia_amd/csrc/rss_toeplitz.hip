@@ -1995,11 +1995,14 @@ bool fold_ticket() {
     return e && strcmp(e, "ticket") == 0;
 }
 
-// RSS_PREFETCH=1: small-table passes issue the next group's loads before this group's LDS
-// work (A/B; read at every launch)
-bool prefetch_enabled() {
+// Small-table passes without per-tuple outputs (counts only, no scratch column) issue the
+// next group's loads before this group's LDS work: 0.62 vs 0.66 ms at Q = 65536 / 131072,
+// where with outputs it cost 1-2 % and the balanced tail gains 4 % instead
+// (profiles/r04/small_tables/prefetch_ab.jsonl).  RSS_PREFETCH=0/1 forces it (A/B).
+bool prefetch_for(bool has_outputs) {
     const char* e = getenv("RSS_PREFETCH");
-    return e && e[0] == '1';
+    if (e && (e[0] == '0' || e[0] == '1')) return e[0] == '1';
+    return !has_outputs;
 }
 
 // RSS_OFF32=0: 64-bit addressing even where 32-bit byte offsets fit (A/B, tests)
@@ -2319,7 +2322,7 @@ int launch_range8(KernelFn fn, FallbackFn fallback, unsigned grid, int cu_count,
     // balanced tail (walk_rows): its unit counter in the zeroed block, its LDS slot past the
     // small tables; the last tenth of the rows goes out per workgroup slot
     const uint32_t tail_rows = balanced_tail_rows(p.n / 4, grid);
-    if (tail_rows && balance_enabled()) {
+    if (tail_rows && balance_enabled() && !p.prefetch) {
         p.tail_rows = tail_rows;
         p.tail_ctr = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(tail) +
                                                            range8_ctr_offset(p.q_span));
@@ -2414,7 +2417,7 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
     p.tuples = d_tuples;
     p.hash_out = d_hash;
     p.queue_out = d_queue;
-    p.prefetch = prefetch_enabled();
+    p.prefetch = prefetch_for(d_hash || d_queue);
 
     p.counts = reinterpret_cast<unsigned long long*>(d_counts);
     p.n = n;
@@ -2507,6 +2510,7 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
             }
             if (ranged) {
                 p.queue_out = qcol;
+                p.prefetch = prefetch_for(true);  // the pass writes a column
                 p.q_lo = 0;
                 const bool v4 = vec4 && ((uintptr_t)qcol % (qw == QW_U32 ? 16 : 8)) == 0;
                 // the first range: the bins the first pass's tables leave (small tables: 4-tuple
