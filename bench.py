@@ -530,19 +530,25 @@ def extra_lines(torch, _native, dev, stream, key_bytes):
     rate = nk * nt / (ms / 1e3)
     out["key_search"] = {"keys": nk, "tuples": nt, "kernel_ms": ms,
                          "key_tuple_evals_per_s": rate, "htable": 128, "queues": 24,
-                         "bound": "lds", "peak_evals_per_s": KEYSEARCH_LDS_PEAK,
-                         "frac": rate / KEYSEARCH_LDS_PEAK,
-                         "bound_note": "LDS-array cycles, conflict-free: 9 ds_read_b64 + 8 "
-                                       "ds_add_u32 (2 cycles each) per 64 tuples x 8 keys, 256 CUs "
-                                       "at 2.4 GHz; PMC (profiles/r04/pmc_keysearch/summary.json): "
-                                       "the LDS array is 78 % busy, 55 % of its cycles bank "
-                                       "conflicts of the random table reads; VALU issue 32 %"}
+                         "bound": "valu", "peak_evals_per_s": KEYSEARCH_VALU_PEAK,
+                         "frac": rate / KEYSEARCH_VALU_PEAK,
+                         "lds_peak_evals_per_s": KEYSEARCH_LDS_PEAK,
+                         "lds_frac": rate / KEYSEARCH_LDS_PEAK,
+                         "bound_note": "rss_key_search_packed_kernel on conflict-free tables "
+                                       "(PMC, profiles/r04/pmc_keysearch_small/summary.json): per "
+                                       "64 tuples x 8 keys 99 VALU (4 cycles each on a SIMD) and "
+                                       "29 LDS instructions (58 LDS-array cycles, 0 bank "
+                                       "conflicts) -- VALU issue binds; peaks at 2.4 GHz: VALU "
+                                       "1024 SIMDs / (4 x 99) per 512 evaluations, LDS 256 CUs / "
+                                       "58 per 512"}
     return out
 
 
-# rss_key_search_packed_kernel's LDS bound: per wave-step of 64 tuples x 8 keys
-# 17 LDS instructions x 2 LDS-array cycles when conflict-free; 256 CUs at 2.4 GHz
-KEYSEARCH_LDS_PEAK = 256 * 2.4e9 / (17 * 2) * 512
+# rss_key_search_packed_kernel's bounds, per wave-step of 64 tuples x 8 keys
+# (= 512 evaluations; PMC of the current kernel): 99 VALU instructions at 4 cycles on one of
+# 1024 SIMDs, 58 LDS-array cycles on one of 256 CUs; 2.4 GHz
+KEYSEARCH_VALU_PEAK = 1024 * 2.4e9 / (4 * 99) * 512
+KEYSEARCH_LDS_PEAK = 256 * 2.4e9 / 58 * 512
 
 
 def main():

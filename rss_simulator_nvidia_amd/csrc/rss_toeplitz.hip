@@ -1180,18 +1180,96 @@ __global__ __launch_bounds__(kBlock, 2) void rss_counts_perm_kernel(const PermPa
 // Key search: per-queue counts of the same tuples under many
 // keys.  A table index depends only on the tuple, so one table can serve two keys: entry
 // v holds (key A's XOR of windows, key B's) as 8 bytes and ONE ds_read_b64 -- 64 banks,
-// 256 B/clk (twice ds_read_b32's rate) -- fetches both keys' terms.  The tables are the
-// small tables' 21 fields (5, 5, 5, 5, 5, 5, 2 bits of each word, LSB first; kSmallLut) with
-// 8-byte entries: 32 entries x 8 B = 256 B cover the 64 banks exactly once, so every entry
-// sits on its own bank pair and a random index never conflicts -- 21 conflict-free reads
-// (2 LDS cycles each) per tuple where the round-1..3 tables (nine of 11 / 10 input bits,
-// 120 KiB) took 9 random reads at ~7 cycles each (PMC: 44 of the 80 LDS cycles per 64
-// tuples x 8 keys were bank conflicts, profiles/r04/pmc_keysearch/).  5.25 KiB of tables
-// also leave ~155 KiB of the LDS to the bins.  blockIdx.y selects the pair; each workgroup
-// histograms its grid-stride share of the tuples into counts rows 2y, 2y+1.  With the
-// tuples resident in the 256 MiB Infinity Cache the re-reads stay on die.
-constexpr uint32_t kPairLutBytes = kSmallTables * 256;            // 5376
-constexpr uint32_t kPairBinBytesMax = kLdsBytes - kPairLutBytes;  // 154.75 KiB for the bins
+// 256 B/clk (twice ds_read_b32's rate) -- fetches both keys' terms.  Two table sets:
+// * the packed kernel (power-of-two H, several keys' low bits per entry) reads the small
+//   tables' 21 fields (5, 5, 5, 5, 5, 5, 2 bits of each word, LSB first; kSmallLut) with
+//   8-byte entries: 32 entries x 8 B = 256 B cover the 64 banks exactly once, so every entry
+//   sits on its own bank pair and a random index never conflicts -- 21 conflict-free reads
+//   (2 LDS cycles each) per tuple against 9 random reads at ~7 cycles each on the wide
+//   tables below (PMC: 0 against 44 of 80 LDS cycles per 64 tuples x 8 keys in bank
+//   conflicts, profiles/r04/pmc_keysearch*/); at Q = 24 the two run equal (the small tables'
+//   extra address VALU makes it VALU-bound instead), but 5.25 KiB of tables leave ~155 KiB to
+//   the bins: 8 keys per workgroup up to Q = 154 (wide tables: 40) and 4 up to 309 (80);
+// * the pair kernel (any H: two full 32-bit hashes, their Lemire remainders and two adds per
+//   tuple) keeps the nine wide tables of 2048 / 1024 entries (11 / 10 input bits, field LSBs
+//   first as in the hash kernel's partition), whose 9 lookups cost less VALU than 21:
+//     t0 w0[10:0]  t1 w0[21:11]  t2 w1[10:0]  t3 w2[15:11] | w2[31:27] << 5  t4 w0[31:22]
+//     t5 w1[21:11] t6 w2[10:0]   t7 w2[26:16] t8 w1[31:22]
+//   = 6 x 16 + 3 x 8 KiB = 120 KiB; on the small tables it ran 0.77 against 0.97 T
+//   evaluations/s at H = 100, Q = 24 (profiles/r04/small_tables/keysearch_configs.jsonl).
+// blockIdx.y selects the pair; each workgroup histograms its grid-stride share of the
+// tuples into counts rows 2y, 2y+1.  With the tuples resident in the 256 MiB Infinity Cache
+// the re-reads stay on die.
+constexpr uint32_t kPairLutBytes = kSmallTables * 256;            // 5376 (packed kernel)
+constexpr uint32_t kPackedBinBytesMax = kLdsBytes - kPairLutBytes;  // 154.75 KiB for the bins
+constexpr uint32_t kWidePairLutBytes = 6 * 16384 + 3 * 8192;     // 122880 (pair kernel)
+constexpr uint32_t kWidePairBinBytesMax = kLdsBytes - kWidePairLutBytes;  // 40 KiB, 2 x Q bins
+
+__host__ __device__ constexpr int wide_pair_width(int t) {
+    return (t == 3 || t == 4 || t == 8) ? 10 : 11;
+}
+__host__ __device__ constexpr uint32_t wide_pair_table(int t) {  // byte offset
+    return t == 0 ? 0u : t == 1 ? 16384u : t == 2 ? 32768u : t == 3 ? 49152u : t == 4 ? 57344u
+         : t == 5 ? 65536u : t == 6 ? 81920u : t == 7 ? 98304u : 114688u;
+}
+// input bit (0 = MSB of the source ip) feeding bit b of table t's index
+__host__ __device__ constexpr int wide_pair_bit(int t, int b) {
+    return t == 0 ? 31 - b : t == 1 ? 20 - b : t == 2 ? 63 - b
+         : t == 3 ? (b < 5 ? 84 - b : 73 - b)
+         : t == 4 ? 9 - b : t == 5 ? 52 - b : t == 6 ? 95 - b : t == 7 ? 79 - b : 41 - b;
+}
+
+template <int kT>
+__device__ __forceinline__ void build_wide_pair_table(uint2* lut, const uint32_t* __restrict__ wa,
+                                                      const uint32_t* __restrict__ wb, uint32_t tid) {
+    uint32_t a = 0, b = 0;
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+        const bool set = (tid >> j) & 1u;
+        a ^= set ? wa[wide_pair_bit(kT, j)] : 0u;
+        b ^= set ? wb[wide_pair_bit(kT, j)] : 0u;
+    }
+    uint2* dst = lut + wide_pair_table(kT) / 8;
+    dst[tid] = make_uint2(a, b);
+    if constexpr (wide_pair_width(kT) == 11)
+        dst[tid + 1024] = make_uint2(a ^ wa[wide_pair_bit(kT, 10)], b ^ wb[wide_pair_bit(kT, 10)]);
+}
+
+// byte address of wide table t's entry: 2 VALU (4 for the two-field t3); tables 5..8 take
+// their 64 KiB base from the opaque register `hi`
+template <int kT>
+__device__ __forceinline__ uint32_t wide_pair_offset(uint32_t w0, uint32_t w1, uint32_t w2,
+                                                     uint32_t hi) {
+    if constexpr (kT == 0) return (w0 << 3) & 0x3FF8u;
+    if constexpr (kT == 1) return (w0 >> 8) & 0x3FF8u;
+    if constexpr (kT == 2) return (w1 << 3) & 0x3FF8u;
+    if constexpr (kT == 3) return ((w2 >> 8) & 0xF8u) | ((w2 >> 19) & 0x1F00u);
+    if constexpr (kT == 4) return (w0 >> 19) & 0x1FF8u;
+    if constexpr (kT == 5) return ((w1 >> 8) & 0x3FF8u) | hi;
+    if constexpr (kT == 6) return ((w2 << 3) & 0x3FF8u) | hi;
+    if constexpr (kT == 7) return ((w2 >> 13) & 0x3FF8u) | hi;
+    return ((w1 >> 19) & 0x1FF8u) | hi;
+}
+
+template <int kT>
+__device__ __forceinline__ uint2 wide_pair_term(const char* lut, uint32_t w0, uint32_t w1,
+                                                uint32_t w2, uint32_t hi) {
+    constexpr uint32_t kImm = wide_pair_table(kT) & 0xFFFFu;
+    return *reinterpret_cast<const uint2*>(lut + kImm + wide_pair_offset<kT>(w0, w1, w2, hi));
+}
+
+// (hash under key A, hash under key B) of one tuple on the wide tables
+__device__ __forceinline__ uint2 toeplitz_hash_wide_pair(const uint2* __restrict__ lut, uint32_t w0,
+                                                         uint32_t w1, uint32_t w2, uint32_t hi) {
+    const char* base = reinterpret_cast<const char*>(lut);
+    const uint2 t0 = wide_pair_term<0>(base, w0, w1, w2, hi), t1 = wide_pair_term<1>(base, w0, w1, w2, hi);
+    const uint2 t2 = wide_pair_term<2>(base, w0, w1, w2, hi), t3 = wide_pair_term<3>(base, w0, w1, w2, hi);
+    const uint2 t4 = wide_pair_term<4>(base, w0, w1, w2, hi), t5 = wide_pair_term<5>(base, w0, w1, w2, hi);
+    const uint2 t6 = wide_pair_term<6>(base, w0, w1, w2, hi), t7 = wide_pair_term<7>(base, w0, w1, w2, hi);
+    const uint2 t8 = wide_pair_term<8>(base, w0, w1, w2, hi);
+    return make_uint2(xor3(xor3(t0.x, t1.x, t2.x), xor3(t3.x, t4.x, t5.x), xor3(t6.x, t7.x, t8.x)),
+                      xor3(xor3(t0.y, t1.y, t2.y), xor3(t3.y, t4.y, t5.y), xor3(t6.y, t7.y, t8.y)));
+}
 
 // entry e = 32 t + v of the 21 pair tables: (XOR of key A's windows, of key B's) over the
 // input bits set in v; `win(i)` gives the two keys' window i as a uint2
@@ -1272,7 +1350,7 @@ __device__ __forceinline__ void flush_bins(const uint32_t* bins, unsigned long l
 
 template <bool kHPow2, int kQMode, int kHist, bool kVec4>
 __global__ __launch_bounds__(kBlock) void rss_key_search_kernel(const LaunchParams p) {
-    __shared__ uint2 lut[kPairLutBytes / 8];
+    __shared__ uint2 lut[kWidePairLutBytes / 8];
     extern __shared__ uint32_t bins[];
     const uint32_t tid = threadIdx.x;
     // keys 2y and 2y+1; an odd last key is paired with itself and its copy discarded
@@ -1281,7 +1359,15 @@ __global__ __launch_bounds__(kBlock) void rss_key_search_kernel(const LaunchPara
     const uint32_t key_b = has_b ? key_a + 1 : key_a;
     const uint32_t* wa = p.key_windows + (size_t)RSS_INPUT_BITS * key_a;
     const uint32_t* wb = p.key_windows + (size_t)RSS_INPUT_BITS * key_b;
-    build_small_pair_lut(lut, [&](int i) { return make_uint2(wa[i], wb[i]); }, tid);
+    build_wide_pair_table<0>(lut, wa, wb, tid);
+    build_wide_pair_table<1>(lut, wa, wb, tid);
+    build_wide_pair_table<2>(lut, wa, wb, tid);
+    build_wide_pair_table<3>(lut, wa, wb, tid);
+    build_wide_pair_table<4>(lut, wa, wb, tid);
+    build_wide_pair_table<5>(lut, wa, wb, tid);
+    build_wide_pair_table<6>(lut, wa, wb, tid);
+    build_wide_pair_table<7>(lut, wa, wb, tid);
+    build_wide_pair_table<8>(lut, wa, wb, tid);
     const uint32_t per_key =
         kHist == HIST_PRIVATE ? p.Q * kBinCols : (kHist == HIST_SHARED ? p.Q : 0u);
     for (uint32_t e = tid; e < 2 * per_key; e += kBlock) bins[e] = 0;
@@ -1293,6 +1379,8 @@ __global__ __launch_bounds__(kBlock) void rss_key_search_kernel(const LaunchPara
     uint32_t* bins_a = bins;
     uint32_t* bins_b = bins + per_key;
     const uint32_t col = tid & (kBinCols - 1);
+    uint32_t hi = 65536u;
+    asm volatile("" : "+v"(hi));
     const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
     const uint64_t gstride = (uint64_t)gridDim.x * kBlock;
     uint64_t tail_begin = 0;
@@ -1303,16 +1391,16 @@ __global__ __launch_bounds__(kBlock) void rss_key_search_kernel(const LaunchPara
             const uint4 a = src[3 * g + 0];
             const uint4 b = src[3 * g + 1];
             const uint4 c = src[3 * g + 2];
-            count_pair<kHPow2, kQMode, kHist>(bins_a, bins_b, toeplitz_hash_pair(lut, a.x, a.y, a.z), col, qa, qb);
-            count_pair<kHPow2, kQMode, kHist>(bins_a, bins_b, toeplitz_hash_pair(lut, a.w, b.x, b.y), col, qa, qb);
-            count_pair<kHPow2, kQMode, kHist>(bins_a, bins_b, toeplitz_hash_pair(lut, b.z, b.w, c.x), col, qa, qb);
-            count_pair<kHPow2, kQMode, kHist>(bins_a, bins_b, toeplitz_hash_pair(lut, c.y, c.z, c.w), col, qa, qb);
+            count_pair<kHPow2, kQMode, kHist>(bins_a, bins_b, toeplitz_hash_wide_pair(lut, a.x, a.y, a.z, hi), col, qa, qb);
+            count_pair<kHPow2, kQMode, kHist>(bins_a, bins_b, toeplitz_hash_wide_pair(lut, a.w, b.x, b.y, hi), col, qa, qb);
+            count_pair<kHPow2, kQMode, kHist>(bins_a, bins_b, toeplitz_hash_wide_pair(lut, b.z, b.w, c.x, hi), col, qa, qb);
+            count_pair<kHPow2, kQMode, kHist>(bins_a, bins_b, toeplitz_hash_wide_pair(lut, c.y, c.z, c.w, hi), col, qa, qb);
         }
         tail_begin = ngroups << 2;
     }
     for (uint64_t i = tail_begin + gtid; i < p.n; i += gstride) {
         const uint32_t* t = reinterpret_cast<const uint32_t*>(p.tuples) + 3 * i;
-        count_pair<kHPow2, kQMode, kHist>(bins_a, bins_b, toeplitz_hash_pair(lut, t[0], t[1], t[2]), col, qa, qb);
+        count_pair<kHPow2, kQMode, kHist>(bins_a, bins_b, toeplitz_hash_wide_pair(lut, t[0], t[1], t[2], hi), col, qa, qb);
     }
     if constexpr (kHist == HIST_PRIVATE || kHist == HIST_SHARED) {
         __syncthreads();
@@ -1923,18 +2011,18 @@ int launch_search(const uint32_t* d_windows, size_t nkeys, const rss_tuple4* d_t
     int qmode, hist;
     uint32_t bin_bytes;  // per key; a workgroup holds the bins of its two keys
     const bool h_pow2 = setup_modes(&p, htable, q_eff, true, &qmode, &hist, &bin_bytes,
-                                    kPairBinBytesMax / 2, false);
+                                    kWidePairBinBytesMax / 2, false);
     const bool vec4 = aligned16(d_tuples);
     DeviceInfo info;
     int rc = device_info(&info);
     if (rc) return rc;
     // packed buckets (8 keys per table entry for H <= 256, 4 for H <= 65536) whenever
     // their private bins fit (8 keys: Q <= 154, 4 keys: Q <= 309); else pairs of full hashes
-    const bool bytes_fit = (uint64_t)q_eff * 8 * kBinCols * 4 <= kPairBinBytesMax;
+    const bool bytes_fit = (uint64_t)q_eff * 8 * kBinCols * 4 <= kPackedBinBytesMax;
     const int lane_bits = htable <= 256u && bytes_fit ? 8 : 16;
     const uint32_t keys_per_wg = 64 / lane_bits;
     const uint64_t packed_bins = (uint64_t)q_eff * keys_per_wg * kBinCols * 4;
-    if (h_pow2 && htable <= 65536u && packed_bins <= kPairBinBytesMax) {
+    if (h_pow2 && htable <= 65536u && packed_bins <= kPackedBinBytesMax) {
         p.q_m16 = 65536u / q_eff + (65536u % q_eff != 0);
         KernelFn fn = pick_packed(lane_bits, qmode, vec4);
         const unsigned gx = search_grid_x(n, info.cu_count);

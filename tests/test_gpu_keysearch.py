@@ -24,11 +24,11 @@ def native():
                                    (256, 255, 5000), (65536, 80, 40003), (1024, 81, 4001),
                                    (4096, 64, 12345), (128, 1, 777), (128, 64, 5555), (256, 80, 6000),
                                    (256, 81, 3000),
-                                   # round 4 (5.25 KiB of conflict-free tables): the new budget
-                                   # edges -- 8 keys to Q = 154, 4 keys to 309, pair kernel
-                                   # private bins to 619
+                                   # round 4 (packed kernel on 5.25 KiB of conflict-free
+                                   # tables): its new budget edges -- 8 keys to Q = 154, 4 keys
+                                   # to 309 -- and the pair kernel's private / shared bin edge
                                    (256, 154, 7001), (256, 155, 6003), (65536, 309, 8001),
-                                   (1024, 310, 5003), (1000, 619, 4001), (1000, 620, 4001)])
+                                   (1024, 310, 5003), (1000, 160, 4001), (1000, 161, 4001)])
 def test_key_search_matches_oracle(native, oracle_lib, H, Q, n):
     from rss_simulator_nvidia_amd import keysearch
     keys = keysearch.random_keys(19, seed=H + Q) + [[int(x) for x in range(52)]]
