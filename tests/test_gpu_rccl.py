@@ -137,7 +137,10 @@ def test_bench_under_torchrun_nproc1_reports_baseline_and_roofline(tmp_path):
     assert rec["n_gpus"] == 1 and rec["steps"] == 3 and rec["warmup"] == 1
     assert "RCCL all-reduce" in rec["config"]["parallelism"]
     assert "rccl.RcclComm" in rec["config"]["parallelism"]  # the default per-step exchange
-    assert "8 steps per collective" in rec["config"]["parallelism"]  # --allreduce-bucket 8
+    # one all-reduce per batch (the default); 8 batches per collective only as `bucketed`
+    assert "one collective per batch" in rec["config"]["parallelism"]
+    assert rec["config"]["collectives_per_batch"] == 1.0
+    assert rec["bucketed"]["steps_per_collective"] == 8 and rec["bucketed"]["value"] > 0
     base = rec["cpu_baseline"]
     assert base is not None and base["value"] > 0 and base["cores"] == 2
     assert rec["settle"]["launches"] >= 16  # clock-settle launches before the warmup
