@@ -124,6 +124,10 @@ struct LaunchParams {
     uint32_t* poison;             // HIST_RANGE8: set when a u8 bin wrapped (results discarded)
     uint32_t prefetch;            // small-table passes: next group's loads before this group's LDS work
     unsigned long long* tail_ctr; // balanced tail's unit counter when the launch has no ws (HIST_RANGE8)
+    void* resid_out;              // HIST_RANGE8 counts only: per-workgroup lists of q - q_span for the
+    uint32_t* resid_counts;       //   tuples past the LDS range (u16 when resid_u16, else u32), each
+    uint64_t resid_cap;           //   workgroup's at resid_out + blockIdx.x * resid_cap entries, its
+    uint32_t resid_u16;           //   length in resid_counts[blockIdx.x] (no queue column)
     uint16_t reta[kRetaMax];      // QM_TABLE: queue of bucket b (ethtool -X indirection)
 };
 
@@ -603,6 +607,44 @@ inline uint32_t balanced_tail_rows(uint64_t ngroups, unsigned grid) {
     return rows >= 16 ? (uint32_t)std::max<uint64_t>(1, rows / 10) : 0u;
 }
 
+// HIST_RANGE8 counts only, queues past the pass's LDS range (q >= q_span): instead of a queue
+// column with every tuple's queue, append q - q_span to this workgroup's list (K queues per
+// lane): a ballot per slot, one LDS atomic per wave on the workgroup's list length `ctr`,
+// stores at consecutive entries.  A workgroup's list never exceeds its tuples (the launcher
+// sizes resid_cap for the static walk), and the entries are exact whether or not the bins
+// are poisoned.
+template <int K>
+__device__ __forceinline__ void resid_append(const LaunchParams& p, uint32_t* ctr, const uint32_t* q) {
+    uint64_t m[K];
+    uint32_t total = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        m[k] = __ballot(q[k] >= p.q_span);
+        total += (uint32_t)__popcll(m[k]);
+    }
+    if (total == 0) return;  // uniform
+    const uint32_t lane = __lane_id();
+    const int leader = __ffsll((long long)__ballot(1)) - 1;  // first active lane (uniform)
+    uint32_t base = 0;
+    if ((int)lane == leader)
+        base = __hip_atomic_fetch_add(ctr, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    base = __builtin_amdgcn_readlane(base, leader);
+    const uint64_t first = (uint64_t)blockIdx.x * p.resid_cap;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        if (q[k] >= p.q_span) {
+            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m[k] >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m[k], 0u));
+            const uint64_t at = first + base + below;
+            if (p.resid_u16)
+                static_cast<uint16_t*>(p.resid_out)[at] = (uint16_t)(q[k] - p.q_span);
+            else
+                static_cast<uint32_t*>(p.resid_out)[at] = q[k] - p.q_span;
+        }
+        base += (uint32_t)__popcll(m[k]);
+    }
+}
+
 template <bool kHPow2, int kQMode, int kHist, int kQWidth, bool kSmallLut>
 __device__ __forceinline__ void one_tuple(const uint32_t* lut, uint32_t* bins, uint64_t i,
                                           uint32_t col, uint32_t hi, const uint32_t* reta_lds,
@@ -612,6 +654,12 @@ __device__ __forceinline__ void one_tuple(const uint32_t* lut, uint32_t* bins, u
     const uint32_t q = queue_lookup<kQMode>(bucket_of<kHPow2>(h, p), p, reta_lds);
     if (p.hash_out) stream_store(p.hash_out + i, h);
     if (p.queue_out) store_queue1<kStoreWidth<kQWidth>>(p.queue_out, i, column_queue<kQWidth>(q, p));
+    if constexpr (kSmallLut && kHist == HIST_RANGE8) {
+        if (p.resid_out) {
+            const uint32_t qq[1] = {q};
+            resid_append<1>(p, const_cast<uint32_t*>(lut) + kSmallLutDwords, qq);
+        }
+    }
     count_queue<kHist>(bins, q, col, p);
 }
 
@@ -629,10 +677,12 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
     extern __shared__ uint32_t bins[];    // histogram bins, sized at launch
     const uint32_t tid = threadIdx.x;
 
-    if constexpr (kSmallLut)
+    if constexpr (kSmallLut) {
         build_small_lut(lut, p.window, tid);
-    else
+        if (tid == 0) lut[kSmallLutDwords] = 0u;  // the residual list's length (resid_out)
+    } else {
         build_lut(lut, p.window, tid);
+    }
     const uint32_t nbins = kHist == HIST_PRIVATE   ? p.Q * kBinCols
                          : kHist == HIST_SHARED    ? p.Q
                          : kHist == HIST_RANGE     ? p.q_span
@@ -694,6 +744,12 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
                     store_queue4<kW>(p.queue_out, (uint32_t)g, c0, c1, c2, c3);
                 else
                     store_queue4<kW>(p.queue_out, g, c0, c1, c2, c3);
+            }
+            if constexpr (kSmallLut && kHist == HIST_RANGE8) {
+                if (p.resid_out) {
+                    const uint32_t qq[4] = {q0, q1, q2, q3};
+                    resid_append<4>(p, lut + kSmallLutDwords, qq);
+                }
             }
             if constexpr (kHist == HIST_RANGE16) {
                 const uint32_t o0 = range16_add(bins, q0, p), o1 = range16_add(bins, q1, p);
@@ -786,6 +842,8 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
         __syncthreads();  // one row of the u8 partial matrix (the launcher always gives one)
         uint32_t* row = p.partial + (size_t)blockIdx.x * p.partial_stride;
         for (uint32_t w = tid; w < nbins; w += kBlock) row[w] = bins[w];
+        if constexpr (kSmallLut)
+            if (p.resid_out && tid == 0) p.resid_counts[blockIdx.x] = lut[kSmallLutDwords];
     }
 }
 
@@ -850,11 +908,15 @@ constexpr uint32_t kNarrowSpan = 16384;  // rss_queue_hist_kernel: u32 bins, two
 // kBits = 8: u8 bins, four per dword, with HIST_RANGE8's guard (0x7F -> a move of 128 into
 // ovf[r]) and poison word (a field that wrapped; the reduce is gated on it and
 // rss_range8_fallback_col_kernel recounts the range) -- 163840 queues per read of the column.
+// regions (region_counts != NULL): the column is one list per workgroup -- workgroup x reads
+// the region_counts[x] entries at queues + x * region_cap (the hash pass's residual lists,
+// resid_append) instead of grid-striding over n entries.
 template <typename T, int kBits = 16>
 __global__ __launch_bounds__(kBlock) void rss_queue_hist_wide_kernel(
         const T* __restrict__ queues, uint64_t n, uint32_t q_lo, uint32_t q_span,
         uint32_t* __restrict__ partial, uint32_t stride_words, unsigned long long* counts,
-        uint32_t* __restrict__ ovf, uint32_t* __restrict__ poison) {
+        uint32_t* __restrict__ ovf, uint32_t* __restrict__ poison,
+        const uint32_t* __restrict__ region_counts, uint64_t region_cap) {
     constexpr uint32_t kPerWord = 32 / kBits, kField = (1u << kBits) - 1u;
     constexpr uint32_t kHalf = 1u << (kBits - 1);  // the guard's move
     extern __shared__ uint32_t bins[];
@@ -862,8 +924,14 @@ __global__ __launch_bounds__(kBlock) void rss_queue_hist_wide_kernel(
     const uint32_t words = (q_span + kPerWord - 1) / kPerWord;
     for (uint32_t e = tid; e < words; e += kBlock) bins[e] = 0;
     __syncthreads();
-    const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
-    const uint64_t gstride = (uint64_t)gridDim.x * kBlock;
+    uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
+    uint64_t gstride = (uint64_t)gridDim.x * kBlock;
+    if (region_counts) {
+        queues += (uint64_t)blockIdx.x * region_cap;
+        n = region_counts[blockIdx.x];
+        gtid = tid;
+        gstride = kBlock;
+    }
     // the add of one queue; returns the bin's previous value (0 when q is out of range)
     auto add = [&](uint32_t q) -> uint32_t {
         const uint32_t r = q - q_lo;  // wraps for q < q_lo
@@ -1033,12 +1101,19 @@ __global__ __launch_bounds__(kBlock) void rss_range8_fallback_kernel(const Launc
 template <typename T>
 __global__ __launch_bounds__(kBlock) void rss_range8_fallback_col_kernel(
         const T* __restrict__ col, uint64_t n, uint32_t q_lo, uint32_t q_span,
-        unsigned long long* counts, const uint32_t* __restrict__ poison) {
+        unsigned long long* counts, const uint32_t* __restrict__ poison,
+        const uint32_t* __restrict__ region_counts, uint64_t region_cap) {
     if (!*poison) return;  // uniform across the grid
     extern __shared__ uint32_t bins[];
     const uint32_t tid = threadIdx.x;
-    const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
-    const uint64_t gstride = (uint64_t)gridDim.x * kBlock;
+    uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
+    uint64_t gstride = (uint64_t)gridDim.x * kBlock;
+    if (region_counts) {  // one residual list per workgroup (see rss_queue_hist_wide_kernel)
+        col += (uint64_t)blockIdx.x * region_cap;
+        n = region_counts[blockIdx.x];
+        gtid = tid;
+        gstride = kBlock;
+    }
     for (uint32_t lo = 0; lo < q_span; lo += kFallbackColSpan) {
         const uint32_t span = min(kFallbackColSpan, q_span - lo);
         for (uint32_t e = tid; e < span; e += kBlock) bins[e] = 0;
@@ -2159,6 +2234,13 @@ int launch_counts_perm(const uint32_t* window, const void* tuples, uint64_t n, u
     return RSS_OK;
 }
 
+// RSS_RESID=0: counts-only launches past 161144 queues write a scratch queue column instead of
+// per-workgroup residual lists (A/B, tests)
+bool resid_enabled() {
+    const char* e = getenv("RSS_RESID");
+    return !(e && e[0] == '0');
+}
+
 bool wide_hist_enabled() {
     const char* e = getenv("RSS_WIDE_HIST");
     return !(e && e[0] == '0');
@@ -2199,7 +2281,8 @@ int range8_debug() {
 // RSS_ENOMEM without launching anything when the block cannot be allocated.
 template <typename T>
 int launch_wide8(const T* qcol, uint64_t n, uint32_t lo, uint32_t sp, unsigned long long* counts,
-                 unsigned grid, int cu_count, hipStream_t stream) {
+                 unsigned grid, int cu_count, hipStream_t stream,
+                 const uint32_t* region_counts = nullptr, uint64_t region_cap = 0) {
     const uint32_t words = (sp + 3) / 4;
     const size_t rows_bytes = (size_t)grid * words * 4, tail_bytes = ((size_t)sp + 4) * 4;
     void* buf = nullptr;
@@ -2215,7 +2298,8 @@ int launch_wide8(const T* qcol, uint64_t n, uint32_t lo, uint32_t sp, unsigned l
     if (e == hipSuccess && debug == 1) e = hipMemsetD32Async(poison, 1, 1, stream);
     if (e == hipSuccess) {
         hipLaunchKernelGGL((rss_queue_hist_wide_kernel<T, 8>), dim3(grid), dim3(kBlock), words * 4,
-                           stream, qcol, n, lo, sp, partial, words, counts, ovf, poison);
+                           stream, qcol, n, lo, sp, partial, words, counts, ovf, poison,
+                           region_counts, region_cap);
         e = hipGetLastError();
     }
     if (e == hipSuccess) {
@@ -2227,9 +2311,10 @@ int launch_wide8(const T* qcol, uint64_t n, uint32_t lo, uint32_t sp, unsigned l
         e = hipGetLastError();
     }
     if (e == hipSuccess && debug != 2) {
-        hipLaunchKernelGGL(rss_range8_fallback_col_kernel<T>, dim3(cu_count), dim3(kBlock),
+        hipLaunchKernelGGL(rss_range8_fallback_col_kernel<T>,
+                           dim3(region_counts ? grid : (unsigned)cu_count), dim3(kBlock),
                            std::min(kFallbackColSpan, sp) * 4, stream, qcol, n, lo, sp, counts,
-                           static_cast<const uint32_t*>(poison));
+                           static_cast<const uint32_t*>(poison), region_counts, region_cap);
         e = hipGetLastError();
     }
     int rc = e == hipSuccess ? RSS_OK
@@ -2244,16 +2329,21 @@ int launch_wide8(const T* qcol, uint64_t n, uint32_t lo, uint32_t sp, unsigned l
 // (u16 or u32) the first pass wrote: one wide pass (u16 LDS bins, rows of a u16 partial
 // matrix, then a reduce) per kWideSpan queues; RSS_WIDE_HIST=0 (or no memory for the
 // partial matrix) keeps one rss_queue_hist_kernel pass per `span` queues.
+// Regions (region_counts != NULL): the "column" is one residual list per hash-pass workgroup
+// (resid_append), `region_grid` of them; only wide passes read them, one workgroup per list.
 int launch_queue_ranges(const void* qcol, int qw, uint64_t n, uint32_t first, uint32_t nqueues,
-                        unsigned long long* counts, int cu_count, hipStream_t stream) {
+                        unsigned long long* counts, int cu_count, hipStream_t stream,
+                        const uint32_t* region_counts = nullptr, uint64_t region_cap = 0,
+                        unsigned region_grid = 0) {
     if (first >= nqueues) return RSS_OK;
     const uint32_t span = kNarrowSpan;
     // a wide pass costs about two narrow ones (2^28 tuples: ~0.2 vs ~0.1 ms over a u16
     // column, profiles/r03/d/config_sweep.jsonl), so it pays from three narrow passes on
     const uint64_t narrow_passes = ((uint64_t)nqueues - first + span - 1) / span;
-    if (wide_hist_enabled() && narrow_passes >= 3) {
+    if (region_counts || (wide_hist_enabled() && narrow_passes >= 3)) {
         const uint64_t want = (n + 8ull * kBlock - 1) / (8ull * kBlock);
-        const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, cu_count));
+        const unsigned grid = region_counts ? region_grid
+                                            : (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, cu_count));
         const uint32_t stride_words = kWideSpan / 2;
         void* partial = nullptr;
         if (hipMallocAsync(&partial, (size_t)grid * stride_words * 4, stream) == hipSuccess) {
@@ -2264,8 +2354,10 @@ int launch_queue_ranges(const void* qcol, int qw, uint64_t n, uint32_t first, ui
                 if (range8_enabled() && nqueues - lo > kWideSpan) {
                     const uint32_t sp8 = std::min<uint32_t>(kWideSpan8, nqueues - lo);
                     rc = qw == QW_U16
-                             ? launch_wide8(static_cast<const uint16_t*>(qcol), n, lo, sp8, counts, grid, cu_count, stream)
-                             : launch_wide8(static_cast<const uint32_t*>(qcol), n, lo, sp8, counts, grid, cu_count, stream);
+                             ? launch_wide8(static_cast<const uint16_t*>(qcol), n, lo, sp8, counts, grid,
+                                            cu_count, stream, region_counts, region_cap)
+                             : launch_wide8(static_cast<const uint32_t*>(qcol), n, lo, sp8, counts, grid,
+                                            cu_count, stream, region_counts, region_cap);
                     if (rc == RSS_OK) {
                         lo += sp8;
                         continue;
@@ -2279,12 +2371,14 @@ int launch_queue_ranges(const void* qcol, int qw, uint64_t n, uint32_t first, ui
                     hipLaunchKernelGGL(rss_queue_hist_wide_kernel<uint16_t>, dim3(grid), dim3(kBlock), lds,
                                        stream, static_cast<const uint16_t*>(qcol), n, lo, sp,
                                        static_cast<uint32_t*>(partial), stride_words, counts,
-                                       (uint32_t*)nullptr, (uint32_t*)nullptr);
+                                       (uint32_t*)nullptr, (uint32_t*)nullptr, region_counts,
+                                       region_cap);
                 else
                     hipLaunchKernelGGL(rss_queue_hist_wide_kernel<uint32_t>, dim3(grid), dim3(kBlock), lds,
                                        stream, static_cast<const uint32_t*>(qcol), n, lo, sp,
                                        static_cast<uint32_t*>(partial), stride_words, counts,
-                                       (uint32_t*)nullptr, (uint32_t*)nullptr);
+                                       (uint32_t*)nullptr, (uint32_t*)nullptr, region_counts,
+                                       region_cap);
                 hipError_t e = hipGetLastError();
                 if (e == hipSuccess) {
                     const uint32_t words = (sp + 1) / 2;
@@ -2306,6 +2400,8 @@ int launch_queue_ranges(const void* qcol, int qw, uint64_t n, uint32_t first, ui
             return rc;
         }
         (void)hipGetLastError();  // no room for the partial matrix: the narrow passes below
+        if (region_counts)        // (which read a dense column, not residual lists)
+            return set_error(RSS_ENOMEM, "rss_hash_device: no memory for the wide pass's rows");
     }
     const uint64_t qwant = (n + 8ull * kBlock - 1) / (8ull * kBlock);
     const unsigned qgrid = (unsigned)std::min<uint64_t>(qwant, (uint64_t)cu_count * 2);
@@ -2410,7 +2506,7 @@ int launch_range8(KernelFn fn, FallbackFn fallback, unsigned grid, int cu_count,
     // balanced tail (walk_rows): its unit counter in the zeroed block, its LDS slot past the
     // small tables; the last tenth of the rows goes out per workgroup slot
     const uint32_t tail_rows = balanced_tail_rows(p.n / 4, grid);
-    if (tail_rows && balance_enabled() && !p.prefetch) {
+    if (tail_rows && balance_enabled() && !p.prefetch && !p.resid_out) {  // (lists: static walk)
         p.tail_rows = tail_rows;
         p.tail_ctr = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(tail) +
                                                            range8_ctr_offset(p.q_span));
@@ -2434,7 +2530,8 @@ int launch_range8(KernelFn fn, FallbackFn fallback, unsigned grid, int cu_count,
         if (qcol)
             hipLaunchKernelGGL(rss_range8_fallback_col_kernel<uint32_t>, dim3(cu_count), dim3(kBlock),
                                std::min(kFallbackColSpan, p.q_span) * 4, stream, qcol, p.n, p.q_lo,
-                               p.q_span, p.counts, static_cast<const uint32_t*>(p.poison));
+                               p.q_span, p.counts, static_cast<const uint32_t*>(p.poison),
+                               (const uint32_t*)nullptr, (uint64_t)0);
         else
             hipLaunchKernelGGL(fallback, dim3(cu_count), dim3(kBlock),
                                std::min(kFallbackSpan, p.q_span) * 4, stream, p);
@@ -2577,6 +2674,45 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
             // the caller's u32 column holds the queues (exact even when the bins are poisoned)
             const uint32_t* col = d_queue ? static_cast<const uint32_t*>(d_queue) : nullptr;
             return launch_range8(fn, fb8, grid, info.cu_count, p, col, r8buf, stream);
+        }
+        // Counts only past span8 (u8 hash pass + wide passes): the queues past the pass's LDS
+        // range go to per-workgroup residual lists (resid_append) instead of a queue column --
+        // only those tuples' queues are written and read again, not every tuple's (DESIGN.md
+        // §3 "Many queues").  RSS_RESID=0 keeps the scratch column (A/B).
+        if (r8buf && !d_queue && q_eff > span8 && wide_hist_enabled() && resid_enabled()) {
+            // the static walk gives a workgroup at most `rows` groups of 4 tuples per row, plus
+            // the < 4 tail tuples (workgroup 0)
+            const uint64_t per_row = (uint64_t)grid * kBlock;
+            const uint64_t rows = (n / 4 + per_row - 1) / per_row;
+            const uint64_t cap = (rows * 4 * kBlock + 4 + 7) & ~7ull;
+            const uint32_t nres = q_eff - span8;
+            const size_t esize = nres <= 65536u ? 2 : 4;
+            const size_t list_bytes = ((size_t)grid * cap * esize + 15) & ~(size_t)15;
+            void* lists = nullptr;
+            if (hipMallocAsync(&lists, list_bytes + (size_t)grid * 4, stream) == hipSuccess) {
+                uint32_t* list_counts = reinterpret_cast<uint32_t*>(static_cast<char*>(lists) + list_bytes);
+                p.queue_out = nullptr;
+                p.resid_out = lists;
+                p.resid_counts = list_counts;
+                p.resid_cap = cap;
+                p.resid_u16 = esize == 2;
+                p.prefetch = prefetch_for(false);
+                p.q_lo = 0;
+                p.q_span = span8;
+                KernelFn fn = h_pow2 ? pick_queue<true>(qmode, HIST_RANGE8, QW_U32, VM_SMALL_LUT)
+                                     : pick_queue<false>(qmode, HIST_RANGE8, QW_U32, VM_SMALL_LUT);
+                rc = launch_range8(fn, fb8, grid, info.cu_count, p, nullptr, r8buf, stream);
+                p.resid_out = nullptr;
+                if (rc == RSS_OK)
+                    rc = launch_queue_ranges(lists, esize == 2 ? QW_U16 : QW_U32, n, 0, nres,
+                                             p.counts + span8, info.cu_count, stream, list_counts,
+                                             cap, grid);
+                const hipError_t fe = hipFreeAsync(lists, stream);  // after its readers
+                if (fe != hipSuccess && rc == RSS_OK)
+                    rc = set_error(RSS_EIO, "hipFreeAsync failed: %s", hipGetErrorString(fe));
+                return rc;
+            }
+            (void)hipGetLastError();  // no room for the lists: the scratch column below
         }
         if (ranged_histogram_ok(q_eff, kNarrowSpan, qbytes)) {
             void* qcol = d_queue;

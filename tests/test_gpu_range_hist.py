@@ -292,14 +292,18 @@ def test_range8_u8_bins_equal_oracle(native, oracle_lib, example_key, Q):
     queues each in u8 bins while more than 65536 are left (one u16 pass for the rest).  On uniform input the u8 path alone
     (RSS_RANGE8_DEBUG=nofallback: no gate, no recount), the recount alone
     (RSS_RANGE8_DEBUG=force), the default and the u16 path (RSS_RANGE8=0) all give the
-    oracle's hashes, queues and counts, with and without per-tuple outputs."""
+    oracle's hashes, queues and counts, with and without per-tuple outputs.  Counts only past
+    161144 queues the hash pass appends the residual queues to per-workgroup lists that the
+    wide passes read one workgroup per list (default), or writes the scratch column
+    (RSS_RESID=0); both with the load prefetch and with the static walk (RSS_PREFETCH=0)."""
     n, H = (1 << 21) + 5, 1 << 30
     host = oracle_lib.generate(31, 0, n)
     tup = torch.from_numpy(host.view(np.int32).reshape(-1)).to("cuda:0")
     key = native.prepare_key(example_key)
     ho, qo, co = oracle_lib.run(example_key, host, H, Q)
     runs = [("RSS_RANGE8_DEBUG", "nofallback"), ("RSS_RANGE8_DEBUG", "force"),
-            ("RSS_RANGE8", "1"), ("RSS_RANGE8", "0")]
+            ("RSS_RANGE8", "1"), ("RSS_RANGE8", "0"), ("RSS_RESID", "0"),
+            ("RSS_PREFETCH", "0")]
     for name, value in runs:
         for outputs in (True, False):
             h, q, c = _with_env(name, value,

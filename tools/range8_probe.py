@@ -25,7 +25,8 @@ tup = torch.empty(3 * n, dtype=torch.int32, device=dev)
 _native.generate_device(SEED, 0, n, tup.data_ptr(), s.cuda_stream)
 h = torch.empty(n, dtype=torch.int32, device=dev)
 q = torch.empty(n, dtype=torch.int32, device=dev)
-VARIANTS = {"u8": {}, "u16": {"RSS_RANGE8": "0"}, "force": {"RSS_RANGE8_DEBUG": "force"}}
+VARIANTS = {"u8": {}, "u16": {"RSS_RANGE8": "0"}, "force": {"RSS_RANGE8_DEBUG": "force"},
+            "column": {"RSS_RESID": "0"}}
 
 
 def timed(Q, outputs, env, reps=10, warm=5):
