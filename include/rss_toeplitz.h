@@ -135,10 +135,11 @@ int rss_key_select_fields(rss_key* key, uint32_t fields);
  * for up to 16384 queues beside the 12-bit tables and up to 80572 beside the 2.6 KiB
  * small tables (4-tuple body, no indirection table), u8 bins for up to 161144 (a bin that
  * wraps poisons the pass and a gated recount replaces its counts) -- whose per-workgroup
- * rows a reduce launch sums; the queues past that are gathered from the queue column (one
- * wide pass per 163840 queues in u8 bins, 65536 in u16): d_queue when given, else a
- * stream-ordered scratch column of 2 bytes per tuple (for nqueues <= 226679 the queue minus
- * 161144) or 4 (hipMallocAsync / hipFreeAsync on `stream`, like the per-workgroup rows).
+ * rows a reduce launch sums; the queues past that are counted by wide passes (163840 queues
+ * per pass in u8 bins, 65536 in u16) over d_queue when given, else -- counts only -- over
+ * per-wave lists of the tuples whose queue lies past the LDS range (the queue minus 161144,
+ * 2 bytes per entry for nqueues <= 226680, else 4; stream-ordered hipMallocAsync /
+ * hipFreeAsync on `stream`, like the per-workgroup rows).
  */
 int rss_hash_device(const rss_key* key, const rss_tuple4* d_tuples, size_t n,
                     uint32_t htable, uint32_t nqueues, uint32_t* d_hash,

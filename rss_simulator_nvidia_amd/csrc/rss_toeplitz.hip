@@ -124,10 +124,11 @@ struct LaunchParams {
     uint32_t* poison;             // HIST_RANGE8: set when a u8 bin wrapped (results discarded)
     uint32_t prefetch;            // small-table passes: next group's loads before this group's LDS work
     unsigned long long* tail_ctr; // balanced tail's unit counter when the launch has no ws (HIST_RANGE8)
-    void* resid_out;              // HIST_RANGE8 counts only: per-workgroup lists of q - q_span for the
-    uint32_t* resid_counts;       //   tuples past the LDS range (u16 when resid_u16, else u32), each
-    uint64_t resid_cap;           //   workgroup's at resid_out + blockIdx.x * resid_cap entries, its
-    uint32_t resid_u16;           //   length in resid_counts[blockIdx.x] (no queue column)
+    void* resid_out;              // HIST_RANGE8 counts only: per-wave lists of q - q_span for the
+    uint32_t* resid_counts;       //   tuples past the LDS range (u16 when resid_u16, else u32), wave
+    uint64_t resid_cap;           //   v of workgroup x's at resid_out + (16 x + v) * resid_cap entries,
+    uint32_t resid_u16;           //   its length in resid_counts[16 x + v] (no queue column)
+    uint32_t resid_debug;         // timing probes only (RSS_RESID_DEBUG): 1 no stores, 2 no appends
     uint16_t reta[kRetaMax];      // QM_TABLE: queue of bucket b (ethtool -X indirection)
 };
 
@@ -608,47 +609,45 @@ inline uint32_t balanced_tail_rows(uint64_t ngroups, unsigned grid) {
 }
 
 // HIST_RANGE8 counts only, queues past the pass's LDS range (q >= q_span): instead of a queue
-// column with every tuple's queue, append q - q_span to this workgroup's list (K queues per
-// lane): a ballot per slot, one LDS atomic per wave on the workgroup's list length `ctr`,
-// stores at consecutive entries.  A workgroup's list never exceeds its tuples (the launcher
-// sizes resid_cap for the static walk), and the entries are exact whether or not the bins
-// are poisoned.
+// column with every tuple's queue, each wave appends r = q - q_span to a list of its own (K
+// queues per lane): a ballot per slot, the entries at the wave's running length `count` plus
+// the lanes below (mbcnt), stored at 32-bit offsets from the wave's list (`list`, uniform).
+// No atomic: the length is the same in every lane (sums of ballot popcounts), and a wave's
+// list never exceeds its tuples (the launcher sizes resid_cap for the static walk's share of a
+// wave).  The entries are exact whether or not the bins are poisoned.
+constexpr uint32_t kWavesPerBlock = kBlock / 64;
+__device__ __forceinline__ char* resid_list(const LaunchParams& p) {
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    return static_cast<char*>(p.resid_out) +
+           ((uint64_t)blockIdx.x * kWavesPerBlock + wave) * p.resid_cap * (p.resid_u16 ? 2 : 4);
+}
 template <int K>
-__device__ __forceinline__ void resid_append(const LaunchParams& p, uint32_t* ctr, const uint32_t* q) {
-    uint64_t m[K];
-    uint32_t total = 0;
+__device__ __forceinline__ void resid_append(const LaunchParams& p, char* list, uint32_t& count,
+                                             const uint32_t* q) {
+    if (p.resid_debug == 2) return;  // (timing probes only: RSS_RESID_DEBUG)
+    // the first active lane took part in every earlier append of its wave (lanes leave the
+    // walk from the top, and the < 4 tail tuples are lanes 0..2): its length is the wave's
+    uint32_t c = __builtin_amdgcn_readfirstlane(count);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        m[k] = __ballot(q[k] >= p.q_span);
-        total += (uint32_t)__popcll(m[k]);
-    }
-    if (total == 0) return;  // uniform
-    const uint32_t lane = __lane_id();
-    const int leader = __ffsll((long long)__ballot(1)) - 1;  // first active lane (uniform)
-    uint32_t base = 0;
-    if ((int)lane == leader)
-        base = __hip_atomic_fetch_add(ctr, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    base = __builtin_amdgcn_readlane(base, leader);
-    const uint64_t first = (uint64_t)blockIdx.x * p.resid_cap;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        if (q[k] >= p.q_span) {
-            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m[k] >> 32),
-                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m[k], 0u));
-            const uint64_t at = first + base + below;
+        const uint64_t m = __ballot(q[k] >= p.q_span);
+        if (q[k] >= p.q_span && p.resid_debug != 1) {
+            const uint32_t at = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, c));
             if (p.resid_u16)
-                static_cast<uint16_t*>(p.resid_out)[at] = (uint16_t)(q[k] - p.q_span);
+                *reinterpret_cast<uint16_t*>(list + 2u * at) = (uint16_t)(q[k] - p.q_span);
             else
-                static_cast<uint32_t*>(p.resid_out)[at] = q[k] - p.q_span;
+                *reinterpret_cast<uint32_t*>(list + 4u * at) = q[k] - p.q_span;
         }
-        base += (uint32_t)__popcll(m[k]);
+        c += (uint32_t)__popcll(m);
     }
+    count = c;
 }
 
 template <bool kHPow2, int kQMode, int kHist, int kQWidth, bool kSmallLut>
 __device__ __forceinline__ void one_tuple(const uint32_t* lut, uint32_t* bins, uint64_t i,
                                           uint32_t col, uint32_t hi, const uint32_t* reta_lds,
-                                          const LaunchParams& p) {
+                                          const LaunchParams& p, char* rlist, uint32_t& rcount) {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(p.tuples) + 3 * i;
     const uint32_t h = hash_of<kSmallLut>(lut, src[0], src[1], src[2], hi);
     const uint32_t q = queue_lookup<kQMode>(bucket_of<kHPow2>(h, p), p, reta_lds);
@@ -657,7 +656,7 @@ __device__ __forceinline__ void one_tuple(const uint32_t* lut, uint32_t* bins, u
     if constexpr (kSmallLut && kHist == HIST_RANGE8) {
         if (p.resid_out) {
             const uint32_t qq[1] = {q};
-            resid_append<1>(p, const_cast<uint32_t*>(lut) + kSmallLutDwords, qq);
+            resid_append<1>(p, rlist, rcount, qq);
         }
     }
     count_queue<kHist>(bins, q, col, p);
@@ -679,7 +678,6 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
 
     if constexpr (kSmallLut) {
         build_small_lut(lut, p.window, tid);
-        if (tid == 0) lut[kSmallLutDwords] = 0u;  // the residual list's length (resid_out)
     } else {
         build_lut(lut, p.window, tid);
     }
@@ -700,6 +698,11 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
     const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
     const uint64_t gstride = (uint64_t)gridDim.x * kBlock;
     uint64_t tail_begin = 0;
+    // HIST_RANGE8 counts only past the LDS range: this wave's residual list and its length
+    char* rlist = nullptr;
+    uint32_t rcount = 0;
+    if constexpr (kSmallLut && kHist == HIST_RANGE8)
+        if (p.resid_out) rlist = resid_list(p);
 
     if constexpr (kVec4) {
         // 4 consecutive tuples per lane: 48 B = 3 x dwordx4, 16-B aligned.
@@ -748,7 +751,7 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
             if constexpr (kSmallLut && kHist == HIST_RANGE8) {
                 if (p.resid_out) {
                     const uint32_t qq[4] = {q0, q1, q2, q3};
-                    resid_append<4>(p, lut + kSmallLutDwords, qq);
+                    resid_append<4>(p, rlist, rcount, qq);
                 }
             }
             if constexpr (kHist == HIST_RANGE16) {
@@ -806,7 +809,8 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
         tail_begin = ngroups << 2;
     }
     for (uint64_t i = tail_begin + gtid; i < p.n; i += gstride)
-        one_tuple<kHPow2, kQMode, kHist, kQWidth, kSmallLut>(lut, bins, i, col, hi, reta_lds, p);
+        one_tuple<kHPow2, kQMode, kHist, kQWidth, kSmallLut>(lut, bins, i, col, hi, reta_lds, p, rlist,
+                                                             rcount);
 
     // Epilogue: fold this workgroup's bins into the global uint64 counts.
     if constexpr (kHist == HIST_PRIVATE || kHist == HIST_SHARED) {
@@ -842,8 +846,9 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
         __syncthreads();  // one row of the u8 partial matrix (the launcher always gives one)
         uint32_t* row = p.partial + (size_t)blockIdx.x * p.partial_stride;
         for (uint32_t w = tid; w < nbins; w += kBlock) row[w] = bins[w];
-        if constexpr (kSmallLut)
-            if (p.resid_out && tid == 0) p.resid_counts[blockIdx.x] = lut[kSmallLutDwords];
+        if constexpr (kSmallLut)  // (lane 0 took part in every append of its wave)
+            if (p.resid_out && (tid & 63u) == 0)
+                p.resid_counts[(uint64_t)blockIdx.x * kWavesPerBlock + (tid >> 6)] = rcount;
     }
 }
 
@@ -908,9 +913,9 @@ constexpr uint32_t kNarrowSpan = 16384;  // rss_queue_hist_kernel: u32 bins, two
 // kBits = 8: u8 bins, four per dword, with HIST_RANGE8's guard (0x7F -> a move of 128 into
 // ovf[r]) and poison word (a field that wrapped; the reduce is gated on it and
 // rss_range8_fallback_col_kernel recounts the range) -- 163840 queues per read of the column.
-// regions (region_counts != NULL): the column is one list per workgroup -- workgroup x reads
-// the region_counts[x] entries at queues + x * region_cap (the hash pass's residual lists,
-// resid_append) instead of grid-striding over n entries.
+// regions (region_counts != NULL): the column is one list per hash-pass wave -- wave v of
+// workgroup x reads the region_counts[16 x + v] entries at queues + (16 x + v) * region_cap
+// (the hash pass's residual lists, resid_append) instead of grid-striding over n entries.
 template <typename T, int kBits = 16>
 __global__ __launch_bounds__(kBlock) void rss_queue_hist_wide_kernel(
         const T* __restrict__ queues, uint64_t n, uint32_t q_lo, uint32_t q_span,
@@ -926,11 +931,12 @@ __global__ __launch_bounds__(kBlock) void rss_queue_hist_wide_kernel(
     __syncthreads();
     uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
     uint64_t gstride = (uint64_t)gridDim.x * kBlock;
-    if (region_counts) {
-        queues += (uint64_t)blockIdx.x * region_cap;
-        n = region_counts[blockIdx.x];
-        gtid = tid;
-        gstride = kBlock;
+    if (region_counts) {  // wave v reads list 16 x + v
+        const uint64_t list = (uint64_t)blockIdx.x * kWavesPerBlock + (tid >> 6);
+        queues += list * region_cap;
+        n = region_counts[list];
+        gtid = tid & 63u;
+        gstride = 64;
     }
     // the add of one queue; returns the bin's previous value (0 when q is out of range)
     auto add = [&](uint32_t q) -> uint32_t {
@@ -1108,11 +1114,12 @@ __global__ __launch_bounds__(kBlock) void rss_range8_fallback_col_kernel(
     const uint32_t tid = threadIdx.x;
     uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
     uint64_t gstride = (uint64_t)gridDim.x * kBlock;
-    if (region_counts) {  // one residual list per workgroup (see rss_queue_hist_wide_kernel)
-        col += (uint64_t)blockIdx.x * region_cap;
-        n = region_counts[blockIdx.x];
-        gtid = tid;
-        gstride = kBlock;
+    if (region_counts) {  // one residual list per wave (see rss_queue_hist_wide_kernel)
+        const uint64_t list = (uint64_t)blockIdx.x * kWavesPerBlock + (tid >> 6);
+        col += list * region_cap;
+        n = region_counts[list];
+        gtid = tid & 63u;
+        gstride = 64;
     }
     for (uint32_t lo = 0; lo < q_span; lo += kFallbackColSpan) {
         const uint32_t span = min(kFallbackColSpan, q_span - lo);
@@ -2235,10 +2242,18 @@ int launch_counts_perm(const uint32_t* window, const void* tuples, uint64_t n, u
 }
 
 // RSS_RESID=0: counts-only launches past 161144 queues write a scratch queue column instead of
-// per-workgroup residual lists (A/B, tests)
+// per-wave residual lists (A/B, tests)
 bool resid_enabled() {
     const char* e = getenv("RSS_RESID");
     return !(e && e[0] == '0');
+}
+
+// Timing probes only (wrong counts): RSS_RESID_DEBUG=nostore skips the residual lists'
+// stores, =noappend the whole append -- what the lists cost inside the hash pass
+uint32_t resid_debug() {
+    const char* e = getenv("RSS_RESID_DEBUG");
+    if (!e) return 0;
+    return strcmp(e, "nostore") == 0 ? 1u : (strcmp(e, "noappend") == 0 ? 2u : 0u);
 }
 
 bool wide_hist_enabled() {
@@ -2329,8 +2344,9 @@ int launch_wide8(const T* qcol, uint64_t n, uint32_t lo, uint32_t sp, unsigned l
 // (u16 or u32) the first pass wrote: one wide pass (u16 LDS bins, rows of a u16 partial
 // matrix, then a reduce) per kWideSpan queues; RSS_WIDE_HIST=0 (or no memory for the
 // partial matrix) keeps one rss_queue_hist_kernel pass per `span` queues.
-// Regions (region_counts != NULL): the "column" is one residual list per hash-pass workgroup
-// (resid_append), `region_grid` of them; only wide passes read them, one workgroup per list.
+// Regions (region_counts != NULL): the "column" is one residual list per hash-pass wave
+// (resid_append), 16 per workgroup of `region_grid`; only wide passes read them, one wave per
+// list.
 int launch_queue_ranges(const void* qcol, int qw, uint64_t n, uint32_t first, uint32_t nqueues,
                         unsigned long long* counts, int cu_count, hipStream_t stream,
                         const uint32_t* region_counts = nullptr, uint64_t region_cap = 0,
@@ -2676,26 +2692,28 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
             return launch_range8(fn, fb8, grid, info.cu_count, p, col, r8buf, stream);
         }
         // Counts only past span8 (u8 hash pass + wide passes): the queues past the pass's LDS
-        // range go to per-workgroup residual lists (resid_append) instead of a queue column --
+        // range go to per-wave residual lists (resid_append) instead of a queue column --
         // only those tuples' queues are written and read again, not every tuple's (DESIGN.md
         // §3 "Many queues").  RSS_RESID=0 keeps the scratch column (A/B).
         if (r8buf && !d_queue && q_eff > span8 && wide_hist_enabled() && resid_enabled()) {
-            // the static walk gives a workgroup at most `rows` groups of 4 tuples per row, plus
-            // the < 4 tail tuples (workgroup 0)
+            // the static walk gives a wave at most `rows` groups of 4 tuples per lane, plus the
+            // < 4 tail tuples (wave 0 of workgroup 0); 8 entries more keep every list 16-B aligned
             const uint64_t per_row = (uint64_t)grid * kBlock;
             const uint64_t rows = (n / 4 + per_row - 1) / per_row;
-            const uint64_t cap = (rows * 4 * kBlock + 4 + 7) & ~7ull;
+            const uint64_t cap = (rows * 4 * 64 + 4 + 7) & ~7ull;
             const uint32_t nres = q_eff - span8;
             const size_t esize = nres <= 65536u ? 2 : 4;
-            const size_t list_bytes = ((size_t)grid * cap * esize + 15) & ~(size_t)15;
+            const size_t nlists = (size_t)grid * kWavesPerBlock;
+            const size_t list_bytes = nlists * cap * esize;
             void* lists = nullptr;
-            if (hipMallocAsync(&lists, list_bytes + (size_t)grid * 4, stream) == hipSuccess) {
+            if (hipMallocAsync(&lists, list_bytes + nlists * 4, stream) == hipSuccess) {
                 uint32_t* list_counts = reinterpret_cast<uint32_t*>(static_cast<char*>(lists) + list_bytes);
                 p.queue_out = nullptr;
                 p.resid_out = lists;
                 p.resid_counts = list_counts;
                 p.resid_cap = cap;
                 p.resid_u16 = esize == 2;
+                p.resid_debug = resid_debug();
                 p.prefetch = prefetch_for(false);
                 p.q_lo = 0;
                 p.q_span = span8;

@@ -1,0 +1,59 @@
+"""What the residual lists cost inside a counts-only many-queues launch (tool, not product):
+2^28 uniform tuples, H = 2^30, counts only; medians of 10 launches after 5 warm ones, variants
+alternated over three rounds (best round kept): the default (per-wave lists), the lists'
+stores skipped (RSS_RESID_DEBUG=nostore) and the whole append skipped (=noappend) -- both
+give wrong counts beyond the LDS range, timing only -- and the scratch column (RSS_RESID=0).
+One JSON line per Q.
+
+usage: python tools/resid_probe.py [Q ...]"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from bench import EXAMPLE_KEY, SEED  # noqa: E402
+from rss_simulator_nvidia_amd import _native  # noqa: E402
+
+n, H = 1 << 28, 1 << 30
+dev = torch.device("cuda:0")
+s = torch.cuda.current_stream(dev)
+key = _native.prepare_key([int(x, 16) for x in EXAMPLE_KEY.split(":")])
+tup = torch.empty(3 * n, dtype=torch.int32, device=dev)
+_native.generate_device(SEED, 0, n, tup.data_ptr(), s.cuda_stream)
+VARIANTS = {"lists": {}, "nostore": {"RSS_RESID_DEBUG": "nostore"},
+            "noappend": {"RSS_RESID_DEBUG": "noappend"}, "column": {"RSS_RESID": "0"}}
+
+
+def timed(Q, env, reps=10, warm=5):
+    os.environ.update(env)
+    try:
+        c = torch.zeros(Q, dtype=torch.int64, device=dev)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(reps)]
+        for i in range(-warm, reps):
+            if i >= 0:
+                ev[i][0].record(s)
+            _native.hash_device(key, tup.data_ptr(), n, H, Q, None, None, c.data_ptr(), 0,
+                                s.cuda_stream)
+            if i >= 0:
+                ev[i][1].record(s)
+        torch.cuda.synchronize()
+        x = sorted(a.elapsed_time(b) for a, b in ev)
+        return x[len(x) // 2]
+    finally:
+        for k in env:
+            os.environ.pop(k, None)
+
+
+for Q in [int(x) for x in sys.argv[1:]] or [131072, 262144]:
+    rec = {"Q": Q, "tuples": n}
+    for rnd in range(3):
+        for name, env in VARIANTS.items():
+            k = name + "_counts_ms"
+            t = round(timed(Q, env), 4)
+            rec[k] = min(t, rec.get(k, t))
+    print(json.dumps(rec), flush=True)
