@@ -128,7 +128,6 @@ struct LaunchParams {
     uint32_t* resid_counts;       //   tuples past the LDS range (u16 when resid_u16, else u32), wave
     uint64_t resid_cap;           //   v of workgroup x's at resid_out + (16 x + v) * resid_cap entries,
     uint32_t resid_u16;           //   its length in resid_counts[16 x + v] (no queue column)
-    uint32_t resid_debug;         // timing probes only (RSS_RESID_DEBUG): 1 no stores, 2 no appends
     uint16_t reta[kRetaMax];      // QM_TABLE: queue of bucket b (ethtool -X indirection)
 };
 
@@ -624,24 +623,27 @@ __device__ __forceinline__ char* resid_list(const LaunchParams& p) {
 template <int K>
 __device__ __forceinline__ void resid_append(const LaunchParams& p, char* list, uint32_t& count,
                                              const uint32_t* q) {
-    if (p.resid_debug == 2) return;  // (timing probes only: RSS_RESID_DEBUG)
-    // the first active lane took part in every earlier append of its wave (lanes leave the
-    // walk from the top, and the < 4 tail tuples are lanes 0..2): its length is the wave's
-    uint32_t c = __builtin_amdgcn_readfirstlane(count);
+    // The first active lane took part in every earlier append of its wave (lanes leave the
+    // walk from the top, and the < 4 tail tuples are lanes 0..2): its length is the wave's.
+    // Per slot: the ballot's compare, two mbcnt and one shift-add for the address (the
+    // length's byte offset stays scalar), one subtract for the entry.
+    const uint32_t sh = p.resid_u16 ? 1u : 2u;
+    uint32_t at = __builtin_amdgcn_readfirstlane(count) << sh;  // byte offset of the next entry
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const uint64_t m = __ballot(q[k] >= p.q_span);
-        if (q[k] >= p.q_span && p.resid_debug != 1) {
-            const uint32_t at = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, c));
+        if (q[k] >= p.q_span) {
+            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            char* dst = list + (at + (below << sh));
             if (p.resid_u16)
-                *reinterpret_cast<uint16_t*>(list + 2u * at) = (uint16_t)(q[k] - p.q_span);
+                *reinterpret_cast<uint16_t*>(dst) = (uint16_t)(q[k] - p.q_span);
             else
-                *reinterpret_cast<uint32_t*>(list + 4u * at) = q[k] - p.q_span;
+                *reinterpret_cast<uint32_t*>(dst) = q[k] - p.q_span;
         }
-        c += (uint32_t)__popcll(m);
+        at += (uint32_t)__popcll(m) << sh;
     }
-    count = c;
+    count = at >> sh;
 }
 
 template <bool kHPow2, int kQMode, int kHist, int kQWidth, bool kSmallLut>
@@ -2248,14 +2250,6 @@ bool resid_enabled() {
     return !(e && e[0] == '0');
 }
 
-// Timing probes only (wrong counts): RSS_RESID_DEBUG=nostore skips the residual lists'
-// stores, =noappend the whole append -- what the lists cost inside the hash pass
-uint32_t resid_debug() {
-    const char* e = getenv("RSS_RESID_DEBUG");
-    if (!e) return 0;
-    return strcmp(e, "nostore") == 0 ? 1u : (strcmp(e, "noappend") == 0 ? 2u : 0u);
-}
-
 bool wide_hist_enabled() {
     const char* e = getenv("RSS_WIDE_HIST");
     return !(e && e[0] == '0');
@@ -2713,7 +2707,6 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
                 p.resid_counts = list_counts;
                 p.resid_cap = cap;
                 p.resid_u16 = esize == 2;
-                p.resid_debug = resid_debug();
                 p.prefetch = prefetch_for(false);
                 p.q_lo = 0;
                 p.q_span = span8;

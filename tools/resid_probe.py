@@ -1,8 +1,7 @@
 """What the residual lists cost inside a counts-only many-queues launch (tool, not product):
 2^28 uniform tuples, H = 2^30, counts only; medians of 10 launches after 5 warm ones, variants
-alternated over three rounds (best round kept): the default (per-wave lists), the lists'
-stores skipped (RSS_RESID_DEBUG=nostore) and the whole append skipped (=noappend) -- both
-give wrong counts beyond the LDS range, timing only -- and the scratch column (RSS_RESID=0).
+alternated over three rounds (best round kept): the default (per-wave lists, load
+prefetch), the lists on the static walk (RSS_PREFETCH=0) and the scratch column (RSS_RESID=0).
 One JSON line per Q.
 
 usage: python tools/resid_probe.py [Q ...]"""
@@ -24,8 +23,7 @@ s = torch.cuda.current_stream(dev)
 key = _native.prepare_key([int(x, 16) for x in EXAMPLE_KEY.split(":")])
 tup = torch.empty(3 * n, dtype=torch.int32, device=dev)
 _native.generate_device(SEED, 0, n, tup.data_ptr(), s.cuda_stream)
-VARIANTS = {"lists": {}, "nostore": {"RSS_RESID_DEBUG": "nostore"},
-            "noappend": {"RSS_RESID_DEBUG": "noappend"}, "column": {"RSS_RESID": "0"}}
+VARIANTS = {"lists": {}, "static": {"RSS_PREFETCH": "0"}, "column": {"RSS_RESID": "0"}}
 
 
 def timed(Q, env, reps=10, warm=5):
