@@ -604,7 +604,10 @@ __device__ __forceinline__ void walk_rows(Group group, uint64_t ngroups, uint32_
 inline uint32_t balanced_tail_rows(uint64_t ngroups, unsigned grid) {
     const uint64_t per_row = (uint64_t)grid * kBlock;
     const uint64_t rows = (ngroups + per_row - 1) / per_row;
-    return rows >= 16 ? (uint32_t)std::max<uint64_t>(1, rows / 10) : 0u;
+    const char* e = getenv("RSS_TAIL_DIV");  // (A/B) the tail is rows / div, default 10
+    const long v = e ? atol(e) : 10;
+    const uint64_t div = v >= 2 ? (uint64_t)v : 10u;
+    return rows >= 16 ? (uint32_t)std::max<uint64_t>(1, rows / div) : 0u;
 }
 
 // HIST_RANGE8 counts only, queues past the pass's LDS range (q >= q_span): instead of a queue
