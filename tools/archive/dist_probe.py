@@ -7,7 +7,7 @@ dispatch order is: uniform counts, uniform full, flow counts, flow full (3 each)
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402

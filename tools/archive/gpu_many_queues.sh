@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU box: many queues -- the range-hist, bench-launch and single-pass tests, the many-queues
 # rows of the config sweep (byte vs 12-bit tables), and the same-buffer A/B of the bench's
-# step incl. RSS_OFF32=0.  usage: tools/gpu_many_queues.sh TAG
+# step incl. RSS_OFF32=0.  usage: tools/archive/gpu_many_queues.sh TAG
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/${1:-r03/e}

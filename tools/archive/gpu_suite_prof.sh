@@ -3,7 +3,7 @@
 # --kernel-trace --stats of the same command (+ its timed-launch summary) -- the final
 # validation without the PMC passes, A/B and sweep of gpu_validate.sh.  Every GPU step has
 # its own time limit and the first failure ends the call.
-# usage: tools/gpu_suite_prof.sh TAG     (outputs under gpurun_out/TAG/)
+# usage: tools/archive/gpu_suite_prof.sh TAG     (outputs under gpurun_out/TAG/)
 set -eo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/${1:-suite_prof}
