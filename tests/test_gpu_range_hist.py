@@ -283,7 +283,8 @@ def _with_env(name, value, fn):
 
 
 @pytest.mark.parametrize("Q", [SPAN16 + 1, 131072, SPAN8, SPAN8 + 1, SPAN8 + 65535, SPAN8 + 65536,
-                               262144, SPAN8 + 65536 + WIDE8 + 1, 10 ** 6])
+                               262144, SPAN8 + 65536 + WIDE8 + 1, 10 ** 6,
+                               SPAN8 + 9 * WIDE8, SPAN8 + 9 * WIDE8 + 1])
 def test_range8_u8_bins_equal_oracle(native, oracle_lib, example_key, Q):
     """Past 80572 queues the small-table pass counts up to 161144 of them in u8 LDS bins
     (HIST_RANGE8: guard at 0x80, moves into a u32 per queue, poison-gated recount); past
@@ -343,14 +344,18 @@ def test_range8_guard_moves(native, oracle_lib, example_key, Q):
 @pytest.mark.parametrize("Q,outputs,lo,hi", [(131072, True, 0, SPAN8), (131072, False, 0, SPAN8),
                                              (200000, True, 0, SPAN8), (200000, False, 0, SPAN8),
                                              (400000, True, SPAN8, SPAN8 + WIDE8),
-                                             (400000, False, SPAN8, SPAN8 + WIDE8)])
+                                             (400000, False, SPAN8, SPAN8 + WIDE8),
+                                             (10 ** 6, True, SPAN8 + 2 * WIDE8, SPAN8 + 3 * WIDE8),
+                                             (10 ** 6, False, SPAN8 + 2 * WIDE8, SPAN8 + 3 * WIDE8)])
 def test_range8_poisoned_pass_recounts(native, oracle_lib, example_key, Q, outputs, lo, hi):
     """2^22 copies of one tuple whose queue lies in a u8 range -- the hash pass's [0, 161144),
     or (Q = 400000) the first u8 wide pass's [161144, 324984) over the queue column -- plus
     4099 random tuples: every workgroup piles thousands of in-flight adds onto one u8 bin,
     which wraps; the add that wraps it raises the poison word, the reduce skips the pass's
     rows and the recount (from the u32 queue column, or by rehashing for a counts-only hash
-    pass) gives the exact counts -- also when accumulating onto the caller's counts."""
+    pass) gives the exact counts -- also when accumulating onto the caller's counts.  Q = 10^6:
+    the wrapping bin is the third u8 wide pass's (over the u32 queue column, or over the
+    residual lists)."""
     n_same, n_rand, H = 1 << 22, 4099, 1 << 30
     rnd = oracle_lib.generate(33, 0, n_rand)
     _, q_rnd, _ = oracle_lib.run(example_key, rnd, H, Q)
@@ -374,7 +379,8 @@ def test_range8_poisoned_pass_recounts(native, oracle_lib, example_key, Q, outpu
     assert not np.array_equal(bad.cpu().numpy().view(np.uint64), want)
 
 
-@pytest.mark.parametrize("Q,outputs", [(131072, True), (131072, False), (400000, False)])
+@pytest.mark.parametrize("Q,outputs", [(131072, True), (131072, False), (400000, False),
+                                       (10 ** 6, True), (10 ** 6, False)])
 def test_range8_zipf_flows_equal_oracle(native, oracle_lib, example_key, Q, outputs):
     """Skewed traffic: 2^22 tuples drawn Zipf(1.3) from 50000 distinct flows, shuffled -- a
     few flows hold tens of thousands of tuples spread over the batch, most hold a handful.

@@ -2,7 +2,8 @@
 same buffers (tool, not product): 2^28 uniform tuples, H = 2^30, full outputs (hash u32 +
 queue u32) and counts only; medians of 10 launches after 5 warm ones, alternating variants in
 two rounds.  `force` = the poison-gated recount on every launch (RSS_RANGE8_DEBUG=force: what
-a batch that wraps a u8 bin costs).  Prints one JSON line per Q.
+a batch that wraps a u8 bin costs); `column` = counts only through a scratch queue column
+instead of residual lists (RSS_RESID=0).  Prints one JSON line per Q.
 
 usage: python tools/range8_probe.py [Q ...]"""
 import json
