@@ -138,8 +138,7 @@ int rss_key_select_fields(rss_key* key, uint32_t fields);
  * rows a reduce launch sums; the queues past that are counted by wide passes (163840 queues
  * per pass in u8 bins, 65536 in u16) over d_queue when given, else -- counts only -- over
  * per-wave lists of the tuples whose queue lies past the LDS range (the queue minus 161144,
- * 2 bytes per entry for nqueues <= 292216 -- from both ends of a list past 226680 -- else 4;
- * stream-ordered hipMallocAsync /
+ * 2 bytes per entry for nqueues <= 226680, else 4; stream-ordered hipMallocAsync /
  * hipFreeAsync on `stream`, like the per-workgroup rows).
  */
 int rss_hash_device(const rss_key* key, const rss_tuple4* d_tuples, size_t n,
