@@ -128,8 +128,6 @@ struct LaunchParams {
     uint32_t* resid_counts;       //   tuples past the LDS range (u16 when resid_u16, else u32), wave
     uint64_t resid_cap;           //   v of workgroup x's at resid_out + (16 x + v) * resid_cap entries,
     uint32_t resid_u16;           //   its length in resid_counts[16 x + v] (no queue column)
-    uint32_t resid_split;         // u16 lists two-ended: r < 65536 from the front, r - 65536 from
-                                  //   the back, that length in resid_counts[nlists + 16 x + v]
     uint16_t reta[kRetaMax];      // QM_TABLE: queue of bucket b (ethtool -X indirection)
 };
 
@@ -625,41 +623,15 @@ __device__ __forceinline__ char* resid_list(const LaunchParams& p) {
     return static_cast<char*>(p.resid_out) +
            ((uint64_t)blockIdx.x * kWavesPerBlock + wave) * p.resid_cap * (p.resid_u16 ? 2 : 4);
 }
-constexpr uint32_t kResidSplit = 65536;
 template <int K>
-__device__ __forceinline__ void resid_append(const LaunchParams& p, char* list, uint64_t& count,
+__device__ __forceinline__ void resid_append(const LaunchParams& p, char* list, uint32_t& count,
                                              const uint32_t* q) {
-    if (p.resid_split) {
-        // 65536 < Q - q_span <= 131072: u16 entries from both ends of the list -- r below 65536
-        // from the front, r - 65536 (the same u16 truncation) from the back; both lengths in
-        // `count` (front in the low half)
-        uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)count);
-        uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(count >> 32));
-        const uint32_t last = (uint32_t)p.resid_cap - 1u;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const bool res = q[k] >= p.q_span;
-            const bool up = res && q[k] - p.q_span >= kResidSplit;
-            const uint64_t ma = __ballot(res), mh = __ballot(up), ml = ma & ~mh;
-            if (res) {
-                const uint64_t m = up ? mh : ml;
-                const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                const uint32_t slot = up ? last - (hi + below) : lo + below;
-                *reinterpret_cast<uint16_t*>(list + 2u * slot) = (uint16_t)(q[k] - p.q_span);
-            }
-            lo += (uint32_t)__popcll(ml);
-            hi += (uint32_t)__popcll(mh);
-        }
-        count = lo | ((uint64_t)hi << 32);
-        return;
-    }
     // The first active lane took part in every earlier append of its wave (lanes leave the
     // walk from the top, and the < 4 tail tuples are lanes 0..2): its length is the wave's.
     // Per slot: the ballot's compare, two mbcnt and one shift-add for the address (the
     // length's byte offset stays scalar), one subtract for the entry.
     const uint32_t sh = p.resid_u16 ? 1u : 2u;
-    uint32_t at = __builtin_amdgcn_readfirstlane((uint32_t)count) << sh;  // byte offset of the next entry
+    uint32_t at = __builtin_amdgcn_readfirstlane(count) << sh;  // byte offset of the next entry
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const uint64_t m = __ballot(q[k] >= p.q_span);
@@ -680,7 +652,7 @@ __device__ __forceinline__ void resid_append(const LaunchParams& p, char* list, 
 template <bool kHPow2, int kQMode, int kHist, int kQWidth, bool kSmallLut>
 __device__ __forceinline__ void one_tuple(const uint32_t* lut, uint32_t* bins, uint64_t i,
                                           uint32_t col, uint32_t hi, const uint32_t* reta_lds,
-                                          const LaunchParams& p, char* rlist, uint64_t& rcount) {
+                                          const LaunchParams& p, char* rlist, uint32_t& rcount) {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(p.tuples) + 3 * i;
     const uint32_t h = hash_of<kSmallLut>(lut, src[0], src[1], src[2], hi);
     const uint32_t q = queue_lookup<kQMode>(bucket_of<kHPow2>(h, p), p, reta_lds);
@@ -733,7 +705,7 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
     uint64_t tail_begin = 0;
     // HIST_RANGE8 counts only past the LDS range: this wave's residual list and its length
     char* rlist = nullptr;
-    uint64_t rcount = 0;
+    uint32_t rcount = 0;
     if constexpr (kSmallLut && kHist == HIST_RANGE8)
         if (p.resid_out) rlist = resid_list(p);
 
@@ -880,12 +852,8 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
         uint32_t* row = p.partial + (size_t)blockIdx.x * p.partial_stride;
         for (uint32_t w = tid; w < nbins; w += kBlock) row[w] = bins[w];
         if constexpr (kSmallLut)  // (lane 0 took part in every append of its wave)
-            if (p.resid_out && (tid & 63u) == 0) {
-                const uint64_t list = (uint64_t)blockIdx.x * kWavesPerBlock + (tid >> 6);
-                p.resid_counts[list] = (uint32_t)rcount;
-                if (p.resid_split)
-                    p.resid_counts[(uint64_t)gridDim.x * kWavesPerBlock + list] = (uint32_t)(rcount >> 32);
-            }
+            if (p.resid_out && (tid & 63u) == 0)
+                p.resid_counts[(uint64_t)blockIdx.x * kWavesPerBlock + (tid >> 6)] = rcount;
     }
 }
 
@@ -958,7 +926,7 @@ __global__ __launch_bounds__(kBlock) void rss_queue_hist_wide_kernel(
         const T* __restrict__ queues, uint64_t n, uint32_t q_lo, uint32_t q_span,
         uint32_t* __restrict__ partial, uint32_t stride_words, unsigned long long* counts,
         uint32_t* __restrict__ ovf, uint32_t* __restrict__ poison,
-        const uint32_t* __restrict__ region_counts, uint64_t region_cap, uint32_t region_split) {
+        const uint32_t* __restrict__ region_counts, uint64_t region_cap) {
     constexpr uint32_t kPerWord = 32 / kBits, kField = (1u << kBits) - 1u;
     constexpr uint32_t kHalf = 1u << (kBits - 1);  // the guard's move
     extern __shared__ uint32_t bins[];
@@ -966,6 +934,15 @@ __global__ __launch_bounds__(kBlock) void rss_queue_hist_wide_kernel(
     const uint32_t words = (q_span + kPerWord - 1) / kPerWord;
     for (uint32_t e = tid; e < words; e += kBlock) bins[e] = 0;
     __syncthreads();
+    uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
+    uint64_t gstride = (uint64_t)gridDim.x * kBlock;
+    if (region_counts) {  // wave v reads list 16 x + v
+        const uint64_t list = (uint64_t)blockIdx.x * kWavesPerBlock + (tid >> 6);
+        queues += list * region_cap;
+        n = region_counts[list];
+        gtid = tid & 63u;
+        gstride = 64;
+    }
     // the add of one queue; returns the bin's previous value (0 when q is out of range)
     auto add = [&](uint32_t q) -> uint32_t {
         const uint32_t r = q - q_lo;  // wraps for q < q_lo
@@ -995,16 +972,16 @@ __global__ __launch_bounds__(kBlock) void rss_queue_hist_wide_kernel(
         }
     };
     constexpr uint32_t kPer = 16 / sizeof(T);  // queues per 16-B load
-    auto add16 = [&](const uint4 x, uint32_t off) {
+    auto add16 = [&](const uint4 x) {
         const uint32_t w[4] = {x.x, x.y, x.z, x.w};
         uint32_t q[kPer], old[kPer];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             if constexpr (sizeof(T) == 2) {
-                q[2 * k] = (w[k] & 0xFFFFu) + off;
-                q[2 * k + 1] = (w[k] >> 16) + off;
+                q[2 * k] = w[k] & 0xFFFFu;
+                q[2 * k + 1] = w[k] >> 16;
             } else {
-                q[k] = w[k] + off;
+                q[k] = w[k];
             }
         }
 #pragma unroll
@@ -1012,48 +989,28 @@ __global__ __launch_bounds__(kBlock) void rss_queue_hist_wide_kernel(
 #pragma unroll
         for (uint32_t k = 0; k < kPer; ++k) guard(q[k], old[k]);
     };
-    // entries [0, cnt) of qs (each + off), lanes gtid + k * gstride: scalar up to the first 16-B
-    // boundary, 16-B loads from there
-    auto segment = [&](const T* __restrict__ qs, uint64_t cnt, uint32_t off, uint64_t gtid,
-                       uint64_t gstride) {
-        const uint32_t mis = (16u - (uint32_t)((uintptr_t)qs & 15u)) & 15u;
-        const uint64_t head = (mis % sizeof(T)) || mis / sizeof(T) > cnt ? cnt : mis / sizeof(T);
-        for (uint64_t i = gtid; i < head; i += gstride) {
-            const uint32_t q = (uint32_t)qs[i] + off;
-            guard(q, add(q));
-        }
-        qs += head;
-        cnt -= head;
+    uint64_t tail = 0;
+    if (((uintptr_t)queues & 15) == 0) {
         // four 16-B loads in flight per lane: the adds wait for their returned values (the
         // guard check), so one load per iteration would leave the stream latency-bound at
         // one workgroup per CU
         constexpr int kUnroll = 4;
-        const uint4* __restrict__ v = reinterpret_cast<const uint4*>(qs);
-        const uint64_t nv = ((uintptr_t)qs & 15u) ? 0 : cnt / kPer;
+        const uint4* __restrict__ v = reinterpret_cast<const uint4*>(queues);
+        const uint64_t nv = n / kPer;
         uint64_t i = gtid;
         for (; i + (kUnroll - 1) * gstride < nv; i += kUnroll * gstride) {
             uint4 x[kUnroll];
 #pragma unroll
             for (int u = 0; u < kUnroll; ++u) x[u] = v[i + u * gstride];
 #pragma unroll
-            for (int u = 0; u < kUnroll; ++u) add16(x[u], off);
+            for (int u = 0; u < kUnroll; ++u) add16(x[u]);
         }
-        for (; i < nv; i += gstride) add16(v[i], off);
-        for (uint64_t j = nv * kPer + gtid; j < cnt; j += gstride) {
-            const uint32_t q = (uint32_t)qs[j] + off;
-            guard(q, add(q));
-        }
-    };
-    if (region_counts) {  // wave v reads list 16 x + v (and with region_split its back end)
-        const uint64_t list = (uint64_t)blockIdx.x * kWavesPerBlock + (tid >> 6);
-        const T* base = queues + list * region_cap;
-        segment(base, region_counts[list], 0u, tid & 63u, 64);
-        if (region_split) {
-            const uint32_t nb = region_counts[(uint64_t)gridDim.x * kWavesPerBlock + list];
-            segment(base + (region_cap - nb), nb, kResidSplit, tid & 63u, 64);
-        }
-    } else {
-        segment(queues, n, 0u, (uint64_t)blockIdx.x * kBlock + tid, (uint64_t)gridDim.x * kBlock);
+        for (; i < nv; i += gstride) add16(v[i]);
+        tail = nv * kPer;
+    }
+    for (uint64_t i = tail + gtid; i < n; i += gstride) {
+        const uint32_t q = queues[i];
+        guard(q, add(q));
     }
     __syncthreads();
     uint32_t* row = partial + (size_t)blockIdx.x * stride_words;
@@ -1156,32 +1113,27 @@ template <typename T>
 __global__ __launch_bounds__(kBlock) void rss_range8_fallback_col_kernel(
         const T* __restrict__ col, uint64_t n, uint32_t q_lo, uint32_t q_span,
         unsigned long long* counts, const uint32_t* __restrict__ poison,
-        const uint32_t* __restrict__ region_counts, uint64_t region_cap, uint32_t region_split) {
+        const uint32_t* __restrict__ region_counts, uint64_t region_cap) {
     if (!*poison) return;  // uniform across the grid
     extern __shared__ uint32_t bins[];
     const uint32_t tid = threadIdx.x;
+    uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
+    uint64_t gstride = (uint64_t)gridDim.x * kBlock;
+    if (region_counts) {  // one residual list per wave (see rss_queue_hist_wide_kernel)
+        const uint64_t list = (uint64_t)blockIdx.x * kWavesPerBlock + (tid >> 6);
+        col += list * region_cap;
+        n = region_counts[list];
+        gtid = tid & 63u;
+        gstride = 64;
+    }
     for (uint32_t lo = 0; lo < q_span; lo += kFallbackColSpan) {
         const uint32_t span = min(kFallbackColSpan, q_span - lo);
         for (uint32_t e = tid; e < span; e += kBlock) bins[e] = 0;
         __syncthreads();
-        auto count = [&](const T* __restrict__ qs, uint64_t cnt, uint32_t off, uint64_t gtid,
-                         uint64_t gstride) {
-            for (uint64_t i = gtid; i < cnt; i += gstride) {
-                const uint32_t r = (uint32_t)qs[i] + off - q_lo - lo;  // wraps below the slice
-                if (r < span)
-                    __hip_atomic_fetch_add(&bins[r], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-        };
-        if (region_counts) {  // one residual list per wave (see rss_queue_hist_wide_kernel)
-            const uint64_t list = (uint64_t)blockIdx.x * kWavesPerBlock + (tid >> 6);
-            const T* base = col + list * region_cap;
-            count(base, region_counts[list], 0u, tid & 63u, 64);
-            if (region_split) {
-                const uint32_t nb = region_counts[(uint64_t)gridDim.x * kWavesPerBlock + list];
-                count(base + (region_cap - nb), nb, kResidSplit, tid & 63u, 64);
-            }
-        } else {
-            count(col, n, 0u, (uint64_t)blockIdx.x * kBlock + tid, (uint64_t)gridDim.x * kBlock);
+        for (uint64_t i = gtid; i < n; i += gstride) {
+            const uint32_t r = (uint32_t)col[i] - q_lo - lo;  // wraps below the slice
+            if (r < span)
+                __hip_atomic_fetch_add(&bins[r], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         __syncthreads();
         for (uint32_t e = tid; e < span; e += kBlock)
@@ -2301,12 +2253,6 @@ bool resid_enabled() {
     return !(e && e[0] == '0');
 }
 
-// RSS_RESID_SPLIT=0: u32 residual lists past 65536 residual queues instead of two-ended u16 (A/B)
-bool resid_split_enabled() {
-    const char* e = getenv("RSS_RESID_SPLIT");
-    return !(e && e[0] == '0');
-}
-
 bool wide_hist_enabled() {
     const char* e = getenv("RSS_WIDE_HIST");
     return !(e && e[0] == '0');
@@ -2348,8 +2294,7 @@ int range8_debug() {
 template <typename T>
 int launch_wide8(const T* qcol, uint64_t n, uint32_t lo, uint32_t sp, unsigned long long* counts,
                  unsigned grid, int cu_count, hipStream_t stream,
-                 const uint32_t* region_counts = nullptr, uint64_t region_cap = 0,
-                 uint32_t region_split = 0) {
+                 const uint32_t* region_counts = nullptr, uint64_t region_cap = 0) {
     const uint32_t words = (sp + 3) / 4;
     const size_t rows_bytes = (size_t)grid * words * 4, tail_bytes = ((size_t)sp + 4) * 4;
     void* buf = nullptr;
@@ -2366,7 +2311,7 @@ int launch_wide8(const T* qcol, uint64_t n, uint32_t lo, uint32_t sp, unsigned l
     if (e == hipSuccess) {
         hipLaunchKernelGGL((rss_queue_hist_wide_kernel<T, 8>), dim3(grid), dim3(kBlock), words * 4,
                            stream, qcol, n, lo, sp, partial, words, counts, ovf, poison,
-                           region_counts, region_cap, region_split);
+                           region_counts, region_cap);
         e = hipGetLastError();
     }
     if (e == hipSuccess) {
@@ -2381,8 +2326,7 @@ int launch_wide8(const T* qcol, uint64_t n, uint32_t lo, uint32_t sp, unsigned l
         hipLaunchKernelGGL(rss_range8_fallback_col_kernel<T>,
                            dim3(region_counts ? grid : (unsigned)cu_count), dim3(kBlock),
                            std::min(kFallbackColSpan, sp) * 4, stream, qcol, n, lo, sp, counts,
-                           static_cast<const uint32_t*>(poison), region_counts, region_cap,
-                           region_split);
+                           static_cast<const uint32_t*>(poison), region_counts, region_cap);
         e = hipGetLastError();
     }
     int rc = e == hipSuccess ? RSS_OK
@@ -2403,7 +2347,7 @@ int launch_wide8(const T* qcol, uint64_t n, uint32_t lo, uint32_t sp, unsigned l
 int launch_queue_ranges(const void* qcol, int qw, uint64_t n, uint32_t first, uint32_t nqueues,
                         unsigned long long* counts, int cu_count, hipStream_t stream,
                         const uint32_t* region_counts = nullptr, uint64_t region_cap = 0,
-                        unsigned region_grid = 0, uint32_t region_split = 0) {
+                        unsigned region_grid = 0) {
     if (first >= nqueues) return RSS_OK;
     const uint32_t span = kNarrowSpan;
     // a wide pass costs about two narrow ones (2^28 tuples: ~0.2 vs ~0.1 ms over a u16
@@ -2424,9 +2368,9 @@ int launch_queue_ranges(const void* qcol, int qw, uint64_t n, uint32_t first, ui
                     const uint32_t sp8 = std::min<uint32_t>(kWideSpan8, nqueues - lo);
                     rc = qw == QW_U16
                              ? launch_wide8(static_cast<const uint16_t*>(qcol), n, lo, sp8, counts, grid,
-                                            cu_count, stream, region_counts, region_cap, region_split)
+                                            cu_count, stream, region_counts, region_cap)
                              : launch_wide8(static_cast<const uint32_t*>(qcol), n, lo, sp8, counts, grid,
-                                            cu_count, stream, region_counts, region_cap, region_split);
+                                            cu_count, stream, region_counts, region_cap);
                     if (rc == RSS_OK) {
                         lo += sp8;
                         continue;
@@ -2441,13 +2385,13 @@ int launch_queue_ranges(const void* qcol, int qw, uint64_t n, uint32_t first, ui
                                        stream, static_cast<const uint16_t*>(qcol), n, lo, sp,
                                        static_cast<uint32_t*>(partial), stride_words, counts,
                                        (uint32_t*)nullptr, (uint32_t*)nullptr, region_counts,
-                                       region_cap, region_split);
+                                       region_cap);
                 else
                     hipLaunchKernelGGL(rss_queue_hist_wide_kernel<uint32_t>, dim3(grid), dim3(kBlock), lds,
                                        stream, static_cast<const uint32_t*>(qcol), n, lo, sp,
                                        static_cast<uint32_t*>(partial), stride_words, counts,
                                        (uint32_t*)nullptr, (uint32_t*)nullptr, region_counts,
-                                       region_cap, region_split);
+                                       region_cap);
                 hipError_t e = hipGetLastError();
                 if (e == hipSuccess) {
                     const uint32_t words = (sp + 1) / 2;
@@ -2600,7 +2544,7 @@ int launch_range8(KernelFn fn, FallbackFn fallback, unsigned grid, int cu_count,
             hipLaunchKernelGGL(rss_range8_fallback_col_kernel<uint32_t>, dim3(cu_count), dim3(kBlock),
                                std::min(kFallbackColSpan, p.q_span) * 4, stream, qcol, p.n, p.q_lo,
                                p.q_span, p.counts, static_cast<const uint32_t*>(p.poison),
-                               (const uint32_t*)nullptr, (uint64_t)0, 0u);
+                               (const uint32_t*)nullptr, (uint64_t)0);
         else
             hipLaunchKernelGGL(fallback, dim3(cu_count), dim3(kBlock),
                                std::min(kFallbackSpan, p.q_span) * 4, stream, p);
@@ -2755,20 +2699,17 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
             const uint64_t rows = (n / 4 + per_row - 1) / per_row;
             const uint64_t cap = (rows * 4 * 64 + 4 + 7) & ~7ull;
             const uint32_t nres = q_eff - span8;
-            // u16 entries up to 65536 residual queues, two-ended u16 lists up to 131072
-            const bool split = nres > kResidSplit && nres <= 2 * kResidSplit && resid_split_enabled();
-            const size_t esize = nres <= kResidSplit || split ? 2 : 4;
+            const size_t esize = nres <= 65536u ? 2 : 4;
             const size_t nlists = (size_t)grid * kWavesPerBlock;
             const size_t list_bytes = nlists * cap * esize;
             void* lists = nullptr;
-            if (hipMallocAsync(&lists, list_bytes + nlists * 4 * (split ? 2 : 1), stream) == hipSuccess) {
+            if (hipMallocAsync(&lists, list_bytes + nlists * 4, stream) == hipSuccess) {
                 uint32_t* list_counts = reinterpret_cast<uint32_t*>(static_cast<char*>(lists) + list_bytes);
                 p.queue_out = nullptr;
                 p.resid_out = lists;
                 p.resid_counts = list_counts;
                 p.resid_cap = cap;
                 p.resid_u16 = esize == 2;
-                p.resid_split = split;
                 p.prefetch = prefetch_for(false);
                 p.q_lo = 0;
                 p.q_span = span8;
@@ -2776,11 +2717,10 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
                                      : pick_queue<false>(qmode, HIST_RANGE8, QW_U32, VM_SMALL_LUT);
                 rc = launch_range8(fn, fb8, grid, info.cu_count, p, nullptr, r8buf, stream);
                 p.resid_out = nullptr;
-                p.resid_split = 0;
                 if (rc == RSS_OK)
                     rc = launch_queue_ranges(lists, esize == 2 ? QW_U16 : QW_U32, n, 0, nres,
                                              p.counts + span8, info.cu_count, stream, list_counts,
-                                             cap, grid, split);
+                                             cap, grid);
                 const hipError_t fe = hipFreeAsync(lists, stream);  // after its readers
                 if (fe != hipSuccess && rc == RSS_OK)
                     rc = set_error(RSS_EIO, "hipFreeAsync failed: %s", hipGetErrorString(fe));

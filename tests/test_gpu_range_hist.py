@@ -283,7 +283,7 @@ def _with_env(name, value, fn):
 
 
 @pytest.mark.parametrize("Q", [SPAN16 + 1, 131072, SPAN8, SPAN8 + 1, SPAN8 + 65535, SPAN8 + 65536,
-                               SPAN8 + 65537, 262144, SPAN8 + 131072, SPAN8 + 131073, SPAN8 + 65536 + WIDE8 + 1, 10 ** 6,
+                               262144, SPAN8 + 65536 + WIDE8 + 1, 10 ** 6,
                                SPAN8 + 9 * WIDE8, SPAN8 + 9 * WIDE8 + 1])
 def test_range8_u8_bins_equal_oracle(native, oracle_lib, example_key, Q):
     """Past 80572 queues the small-table pass counts up to 161144 of them in u8 LDS bins
@@ -296,9 +296,7 @@ def test_range8_u8_bins_equal_oracle(native, oracle_lib, example_key, Q):
     oracle's hashes, queues and counts, with and without per-tuple outputs.  Counts only past
     161144 queues the hash pass appends the residual queues to per-workgroup lists that the
     wide passes read one workgroup per list (default), or writes the scratch column
-    (RSS_RESID=0); both with the load prefetch and with the static walk (RSS_PREFETCH=0).
-    Between 65537 and 131072 residual queues the lists are u16 from both ends (residuals past
-    65536 from the back), or u32 (RSS_RESID_SPLIT=0)."""
+    (RSS_RESID=0); both with the load prefetch and with the static walk (RSS_PREFETCH=0)."""
     n, H = (1 << 21) + 5, 1 << 30
     host = oracle_lib.generate(31, 0, n)
     tup = torch.from_numpy(host.view(np.int32).reshape(-1)).to("cuda:0")
@@ -306,7 +304,7 @@ def test_range8_u8_bins_equal_oracle(native, oracle_lib, example_key, Q):
     ho, qo, co = oracle_lib.run(example_key, host, H, Q)
     runs = [("RSS_RANGE8_DEBUG", "nofallback"), ("RSS_RANGE8_DEBUG", "force"),
             ("RSS_RANGE8", "1"), ("RSS_RANGE8", "0"), ("RSS_RESID", "0"),
-            ("RSS_PREFETCH", "0"), ("RSS_RESID_SPLIT", "0")]
+            ("RSS_PREFETCH", "0")]
     for name, value in runs:
         for outputs in (True, False):
             h, q, c = _with_env(name, value,
@@ -347,8 +345,6 @@ def test_range8_guard_moves(native, oracle_lib, example_key, Q):
                                              (200000, True, 0, SPAN8), (200000, False, 0, SPAN8),
                                              (400000, True, SPAN8, SPAN8 + WIDE8),
                                              (400000, False, SPAN8, SPAN8 + WIDE8),
-                                             (262144, False, SPAN8, SPAN8 + 65536),
-                                             (262144, False, SPAN8 + 65536, 262144),
                                              (10 ** 6, True, SPAN8 + 2 * WIDE8, SPAN8 + 3 * WIDE8),
                                              (10 ** 6, False, SPAN8 + 2 * WIDE8, SPAN8 + 3 * WIDE8)])
 def test_range8_poisoned_pass_recounts(native, oracle_lib, example_key, Q, outputs, lo, hi):
@@ -359,8 +355,7 @@ def test_range8_poisoned_pass_recounts(native, oracle_lib, example_key, Q, outpu
     rows and the recount (from the u32 queue column, or by rehashing for a counts-only hash
     pass) gives the exact counts -- also when accumulating onto the caller's counts.  Q = 10^6:
     the wrapping bin is the third u8 wide pass's (over the u32 queue column, or over the
-    residual lists).  Q = 262144 counts only: the wrapping bin is the wide pass's over
-    two-ended residual lists, its queue at the lists' front or back end."""
+    residual lists)."""
     n_same, n_rand, H = 1 << 22, 4099, 1 << 30
     rnd = oracle_lib.generate(33, 0, n_rand)
     _, q_rnd, _ = oracle_lib.run(example_key, rnd, H, Q)
@@ -384,7 +379,7 @@ def test_range8_poisoned_pass_recounts(native, oracle_lib, example_key, Q, outpu
     assert not np.array_equal(bad.cpu().numpy().view(np.uint64), want)
 
 
-@pytest.mark.parametrize("Q,outputs", [(131072, True), (131072, False), (262144, False), (400000, False),
+@pytest.mark.parametrize("Q,outputs", [(131072, True), (131072, False), (400000, False),
                                        (10 ** 6, True), (10 ** 6, False)])
 def test_range8_zipf_flows_equal_oracle(native, oracle_lib, example_key, Q, outputs):
     """Skewed traffic: 2^22 tuples drawn Zipf(1.3) from 50000 distinct flows, shuffled -- a

@@ -3,8 +3,7 @@ same buffers (tool, not product): 2^28 uniform tuples, H = 2^30, full outputs (h
 queue u32) and counts only; medians of 10 launches after 5 warm ones, alternating variants in
 two rounds.  `force` = the poison-gated recount on every launch (RSS_RANGE8_DEBUG=force: what
 a batch that wraps a u8 bin costs); `column` = counts only through a scratch queue column
-instead of residual lists (RSS_RESID=0); `u32lists` = counts only with u32 residual lists
-where two-ended u16 ones would do (RSS_RESID_SPLIT=0).  Prints one JSON line per Q.
+instead of residual lists (RSS_RESID=0).  Prints one JSON line per Q.
 
 usage: python tools/range8_probe.py [Q ...]"""
 import json
@@ -28,7 +27,7 @@ _native.generate_device(SEED, 0, n, tup.data_ptr(), s.cuda_stream)
 h = torch.empty(n, dtype=torch.int32, device=dev)
 q = torch.empty(n, dtype=torch.int32, device=dev)
 VARIANTS = {"u8": {}, "u16": {"RSS_RANGE8": "0"}, "force": {"RSS_RANGE8_DEBUG": "force"},
-            "column": {"RSS_RESID": "0"}, "u32lists": {"RSS_RESID_SPLIT": "0"}}
+            "column": {"RSS_RESID": "0"}}
 
 
 def timed(Q, outputs, env, reps=10, warm=5):
@@ -65,7 +64,7 @@ for Q in qs:
         for name, env in VARIANTS.items():
             if name == "force" and rnd:
                 continue
-            for outputs in ((True, False) if name != "u32lists" else (False,)):
+            for outputs in (True, False):
                 k = "%s_%s_ms" % (name, "full" if outputs else "counts")
                 t = timed(Q, outputs, env)
                 rec[k] = round(min(t, rec.get(k, t)), 4)
