@@ -963,12 +963,12 @@ __global__ __launch_bounds__(kBlock) void rss_queue_hist_wide_kernel(
         if (f == kHalf - 1u) {
             __hip_atomic_fetch_sub(&bins[r / kPerWord], kHalf << sh, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_WORKGROUP);
-            if constexpr (kBits == 8)
+            if (ovf)  // (always for u8; u16 passes of launch_queue_ranges too)
                 atomicAdd(&ovf[r], 1u);
             else
                 atomicAdd(&counts[q], (unsigned long long)kHalf);
-        } else if constexpr (kBits == 8) {
-            if (f == kField) __hip_atomic_store(poison, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (f == kField && poison) {
+            __hip_atomic_store(poison, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     };
     constexpr uint32_t kPer = 16 / sizeof(T);  // queues per 16-B load
@@ -1065,7 +1065,7 @@ __global__ __launch_bounds__(kReduceCols * kReduceGroups) void rss_partial_reduc
             for (uint32_t g = 1; g < kReduceGroups; ++g) acc[f] += part[g][col][f];
             const uint32_t q = kPer * word + f;
             if (q < q_span) {
-                const unsigned long long v = acc[f] + (ovf ? 128ull * ovf[q] : 0ull);
+                const unsigned long long v = acc[f] + (ovf ? (1ull << (kBits - 1)) * ovf[q] : 0ull);
                 if (v) counts[q_lo + q] += v;
             }
         }
@@ -2380,29 +2380,60 @@ int launch_queue_ranges(const void* qcol, int qw, uint64_t n, uint32_t first, ui
                 }
                 const uint32_t sp = std::min<uint32_t>(kWideSpan, nqueues - lo);
                 const uint32_t lds = ((sp + 1) / 2) * 4;
-                if (qw == QW_U16)
-                    hipLaunchKernelGGL(rss_queue_hist_wide_kernel<uint16_t>, dim3(grid), dim3(kBlock), lds,
-                                       stream, static_cast<const uint16_t*>(qcol), n, lo, sp,
-                                       static_cast<uint32_t*>(partial), stride_words, counts,
-                                       (uint32_t*)nullptr, (uint32_t*)nullptr, region_counts,
-                                       region_cap);
-                else
-                    hipLaunchKernelGGL(rss_queue_hist_wide_kernel<uint32_t>, dim3(grid), dim3(kBlock), lds,
-                                       stream, static_cast<const uint32_t*>(qcol), n, lo, sp,
-                                       static_cast<uint32_t*>(partial), stride_words, counts,
-                                       (uint32_t*)nullptr, (uint32_t*)nullptr, region_counts,
-                                       region_cap);
-                hipError_t e = hipGetLastError();
+                // the guard moves (u32 per queue, units of 2^15) and a poison word: a bin that
+                // wraps anyway (the in-flight bound of the guard failed) discards the pass's
+                // rows and moves, and the column recount replaces them, as for u8 passes
+                void* tail = nullptr;
+                if (hipMallocAsync(&tail, ((size_t)sp + 4) * 4, stream) != hipSuccess) {
+                    (void)hipGetLastError();
+                    rc = set_error(RSS_ENOMEM, "rss_hash_device: no memory for a wide pass's guard moves");
+                    break;
+                }
+                uint32_t* ovf = static_cast<uint32_t*>(tail);
+                uint32_t* poison = ovf + sp;
+                const int debug = range8_debug();
+                hipError_t e = hipMemsetAsync(tail, 0, ((size_t)sp + 4) * 4, stream);
+                if (e == hipSuccess && debug == 1) e = hipMemsetD32Async(poison, 1, 1, stream);
+                if (e == hipSuccess) {
+                    if (qw == QW_U16)
+                        hipLaunchKernelGGL(rss_queue_hist_wide_kernel<uint16_t>, dim3(grid), dim3(kBlock), lds,
+                                           stream, static_cast<const uint16_t*>(qcol), n, lo, sp,
+                                           static_cast<uint32_t*>(partial), stride_words, counts, ovf,
+                                           poison, region_counts, region_cap);
+                    else
+                        hipLaunchKernelGGL(rss_queue_hist_wide_kernel<uint32_t>, dim3(grid), dim3(kBlock), lds,
+                                           stream, static_cast<const uint32_t*>(qcol), n, lo, sp,
+                                           static_cast<uint32_t*>(partial), stride_words, counts, ovf,
+                                           poison, region_counts, region_cap);
+                    e = hipGetLastError();
+                }
                 if (e == hipSuccess) {
                     const uint32_t words = (sp + 1) / 2;
                     hipLaunchKernelGGL(rss_partial_reduce_kernel<16>,
                                        dim3((words + kReduceCols - 1) / kReduceCols),
                                        dim3(kReduceCols * kReduceGroups), 0, stream,
                                        static_cast<const uint32_t*>(partial), grid, stride_words,
-                                       lo, sp, counts, (const uint32_t*)nullptr,
-                                       (const uint32_t*)nullptr);
+                                       lo, sp, counts, static_cast<const uint32_t*>(ovf),
+                                       debug == 2 ? nullptr : static_cast<const uint32_t*>(poison));
                     e = hipGetLastError();
                 }
+                if (e == hipSuccess && debug != 2) {
+                    const unsigned fgrid = region_counts ? grid : (unsigned)cu_count;
+                    const uint32_t flds = std::min(kFallbackColSpan, sp) * 4;
+                    if (qw == QW_U16)
+                        hipLaunchKernelGGL(rss_range8_fallback_col_kernel<uint16_t>, dim3(fgrid), dim3(kBlock),
+                                           flds, stream, static_cast<const uint16_t*>(qcol), n, lo, sp,
+                                           counts, static_cast<const uint32_t*>(poison), region_counts,
+                                           region_cap);
+                    else
+                        hipLaunchKernelGGL(rss_range8_fallback_col_kernel<uint32_t>, dim3(fgrid), dim3(kBlock),
+                                           flds, stream, static_cast<const uint32_t*>(qcol), n, lo, sp,
+                                           counts, static_cast<const uint32_t*>(poison), region_counts,
+                                           region_cap);
+                    e = hipGetLastError();
+                }
+                const hipError_t te = hipFreeAsync(tail, stream);  // after its readers
+                if (e == hipSuccess) e = te;
                 if (e != hipSuccess)
                     rc = set_error(RSS_EIO, "wide queue histogram launch failed: %s", hipGetErrorString(e));
                 lo += sp;
