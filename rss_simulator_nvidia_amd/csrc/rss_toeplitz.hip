@@ -918,6 +918,8 @@ constexpr uint32_t kNarrowSpan = 16384;  // rss_queue_hist_kernel: u32 bins, two
 // kBits = 8: u8 bins, four per dword, with HIST_RANGE8's guard (0x7F -> a move of 128 into
 // ovf[r]) and poison word (a field that wrapped; the reduce is gated on it and
 // rss_range8_fallback_col_kernel recounts the range) -- 163840 queues per read of the column.
+// u16 passes with ovf / poison (launch_queue_ranges) the same with moves of 2^15: their
+// in-flight bound held in every run but one, and a wrap must not go unseen.
 // regions (region_counts != NULL): the column is one list per hash-pass wave -- wave v of
 // workgroup x reads the region_counts[16 x + v] entries at queues + (16 x + v) * region_cap
 // (the hash pass's residual lists, resid_append) instead of grid-striding over n entries.
@@ -2278,9 +2280,10 @@ bool range8_enabled() {
     return !(e && e[0] == '0');
 }
 
-// Tests only: RSS_RANGE8_DEBUG=force sets the poison word before the pass (the fallback then
-// recounts every launch); =nofallback drops the gate and the fallback (a wrap would then show
-// as wrong counts -- proves a launch's counts came from the u8 bins and their guard moves)
+// Tests only: RSS_RANGE8_DEBUG=force sets the poison word before every u8 pass and u16 wide
+// pass (the fallback then recounts every launch); =nofallback drops the gate and the fallback
+// (a wrap would then show as wrong counts -- proves a launch's counts came from the bins and
+// their guard moves)
 int range8_debug() {
     const char* e = getenv("RSS_RANGE8_DEBUG");
     if (!e) return 0;
