@@ -84,8 +84,7 @@ enum HistMode { HIST_PRIVATE = 0, HIST_SHARED = 1, HIST_GLOBAL = 2, HIST_NONE = 
 // guard at 0x80 and a poison word for a bin that wraps (range8_guard) -- 161144 queues in the
 // LDS beside the small tables, one pass.
 // HIST_RANGE16 (IPv4 kernel): HIST_RANGE with u16 bins, two per dword, twice the queues in the
-// same LDS -- with the wide pass's guard bit (rss_queue_hist_wide_kernel): the add that
-// returns 0x7FFF moves 2^15 of its bin into the global counts.
+// same LDS -- a guard at 0x8000 and a poison word like HIST_RANGE8's (range16_guard).
 // HIST_RANGE: shared u32 LDS bins for queues [q_lo, q_lo + q_span) only -- the IPv6 kernel's
 // first range of a multi-pass launch for nqueues whose bins do not fit the LDS beside its
 // tables (launch_hash6), instead of one global atomic per tuple (13x slower).
@@ -102,7 +101,7 @@ struct LaunchParams {
     void* queue_out;
     unsigned long long* counts;
     unsigned long long* ws;       // single-pass counts workspace (rss_hash_device_ws) or NULL
-    uint32_t accumulate;          // with ws: fold mode (kFoldAccumulate | kFoldOrdered)
+    uint32_t accumulate;          // with ws: fold mode (kFoldAccumulate)
     uint64_t n;
     uint64_t h_m64;     // ceil(2^64 / H) for the non-power-of-two htable path
     uint32_t h_mask;    // H - 1 when H is a power of two
@@ -115,13 +114,14 @@ struct LaunchParams {
     uint32_t q_m16;     // ceil(2^16 / Q): exact b % Q for b < 256 (QM_FAST8, packed search)
     const uint32_t* key_windows;  // key search: nkeys x 96 windows in device memory
     uint32_t q_lo, q_span;        // HIST_RANGE: the queues this pass counts
-    uint32_t* partial;            // HIST_RANGE16: u16 [grid][partial_stride] rows, or NULL
-    uint32_t partial_stride;      //   (atomics into counts); dwords per row
+    uint32_t* partial;            // HIST_RANGE16 / RANGE8: u16 / u8 [grid][partial_stride] rows;
+    uint32_t partial_stride;      //   dwords per row
     uint32_t q_stride;            // key search: row stride of the [keys, nqueues] counts (>= Q)
     uint32_t tail_rows;           // balanced tail: rows handed out as units (0 = static grid-stride)
     uint32_t bal_off;             // balanced tail: byte offset of its LDS slot (dynamic LDS)
-    uint32_t* ovf;                // HIST_RANGE8: u32 [q_span] guard moves (units of 128)
-    uint32_t* poison;             // HIST_RANGE8: set when a u8 bin wrapped (results discarded)
+    uint32_t* ovf;                // HIST_RANGE16 / RANGE8: u32 [q_span] guard moves (2^15 / 128)
+    uint32_t* poison;             //   set when a bin wrapped (rows and moves discarded)
+    uint32_t fb_span;             // the recount's queues per slice (its u32 bins in the LDS)
     uint32_t prefetch;            // small-table passes: next group's loads before this group's LDS work
     unsigned long long* tail_ctr; // balanced tail's unit counter when the launch has no ws (HIST_RANGE8)
     void* resid_out;              // HIST_RANGE8 counts only: per-wave lists of q - q_span for the
@@ -336,9 +336,36 @@ __device__ __forceinline__ uint32_t queue_lookup(uint32_t b, const LaunchParams&
     }
 }
 
+#ifdef RSS_TEST_HOOKS
+// Test-hooks build only: the largest number of adds that landed on a guarded bin between the
+// add that took it to half range and the guard's subtract, per guard kind (kMarginHash16: the
+// hash pass's u16 bins, kMarginWide16: the u16 wide passes, kMarginHash8 / kMarginWide8: the
+// u8 ones, modulo 256) -- read by rss_test_guard_margin.
+enum { kMarginHash16 = 0, kMarginWide16 = 1, kMarginHash8 = 2, kMarginWide8 = 3, kMargins = 4 };
+__device__ uint32_t g_guard_margin[kMargins];
+// `at`: the field's value when the subtract landed = half + the adds in between (mod 2^bits)
+template <int kBits>
+__device__ __forceinline__ void record_margin(int kind, uint32_t at) {
+    constexpr uint32_t kHalf = 1u << (kBits - 1), kField = (1u << kBits) - 1u;
+    __hip_atomic_fetch_max(&g_guard_margin[kind], (at - kHalf) & kField, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+#define RSS_RECORD_MARGIN(bits, kind, at) record_margin<bits>(kind, at)
+#else
+#define RSS_RECORD_MARGIN(bits, kind, at) ((void)(at))
+#endif
+
 // HIST_RANGE16's two halves: the add (returns the dword's previous value, 0 out of range)
-// and the guard bit (the add that returned 0x7FFF moves 2^15 out of its bin).  The 4-tuple
-// body issues its four adds before the four guards, so they do not wait for each other.
+// and the guard (the add that returned 0x7FFF, so that its bin now holds 0x8000, subtracts
+// 0x8000 from the bin and counts one move of 2^15 in p.ovf[r]).  The 4-tuple body issues its
+// four adds before the four guards, so they do not wait for each other.
+// Nothing bounds the adds that land on the bin between that add and the subtract: the
+// workgroup's other waves keep adding while the guard's wave waits for its returns, and wave
+// issue is not fair.  So a bin can pass 0xFFFF and carry into its neighbour (observed once in
+// a u16 wide pass, profiles/r04/u16_guard/).  Exactly the add that takes a field past 0xFFFF
+// returns 0xFFFF, and it raises *p.poison: the launch's rows and moves are then discarded (the
+// reduce is gated on !poison) and rss_range_fallback_kernel / rss_range_fallback_col_kernel
+// recount the range with u32 bins (gated on poison) -- exact whatever the timing.
 __device__ __forceinline__ uint32_t range16_add(uint32_t* bins, uint32_t q, const LaunchParams& p) {
     const uint32_t r = q - p.q_lo;  // wraps for q < q_lo
     if (r >= p.q_span) return 0u;
@@ -349,11 +376,16 @@ __device__ __forceinline__ uint32_t range16_add(uint32_t* bins, uint32_t q, cons
 __device__ __forceinline__ void range16_guard(uint32_t* bins, uint32_t q, uint32_t old,
                                               const LaunchParams& p) {
     const uint32_t r = q - p.q_lo;
+    if (r >= p.q_span) return;
     const uint32_t sh = (r & 1u) * 16u;
-    if (r < p.q_span && ((old >> sh) & 0xFFFFu) == 0x7FFFu) {
-        __hip_atomic_fetch_sub(&bins[r >> 1], 0x8000u << sh, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
-        atomicAdd(&p.counts[q], 0x8000ull);
+    const uint32_t f = (old >> sh) & 0xFFFFu;
+    if (f == 0x7FFFu) {
+        const uint32_t at = __hip_atomic_fetch_sub(&bins[r >> 1], 0x8000u << sh, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+        RSS_RECORD_MARGIN(16, kMarginHash16, (at >> sh) & 0xFFFFu);
+        atomicAdd(&p.ovf[r], 1u);
+    } else if (f == 0xFFFFu) {
+        __hip_atomic_store(p.poison, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -381,8 +413,9 @@ __device__ __forceinline__ void range8_guard(uint32_t* bins, uint32_t q, uint32_
     const uint32_t sh = (r & 3u) * 8u;
     const uint32_t f = (old >> sh) & 0xFFu;
     if (f == 0x7Fu) {
-        __hip_atomic_fetch_sub(&bins[r >> 2], 0x80u << sh, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint32_t at = __hip_atomic_fetch_sub(&bins[r >> 2], 0x80u << sh, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+        RSS_RECORD_MARGIN(8, kMarginHash8, (at >> sh) & 0xFFu);
         atomicAdd(&p.ovf[r], 1u);
     } else if (f == 0xFFu) {
         __hip_atomic_store(p.poison, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -463,30 +496,17 @@ __device__ __forceinline__ void store_queue4(void* out, Idx g, uint32_t q0, uint
 // a hipMemsetAsync before the launch).  With one (rss_hash_device_ws, single-pass counts) the
 // launch writes the batch's counts itself (overwriting, or adding when `mode &
 // kFoldAccumulate`) and leaves the workspace zero for the next launch -- so a batch's counts
-// need no zeroing launch before it:
-// * arrival fold (default, round 3): each workgroup adds (1 << 44) | total into ws[1 + q] for
-//   every queue; the add whose returned arrival count is gridDim.x - 1 is the queue's last, so
-//   its workgroup writes counts[q] = old sum + its own and resets ws[1 + q].  Every queue is
-//   finalised by one atomic round trip and needs no release/acquire: its count travels in
-//   the atomics on one location (the balanced tail's unit counter is reset in walk_rows by
-//   the launch's final claim, also one location).
-// * ticket fold (`mode & kFoldTicket`, RSS_FOLD=ticket; rounds 2-3): the totals go into
-//   ws[1..Q], each workgroup then takes a ticket (ws[0]), and the last of the gridDim.x
-//   workgroups exchanges the sums into the counts -- adds, ticket and exchanges are three
-//   serialised round trips on the last workgroup's path.  Ordered: the ticket is an
-//   agent-scope RELEASE and the last workgroup fences with an ACQUIRE before reading the sums
-//   (+1.3-1.5 us per 2^28-tuple launch over the relaxed form, tools/ws_order_ab.py; a full
-//   __threadfence around the ticket cost 90 us).  Relaxed, it relies on gfx950 performing
-//   device-scope atomics at one coherence point past the XCDs' L2s and on every lane waiting
-//   for its adds' return values before the barrier that precedes the ticket.
-// `flag` is one LDS word the caller no longer reads (its bins, after every lane has summed
-// them); both folds are stress-tested in tests/test_gpu_single_pass.py.
-constexpr uint32_t kFoldAccumulate = 1u, kFoldOrdered = 2u, kFoldTicket = 4u;
-// Arrival fold (default): ws[1 + q] = (arrivals << kArrivalShift) | sum -- every workgroup adds
-// (1 << kArrivalShift) | its total for every queue, and the add that returns arrivals ==
-// gridDim.x - 1 holds the queue's final sum (old + own): one atomic round trip on the last
-// workgroup's path instead of three (adds, ticket, exchanges).  Sums stay below 2^44 (a launch
-// is < 2^44 tuples) and arrivals below 2^20 workgroups.
+// need no zeroing launch before it.  Arrival fold: each workgroup adds (1 << kArrivalShift) |
+// total into ws[1 + q] for every queue; the add whose returned arrival count is gridDim.x - 1
+// is the queue's last, so its workgroup writes counts[q] = old sum + its own and resets
+// ws[1 + q].  Every queue is finalised by one atomic round trip and needs no release/acquire:
+// its count travels in the atomics on one location (the balanced tail's unit counter is
+// reset in walk_rows by the launch's final claim, also one location).  Stress-tested in
+// tests/test_gpu_single_pass.py.  (Rounds 2-3 used a ticket fold -- totals, a ticket, the
+// last workgroup's exchanges: three serialised round trips on the last workgroup's path.)
+constexpr uint32_t kFoldAccumulate = 1u;
+// ws[1 + q] = (arrivals << kArrivalShift) | sum.  Sums stay below 2^44 (a launch is < 2^44
+// tuples) and arrivals below 2^20 workgroups.
 constexpr uint32_t kArrivalShift = 44;
 constexpr unsigned long long kArrivalOne = 1ull << kArrivalShift;
 constexpr unsigned long long kSumMask = kArrivalOne - 1;
@@ -498,8 +518,7 @@ __host__ __device__ __forceinline__ unsigned long long* ws_tail_counter(unsigned
 
 template <typename SumOf>
 __device__ __forceinline__ void fold_counts(SumOf sum_of, uint32_t Q, unsigned long long* counts,
-                                            unsigned long long* ws, uint32_t mode,
-                                            uint32_t* flag) {
+                                            unsigned long long* ws, uint32_t mode) {
     const uint32_t tid = threadIdx.x;
     if (!ws) {
         for (uint32_t q = tid; q < Q; q += blockDim.x) {
@@ -508,47 +527,17 @@ __device__ __forceinline__ void fold_counts(SumOf sum_of, uint32_t Q, unsigned l
         }
         return;
     }
-    if (!(mode & kFoldTicket)) {
-        const bool accumulate = (mode & kFoldAccumulate) != 0;
-        const unsigned long long last = (unsigned long long)gridDim.x - 1;
-        for (uint32_t q = tid; q < Q; q += blockDim.x) {
-            const unsigned long long add = kArrivalOne | sum_of(q);
-            // the sums travel in the atomics on one word each: no fence is needed
-            const unsigned long long old = atomicAdd(&ws[1 + q], add);
-            if ((old >> kArrivalShift) == last) {  // every other workgroup's add is in `old`
-                const unsigned long long total = (old & kSumMask) + (add & kSumMask);
-                counts[q] = accumulate ? counts[q] + total : total;
-                atomicExch(&ws[1 + q], 0ull);  // after every add of this launch to it
-            }
-        }
-        return;
-    }
-    // Ticket fold (RSS_FOLD=ticket, rounds 2-3): sums into ws[1..Q], a ticket at ws[0], and the
-    // last of the gridDim.x workgroups exchanges the sums into the counts
+    const bool accumulate = (mode & kFoldAccumulate) != 0;
+    const unsigned long long last = (unsigned long long)gridDim.x - 1;
     for (uint32_t q = tid; q < Q; q += blockDim.x) {
-        const uint32_t s = sum_of(q);
-        if (s) {
-            const unsigned long long old = atomicAdd(&ws[1 + q], (unsigned long long)s);
-            asm volatile("" ::"v"((uint32_t)old));  // wait for the performed add
+        const unsigned long long add = kArrivalOne | sum_of(q);
+        // the sums travel in the atomics on one word each: no fence is needed
+        const unsigned long long old = atomicAdd(&ws[1 + q], add);
+        if ((old >> kArrivalShift) == last) {  // every other workgroup's add is in `old`
+            const unsigned long long total = (old & kSumMask) + (add & kSumMask);
+            counts[q] = accumulate ? counts[q] + total : total;
+            atomicExch(&ws[1 + q], 0ull);  // after every add of this launch to it
         }
-    }
-    __syncthreads();   // every lane's adds performed, every lane done reading the bins
-    if (tid == 0) {
-        const unsigned long long ticket =
-            (mode & kFoldOrdered)
-                ? __hip_atomic_fetch_add(&ws[0], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT)
-                : atomicAdd(&ws[0], 1ull);
-        *flag = ticket == (unsigned long long)gridDim.x - 1;
-    }
-    __syncthreads();
-    if (*flag) {       // uniform across the workgroup
-        if (mode & kFoldOrdered) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        const bool accumulate = (mode & kFoldAccumulate) != 0;
-        for (uint32_t q = tid; q < Q; q += blockDim.x) {
-            const unsigned long long v = atomicExch(&ws[1 + q], 0ull);  // read + reset
-            counts[q] = accumulate ? counts[q] + v : v;
-        }
-        if (tid == 0) atomicExch(&ws[0], 0ull);
     }
 }
 
@@ -604,10 +593,7 @@ __device__ __forceinline__ void walk_rows(Group group, uint64_t ngroups, uint32_
 inline uint32_t balanced_tail_rows(uint64_t ngroups, unsigned grid) {
     const uint64_t per_row = (uint64_t)grid * kBlock;
     const uint64_t rows = (ngroups + per_row - 1) / per_row;
-    const char* e = getenv("RSS_TAIL_DIV");  // (A/B) the tail is rows / div, default 10
-    const long v = e ? atol(e) : 10;
-    const uint64_t div = v >= 2 ? (uint64_t)v : 10u;
-    return rows >= 16 ? (uint32_t)std::max<uint64_t>(1, rows / div) : 0u;
+    return rows >= 16 ? (uint32_t)std::max<uint64_t>(1, rows / 10) : 0u;
 }
 
 // HIST_RANGE8 counts only, queues past the pass's LDS range (q >= q_span): instead of a queue
@@ -829,26 +815,17 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz_kernel(const LaunchParams
             } else {
                 return bins[q];
             }
-        }, p.Q, p.counts, p.ws, p.accumulate, bins);
+        }, p.Q, p.counts, p.ws, p.accumulate);
     } else if constexpr (kHist == HIST_RANGE) {
         __syncthreads();
         for (uint32_t r = tid; r < p.q_span; r += kBlock)
             if (bins[r]) atomicAdd(&p.counts[p.q_lo + r], (unsigned long long)bins[r]);
     } else if constexpr (kHist == HIST_RANGE16) {
-        __syncthreads();
-        if (p.partial) {  // one row of the u16 partial matrix (rss_partial_reduce_kernel)
-            uint32_t* row = p.partial + (size_t)blockIdx.x * p.partial_stride;
-            for (uint32_t w = tid; w < nbins; w += kBlock) row[w] = bins[w];
-            return;
-        }
-        for (uint32_t w = tid; w < nbins; w += kBlock) {
-            const uint32_t x = bins[w], r = 2 * w;
-            if (x & 0xFFFFu) atomicAdd(&p.counts[p.q_lo + r], (unsigned long long)(x & 0xFFFFu));
-            if ((x >> 16) && r + 1 < p.q_span)
-                atomicAdd(&p.counts[p.q_lo + r + 1], (unsigned long long)(x >> 16));
-        }
+        __syncthreads();  // one row of the u16 partial matrix (rss_partial_reduce_kernel)
+        uint32_t* row = p.partial + (size_t)blockIdx.x * p.partial_stride;
+        for (uint32_t w = tid; w < nbins; w += kBlock) row[w] = bins[w];
     } else if constexpr (kHist == HIST_RANGE8) {
-        __syncthreads();  // one row of the u8 partial matrix (the launcher always gives one)
+        __syncthreads();  // one row of the u8 partial matrix
         uint32_t* row = p.partial + (size_t)blockIdx.x * p.partial_stride;
         for (uint32_t w = tid; w < nbins; w += kBlock) row[w] = bins[w];
         if constexpr (kSmallLut)  // (lane 0 took part in every append of its wave)
@@ -903,30 +880,25 @@ __global__ __launch_bounds__(kBlock) void rss_queue_hist_kernel(const T* __restr
 }
 
 // Queue ranges past the first pass's LDS bins, wide: ONE pass over the queue column per
-// range of up to kWideSpan queues (instead of one per 8192).  Bins are u16 in LDS, two per
-// dword, with a guard bit: the add that returns 0x7FFF (so the bin now holds 0x8000) moves
-// 2^15 out of the bin into the global counts itself.  Exactly one add sees 0x7FFF per wrap,
-// and the bin cannot reach 0x10000 (a carry into its neighbour) before that lane's subtract
-// lands: the other adds in flight meanwhile are bounded by the workgroup's lanes, far below
-// 2^15.  Each workgroup then stores its bins as one row of a u16 [grid][stride] matrix with
-// plain coalesced stores -- not Q atomics per workgroup, which would cost more than the pass
-// at Q = 65536 -- and rss_partial_reduce_kernel sums the rows into the counts.
+// range of up to kWideSpan (u16 bins) or kWideSpan8 (u8 bins) queues instead of one per
+// 16384 u32 bins.  The bins carry the hash pass's guard and poison word (range16_guard /
+// range8_guard): the add that takes a field to half range moves half into ovf[r], the add
+// that sees a full field (a wrap) poisons the pass, whose rows and moves the reduce then
+// discards while rss_range_fallback_col_kernel recounts the range.  Each workgroup stores its
+// bins as one row of a [grid][stride] matrix with plain coalesced stores -- not Q atomics per
+// workgroup, which would cost more than the pass at Q = 65536 -- and
+// rss_partial_reduce_kernel sums the rows and moves into the counts.
 constexpr uint32_t kWideSpan = 65536;  // 128 KiB of u16 bins: one workgroup per CU
 constexpr uint32_t kWideSpan8 = 163840;  // u8 bins (kBits = 8): the whole 160 KiB LDS
 constexpr uint32_t kNarrowSpan = 16384;  // rss_queue_hist_kernel: u32 bins, two workgroups per CU
 
-// kBits = 8: u8 bins, four per dword, with HIST_RANGE8's guard (0x7F -> a move of 128 into
-// ovf[r]) and poison word (a field that wrapped; the reduce is gated on it and
-// rss_range8_fallback_col_kernel recounts the range) -- 163840 queues per read of the column.
-// u16 passes with ovf / poison (launch_queue_ranges) the same with moves of 2^15: their
-// in-flight bound held in every run but one, and a wrap must not go unseen.
 // regions (region_counts != NULL): the column is one list per hash-pass wave -- wave v of
 // workgroup x reads the region_counts[16 x + v] entries at queues + (16 x + v) * region_cap
 // (the hash pass's residual lists, resid_append) instead of grid-striding over n entries.
 template <typename T, int kBits = 16>
 __global__ __launch_bounds__(kBlock) void rss_queue_hist_wide_kernel(
         const T* __restrict__ queues, uint64_t n, uint32_t q_lo, uint32_t q_span,
-        uint32_t* __restrict__ partial, uint32_t stride_words, unsigned long long* counts,
+        uint32_t* __restrict__ partial, uint32_t stride_words,
         uint32_t* __restrict__ ovf, uint32_t* __restrict__ poison,
         const uint32_t* __restrict__ region_counts, uint64_t region_cap) {
     constexpr uint32_t kPerWord = 32 / kBits, kField = (1u << kBits) - 1u;
@@ -954,22 +926,20 @@ __global__ __launch_bounds__(kBlock) void rss_queue_hist_wide_kernel(
                                       __HIP_MEMORY_SCOPE_WORKGROUP);
     };
     // the guard: the add that returned kHalf - 1 (its bin now holds kHalf) moves kHalf out.
-    // Checked after a group's adds are all issued, so they do not wait for each other.  u16:
-    // the adds in flight meanwhile are bounded by the workgroup's lanes, far below 2^15; u8:
-    // not bounded below 128, so the add that sees 0xFF (a wrap) poisons the pass.
+    // Checked after a group's adds are all issued, so they do not wait for each other.  The
+    // adds that land before its subtract are not bounded (range16_guard), so the add that sees
+    // kField (a wrap) poisons the pass.
     auto guard = [&](uint32_t q, uint32_t old) {
         const uint32_t r = q - q_lo;
         if (r >= q_span) return;
         const uint32_t sh = (r % kPerWord) * kBits;
         const uint32_t f = (old >> sh) & kField;
         if (f == kHalf - 1u) {
-            __hip_atomic_fetch_sub(&bins[r / kPerWord], kHalf << sh, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (ovf)  // (always for u8; u16 passes of launch_queue_ranges too)
-                atomicAdd(&ovf[r], 1u);
-            else
-                atomicAdd(&counts[q], (unsigned long long)kHalf);
-        } else if (f == kField && poison) {
+            const uint32_t at = __hip_atomic_fetch_sub(&bins[r / kPerWord], kHalf << sh,
+                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            RSS_RECORD_MARGIN(kBits, kBits == 16 ? kMarginWide16 : kMarginWide8, (at >> sh) & kField);
+            atomicAdd(&ovf[r], 1u);
+        } else if (f == kField) {
             __hip_atomic_store(poison, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     };
@@ -1020,14 +990,13 @@ __global__ __launch_bounds__(kBlock) void rss_queue_hist_wide_kernel(
 }
 
 // counts[q_lo + q] += sum over the `rows` rows of the u16 (kBits = 16) or u8 (kBits = 8)
-// partial matrix (column q).  A workgroup takes a strip of 64 dwords (128 or 256 queues) of
-// every row: its 256 threads are 64 columns x 4 row groups, each summing its rows' dword with
-// eight loads in flight, then the 4 row groups meet in LDS.  (One thread per queue summing all
-// rows ran 60 us per 65536-queue range at 2^28 tuples -- as long as half the wide pass;
-// profiles/r03/mqprof.)  The guard-bit adds landed in a previous launch, so a plain
-// read-modify-write of the counts suffices.  HIST_RANGE8 passes its guard moves (`ovf`, u32
-// per queue in units of 128) and its poison word: a poisoned launch's rows are discarded here
-// and rss_range8_fallback_kernel recounts the range.
+// partial matrix (column q) + 2^(kBits - 1) x its guard moves ovf[q].  A workgroup takes a
+// strip of 64 dwords (128 or 256 queues) of every row: its 256 threads are 64 columns x 4 row
+// groups, each summing its rows' dword with eight loads in flight, then the 4 row groups meet
+// in LDS.  (One thread per queue summing all rows ran 60 us per 65536-queue range at 2^28
+// tuples -- as long as half the wide pass; profiles/r03/mqprof.)  A poisoned pass's rows and
+// moves are discarded here (a bin wrapped): the recount (rss_range_fallback_kernel /
+// rss_range_fallback_col_kernel, gated on the same word) takes the range instead.
 constexpr uint32_t kReduceCols = 64, kReduceGroups = 4;
 template <int kBits>
 __global__ __launch_bounds__(kReduceCols * kReduceGroups) void rss_partial_reduce_kernel(
@@ -1035,7 +1004,7 @@ __global__ __launch_bounds__(kReduceCols * kReduceGroups) void rss_partial_reduc
         uint32_t q_span, unsigned long long* counts, const uint32_t* __restrict__ ovf,
         const uint32_t* __restrict__ poison) {
     constexpr uint32_t kPer = 32 / kBits, kMask = (1u << kBits) - 1u;
-    if (poison && *poison) return;  // uniform: the fallback recounts this range
+    if (*poison) return;  // uniform: the recount takes this range
     __shared__ unsigned long long part[kReduceGroups][kReduceCols][kPer];
     const uint32_t col = threadIdx.x % kReduceCols, grp = threadIdx.x / kReduceCols;
     const uint32_t word = blockIdx.x * kReduceCols + col;  // queues kPer * word + f
@@ -1067,40 +1036,44 @@ __global__ __launch_bounds__(kReduceCols * kReduceGroups) void rss_partial_reduc
             for (uint32_t g = 1; g < kReduceGroups; ++g) acc[f] += part[g][col][f];
             const uint32_t q = kPer * word + f;
             if (q < q_span) {
-                const unsigned long long v = acc[f] + (ovf ? (1ull << (kBits - 1)) * ovf[q] : 0ull);
+                const unsigned long long v = acc[f] + (1ull << (kBits - 1)) * ovf[q];
                 if (v) counts[q_lo + q] += v;
             }
         }
     }
 }
 
-// HIST_RANGE8's recount (see range8_guard), launched after every u8 pass: returns at once
-// unless the pass raised its poison word.  Then every workgroup counts the range in slices
-// with u32 LDS bins (no guard needed: a bin holds one workgroup's share of the batch) and
-// folds each slice with atomics into the counts.  Slow (a pass over the batch per slice),
-// exact, and only ever run on inputs that pile thousands of tuples into one bin at once.
-// Two forms: this one hashes the tuples again on the small tables (a counts-only hash pass);
-// rss_range8_fallback_col_kernel reads a queue column (a wide pass, or a hash pass whose
-// caller's u32 column holds the queues).
-constexpr uint32_t kFallbackSpan = 40192;     // 157 KiB of u32 bins beside the small tables
+// The recount of a guarded pass (range16_guard / range8_guard), launched after each one:
+// returns at once unless the pass raised its poison word.  Then every workgroup counts the
+// range in slices with u32 LDS bins (no guard needed: a bin holds one workgroup's share of
+// the batch) and folds each slice with atomics into the counts.  Slow (a pass over the batch
+// per slice), exact, and only ever run on inputs that pile thousands of tuples into one bin
+// at once.  Two forms: this one hashes the tuples again on the small tables (a hash pass that
+// writes no column holding the queues; any table partition gives the exact hash) with
+// p.fb_span u32 bins per slice and, for QM_TABLE, the indirection table after them;
+// rss_range_fallback_col_kernel reads a queue column (a wide pass, or a hash pass whose
+// column holds the queues).
 constexpr uint32_t kFallbackColSpan = 40960;  // 160 KiB of u32 bins
 template <bool kHPow2, int kQMode>
-__global__ __launch_bounds__(kBlock) void rss_range8_fallback_kernel(const LaunchParams p) {
+__global__ __launch_bounds__(kBlock) void rss_range_fallback_kernel(const LaunchParams p) {
     if (!*p.poison) return;  // uniform across the grid: no wave is left behind
     __shared__ uint32_t lut[kSmallLutDwords];
     extern __shared__ uint32_t bins[];
+    uint32_t* reta_lds = bins + p.fb_span;  // QM_TABLE: H entries after the bins
     const uint32_t tid = threadIdx.x;
     build_small_lut(lut, p.window, tid);
+    if constexpr (kQMode == QM_TABLE)
+        for (uint32_t e = tid; e < p.H; e += kBlock) reta_lds[e] = p.reta[e];
     const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
     const uint64_t gstride = (uint64_t)gridDim.x * kBlock;
-    for (uint32_t lo = 0; lo < p.q_span; lo += kFallbackSpan) {
-        const uint32_t span = min(kFallbackSpan, p.q_span - lo);
+    for (uint32_t lo = 0; lo < p.q_span; lo += p.fb_span) {
+        const uint32_t span = min(p.fb_span, p.q_span - lo);
         for (uint32_t e = tid; e < span; e += kBlock) bins[e] = 0;
         __syncthreads();
         for (uint64_t i = gtid; i < p.n; i += gstride) {
             const uint32_t* src = reinterpret_cast<const uint32_t*>(p.tuples) + 3 * i;
             const uint32_t h = toeplitz_hash_small(lut, src[0], src[1], src[2]);
-            const uint32_t r = queue_of<kQMode>(bucket_of<kHPow2>(h, p), p) - p.q_lo - lo;
+            const uint32_t r = queue_lookup<kQMode>(bucket_of<kHPow2>(h, p), p, reta_lds) - p.q_lo - lo;
             if (r < span)  // (wraps below the slice)
                 __hip_atomic_fetch_add(&bins[r], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
@@ -1112,7 +1085,7 @@ __global__ __launch_bounds__(kBlock) void rss_range8_fallback_kernel(const Launc
 }
 
 template <typename T>
-__global__ __launch_bounds__(kBlock) void rss_range8_fallback_col_kernel(
+__global__ __launch_bounds__(kBlock) void rss_range_fallback_col_kernel(
         const T* __restrict__ col, uint64_t n, uint32_t q_lo, uint32_t q_span,
         unsigned long long* counts, const uint32_t* __restrict__ poison,
         const uint32_t* __restrict__ region_counts, uint64_t region_cap) {
@@ -1263,7 +1236,7 @@ __global__ __launch_bounds__(kBlock, 2) void rss_counts_perm_kernel(const PermPa
         uint32_t s = 0;
         for (uint32_t c = 0; c < kBinCols; ++c) s += bins[q * kBinCols + ((c + q) & (kBinCols - 1))];
         return s;
-    }, p.Q, p.counts, p.ws, p.accumulate, bins);
+    }, p.Q, p.counts, p.ws, p.accumulate);
 }
 
 // Key search: per-queue counts of the same tuples under many
@@ -1851,7 +1824,7 @@ __global__ __launch_bounds__(kBlock) void rss_toeplitz6_kernel(const LaunchParam
             } else {
                 return bins[k];
             }
-        }, p.Q, p.counts, p6.ws, p6.accumulate, bins);
+        }, p.Q, p.counts, p6.ws, p6.accumulate);
     } else if constexpr (kHist == HIST_RANGE) {
         __syncthreads();
         for (uint32_t r = tid; r < p.q_span; r += kBlock)
@@ -2157,48 +2130,35 @@ int check_reta(const uint32_t* reta, uint32_t htable, uint32_t nqueues, const ch
     return RSS_OK;
 }
 
-// Single-pass counts hand off with release/acquire (fold_counts, kFoldOrdered) unless
-// RSS_WS_ORDER=relaxed; read at every launch (tens of ns) so one process can A/B both orders
-// on the same buffers (tools/ws_order_ab.py: +1.3-1.5 us per 2^28-tuple launch)
-bool ws_order_acqrel() {
-    const char* e = getenv("RSS_WS_ORDER");
-    return !(e && strcmp(e, "relaxed") == 0);
-}
-
-// RSS_FOLD=ticket: the single-pass fold of rounds 2-3 (adds, a ticket, the last workgroup's
-// exchanges) instead of the arrival fold (A/B, tests); read at every launch
-bool fold_ticket() {
-    const char* e = getenv("RSS_FOLD");
-    return e && strcmp(e, "ticket") == 0;
-}
+// ---------------------------------------------------------- path options ----
+// A launch takes its path from its arguments and from the scratch memory it gets.  The
+// tests force the other paths (the ones a launch takes when memory runs short, and the
+// recount of a guarded pass) through a test-hooks build of this file (-DRSS_TEST_HOOKS:
+// librss_toeplitz_hooks.so, loaded by tests/ only, rss_test_set_option in rss_test_hooks.h).
+// In the product library these are constants: it reads no environment.
+struct Options {
+    int recount = 0;          // guarded passes: 1 poisons every pass (the recount takes it), 2 runs
+                              // no gate and no recount (counts from the bins and moves alone)
+    bool range8 = true;       // u8 bins past the u16 bins' reach (else u16 bins + more passes)
+    bool small_lut = true;    // the small tables for many-queues hash passes (else 12-bit tables)
+    int prefetch = -1;        // small-table passes' load prefetch: -1 counts only, 0 / 1 forced
+    bool balance = true;      // the balanced tail (walk_rows) of single-pass and u8 launches
+    bool counts_perm = true;  // the register-table counts-only kernel
+    bool resid = true;        // counts only past 161144 queues: residual lists (else a column)
+    bool wide = true;         // wide passes over a queue column (else u32 passes of 16384)
+};
+#ifdef RSS_TEST_HOOKS
+Options g_opt;
+#else
+constexpr Options g_opt{};
+#endif
 
 // Small-table passes without per-tuple outputs (counts only, no scratch column) issue the
 // next group's loads before this group's LDS work: 0.62 vs 0.66 ms at Q = 65536 / 131072,
 // where with outputs it cost 1-2 % and the balanced tail gains 4 % instead
-// (profiles/r04/small_tables/prefetch_ab.jsonl).  RSS_PREFETCH=0/1 forces it (A/B).
+// (profiles/r04/small_tables/prefetch_ab.jsonl).
 bool prefetch_for(bool has_outputs) {
-    const char* e = getenv("RSS_PREFETCH");
-    if (e && (e[0] == '0' || e[0] == '1')) return e[0] == '1';
-    return !has_outputs;
-}
-
-// RSS_OFF32=0: 64-bit addressing even where 32-bit byte offsets fit (A/B, tests)
-bool off32_enabled() {
-    const char* e = getenv("RSS_OFF32");
-    return !(e && e[0] == '0');
-}
-
-// RSS_BALANCE=0: single-pass launches keep the static grid-stride to the end (A/B, tests);
-// read at every launch like RSS_WS_ORDER
-bool balance_enabled() {
-    const char* e = getenv("RSS_BALANCE");
-    return !(e && e[0] == '0');
-}
-
-// RSS_COUNTS_PERM=0 routes counts-only launches to the LUT kernel too (A/B, tests)
-bool counts_perm_enabled() {
-    const char* e = getenv("RSS_COUNTS_PERM");
-    return !(e && e[0] == '0');
+    return g_opt.prefetch >= 0 ? g_opt.prefetch == 1 : !has_outputs;
 }
 
 // Counts only, power-of-two H <= 256, 16-B aligned tuples: rss_counts_perm_kernel with the
@@ -2213,7 +2173,7 @@ int launch_counts_perm(const uint32_t* window, const void* tuples, uint64_t n, u
     pp.tuples = static_cast<const uint32_t*>(tuples);
     pp.counts = counts;
     pp.ws = ws;
-    pp.accumulate = fold_mode;  // kFoldAccumulate | kFoldOrdered
+    pp.accumulate = fold_mode;  // kFoldAccumulate
     pp.n = n;
     pp.Q = Q;
     pp.q_mask = q_mask;
@@ -2229,11 +2189,9 @@ int launch_counts_perm(const uint32_t* window, const void* tuples, uint64_t n, u
                 pp.lo[id] = e[0] | e[1] << 8 | e[2] << 16 | (uint32_t)e[3] << 24;
                 pp.hi[id] = e[4] | e[5] << 8 | e[6] << 16 | (uint32_t)e[7] << 24;
             }
-    // no LUT and <= 64 VGPRs: two 1024-lane workgroups fit a CU (RSS_COUNTS_PERM_WGS=1|2)
-    const char* wgs_env = getenv("RSS_COUNTS_PERM_WGS");
-    const uint64_t wgs = wgs_env && wgs_env[0] == '1' ? 1 : 2;
+    // no LUT and <= 64 VGPRs: two 1024-lane workgroups fit a CU
     const uint64_t want = (n + 4 * kBlock - 1) / (4 * kBlock);
-    const unsigned grid = (unsigned)(want < wgs * cu_count ? want : wgs * cu_count);
+    const unsigned grid = (unsigned)(want < 2ull * cu_count ? want : 2ull * cu_count);
     // no balanced tail here (pp.tail_rows = 0, walk_rows' static loop): on this read-only,
     // two-workgroups-per-CU kernel it measured 5 % SLOWER (0.562 vs 0.536 ms per 2^28
     // tuples, profiles/r03/c/ab.json), where the full-output kernel gains 3 %
@@ -2248,210 +2206,169 @@ int launch_counts_perm(const uint32_t* window, const void* tuples, uint64_t n, u
     return RSS_OK;
 }
 
-// RSS_RESID=0: counts-only launches past 161144 queues write a scratch queue column instead of
-// per-wave residual lists (A/B, tests)
-bool resid_enabled() {
-    const char* e = getenv("RSS_RESID");
-    return !(e && e[0] == '0');
-}
-
-bool wide_hist_enabled() {
-    const char* e = getenv("RSS_WIDE_HIST");
-    return !(e && e[0] == '0');
-}
-
 // Whether a many-queues launch counts its queues from the queue column (launch_queue_ranges)
-// rather than with one global atomic per tuple: up to 64 wide passes (4M queues), or 64 / 32
-// narrow passes of `span` queues (u16 / u32 column) with RSS_WIDE_HIST=0.
-bool ranged_histogram_ok(uint32_t q_eff, uint32_t span, uint32_t qbytes) {
-    if (wide_hist_enabled()) return (uint64_t)q_eff <= 64ull * kWideSpan;
-    return ((uint64_t)q_eff + span - 1) / span <= (qbytes == 2 ? 64u : 32u);
-}
+// rather than with one global atomic per tuple: up to 64 wide passes (4M queues).
+bool ranged_histogram_ok(uint32_t q_eff) { return (uint64_t)q_eff <= 64ull * kWideSpan; }
 
-// The small tables for a many-queues launch (kSmallLut); RSS_SMALL_LUT=0 keeps the 12-bit tables.
-bool small_lut_enabled() {
-    const char* e = getenv("RSS_SMALL_LUT");
-    return !(e && e[0] == '0');
+// --------------------------------------------------------- guarded passes --
+// Scratch block of a guarded pass (u16 / u8 bins with guard moves and a poison word: the
+// hash pass's HIST_RANGE16 / HIST_RANGE8, the wide passes over a queue column):
+//   the partial matrix (a row of `words` dwords per workgroup, rounded to 16 B)
+//   | ovf[q_span] | poison | zero (never written: the ungated reduce's word) | pad
+//   | the balanced tail's unit counter (u64)
+size_t guard_rows_bytes(unsigned grid, uint32_t words) {
+    return ((size_t)grid * words * 4 + 15) & ~(size_t)15;
 }
+size_t guard_ctr_offset(uint32_t q_span) { return (((size_t)q_span + 2) * 4 + 7) & ~(size_t)7; }
+size_t guard_tail_bytes(uint32_t q_span) { return guard_ctr_offset(q_span) + 8; }
+uint32_t guard_words(int bits, uint32_t q_span) { return bits == 8 ? (q_span + 3) / 4 : (q_span + 1) / 2; }
 
-// RSS_RANGE8=0 keeps u16 bins (+ queue-column passes) past 80572 queues (A/B, tests)
-bool range8_enabled() {
-    const char* e = getenv("RSS_RANGE8");
-    return !(e && e[0] == '0');
-}
-
-// Tests only: RSS_RANGE8_DEBUG=force sets the poison word before every u8 pass and u16 wide
-// pass (the fallback then recounts every launch); =nofallback drops the gate and the fallback
-// (a wrap would then show as wrong counts -- proves a launch's counts came from the bins and
-// their guard moves)
-int range8_debug() {
-    const char* e = getenv("RSS_RANGE8_DEBUG");
-    if (!e) return 0;
-    return strcmp(e, "force") == 0 ? 1 : (strcmp(e, "nofallback") == 0 ? 2 : 0);
-}
-
-// One u8 wide pass over [lo, lo + sp) of a queue column (rss_queue_hist_wide_kernel<T, 8>):
-// a scratch block of the u8 partial matrix, the guard moves and the poison word (zeroed),
-// the pass, the reduce (gated on !poison) and the column recount (gated on poison).  Returns
-// RSS_ENOMEM without launching anything when the block cannot be allocated.
-template <typename T>
-int launch_wide8(const T* qcol, uint64_t n, uint32_t lo, uint32_t sp, unsigned long long* counts,
-                 unsigned grid, int cu_count, hipStream_t stream,
-                 const uint32_t* region_counts = nullptr, uint64_t region_cap = 0) {
-    const uint32_t words = (sp + 3) / 4;
-    const size_t rows_bytes = (size_t)grid * words * 4, tail_bytes = ((size_t)sp + 4) * 4;
+void* alloc_block(size_t bytes, hipStream_t stream) {
     void* buf = nullptr;
-    if (hipMallocAsync(&buf, rows_bytes + tail_bytes, stream) != hipSuccess) {
+    if (hipMallocAsync(&buf, bytes, stream) != hipSuccess) {
         (void)hipGetLastError();
-        return RSS_ENOMEM;
+        return nullptr;
     }
-    uint32_t* partial = static_cast<uint32_t*>(buf);
-    uint32_t* ovf = reinterpret_cast<uint32_t*>(static_cast<char*>(buf) + rows_bytes);
-    uint32_t* poison = ovf + sp;
-    const int debug = range8_debug();
-    hipError_t e = hipMemsetAsync(ovf, 0, tail_bytes, stream);
-    if (e == hipSuccess && debug == 1) e = hipMemsetD32Async(poison, 1, 1, stream);
-    if (e == hipSuccess) {
-        hipLaunchKernelGGL((rss_queue_hist_wide_kernel<T, 8>), dim3(grid), dim3(kBlock), words * 4,
-                           stream, qcol, n, lo, sp, partial, words, counts, ovf, poison,
-                           region_counts, region_cap);
-        e = hipGetLastError();
-    }
-    if (e == hipSuccess) {
-        hipLaunchKernelGGL(rss_partial_reduce_kernel<8>, dim3((words + kReduceCols - 1) / kReduceCols),
-                           dim3(kReduceCols * kReduceGroups), 0, stream,
-                           static_cast<const uint32_t*>(partial), grid, words, lo, sp, counts,
-                           static_cast<const uint32_t*>(ovf),
-                           debug == 2 ? nullptr : static_cast<const uint32_t*>(poison));
-        e = hipGetLastError();
-    }
-    if (e == hipSuccess && debug != 2) {
-        hipLaunchKernelGGL(rss_range8_fallback_col_kernel<T>,
-                           dim3(region_counts ? grid : (unsigned)cu_count), dim3(kBlock),
-                           std::min(kFallbackColSpan, sp) * 4, stream, qcol, n, lo, sp, counts,
-                           static_cast<const uint32_t*>(poison), region_counts, region_cap);
-        e = hipGetLastError();
-    }
-    int rc = e == hipSuccess ? RSS_OK
-                             : set_error(RSS_EIO, "wide queue histogram launch failed: %s", hipGetErrorString(e));
-    const hipError_t fe = hipFreeAsync(buf, stream);  // stream-ordered after its readers
+    return buf;
+}
+void* alloc_guarded(int bits, unsigned grid, uint32_t q_span, hipStream_t stream) {
+    return alloc_block(guard_rows_bytes(grid, guard_words(bits, q_span)) + guard_tail_bytes(q_span),
+                       stream);
+}
+
+// frees `buf` stream-ordered after its readers; the first error wins
+int free_block(void* buf, int rc, hipStream_t stream) {
+    if (!buf) return rc;
+    const hipError_t fe = hipFreeAsync(buf, stream);
     if (fe != hipSuccess && rc == RSS_OK)
         rc = set_error(RSS_EIO, "hipFreeAsync failed: %s", hipGetErrorString(fe));
     return rc;
 }
 
-// Queue ranges [span, nqueues) of a many-queues launch, histogrammed from the queue column
-// (u16 or u32) the first pass wrote: one wide pass (u16 LDS bins, rows of a u16 partial
-// matrix, then a reduce) per kWideSpan queues; RSS_WIDE_HIST=0 (or no memory for the
-// partial matrix) keeps one rss_queue_hist_kernel pass per `span` queues.
-// Regions (region_counts != NULL): the "column" is one residual list per hash-pass wave
-// (resid_append), 16 per workgroup of `region_grid`; only wide passes read them, one wave per
-// list.
+// The tail of a guarded pass's block zeroed (and, under the recount hook, the poison word
+// raised); returns the word the reduce is gated on.
+hipError_t arm_guard(uint32_t* ovf, uint32_t q_span, const uint32_t** gate, hipStream_t stream) {
+    uint32_t* poison = ovf + q_span;
+    hipError_t e = hipMemsetAsync(ovf, 0, guard_tail_bytes(q_span), stream);
+    if (e == hipSuccess && g_opt.recount == 1) e = hipMemsetD32Async(poison, 1, 1, stream);
+    *gate = g_opt.recount == 2 ? poison + 1 : poison;
+    return e;
+}
+
+template <int kBits>
+void launch_reduce(const uint32_t* partial, unsigned rows, uint32_t words, uint32_t q_lo,
+                   uint32_t q_span, unsigned long long* counts, const uint32_t* ovf,
+                   const uint32_t* gate, hipStream_t stream) {
+    hipLaunchKernelGGL(rss_partial_reduce_kernel<kBits>, dim3((words + kReduceCols - 1) / kReduceCols),
+                       dim3(kReduceCols * kReduceGroups), 0, stream, partial, rows, words, q_lo,
+                       q_span, counts, ovf, gate);
+}
+
+// The recount from a column of queues (or, with region_counts, residual lists), gated on
+// `poison`; no-op under the "no recount" hook
+template <typename T>
+void launch_recount_col(const T* col, uint64_t n, uint32_t q_lo, uint32_t q_span,
+                        unsigned long long* counts, const uint32_t* poison, unsigned grid,
+                        hipStream_t stream, const uint32_t* region_counts = nullptr,
+                        uint64_t region_cap = 0) {
+    if (g_opt.recount == 2) return;
+    hipLaunchKernelGGL(rss_range_fallback_col_kernel<T>, dim3(grid), dim3(kBlock),
+                       std::min(kFallbackColSpan, q_span) * 4, stream, col, n, q_lo, q_span, counts,
+                       poison, region_counts, region_cap);
+}
+
+// ------------------------------------------------------------ wide passes --
+// Scratch of the wide passes of one launch: ONE block for all of them (the passes are
+// stream-ordered, so each reuses the rows and re-zeroes the tail), allocated before the
+// launch's first pass touches the counts -- a launch that cannot get it takes the narrow
+// passes (or, for residual lists, the scratch column) with the counts untouched.
+constexpr uint32_t kWideRowWords = kWideSpan8 / 4;  // >= kWideSpan / 2 (u16 rows)
+struct WideScratch {
+    void* buf = nullptr;
+    unsigned grid = 0;
+    uint32_t* partial() const { return static_cast<uint32_t*>(buf); }
+    uint32_t* ovf() const {
+        return reinterpret_cast<uint32_t*>(static_cast<char*>(buf) + guard_rows_bytes(grid, kWideRowWords));
+    }
+};
+unsigned wide_grid(uint64_t n, int cu_count) {
+    const uint64_t want = (n + 8ull * kBlock - 1) / (8ull * kBlock);
+    return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, cu_count));
+}
+WideScratch alloc_wide(unsigned grid, hipStream_t stream) {
+    WideScratch s;
+    s.grid = grid;
+    s.buf = alloc_block(guard_rows_bytes(grid, kWideRowWords) + guard_tail_bytes(kWideSpan8), stream);
+    return s;
+}
+// a wide pass costs about two narrow ones (2^28 tuples: ~0.2 vs ~0.1 ms over a u16 column,
+// profiles/r03/d/config_sweep.jsonl), so it pays from three narrow passes on
+bool wide_pays(uint32_t nranged) {
+    return g_opt.wide && ((uint64_t)nranged + kNarrowSpan - 1) / kNarrowSpan >= 3;
+}
+
+// One guarded wide pass over [lo, lo + sp) of a queue column (rss_queue_hist_wide_kernel):
+// the pass, the reduce (gated on !poison) and the column recount (gated on poison).
+template <typename T, int kBits>
+hipError_t wide_pass(const T* qcol, uint64_t n, uint32_t lo, uint32_t sp, unsigned long long* counts,
+                     const WideScratch& sc, int cu_count, hipStream_t stream,
+                     const uint32_t* region_counts, uint64_t region_cap) {
+    const uint32_t words = guard_words(kBits, sp);
+    uint32_t* ovf = sc.ovf();
+    const uint32_t* gate = nullptr;
+    hipError_t e = arm_guard(ovf, sp, &gate, stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((rss_queue_hist_wide_kernel<T, kBits>), dim3(sc.grid), dim3(kBlock), words * 4,
+                       stream, qcol, n, lo, sp, sc.partial(), words, ovf, ovf + sp, region_counts,
+                       region_cap);
+    launch_reduce<kBits>(sc.partial(), sc.grid, words, lo, sp, counts, ovf, gate, stream);
+    launch_recount_col(qcol, n, lo, sp, counts, ovf + sp, region_counts ? sc.grid : (unsigned)cu_count,
+                       stream, region_counts, region_cap);
+    return hipGetLastError();
+}
+
+// Queue ranges [first, nqueues) of a many-queues launch, histogrammed from the queue column
+// (u16 or u32) the first pass wrote.  With a wide scratch block: one wide pass per 163840
+// queues in u8 bins while more than 65536 are left, then one in u16 bins -- 2.5 times the
+// queues per read of the column.  Without: one rss_queue_hist_kernel pass (u32 bins, no
+// guard) per 16384 queues.  Regions (region_counts != NULL, wide only): the "column" is one
+// residual list per hash-pass wave (resid_append), 16 per workgroup of wsc->grid, read one
+// wave per list.
 int launch_queue_ranges(const void* qcol, int qw, uint64_t n, uint32_t first, uint32_t nqueues,
                         unsigned long long* counts, int cu_count, hipStream_t stream,
-                        const uint32_t* region_counts = nullptr, uint64_t region_cap = 0,
-                        unsigned region_grid = 0) {
+                        const WideScratch* wsc, const uint32_t* region_counts = nullptr,
+                        uint64_t region_cap = 0) {
     if (first >= nqueues) return RSS_OK;
-    const uint32_t span = kNarrowSpan;
-    // a wide pass costs about two narrow ones (2^28 tuples: ~0.2 vs ~0.1 ms over a u16
-    // column, profiles/r03/d/config_sweep.jsonl), so it pays from three narrow passes on
-    const uint64_t narrow_passes = ((uint64_t)nqueues - first + span - 1) / span;
-    if (region_counts || (wide_hist_enabled() && narrow_passes >= 3)) {
-        const uint64_t want = (n + 8ull * kBlock - 1) / (8ull * kBlock);
-        const unsigned grid = region_counts ? region_grid
-                                            : (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, cu_count));
-        const uint32_t stride_words = kWideSpan / 2;
-        void* partial = nullptr;
-        if (hipMallocAsync(&partial, (size_t)grid * stride_words * 4, stream) == hipSuccess) {
-            int rc = RSS_OK;
-            for (uint32_t lo = first; lo < nqueues && rc == RSS_OK;) {
-                // more queues left than one u16 pass holds: a u8 pass (163840 queues, poison-
-                // gated recount) -- 2.5 times the queues per read of the column
-                if (range8_enabled() && nqueues - lo > kWideSpan) {
-                    const uint32_t sp8 = std::min<uint32_t>(kWideSpan8, nqueues - lo);
-                    rc = qw == QW_U16
-                             ? launch_wide8(static_cast<const uint16_t*>(qcol), n, lo, sp8, counts, grid,
-                                            cu_count, stream, region_counts, region_cap)
-                             : launch_wide8(static_cast<const uint32_t*>(qcol), n, lo, sp8, counts, grid,
-                                            cu_count, stream, region_counts, region_cap);
-                    if (rc == RSS_OK) {
-                        lo += sp8;
-                        continue;
-                    }
-                    if (rc != RSS_ENOMEM) break;
-                    rc = RSS_OK;  // no room for its scratch block: the u16 pass below
-                }
-                const uint32_t sp = std::min<uint32_t>(kWideSpan, nqueues - lo);
-                const uint32_t lds = ((sp + 1) / 2) * 4;
-                // the guard moves (u32 per queue, units of 2^15) and a poison word: a bin that
-                // wraps anyway (the in-flight bound of the guard failed) discards the pass's
-                // rows and moves, and the column recount replaces them, as for u8 passes
-                void* tail = nullptr;
-                if (hipMallocAsync(&tail, ((size_t)sp + 4) * 4, stream) != hipSuccess) {
-                    (void)hipGetLastError();
-                    rc = set_error(RSS_ENOMEM, "rss_hash_device: no memory for a wide pass's guard moves");
-                    break;
-                }
-                uint32_t* ovf = static_cast<uint32_t*>(tail);
-                uint32_t* poison = ovf + sp;
-                const int debug = range8_debug();
-                hipError_t e = hipMemsetAsync(tail, 0, ((size_t)sp + 4) * 4, stream);
-                if (e == hipSuccess && debug == 1) e = hipMemsetD32Async(poison, 1, 1, stream);
-                if (e == hipSuccess) {
-                    if (qw == QW_U16)
-                        hipLaunchKernelGGL(rss_queue_hist_wide_kernel<uint16_t>, dim3(grid), dim3(kBlock), lds,
-                                           stream, static_cast<const uint16_t*>(qcol), n, lo, sp,
-                                           static_cast<uint32_t*>(partial), stride_words, counts, ovf,
-                                           poison, region_counts, region_cap);
-                    else
-                        hipLaunchKernelGGL(rss_queue_hist_wide_kernel<uint32_t>, dim3(grid), dim3(kBlock), lds,
-                                           stream, static_cast<const uint32_t*>(qcol), n, lo, sp,
-                                           static_cast<uint32_t*>(partial), stride_words, counts, ovf,
-                                           poison, region_counts, region_cap);
-                    e = hipGetLastError();
-                }
-                if (e == hipSuccess) {
-                    const uint32_t words = (sp + 1) / 2;
-                    hipLaunchKernelGGL(rss_partial_reduce_kernel<16>,
-                                       dim3((words + kReduceCols - 1) / kReduceCols),
-                                       dim3(kReduceCols * kReduceGroups), 0, stream,
-                                       static_cast<const uint32_t*>(partial), grid, stride_words,
-                                       lo, sp, counts, static_cast<const uint32_t*>(ovf),
-                                       debug == 2 ? nullptr : static_cast<const uint32_t*>(poison));
-                    e = hipGetLastError();
-                }
-                if (e == hipSuccess && debug != 2) {
-                    const unsigned fgrid = region_counts ? grid : (unsigned)cu_count;
-                    const uint32_t flds = std::min(kFallbackColSpan, sp) * 4;
-                    if (qw == QW_U16)
-                        hipLaunchKernelGGL(rss_range8_fallback_col_kernel<uint16_t>, dim3(fgrid), dim3(kBlock),
-                                           flds, stream, static_cast<const uint16_t*>(qcol), n, lo, sp,
-                                           counts, static_cast<const uint32_t*>(poison), region_counts,
-                                           region_cap);
-                    else
-                        hipLaunchKernelGGL(rss_range8_fallback_col_kernel<uint32_t>, dim3(fgrid), dim3(kBlock),
-                                           flds, stream, static_cast<const uint32_t*>(qcol), n, lo, sp,
-                                           counts, static_cast<const uint32_t*>(poison), region_counts,
-                                           region_cap);
-                    e = hipGetLastError();
-                }
-                const hipError_t te = hipFreeAsync(tail, stream);  // after its readers
-                if (e == hipSuccess) e = te;
-                if (e != hipSuccess)
-                    rc = set_error(RSS_EIO, "wide queue histogram launch failed: %s", hipGetErrorString(e));
-                lo += sp;
+    if (wsc && wsc->buf) {
+        const uint16_t* c16 = static_cast<const uint16_t*>(qcol);
+        const uint32_t* c32 = static_cast<const uint32_t*>(qcol);
+        for (uint32_t lo = first; lo < nqueues;) {
+            hipError_t e;
+            uint32_t sp;
+            if (g_opt.range8 && nqueues - lo > kWideSpan) {
+                sp = std::min<uint32_t>(kWideSpan8, nqueues - lo);
+                e = qw == QW_U16 ? wide_pass<uint16_t, 8>(c16, n, lo, sp, counts, *wsc, cu_count, stream,
+                                                          region_counts, region_cap)
+                                 : wide_pass<uint32_t, 8>(c32, n, lo, sp, counts, *wsc, cu_count, stream,
+                                                          region_counts, region_cap);
+            } else {
+                sp = std::min<uint32_t>(kWideSpan, nqueues - lo);
+                e = qw == QW_U16 ? wide_pass<uint16_t, 16>(c16, n, lo, sp, counts, *wsc, cu_count, stream,
+                                                           region_counts, region_cap)
+                                 : wide_pass<uint32_t, 16>(c32, n, lo, sp, counts, *wsc, cu_count, stream,
+                                                           region_counts, region_cap);
             }
-            const hipError_t fe = hipFreeAsync(partial, stream);
-            if (fe != hipSuccess && rc == RSS_OK)
-                rc = set_error(RSS_EIO, "hipFreeAsync failed: %s", hipGetErrorString(fe));
-            return rc;
+            if (e != hipSuccess)
+                return set_error(RSS_EIO, "wide queue histogram launch failed: %s", hipGetErrorString(e));
+            lo += sp;
         }
-        (void)hipGetLastError();  // no room for the partial matrix: the narrow passes below
-        if (region_counts)        // (which read a dense column, not residual lists)
-            return set_error(RSS_ENOMEM, "rss_hash_device: no memory for the wide pass's rows");
+        return RSS_OK;
     }
+    if (region_counts)
+        return set_error(RSS_EIO, "rss_hash_device: residual lists without the wide passes' scratch");
+    const uint32_t span = kNarrowSpan;
     const uint64_t qwant = (n + 8ull * kBlock - 1) / (8ull * kBlock);
-    const unsigned qgrid = (unsigned)std::min<uint64_t>(qwant, (uint64_t)cu_count * 2);
+    const unsigned qgrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(qwant, (uint64_t)cu_count * 2));
     for (uint32_t lo = first; lo < nqueues; lo += span) {
         const uint32_t sp = std::min<uint32_t>(span, nqueues - lo);
         if (qw == QW_U16)
@@ -2465,130 +2382,74 @@ int launch_queue_ranges(const void* qcol, int qw, uint64_t n, uint32_t first, ui
     return RSS_OK;
 }
 
-// A HIST_RANGE16 hash launch over `span` = p.q_span queues.  A wide range's workgroups store
-// their u16 bins as rows of a partial matrix that rss_partial_reduce_kernel sums into the
-// counts (as the wide pass does) -- grid x span u64 atomics instead would cost ~0.2 ms at
-// 65536 queues (256 x 65536 = 16.8M; profiles/r03/many_queues/config_sweep_many_e1.jsonl); a narrow one,
-// or one with no memory for the matrix, folds its bins with atomics.
-constexpr uint32_t kPartialMinSpan = 2048;
-int launch_range16(KernelFn fn, unsigned grid, uint32_t shmem, LaunchParams& p, hipStream_t stream) {
-    if (!fn) return set_error(RSS_EIO, "rss_hash_device: no kernel instance for this launch");
-    const uint32_t words = (p.q_span + 1) / 2;
-    void* partial = nullptr;
-    if (p.q_span >= kPartialMinSpan &&
-        hipMallocAsync(&partial, (size_t)grid * words * 4, stream) != hipSuccess) {
-        (void)hipGetLastError();
-        partial = nullptr;
-    }
-    p.partial = static_cast<uint32_t*>(partial);
-    p.partial_stride = words;
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), shmem, stream, p);
-    hipError_t e = hipGetLastError();
-    if (e == hipSuccess && partial) {
-        hipLaunchKernelGGL(rss_partial_reduce_kernel<16>, dim3((words + kReduceCols - 1) / kReduceCols),
-                           dim3(kReduceCols * kReduceGroups), 0, stream,
-                           static_cast<const uint32_t*>(partial), grid, words, p.q_lo, p.q_span,
-                           p.counts, (const uint32_t*)nullptr, (const uint32_t*)nullptr);
-        e = hipGetLastError();
-    }
-    int rc = e == hipSuccess ? RSS_OK
-                             : set_error(RSS_EIO, "rss_hash_device: launch failed: %s", hipGetErrorString(e));
-    if (partial) {  // stream-ordered after its reader, on every path
-        const hipError_t fe = hipFreeAsync(partial, stream);
-        if (fe != hipSuccess && rc == RSS_OK)
-            rc = set_error(RSS_EIO, "hipFreeAsync failed: %s", hipGetErrorString(fe));
-    }
-    p.partial = nullptr;
-    return rc;
-}
-
+// ------------------------------------------------------ guarded hash pass --
 using FallbackFn = void (*)(const LaunchParams);
 template <bool kHPow2>
-FallbackFn pick_fallback(int qmode) {
+FallbackFn pick_fallback_q(int qmode) {
     switch (qmode) {
-        case QM_MASK: return rss_range8_fallback_kernel<kHPow2, QM_MASK>;
-        case QM_FAST16: return rss_range8_fallback_kernel<kHPow2, QM_FAST16>;
-        case QM_FAST32: return rss_range8_fallback_kernel<kHPow2, QM_FAST32>;
-        default: return nullptr;  // (FAST8 / TABLE: H <= 1024, never this many queues)
+        case QM_MASK: return rss_range_fallback_kernel<kHPow2, QM_MASK>;
+        case QM_FAST16: return rss_range_fallback_kernel<kHPow2, QM_FAST16>;
+        case QM_FAST32: return rss_range_fallback_kernel<kHPow2, QM_FAST32>;
+        case QM_TABLE: return rss_range_fallback_kernel<kHPow2, QM_TABLE>;
+        default: return nullptr;  // (QM_FAST8: H <= 256 and no table, never this many queues)
     }
 }
-
-// A HIST_RANGE8 hash launch's scratch block: the u8 partial matrix (a row per workgroup),
-// the guard moves (u32 per queue) and the poison word.  NULL when it cannot be allocated (the
-// caller then keeps the u16 path).
-// layout: the rows (rounded to 16 B) | ovf[q_span] | poison | pad | the balanced tail's counter
-size_t range8_rows_bytes(unsigned grid, uint32_t q_span) {
-    return ((size_t)grid * ((q_span + 3) / 4) * 4 + 15) & ~(size_t)15;
-}
-size_t range8_ctr_offset(uint32_t q_span) { return (((size_t)q_span + 1) * 4 + 7) & ~(size_t)7; }
-size_t range8_tail_bytes(uint32_t q_span) { return range8_ctr_offset(q_span) + 8; }
-void* alloc_range8(unsigned grid, uint32_t q_span, hipStream_t stream) {
-    void* buf = nullptr;
-    if (hipMallocAsync(&buf, range8_rows_bytes(grid, q_span) + range8_tail_bytes(q_span), stream) !=
-        hipSuccess) {
-        (void)hipGetLastError();
-        return nullptr;
-    }
-    return buf;
+FallbackFn pick_fallback(bool h_pow2, int qmode) {
+    return h_pow2 ? pick_fallback_q<true>(qmode) : pick_fallback_q<false>(qmode);
 }
 
-// A HIST_RANGE8 hash launch over [p.q_lo, p.q_lo + p.q_span) on the block `buf` (alloc_range8,
-// freed here on every path): the guard moves and the poison word are zeroed, then the pass,
-// the reduce (gated on !poison) and the fallback (gated on poison; `qcol` = a u32 column of
-// the queues the pass writes, else it rehashes).
-int launch_range8(KernelFn fn, FallbackFn fallback, unsigned grid, int cu_count, LaunchParams& p,
-                  const uint32_t* qcol, void* buf, hipStream_t stream) {
-    const uint32_t words = (p.q_span + 3) / 4;
-    const size_t rows_bytes = range8_rows_bytes(grid, p.q_span);
-    const size_t tail_bytes = range8_tail_bytes(p.q_span);
-    if (!fn || !fallback) {
+// A guarded hash pass (HIST_RANGE16 when bits = 16, HIST_RANGE8 when 8) over [p.q_lo, p.q_lo
+// + p.q_span) on the block `buf` (alloc_guarded, freed here on every path): the tail zeroed,
+// the pass (a row of bins per workgroup, guard moves, poison), the reduce (gated on
+// !poison) and the recount (gated on poison) -- from `qcol` when the launch writes a column
+// holding the queues themselves (QW_U32 / QW_U16 `qw`), else by rehashing the tuples.
+int launch_guarded(KernelFn fn, FallbackFn fallback, int bits, unsigned grid, int cu_count,
+                   uint32_t shmem, LaunchParams& p, const void* qcol, int qw, void* buf,
+                   uint32_t reta_bytes, hipStream_t stream) {
+    const bool col = qcol && (qw == QW_U32 || qw == QW_U16);
+    if (!fn || (!col && !fallback)) {
         (void)hipFreeAsync(buf, stream);
         return set_error(RSS_EIO, "rss_hash_device: no kernel instance for this launch");
     }
-    uint32_t* tail = reinterpret_cast<uint32_t*>(static_cast<char*>(buf) + rows_bytes);
+    const uint32_t words = guard_words(bits, p.q_span);
+    uint32_t* tail = reinterpret_cast<uint32_t*>(static_cast<char*>(buf) + guard_rows_bytes(grid, words));
     p.partial = static_cast<uint32_t*>(buf);
     p.partial_stride = words;
     p.ovf = tail;
     p.poison = tail + p.q_span;
-    // balanced tail (walk_rows): its unit counter in the zeroed block, its LDS slot past the
-    // small tables; the last tenth of the rows goes out per workgroup slot
+    // balanced tail (walk_rows, u8 passes on the small tables): its unit counter in the zeroed
+    // tail, its LDS slot past the small tables; the last tenth of the rows goes out per
+    // workgroup slot
     const uint32_t tail_rows = balanced_tail_rows(p.n / 4, grid);
-    if (tail_rows && balance_enabled() && !p.prefetch && !p.resid_out) {  // (lists: static walk)
+    if (bits == 8 && tail_rows && g_opt.balance && !p.prefetch && !p.resid_out) {  // (lists: static walk)
         p.tail_rows = tail_rows;
         p.tail_ctr = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(tail) +
-                                                           range8_ctr_offset(p.q_span));
+                                                           guard_ctr_offset(p.q_span));
     }
-    const int debug = range8_debug();
-    hipError_t e = hipMemsetAsync(tail, 0, tail_bytes, stream);
-    if (e == hipSuccess && debug == 1) e = hipMemsetD32Async(p.poison, 1, 1, stream);
+    const uint32_t* gate = nullptr;
+    hipError_t e = arm_guard(tail, p.q_span, &gate, stream);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), words * 4, stream, p);
-        e = hipGetLastError();
-    }
-    if (e == hipSuccess) {
-        hipLaunchKernelGGL(rss_partial_reduce_kernel<8>, dim3((words + kReduceCols - 1) / kReduceCols),
-                           dim3(kReduceCols * kReduceGroups), 0, stream,
-                           static_cast<const uint32_t*>(p.partial), grid, words, p.q_lo, p.q_span,
-                           p.counts, static_cast<const uint32_t*>(p.ovf),
-                           debug == 2 ? nullptr : static_cast<const uint32_t*>(p.poison));
-        e = hipGetLastError();
-    }
-    if (e == hipSuccess && debug != 2) {
-        if (qcol)
-            hipLaunchKernelGGL(rss_range8_fallback_col_kernel<uint32_t>, dim3(cu_count), dim3(kBlock),
-                               std::min(kFallbackColSpan, p.q_span) * 4, stream, qcol, p.n, p.q_lo,
-                               p.q_span, p.counts, static_cast<const uint32_t*>(p.poison),
-                               (const uint32_t*)nullptr, (uint64_t)0);
+        hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), shmem, stream, p);
+        if (bits == 8)
+            launch_reduce<8>(p.partial, grid, words, p.q_lo, p.q_span, p.counts, p.ovf, gate, stream);
         else
-            hipLaunchKernelGGL(fallback, dim3(cu_count), dim3(kBlock),
-                               std::min(kFallbackSpan, p.q_span) * 4, stream, p);
+            launch_reduce<16>(p.partial, grid, words, p.q_lo, p.q_span, p.counts, p.ovf, gate, stream);
+        if (col && qw == QW_U32)
+            launch_recount_col(static_cast<const uint32_t*>(qcol), p.n, p.q_lo, p.q_span, p.counts,
+                               p.poison, (unsigned)cu_count, stream);
+        else if (col)
+            launch_recount_col(static_cast<const uint16_t*>(qcol), p.n, p.q_lo, p.q_span, p.counts,
+                               p.poison, (unsigned)cu_count, stream);
+        else if (g_opt.recount != 2) {
+            p.fb_span = std::min<uint32_t>(p.q_span, (kLdsBytes - kSmallLutBytes - reta_bytes) / 4);
+            hipLaunchKernelGGL(fallback, dim3(cu_count), dim3(kBlock), p.fb_span * 4 + reta_bytes,
+                               stream, p);
+        }
         e = hipGetLastError();
     }
     int rc = e == hipSuccess ? RSS_OK
                              : set_error(RSS_EIO, "rss_hash_device: launch failed: %s", hipGetErrorString(e));
-    const hipError_t fe = hipFreeAsync(buf, stream);  // stream-ordered after its readers
-    if (fe != hipSuccess && rc == RSS_OK)
-        rc = set_error(RSS_EIO, "hipFreeAsync failed: %s", hipGetErrorString(fe));
+    rc = free_block(buf, rc, stream);
     p.partial = nullptr;
     p.ovf = p.poison = nullptr;
     p.tail_ctr = nullptr;
@@ -2655,8 +2516,7 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
     p.n = n;
     if (single_pass) {
         p.ws = reinterpret_cast<unsigned long long*>(ws);
-        p.accumulate = ((flags & RSS_FLAG_ACCUMULATE) ? kFoldAccumulate : 0u) |
-                       (ws_order_acqrel() ? kFoldOrdered : 0u) | (fold_ticket() ? kFoldTicket : 0u);
+        p.accumulate = (flags & RSS_FLAG_ACCUMULATE) ? kFoldAccumulate : 0u;
     }
     if (reta) {
         qmode = QM_TABLE;
@@ -2672,97 +2532,93 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
     if (rc) return rc;
     if (!d_hash && !d_queue && d_counts && !reta && h_pow2 && htable <= 256u &&
         hist == HIST_PRIVATE && (qmode == QM_MASK || qmode == QM_FAST8) && aligned16(d_tuples) &&
-        counts_perm_enabled())
+        g_opt.counts_perm)
         return launch_counts_perm<3>(key->window, d_tuples, n, p.counts, p.h_mask, p.Q, p.q_mask,
                                      p.q_m16, qmode, bin_bytes, info.cu_count, stream, p.ws,
                                      p.accumulate);
-    // More queues than LDS bins: count them in ranges.  The first pass runs the hash kernel
-    // with shared LDS bins for queues [0, span) and writes the per-tuple outputs -- the
-    // queue column into the caller's buffer or, for a counts-only launch, into a stream-
-    // ordered scratch column; every further range is histogrammed from that column (2 or
-    // 4 B/tuple at the read stream's rate) instead of one global atomic per tuple (13x
-    // slower at 2^28 tuples, DESIGN.md §3 "Many queues").
     const uint64_t per_lane = vec4 ? 4 : 1;
     const uint64_t want = (n + per_lane * kBlock - 1) / (per_lane * kBlock);
     const uint64_t cap = (uint64_t)info.cu_count * kBlocksPerCU;
     const unsigned grid = (unsigned)(want < cap ? want : cap);
     if (hist == HIST_GLOBAL && d_counts) {
-        // u16 bins with the guard bit (HIST_RANGE16): twice the queues of u32 bins in the LDS
-        // the tables leave -- 16384 beside the 12-bit tables, and past that, on the small
-        // tables (4-tuple body, no indirection table), up to 80576 in the hash pass itself; no
-        // queue column for those.  Up to 16384 the 12-bit tables stay: 8 lookups and 3 VALU
-        // per lookup fewer than the small tables' 21 when the bins fit beside them.
+        // More queues than u32 LDS bins (DESIGN.md §3 "Many queues").  Guarded u16 bins
+        // (HIST_RANGE16): twice the queues of u32 bins in the LDS the tables leave -- 16384
+        // beside the 12-bit tables and, on the small tables (4-tuple body, no indirection
+        // table), up to 80572 in one pass.  Up to 16384 the 12-bit tables stay: 8 lookups and
+        // 3 VALU per lookup fewer than the small tables' 21 when the bins fit beside them.
         const uint32_t span12 = ((kBinBytesMax - reta_bytes) / 4) * 2;
-        const bool small_lut = q_eff > span12 && vec4 && !reta && qwidth != QW_U8 && small_lut_enabled();
+        const bool small_lut = q_eff > span12 && vec4 && !reta && qwidth != QW_U8 && g_opt.small_lut;
         const uint32_t lut_bytes = small_lut ? kSmallStaticBytes : kLutBytes;
         const uint32_t span = ((kLdsBytes - lut_bytes - reta_bytes) / 4) * 2;
         const int vm = small_lut ? VM_SMALL_LUT : (vec4 ? VM_VEC4 : VM_SCALAR);
         const uint32_t qbytes = q_eff <= 65536u ? 2 : 4;
+        FallbackFn fb = pick_fallback(h_pow2, qmode);
         if (q_eff <= span) {
             p.q_lo = 0;
             p.q_span = q_eff;
             KernelFn fn = h_pow2 ? pick_queue<true>(qmode, HIST_RANGE16, qwidth, vm)
                                  : pick_queue<false>(qmode, HIST_RANGE16, qwidth, vm);
-            return launch_range16(fn, grid, ((q_eff + 1) / 2) * 4 + reta_bytes, p, stream);
+            void* buf = alloc_guarded(16, grid, q_eff, stream);
+            if (!buf) return set_error(RSS_ENOMEM, "rss_hash_device: no memory for the u16 bins' rows");
+            return launch_guarded(fn, fb, 16, grid, info.cu_count, ((q_eff + 1) / 2) * 4 + reta_bytes, p,
+                                  d_queue, qwidth, buf, reta_bytes, stream);
         }
-        // Past the u16 bins' reach: u8 bins (HIST_RANGE8, a guard at 0x80 and a poison-gated
-        // recount, range8_guard) hold span8 = 161144 queues beside the small tables -- one pass
-        // up to there, and the first range of a queue-column launch beyond.
+        // Past the u16 bins' reach: guarded u8 bins (HIST_RANGE8) hold span8 = 161144 queues
+        // beside the small tables -- one pass up to there, and the first range of a
+        // queue-column launch beyond.
         const uint32_t span8 = kLdsBytes - kSmallStaticBytes;
-        FallbackFn fb8 = h_pow2 ? pick_fallback<true>(qmode) : pick_fallback<false>(qmode);
         void* r8buf = nullptr;  // the u8 pass's scratch block, when it runs
-        if (small_lut && range8_enabled() && fb8)
-            r8buf = alloc_range8(grid, std::min(q_eff, span8), stream);
+        if (small_lut && g_opt.range8 && fb)
+            r8buf = alloc_guarded(8, grid, std::min(q_eff, span8), stream);
         if (r8buf && q_eff <= span8) {
             p.q_lo = 0;
             p.q_span = q_eff;
             KernelFn fn = h_pow2 ? pick_queue<true>(qmode, HIST_RANGE8, qwidth, VM_SMALL_LUT)
                                  : pick_queue<false>(qmode, HIST_RANGE8, qwidth, VM_SMALL_LUT);
-            // the caller's u32 column holds the queues (exact even when the bins are poisoned)
-            const uint32_t* col = d_queue ? static_cast<const uint32_t*>(d_queue) : nullptr;
-            return launch_range8(fn, fb8, grid, info.cu_count, p, col, r8buf, stream);
+            return launch_guarded(fn, fb, 8, grid, info.cu_count, guard_words(8, q_eff) * 4, p, d_queue,
+                                  qwidth, r8buf, 0, stream);
         }
         // Counts only past span8 (u8 hash pass + wide passes): the queues past the pass's LDS
         // range go to per-wave residual lists (resid_append) instead of a queue column --
-        // only those tuples' queues are written and read again, not every tuple's (DESIGN.md
-        // §3 "Many queues").  RSS_RESID=0 keeps the scratch column (A/B).
-        if (r8buf && !d_queue && q_eff > span8 && wide_hist_enabled() && resid_enabled()) {
+        // only those tuples' queues are written and read again, not every tuple's.
+        if (r8buf && !d_queue && q_eff > span8 && g_opt.resid) {
             // the static walk gives a wave at most `rows` groups of 4 tuples per lane, plus the
             // < 4 tail tuples (wave 0 of workgroup 0); 8 entries more keep every list 16-B aligned
             const uint64_t per_row = (uint64_t)grid * kBlock;
             const uint64_t rows = (n / 4 + per_row - 1) / per_row;
-            const uint64_t cap = (rows * 4 * 64 + 4 + 7) & ~7ull;
+            const uint64_t lcap = (rows * 4 * 64 + 4 + 7) & ~7ull;
             const uint32_t nres = q_eff - span8;
             const size_t esize = nres <= 65536u ? 2 : 4;
             const size_t nlists = (size_t)grid * kWavesPerBlock;
-            const size_t list_bytes = nlists * cap * esize;
-            void* lists = nullptr;
-            if (hipMallocAsync(&lists, list_bytes + nlists * 4, stream) == hipSuccess) {
+            const size_t list_bytes = nlists * lcap * esize;
+            void* lists = alloc_block(list_bytes + nlists * 4, stream);
+            WideScratch wsc = lists ? alloc_wide(grid, stream) : WideScratch{};
+            if (lists && wsc.buf) {
                 uint32_t* list_counts = reinterpret_cast<uint32_t*>(static_cast<char*>(lists) + list_bytes);
                 p.queue_out = nullptr;
                 p.resid_out = lists;
                 p.resid_counts = list_counts;
-                p.resid_cap = cap;
+                p.resid_cap = lcap;
                 p.resid_u16 = esize == 2;
                 p.prefetch = prefetch_for(false);
                 p.q_lo = 0;
                 p.q_span = span8;
                 KernelFn fn = h_pow2 ? pick_queue<true>(qmode, HIST_RANGE8, QW_U32, VM_SMALL_LUT)
                                      : pick_queue<false>(qmode, HIST_RANGE8, QW_U32, VM_SMALL_LUT);
-                rc = launch_range8(fn, fb8, grid, info.cu_count, p, nullptr, r8buf, stream);
+                rc = launch_guarded(fn, fb, 8, grid, info.cu_count, guard_words(8, span8) * 4, p, nullptr,
+                                    QW_U32, r8buf, 0, stream);
                 p.resid_out = nullptr;
                 if (rc == RSS_OK)
                     rc = launch_queue_ranges(lists, esize == 2 ? QW_U16 : QW_U32, n, 0, nres,
-                                             p.counts + span8, info.cu_count, stream, list_counts,
-                                             cap, grid);
-                const hipError_t fe = hipFreeAsync(lists, stream);  // after its readers
-                if (fe != hipSuccess && rc == RSS_OK)
-                    rc = set_error(RSS_EIO, "hipFreeAsync failed: %s", hipGetErrorString(fe));
-                return rc;
+                                             p.counts + span8, info.cu_count, stream, &wsc, list_counts,
+                                             lcap);
+                rc = free_block(wsc.buf, rc, stream);
+                return free_block(lists, rc, stream);
             }
-            (void)hipGetLastError();  // no room for the lists: the scratch column below
+            (void)free_block(wsc.buf, RSS_OK, stream);  // no room for the lists: the scratch
+            (void)free_block(lists, RSS_OK, stream);    // column below
         }
-        if (ranged_histogram_ok(q_eff, kNarrowSpan, qbytes)) {
+        if (ranged_histogram_ok(q_eff)) {
             void* qcol = d_queue;
             int qw = qwidth;
             bool scratch = false, ranged = true;
@@ -2772,12 +2628,12 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
             const bool resid = !d_queue && small_lut && q_eff - first_span <= 0xFFFFu;
             const uint32_t sbytes = resid ? 2 : qbytes;
             if (!qcol || qwidth == QW_U8) {  // (u8 queues always fit the bins: q_eff <= 256)
-                if (hipMallocAsync(&qcol, (size_t)n * sbytes, stream) == hipSuccess) {
+                qcol = alloc_block((size_t)n * sbytes, stream);
+                if (qcol) {
                     scratch = true;
                     qw = resid ? QW_U16R : (qbytes == 2 ? QW_U16 : QW_U32);
                 } else {
-                    (void)hipGetLastError();  // no room for a scratch column: one global
-                    ranged = false;           // atomic per tuple below (HIST_GLOBAL) instead
+                    ranged = false;  // no room for a scratch column: one global atomic per tuple
                 }
             }
             if (ranged) {
@@ -2790,43 +2646,44 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
                 const bool b1 = small_lut && v4 && qw != QW_U8;
                 const bool r8 = b1 && r8buf;  // (a caller's u32 column: b1 == small_lut)
                 if (!r8 && r8buf) {
-                    (void)hipFreeAsync(r8buf, stream);
+                    (void)free_block(r8buf, RSS_OK, stream);
                     r8buf = nullptr;
                 }
                 const uint32_t span1 = b1 ? (r8 ? span8 : span) : span12;
                 p.q_span = span1;  // < q_eff here
                 const int vm1 = b1 ? VM_SMALL_LUT : (v4 ? VM_VEC4 : VM_SCALAR);
-                const int hist1 = r8 ? HIST_RANGE8 : HIST_RANGE16;
-                KernelFn fn = h_pow2 ? pick_queue<true>(qmode, hist1, qw, vm1)
-                                     : pick_queue<false>(qmode, hist1, qw, vm1);
+                const int bits1 = r8 ? 8 : 16;
+                KernelFn fn = h_pow2 ? pick_queue<true>(qmode, r8 ? HIST_RANGE8 : HIST_RANGE16, qw, vm1)
+                                     : pick_queue<false>(qmode, r8 ? HIST_RANGE8 : HIST_RANGE16, qw, vm1);
                 const unsigned g1 = v4 ? grid : (unsigned)std::min<uint64_t>((n + kBlock - 1) / kBlock, cap);
-                if (r8) {  // the fallback reads the column when it holds the queues themselves
-                    rc = launch_range8(fn, fb8, g1, info.cu_count, p,
-                                       qw == QW_U32 ? static_cast<const uint32_t*>(qcol) : nullptr,
-                                       r8buf, stream);
-                    r8buf = nullptr;
+                // every scratch block before the first pass touches the counts
+                void* buf1 = r8 ? r8buf : alloc_guarded(16, g1, span1, stream);
+                r8buf = nullptr;
+                const uint32_t nranged = q_eff - span1;
+                WideScratch wsc = buf1 && wide_pays(nranged) ? alloc_wide(wide_grid(n, info.cu_count), stream)
+                                                             : WideScratch{};
+                if (!buf1) {
+                    rc = set_error(RSS_ENOMEM, "rss_hash_device: no memory for the first range's rows");
                 } else {
-                    rc = launch_range16(fn, g1, (span1 / 2) * 4 + reta_bytes, p, stream);
+                    const uint32_t shmem1 = guard_words(bits1, span1) * 4 + (bits1 == 16 ? reta_bytes : 0);
+                    rc = launch_guarded(fn, fb, bits1, g1, info.cu_count, shmem1, p, qcol, qw, buf1,
+                                        reta_bytes, stream);
+                    if (rc == RSS_OK && qw == QW_U16R)  // queues [span1, q_eff) as [0, q_eff - span1)
+                        rc = launch_queue_ranges(qcol, QW_U16, n, 0, nranged, p.counts + span1,
+                                                 info.cu_count, stream, &wsc);
+                    else if (rc == RSS_OK)
+                        rc = launch_queue_ranges(qcol, qw, n, span1, q_eff, p.counts, info.cu_count,
+                                                 stream, &wsc);
                 }
-                if (rc == RSS_OK && qw == QW_U16R)  // queues [span1, q_eff) as [0, q_eff - span1)
-                    rc = launch_queue_ranges(qcol, QW_U16, n, 0, q_eff - span1, p.counts + span1,
-                                             info.cu_count, stream);
-                else if (rc == RSS_OK)
-                    rc = launch_queue_ranges(qcol, qw, n, span1, q_eff, p.counts, info.cu_count, stream);
+                rc = free_block(wsc.buf, rc, stream);
                 // the scratch column goes back on every path (stream-ordered after its readers)
-                if (scratch) {
-                    const hipError_t fe = hipFreeAsync(qcol, stream);
-                    if (fe != hipSuccess && rc == RSS_OK)
-                        rc = set_error(RSS_EIO, "hipFreeAsync failed: %s", hipGetErrorString(fe));
-                }
-                return rc;
+                return free_block(scratch ? qcol : nullptr, rc, stream);
             }
         }
-        if (r8buf) (void)hipFreeAsync(r8buf, stream);  // unused: global atomics below
+        (void)free_block(r8buf, RSS_OK, stream);  // unused: global atomics below
     }
     // 32-bit byte offsets when every stream's bytes fit them (input 12 n B is the largest)
-    const int vmode = vec4 ? (12ull * n < (1ull << 32) && off32_enabled() &&
-                              !(flags & RSS_FLAG_ADDR64) ? 2 : 1) : 0;
+    const int vmode = vec4 ? (12ull * n < (1ull << 32) && !(flags & RSS_FLAG_ADDR64) ? 2 : 1) : 0;
     KernelFn fn = h_pow2 ? pick_queue<true>(qmode, hist, qwidth, vmode)
                          : pick_queue<false>(qmode, hist, qwidth, vmode);
     if (!fn) return set_error(RSS_EIO, "rss_hash_device: no kernel instance for this launch");
@@ -2836,7 +2693,7 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
     // workgroup slot, so the XCDs finish together.  Needs 8 bytes of LDS beside the bins.
     const uint32_t bal_off = (shmem + 7u) & ~7u;
     const uint32_t tail = balanced_tail_rows(n / 4, grid);
-    if (single_pass && vec4 && tail && bal_off + 8 <= kBinBytesMax && balance_enabled()) {
+    if (single_pass && vec4 && tail && bal_off + 8 <= kBinBytesMax && g_opt.balance) {
         p.tail_rows = tail;
         p.bal_off = bal_off;
         shmem = bal_off + 8;
@@ -2941,8 +2798,7 @@ int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint
     p.qwidth = qwidth;
     if (single_pass) {
         p.ws = reinterpret_cast<unsigned long long*>(ws);
-        p.accumulate = ((flags & RSS_FLAG_ACCUMULATE) ? kFoldAccumulate : 0u) |
-                       (ws_order_acqrel() ? kFoldOrdered : 0u) | (fold_ticket() ? kFoldTicket : 0u);
+        p.accumulate = (flags & RSS_FLAG_ACCUMULATE) ? kFoldAccumulate : 0u;
     }
     if (reta)
         for (uint32_t b = 0; b < htable; ++b) p.reta[b] = (uint16_t)reta[b];
@@ -2955,7 +2811,7 @@ int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint
     // counts only, power-of-two H <= 256: the register-table kernel (no LUT, so private bins
     // up to Q = 256 fit beside it)
     if (!d_hash && !d_queue && d_counts && !reta && h_pow2 && htable <= 256u && q_eff <= 256u &&
-        (qmode == QM_MASK || qmode == QM_FAST8) && aligned16(d_tuples) && counts_perm_enabled())
+        (qmode == QM_MASK || qmode == QM_FAST8) && aligned16(d_tuples) && g_opt.counts_perm)
         return launch_counts_perm<9>(key->window, d_tuples, n, p.counts, p.h_mask, p.Q, p.q_mask,
                                      p.q_m16, qmode, q_eff * kBinCols * 4, info.cu_count, stream,
                                      p.ws, p.accumulate);
@@ -2967,16 +2823,16 @@ int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint
     if (hist == HIST_GLOBAL && d_counts) {
         const uint32_t span = budget / 4;
         const uint32_t qbytes = q_eff <= 65536u ? 2 : 4;
-        if (ranged_histogram_ok(q_eff, span, qbytes)) {
+        if (ranged_histogram_ok(q_eff)) {
             void* qcol = d_queue;
             bool scratch = false, ranged = true;
             if (!qcol || qwidth == QW_U8) {
-                if (hipMallocAsync(&qcol, (size_t)n * qbytes, stream) == hipSuccess) {
+                qcol = alloc_block((size_t)n * qbytes, stream);
+                if (qcol) {
                     scratch = true;
                     p.qwidth = qbytes == 2 ? QW_U16 : QW_U32;
                 } else {
-                    (void)hipGetLastError();  // as launch_hash: global atomics below instead
-                    ranged = false;
+                    ranged = false;  // as launch_hash: global atomics below instead
                 }
             }
             if (ranged) {
@@ -2987,18 +2843,18 @@ int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint
                 const bool v4 = vec4 && ((uintptr_t)qcol % (qw == QW_U32 ? 16 : 8)) == 0;
                 KernelFn6 fn = h_pow2 ? pick6<true>(qmode, HIST_RANGE, v4) : pick6<false>(qmode, HIST_RANGE, v4);
                 const unsigned g1 = v4 ? grid : (unsigned)std::min<uint64_t>((n + kBlock - 1) / kBlock, cap);
+                // the wide passes' scratch before the first pass touches the counts
+                WideScratch wsc = wide_pays(q_eff - span) ? alloc_wide(wide_grid(n, info.cu_count), stream)
+                                                          : WideScratch{};
                 hipLaunchKernelGGL(fn, dim3(g1), dim3(kBlock), span * 4 + reta_bytes, stream, p);
                 const hipError_t le = hipGetLastError();
                 rc = le == hipSuccess
-                         ? launch_queue_ranges(qcol, (int)qw, n, span, q_eff, p.counts, info.cu_count, stream)
+                         ? launch_queue_ranges(qcol, (int)qw, n, span, q_eff, p.counts, info.cu_count, stream,
+                                               &wsc)
                          : set_error(RSS_EIO, "rss_hash6_device: range launch failed: %s",
                                      hipGetErrorString(le));
-                if (scratch) {
-                    const hipError_t fe = hipFreeAsync(qcol, stream);
-                    if (fe != hipSuccess && rc == RSS_OK)
-                        rc = set_error(RSS_EIO, "hipFreeAsync failed: %s", hipGetErrorString(fe));
-                }
-                return rc;
+                rc = free_block(wsc.buf, rc, stream);
+                return free_block(scratch ? qcol : nullptr, rc, stream);
             }
         }
     }
@@ -3007,7 +2863,7 @@ int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint
     // the balanced tail of single-pass launches (as launch_hash: 8 bytes of LDS beside the bins)
     const uint32_t bal_off = (shmem + 7u) & ~7u;
     const uint32_t tail = balanced_tail_rows(n / 4, grid);
-    if (single_pass && vec4 && tail && bal_off + 8 <= kBinBytesMax6 && balance_enabled()) {
+    if (single_pass && vec4 && tail && bal_off + 8 <= kBinBytesMax6 && g_opt.balance) {
         p.tail_rows = tail;
         p.bal_off = bal_off;
         shmem = bal_off + 8;
@@ -3220,7 +3076,8 @@ int rss_hash_device(const rss_key* key, const rss_tuple4* d_tuples, size_t n, ui
 int rss_counts_workspace_bytes(uint32_t nqueues, size_t* out) {
     if (!out) return set_error(RSS_EINVAL, "rss_counts_workspace_bytes: NULL argument");
     if (nqueues < 1) return set_error(RSS_EINVAL, "rss_counts_workspace_bytes: nqueues must be >= 1");
-    // ticket + one accumulator per queue + the balanced tail's unit counter (fold_counts)
+    // a reserved word (ws[0], the rounds 2-3 fold's ticket; the size is ABI) + one arrival
+    // accumulator per queue + the balanced tail's unit counter (fold_counts, walk_rows)
     *out = sizeof(uint64_t) * ((size_t)nqueues + 2);
     return RSS_OK;
 }
@@ -3639,3 +3496,40 @@ int rss_key_search_host(rss_ctx* ctx, const rss_key* keys, size_t nkeys,
 }
 
 }  // extern "C"
+
+#ifdef RSS_TEST_HOOKS
+// ------------------------------------------------- test hooks (tests only) --
+// Exported by librss_toeplitz_hooks.so alone (rss_test_hooks.h): the product library has
+// neither these symbols nor the options they set.
+extern "C" {
+
+int rss_test_set_option(const char* name, int value) {
+    if (!name) return set_error(RSS_EINVAL, "rss_test_set_option: NULL name");
+    const std::string n(name);
+    if (n == "recount") g_opt.recount = value;
+    else if (n == "range8") g_opt.range8 = value != 0;
+    else if (n == "small_lut") g_opt.small_lut = value != 0;
+    else if (n == "prefetch") g_opt.prefetch = value;
+    else if (n == "balance") g_opt.balance = value != 0;
+    else if (n == "counts_perm") g_opt.counts_perm = value != 0;
+    else if (n == "resid") g_opt.resid = value != 0;
+    else if (n == "wide") g_opt.wide = value != 0;
+    else return set_error(RSS_EINVAL, "rss_test_set_option: unknown option '%s'", name);
+    return RSS_OK;
+}
+
+void rss_test_reset_options(void) { g_opt = Options{}; }
+
+int rss_test_guard_margin(uint32_t* out, int reset) {
+    if (!out) return set_error(RSS_EINVAL, "rss_test_guard_margin: NULL out");
+    RSS_HIP_CHECK(hipDeviceSynchronize());
+    RSS_HIP_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_guard_margin), sizeof(uint32_t) * kMargins));
+    if (reset) {
+        const uint32_t zero[kMargins] = {};
+        RSS_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_guard_margin), zero, sizeof zero));
+    }
+    return RSS_OK;
+}
+
+}  // extern "C"
+#endif  // RSS_TEST_HOOKS

@@ -1,13 +1,13 @@
 """Counts-only launches with a power-of-two H <= 256 run ``rss_counts_perm_kernel`` (byte
 tables in registers, v_perm lookups) instead of the LDS-table kernel.  Bar: per-queue counts
-bit-exact to the C oracle and to the LDS-table kernel (``RSS_COUNTS_PERM=0``) on the same
+bit-exact to the C oracle and to the LDS-table kernel (the hooks build's ``counts_perm=0``) on the same
 inputs, over every H it takes, every queue mode (mask, identity Q >= H, FAST8), ragged tails
 (n % 4 = 1..3), tiny n, key lengths that wrap, accumulation, and the shapes that must stay on
 the LDS kernel (misaligned tuples, H > 256, Q > 256)."""
-import os
-
 import numpy as np
 import pytest
+
+from hooks import hooks
 
 pytestmark = pytest.mark.gpu
 
@@ -30,16 +30,12 @@ def _counts(native, key, tuples_ptr, n, H, Q, perm, accumulate_from=None):
     if accumulate_from is not None:
         counts.copy_(torch.from_numpy(accumulate_from.view(np.int64)))
         flags = native.FLAG_ACCUMULATE
-    old = os.environ.get("RSS_COUNTS_PERM")
-    os.environ["RSS_COUNTS_PERM"] = "1" if perm else "0"
-    try:
+    if perm:  # the product library
         native.hash_device(key, tuples_ptr, n, H, Q, None, None, counts.data_ptr(), flags, s)
-        torch.cuda.synchronize()
-    finally:
-        if old is None:
-            del os.environ["RSS_COUNTS_PERM"]
-        else:
-            os.environ["RSS_COUNTS_PERM"] = old
+    else:
+        with hooks(counts_perm=0):
+            native.hash_device(key, tuples_ptr, n, H, Q, None, None, counts.data_ptr(), flags, s)
+    torch.cuda.synchronize()
     return counts.cpu().numpy().view(np.uint64)
 
 
@@ -123,12 +119,9 @@ def test_ipv6_counts_equal_lut_kernel(native, example_key, H, Q, n):
     got = {}
     for perm in (True, False):
         c = torch.zeros(Q, dtype=torch.int64, device="cuda:0")
-        os.environ["RSS_COUNTS_PERM"] = "1" if perm else "0"
-        try:
+        with hooks(counts_perm=int(perm)):
             native.hash6_device(key6, words.data_ptr(), n, H, Q, None, None, c.data_ptr(), 0, s)
             torch.cuda.synchronize()
-        finally:
-            os.environ.pop("RSS_COUNTS_PERM", None)
         got[perm] = c.cpu().numpy()
     np.testing.assert_array_equal(got[True], got[False])
     assert int(got[True].sum()) == n

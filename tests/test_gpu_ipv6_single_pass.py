@@ -12,6 +12,7 @@ import ctypes
 import numpy as np
 import pytest
 
+from hooks import hooks
 from oracle import oracle as o
 
 pytestmark = pytest.mark.gpu
@@ -84,9 +85,9 @@ def test_ipv6_single_pass_needs_workspace(native):
 
 
 @pytest.mark.parametrize("n", [(1 << 24) + 5, (1 << 25) + 4 * 1024 + 3])
-def test_ipv6_balanced_tail_equals_static(native, oracle_lib, n, monkeypatch):
+def test_ipv6_balanced_tail_equals_static(native, oracle_lib, n):
     """Launches of >= 16 rows take the balanced tail: every output equals the static
-    grid-stride launch's (RSS_BALANCE=0) and the plain launch's, the counts equal, balanced
+    grid-stride launch's (the hooks build's balance=0) and the plain launch's, the counts equal, balanced
     and static launches alternate on one workspace, and sampled hashes equal the oracle."""
     dev = torch.device("cuda:0")
     s = torch.cuda.current_stream(dev).cuda_stream
@@ -105,13 +106,13 @@ def test_ipv6_balanced_tail_equals_static(native, oracle_lib, n, monkeypatch):
     h = torch.empty_like(ref_h)
     q = torch.empty_like(ref_q)
     c = torch.empty_like(ref_c)
-    for balance in ("1", "0", "1", "1", "0"):
-        monkeypatch.setenv("RSS_BALANCE", balance)
+    for balance in (1, 0, 1, 1, 0):
         h.zero_()
         q.fill_(0xFF)
-        native.hash6_device(k6, raw.data_ptr(), n, H, Q, h.data_ptr(), q.data_ptr(),
-                            c.data_ptr(), native.FLAG_QUEUE_U8, s, ws.data_ptr())
-        torch.cuda.synchronize()
+        with hooks(balance=balance):
+            native.hash6_device(k6, raw.data_ptr(), n, H, Q, h.data_ptr(), q.data_ptr(),
+                                c.data_ptr(), native.FLAG_QUEUE_U8, s, ws.data_ptr())
+            torch.cuda.synchronize()
         assert torch.equal(h, ref_h) and torch.equal(q, ref_q) and torch.equal(c, ref_c), balance
         assert int(ws.abs().sum()) == 0
     assert int(ref_c.sum()) == n

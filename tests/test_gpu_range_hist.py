@@ -9,6 +9,8 @@ one-tuple-per-lane body and unaligned queue columns), ragged n and accumulation.
 import numpy as np
 import pytest
 
+from hooks import hooks
+
 pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
@@ -133,10 +135,10 @@ def test_ipv6_large_q(native, example_key, H, Q, outputs):
 @pytest.mark.parametrize("H,Q", [(1 << 20, 20000), (1 << 30, 65536), (1 << 30, 131072),
                                  (1 << 30, 65536 * 3 + 17)])
 def test_wide_equals_narrow_passes(native, oracle_lib, example_key, H, Q):
-    """The wide pass (u16 guard-bit LDS bins + partial-matrix reduce, one pass per 65536
-    queues) and the round-2 narrow passes (RSS_WIDE_HIST=0, one per 8192) give the oracle's
-    counts on the same launch, with and without per-tuple outputs."""
-    import os
+    """The wide passes (guarded u8 / u16 LDS bins + partial-matrix reduce) and the narrow
+    passes a launch takes when it gets no memory for their scratch (u32 bins, one pass per
+    16384 queues; forced with the hooks build's wide=0) give the oracle's counts on the same
+    launch, with and without per-tuple outputs."""
     n = (1 << 22) + 3
     host = oracle_lib.generate(27, 0, n)
     dev = torch.device("cuda:0")
@@ -144,9 +146,8 @@ def test_wide_equals_narrow_passes(native, oracle_lib, example_key, H, Q):
     tup = torch.from_numpy(host.view(np.int32).reshape(-1)).to(dev)
     want = oracle_lib.run(example_key, host, H, Q, want_hash=False, want_queue=False)[2]
     key = native.prepare_key(example_key)
-    for wide in ("1", "0"):
-        os.environ["RSS_WIDE_HIST"] = wide
-        try:
+    for wide in (1, 0):
+        with hooks(wide=wide):
             for outputs in (True, False):
                 q = (torch.empty(n, dtype=torch.int16 if Q <= 65536 else torch.int32, device=dev)
                      if outputs else None)
@@ -155,9 +156,8 @@ def test_wide_equals_narrow_passes(native, oracle_lib, example_key, H, Q):
                                    q.data_ptr() if outputs else None, c.data_ptr(),
                                    (native.FLAG_QUEUE_U16 if Q <= 65536 else 0) if outputs else 0, s)
                 torch.cuda.synchronize()
-                np.testing.assert_array_equal(c.cpu().numpy().view(np.uint64), want)
-        finally:
-            os.environ.pop("RSS_WIDE_HIST", None)
+                np.testing.assert_array_equal(c.cpu().numpy().view(np.uint64), want,
+                                              err_msg="wide=%d outputs=%s" % (wide, outputs))
 
 
 @pytest.mark.parametrize("Q,lo,hi", [(170000, SPAN8, 170000), (60000, 16384, 60000),
@@ -166,9 +166,15 @@ def test_wide_guard_bit_on_one_hot_queue(native, oracle_lib, example_key, Q, lo,
     """2^25 identical tuples plus 4099 random ones, the identical tuples' queue in [lo, hi):
     every workgroup counts ~2^17 adds into one u16 bin -- of the u16 wide pass after the u8
     hash pass (q >= 161144) or of the hash pass's own u16 range (HIST_RANGE16 on the small
-    tables, Q <= 80572; Q = 12000 is a
-    single pass) -- so the guard bit moves 2^15 out of it again and again; the counts stay
-    exact."""
+    tables, Q <= 80572; Q = 12000 is a single pass on the 12-bit tables) -- so the guard moves
+    2^15 out of it again and again; the counts stay exact, on the product library and on the
+    hooks build, which also records the guard's in-flight margin (the most adds that landed
+    on the bin between its 0x7FFF add and the guard's subtract; a margin of 2^15 or more is a
+    wrap, which poisons the pass and is recounted).  With RSS_MARGIN_LOG set the margins are
+    appended there as JSON lines."""
+    import json
+    import os
+    import hooks as hk
     n_same, n_rand = 1 << 25, 4099
     H = 1 << 30
     rnd = oracle_lib.generate(28, 0, n_rand)
@@ -179,16 +185,33 @@ def test_wide_guard_bit_on_one_hot_queue(native, oracle_lib, example_key, Q, lo,
     dev = torch.device("cuda:0")
     s = torch.cuda.current_stream(dev).cuda_stream
     tup = torch.from_numpy(host.view(np.int32).reshape(-1)).to(dev)
-    c = torch.zeros(Q, dtype=torch.int64, device=dev)
-    native.hash_device(native.prepare_key(example_key), tup.data_ptr(), len(host), H, Q, None,
-                       None, c.data_ptr(), 0, s)
-    torch.cuda.synchronize()
     _, q1, _ = oracle_lib.run(example_key, one, H, Q)
     want = oracle_lib.run(example_key, rnd, H, Q, want_hash=False, want_queue=False)[2]
     want[int(q1[0])] += n_same
-    got = c.cpu().numpy().view(np.uint64)
-    np.testing.assert_array_equal(got, want)
-    assert int(got[int(q1[0])]) >= n_same
+    key = native.prepare_key(example_key)
+    for lib in ("product", "hooks"):
+        c = torch.zeros(Q, dtype=torch.int64, device=dev)
+        with hooks() if lib == "hooks" else _nullcontext():
+            if lib == "hooks":
+                hk.guard_margin(reset=True)
+            native.hash_device(key, tup.data_ptr(), len(host), H, Q, None, None, c.data_ptr(), 0, s)
+            torch.cuda.synchronize()
+            margin = hk.guard_margin(reset=True) if lib == "hooks" else None
+        got = c.cpu().numpy().view(np.uint64)
+        np.testing.assert_array_equal(got, want, err_msg=lib)
+        if margin is not None:
+            kind = "wide16" if lo >= SPAN8 else "hash16"
+            assert margin[kind] > 0, margin  # the guard fired
+            log = os.environ.get("RSS_MARGIN_LOG")
+            if log:
+                with open(log, "a") as f:
+                    f.write(json.dumps({"Q": Q, "queue": int(q1[0]), "n_same": n_same,
+                                        "guard": kind, "margin": margin}) + "\n")
+
+
+def _nullcontext():
+    import contextlib
+    return contextlib.nullcontext()
 
 
 @pytest.mark.parametrize("H,Q", [(1 << 20, 16385), (0xFFFFFFFF, 65536), (1 << 30, SPAN16),
@@ -197,12 +220,11 @@ def test_wide_guard_bit_on_one_hot_queue(native, oracle_lib, example_key, Q, lo,
                                  (60001, 30011)])
 def test_byte_tables_equal_12bit_tables(native, oracle_lib, example_key, H, Q):
     """Many-queues launches hash on the 21 conflict-free 5-bit small tables (kSmallLut: up to
-    80572 queues in the hash pass's u16 bins, 161144 in u8 bins); RSS_SMALL_LUT=0 keeps the
-    12-bit tables (16384 queues, then the queue column).  Counts only past 161144 queues: the
+    80572 queues in the hash pass's u16 bins, 161144 in u8 bins); the hooks build's small_lut=0
+    keeps the 12-bit tables (16384 queues, then the queue column).  Counts only past 161144 queues: the
     scratch column holds q - 161144 as u16 up to Q = 226679 (QW_U16R), the queues themselves
     (u32) from 226680 on.  Both give the oracle's hashes, queues and counts on uniform and flow-like
     input (one address pair, sequential ports), with outputs and counts only."""
-    import os
     n = (1 << 21) + 5
     uni = oracle_lib.generate(29, 0, n)
     flow = uni.copy()
@@ -215,9 +237,8 @@ def test_byte_tables_equal_12bit_tables(native, oracle_lib, example_key, H, Q):
     for host in (uni, flow):
         tup = torch.from_numpy(host.view(np.int32).reshape(-1)).to(dev)
         ho, qo, co = oracle_lib.run(example_key, host, H, Q)
-        for lut in ("1", "0"):
-            os.environ["RSS_SMALL_LUT"] = lut
-            try:
+        for lut in (1, 0):
+            with hooks(small_lut=lut):
                 h = torch.empty(n, dtype=torch.int32, device=dev)
                 q = torch.empty(n, dtype=torch.int16 if u16 else torch.int32, device=dev)
                 c = torch.full((Q,), 9, dtype=torch.int64, device=dev)
@@ -226,8 +247,6 @@ def test_byte_tables_equal_12bit_tables(native, oracle_lib, example_key, H, Q):
                 c2 = torch.full((Q,), 9, dtype=torch.int64, device=dev)
                 native.hash_device(key, tup.data_ptr(), n, H, Q, None, None, c2.data_ptr(), 0, s)
                 torch.cuda.synchronize()
-            finally:
-                os.environ.pop("RSS_SMALL_LUT", None)
             np.testing.assert_array_equal(h.cpu().numpy().view(np.uint32), ho)
             qv = q.cpu().numpy().view(np.uint16 if u16 else np.uint32).astype(np.uint32)
             np.testing.assert_array_equal(qv, qo)
@@ -269,17 +288,12 @@ def _launch(native, key, tup, n, H, Q, outputs, counts_fill=0, flags=0):
     return h, q, c
 
 
-def _with_env(name, value, fn):
-    import os
-    old = os.environ.get(name)
-    os.environ[name] = value
-    try:
+def _with_opt(name, value, fn):
+    """fn() on the hooks build with one option set (name None: the product library)"""
+    if name is None:
         return fn()
-    finally:
-        if old is None:
-            os.environ.pop(name, None)
-        else:
-            os.environ[name] = old
+    with hooks(**{name: value}):
+        return fn()
 
 
 @pytest.mark.parametrize("Q", [SPAN16 + 1, 131072, SPAN8, SPAN8 + 1, SPAN8 + 65535, SPAN8 + 65536,
@@ -290,24 +304,24 @@ def test_range8_u8_bins_equal_oracle(native, oracle_lib, example_key, Q):
     (HIST_RANGE8: guard at 0x80, moves into a u32 per queue, poison-gated recount); past
     161144 it is the first range of a queue-column launch (counts only: a u16 column of
     q - 161144 up to Q = 226679, u32 beyond), whose passes over the column take 163840
-    queues each in u8 bins while more than 65536 are left (one u16 pass for the rest).  On uniform input the u8 path alone
-    (RSS_RANGE8_DEBUG=nofallback: no gate, no recount), the recount alone
-    (RSS_RANGE8_DEBUG=force), the default and the u16 path (RSS_RANGE8=0) all give the
-    oracle's hashes, queues and counts, with and without per-tuple outputs.  Counts only past
-    161144 queues the hash pass appends the residual queues to per-workgroup lists that the
-    wide passes read one workgroup per list (default), or writes the scratch column
-    (RSS_RESID=0); both with the load prefetch and with the static walk (RSS_PREFETCH=0)."""
+    queues each in u8 bins while more than 65536 are left (one u16 pass for the rest).  On
+    uniform input the bins alone (hooks build, recount=2: no gate, no recount), the recount
+    alone (recount=1: every guarded pass poisoned), the default and the u16 path (range8=0)
+    all give the oracle's hashes, queues and counts, with and without per-tuple outputs.
+    Counts only past 161144 queues the hash pass appends the residual queues to per-wave
+    lists that the wide passes read one wave per list (default), or writes the scratch column
+    (resid=0, the path without memory for the lists); both with the load prefetch and with
+    the static walk (prefetch=0)."""
     n, H = (1 << 21) + 5, 1 << 30
     host = oracle_lib.generate(31, 0, n)
     tup = torch.from_numpy(host.view(np.int32).reshape(-1)).to("cuda:0")
     key = native.prepare_key(example_key)
     ho, qo, co = oracle_lib.run(example_key, host, H, Q)
-    runs = [("RSS_RANGE8_DEBUG", "nofallback"), ("RSS_RANGE8_DEBUG", "force"),
-            ("RSS_RANGE8", "1"), ("RSS_RANGE8", "0"), ("RSS_RESID", "0"),
-            ("RSS_PREFETCH", "0")]
+    runs = [("recount", 2), ("recount", 1), (None, None), ("range8", 0), ("resid", 0),
+            ("prefetch", 0)]
     for name, value in runs:
         for outputs in (True, False):
-            h, q, c = _with_env(name, value,
+            h, q, c = _with_opt(name, value,
                                 lambda: _launch(native, key, tup, n, H, Q, outputs, counts_fill=7))
             np.testing.assert_array_equal(c.cpu().numpy().view(np.uint64), co,
                                           err_msg="%s=%s outputs=%s" % (name, value, outputs))
@@ -321,8 +335,8 @@ def test_range8_guard_moves(native, oracle_lib, example_key, Q):
     """1024 distinct tuples repeated over 2^26 tuples: every workgroup adds ~256 times into
     each of their u8 bins, a few at a time, so the 0x80 guard moves 128 out of a bin into its
     u32 again and again without a bin ever wrapping.  With the gate and the recount switched
-    off (RSS_RANGE8_DEBUG=nofallback) the counts come from the u8 bins and the guard moves
-    alone -- and equal the oracle's; the default launch agrees."""
+    off (hooks build, recount=2) the counts come from the u8 bins and the guard moves alone
+    -- and equal the oracle's; the product launch agrees."""
     n, H, base_n = 1 << 26, 1 << 30, 1024
     base = oracle_lib.generate(32, 0, base_n)
     host = np.tile(base, (n // base_n, 1))
@@ -330,9 +344,9 @@ def test_range8_guard_moves(native, oracle_lib, example_key, Q):
     _, qb, _ = oracle_lib.run(example_key, base, H, Q)
     want = np.bincount(qb.astype(np.int64), minlength=Q).astype(np.uint64) * np.uint64(n // base_n)
     key = native.prepare_key(example_key)
-    for value in ("nofallback", "default"):
+    for value in (2, None):
         for outputs in (True, False):
-            _, q, c = _with_env("RSS_RANGE8_DEBUG", value,
+            _, q, c = _with_opt("recount" if value else None, value,
                                 lambda: _launch(native, key, tup, n, H, Q, outputs))
             np.testing.assert_array_equal(c.cpu().numpy().view(np.uint64), want,
                                           err_msg="%s outputs=%s" % (value, outputs))
@@ -374,8 +388,7 @@ def test_range8_poisoned_pass_recounts(native, oracle_lib, example_key, Q, outpu
         got = q.cpu().numpy().view(np.uint32)
         assert np.all(got[2000:2000 + n_same] == q_rnd[pick])
     # the u8 bins alone are wrong here: proof that the poison gate is what kept them out
-    _, _, bad = _with_env("RSS_RANGE8_DEBUG", "nofallback",
-                          lambda: _launch(native, key, tup, n, H, Q, outputs))
+    _, _, bad = _with_opt("recount", 2, lambda: _launch(native, key, tup, n, H, Q, outputs))
     assert not np.array_equal(bad.cpu().numpy().view(np.uint64), want)
 
 
@@ -398,3 +411,111 @@ def test_range8_zipf_flows_equal_oracle(native, oracle_lib, example_key, Q, outp
     np.testing.assert_array_equal(c.cpu().numpy().view(np.uint64), want)
     if outputs:
         np.testing.assert_array_equal(q.cpu().numpy().view(np.uint32), qb[pick])
+
+
+@pytest.mark.parametrize("Q", [12000, 40000, SPAN16])
+@pytest.mark.parametrize("outputs", [True, False])
+def test_range16_recount_and_bins_alone(native, oracle_lib, example_key, Q, outputs):
+    """The hash pass's own u16 bins (HIST_RANGE16: one pass for Q = 12000 on the 12-bit
+    tables, Q = 40000 and 80572 on the small tables) carry the guard (a move of 2^15 into a
+    u32 per queue) and the poison word: on uniform input the bins and moves alone (hooks
+    build, recount=2: no gate, no recount), the recount alone (recount=1: the pass poisoned
+    -- from the caller's queue column, or by rehashing for counts only) and the product
+    launch all give the oracle's counts, accumulating onto the caller's counts too."""
+    n, H = (1 << 21) + 5, 1 << 30
+    host = oracle_lib.generate(35, 0, n)
+    tup = torch.from_numpy(host.view(np.int32).reshape(-1)).to("cuda:0")
+    key = native.prepare_key(example_key)
+    ho, qo, co = oracle_lib.run(example_key, host, H, Q)
+    for name, value in (("recount", 2), ("recount", 1), (None, None)):
+        h, q, c = _with_opt(name, value, lambda: _launch(native, key, tup, n, H, Q, outputs,
+                                                         counts_fill=5, flags=native.FLAG_ACCUMULATE))
+        np.testing.assert_array_equal(c.cpu().numpy().view(np.uint64), co + np.uint64(5),
+                                      err_msg="%s=%s outputs=%s" % (name, value, outputs))
+        if outputs:
+            np.testing.assert_array_equal(h.cpu().numpy().view(np.uint32), ho)
+            np.testing.assert_array_equal(q.cpu().numpy().view(np.uint32), qo)
+
+
+def test_range16_recount_with_reta_and_misaligned(native, oracle_lib, example_key):
+    """The u16 pass's recount by rehashing with an indirection table (QM_TABLE: the table in
+    the recount's LDS beside its u32 bins) and on misaligned tuples (one tuple per lane, the
+    12-bit tables), and from a caller's u16 queue column at a 2-byte offset -- each forced
+    (recount=1) and as measured, against the oracle."""
+    n, H = (1 << 20) + 3, 1024
+    rng = np.random.default_rng(36)
+    reta = rng.integers(0, 12000, H).astype(np.uint32)
+    host = oracle_lib.generate(36, 0, n)
+    flat = host.view(np.int32).reshape(-1)
+    buf = torch.zeros(flat.size + 1, dtype=torch.int32, device="cuda:0")
+    buf[1:] = torch.from_numpy(flat).to("cuda:0")
+    tup = torch.from_numpy(flat).to("cuda:0")
+    key = native.prepare_key(example_key)
+    s = torch.cuda.current_stream().cuda_stream
+    ho, _, _ = oracle_lib.run(example_key, host, 1, 1, want_queue=False)
+    want_reta = np.bincount(reta[ho % H], minlength=12000).astype(np.uint64)
+    Hm, Qm = 1 << 30, 20000
+    _, qo, co = oracle_lib.run(example_key, host, Hm, Qm)
+    for recount in (1, 0):
+        with hooks(recount=recount):
+            c = torch.zeros(12000, dtype=torch.int64, device="cuda:0")
+            native.hash_device_reta(key, tup.data_ptr(), n, H, reta, 12000, None, None,
+                                    c.data_ptr(), 0, s)
+            c2 = torch.zeros(Qm, dtype=torch.int64, device="cuda:0")
+            native.hash_device(key, buf.data_ptr() + 4, n, Hm, Qm, None, None, c2.data_ptr(), 0, s)
+            qbuf = torch.zeros(n + 8, dtype=torch.int16, device="cuda:0")
+            c3 = torch.zeros(Qm, dtype=torch.int64, device="cuda:0")
+            native.hash_device(key, tup.data_ptr(), n, Hm, Qm, None, qbuf.data_ptr() + 2,
+                               c3.data_ptr(), native.FLAG_QUEUE_U16, s)
+            torch.cuda.synchronize()
+        np.testing.assert_array_equal(c.cpu().numpy().view(np.uint64), want_reta)
+        np.testing.assert_array_equal(c2.cpu().numpy().view(np.uint64), co)
+        np.testing.assert_array_equal(c3.cpu().numpy().view(np.uint64), co)
+        np.testing.assert_array_equal(qbuf[1:n + 1].cpu().numpy().view(np.uint16).astype(np.uint32), qo)
+
+
+@pytest.mark.parametrize("Q,outputs", [(50000, False), (50000, True), (12000, False)])
+def test_range16_heavy_hitter(native, oracle_lib, example_key, Q, outputs):
+    """2^24 copies of one tuple plus 4099 random ones at Q = 50000 (the small tables' u16
+    pass) and 12000 (the 12-bit tables'): every workgroup piles ~65536 adds onto one u16 bin,
+    which its guard empties by 2^15 again and again.  The product launch, the recount alone
+    and the bins and moves alone give the oracle's counts (accumulating)."""
+    n_same, n_rand, H = 1 << 24, 4099, 1 << 30
+    rnd = oracle_lib.generate(37, 0, n_rand)
+    _, q_rnd, _ = oracle_lib.run(example_key, rnd, H, Q)
+    one = rnd[:1]
+    host = np.concatenate([rnd[:2000], np.repeat(one, n_same, axis=0), rnd[2000:]])
+    n = len(host)
+    tup = torch.from_numpy(host.view(np.int32).reshape(-1)).to("cuda:0")
+    want = oracle_lib.run(example_key, rnd, H, Q, want_hash=False, want_queue=False)[2]
+    want[int(q_rnd[0])] += n_same
+    key = native.prepare_key(example_key)
+    for name, value in ((None, None), ("recount", 1), ("recount", 2)):
+        _, q, c = _with_opt(name, value, lambda: _launch(native, key, tup, n, H, Q, outputs,
+                                                         counts_fill=11, flags=native.FLAG_ACCUMULATE))
+        np.testing.assert_array_equal(c.cpu().numpy().view(np.uint64), want + np.uint64(11),
+                                      err_msg="%s=%s" % (name, value))
+        if outputs:
+            assert np.all(q.cpu().numpy().view(np.uint32)[2000:2000 + n_same] == q_rnd[0])
+
+
+def test_guard_margin_readout(native, oracle_lib, example_key):
+    """The hooks build records the adds that land on a guarded bin between its half-range add
+    and the guard's subtract: after a heavy-hitter u16 launch the hash pass's margin is read
+    (and is below the 2^15 that would wrap the field, or the launch's counts were recounted)
+    and the read resets it."""
+    import hooks as hk
+    n_same, H, Q = 1 << 24, 1 << 30, 50000
+    rnd = oracle_lib.generate(38, 0, 64)
+    host = np.concatenate([np.repeat(rnd[:1], n_same, axis=0), rnd])
+    tup = torch.from_numpy(host.view(np.int32).reshape(-1)).to("cuda:0")
+    key = native.prepare_key(example_key)
+    with hooks():
+        hk.guard_margin(reset=True)
+        _, _, c = _launch(native, key, tup, len(host), H, Q, False)
+        m = hk.guard_margin(reset=True)
+        m2 = hk.guard_margin(reset=False)
+    assert int(c.sum()) == len(host)
+    print("guard margin", m)
+    assert m["hash16"] > 0  # the guard fired (~65536 adds per workgroup on one bin)
+    assert all(v == 0 for v in m2.values())

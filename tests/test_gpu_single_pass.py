@@ -6,8 +6,12 @@ that take the workspace (LDS-table kernel with private and shared bins, the regi
 counts-only kernel, 4-tuple and 1-tuple lanes) and the shapes that do not (many queues);
 overwrite and RSS_FLAG_ACCUMULATE; one-workgroup grids; n = 0; the workspace left zero after
 every launch and reused over many launches, HIP-graph replay and two streams at once."""
+import contextlib
+
 import numpy as np
 import pytest
+
+from hooks import hooks
 
 pytestmark = pytest.mark.gpu
 
@@ -281,74 +285,13 @@ def test_stress_one_workspace_many_launches(native, oracle_lib, example_key):
     assert int(ws.abs().sum()) == 0
 
 
-VARIANT_SCRIPT = r"""
-import sys
-import numpy as np
-import torch
-sys.path.insert(0, %(root)r)
-from oracle.oracle import OracleLib
-from rss_simulator_nvidia_amd import _native
-lib = OracleLib()
-key_bytes = %(key)r
-H, Q, n = 128, 24, (1 << 20) + 3
-host = lib.generate(7, 0, n)
-want = lib.run(key_bytes, host, H, Q, want_hash=False, want_queue=False)[2]
-dev = torch.device("cuda:0")
-t = torch.from_numpy(host.view(np.int32).reshape(-1)).to(dev)
-ws = torch.zeros(_native.counts_workspace_bytes(H, Q) // 8, dtype=torch.int64, device=dev)
-outs = torch.zeros((300, Q), dtype=torch.int64, device=dev)
-key = _native.prepare_key(key_bytes)
-s = torch.cuda.current_stream().cuda_stream
-for i in range(300):
-    _native.hash_device(key, t.data_ptr(), n, H, Q, None, None, outs[i].data_ptr(), 0, s,
-                        ws.data_ptr())
-got = outs.cpu().numpy().view(np.uint64)
-assert (got == want[None, :]).all(), "mismatch"
-assert int(ws.abs().sum()) == 0
-# balanced-tail launches (>= 16 rows: the fold also resets the unit counter), outputs on
-n2 = (1 << 24) + 4099
-host2 = lib.generate(8, 0, n2)
-want2 = lib.run(key_bytes, host2, H, Q, want_hash=False, want_queue=False, threads=8,
-               fn="oracle_run_tables")[2]
-t2 = torch.from_numpy(host2.view(np.int32).reshape(-1)).to(dev)
-h2 = torch.empty(n2, dtype=torch.int32, device=dev)
-outs2 = torch.zeros((40, Q), dtype=torch.int64, device=dev)
-for i in range(40):
-    _native.hash_device(key, t2.data_ptr(), n2, H, Q, h2.data_ptr(), None, outs2[i].data_ptr(),
-                        0, s, ws.data_ptr())
-got2 = outs2.cpu().numpy().view(np.uint64)
-assert (got2 == want2[None, :]).all(), "balanced-tail mismatch"
-assert int(ws.abs().sum()) == 0
-print("variant ok")
-"""
-
-
-@pytest.mark.parametrize("env", [{"RSS_WS_ORDER": "relaxed"}, {"RSS_FOLD": "ticket"},
-                                 {"RSS_FOLD": "ticket", "RSS_WS_ORDER": "relaxed"}])
-def test_fold_variants(example_key, env):
-    """The other single-pass folds give the same counts launch after launch, static and with
-    the balanced tail: RSS_WS_ORDER=relaxed (no release / acquire: the hardware-assumption
-    hand-off of round 2; the ticket fold is release/acquire since ADVICE r02) and RSS_FOLD=ticket
-    (sums + ticket + the last workgroup's exchanges, rounds 2-3; the default is the arrival
-    fold) -- in a child process, so the variables never leak here."""
-    import os
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    code = VARIANT_SCRIPT % {"root": root, "key": list(example_key)}
-    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240,
-                       env=dict(os.environ, **env))
-    assert p.returncode == 0 and "variant ok" in p.stdout, p.stdout + p.stderr
-
-
 @pytest.mark.parametrize("n", [1 << 24, (1 << 24) + 4099, 3 * (1 << 23) + 5, (1 << 25) + 1234567])
 def test_balanced_tail_equals_oracle(native, oracle_lib, example_key, n):
     """Single-pass launches of >= 16 grid rows hand their last ~1/10 of the rows out per
     workgroup slot (the balanced tail): every tuple is hashed exactly once --
     hashes and u8 queues element-wise equal to the oracle, counts exact, launch after launch
     on one workspace (left zero, its tail counter included) -- and equal to the static
-    grid-stride launch (RSS_BALANCE=0) on the same buffers."""
-    import os
+    grid-stride launch (the hooks build's balance=0) on the same buffers."""
     H, Q = 128, 24
     key = native.prepare_key(example_key)
     s = torch.cuda.current_stream().cuda_stream
@@ -360,13 +303,10 @@ def test_balanced_tail_equals_oracle(native, oracle_lib, example_key, n):
     queues = torch.full((n,), 255, dtype=torch.uint8, device=DEV)
     outs = torch.zeros((12, Q), dtype=torch.int64, device=DEV)
     for i in range(12):
-        if i == 6:  # static launches on the same workspace in between
-            os.environ["RSS_BALANCE"] = "0"
-        elif i == 9:
-            os.environ.pop("RSS_BALANCE", None)
-        native.hash_device(key, t.data_ptr(), n, H, Q, hashes.data_ptr(), queues.data_ptr(),
-                           outs[i].data_ptr(), native.FLAG_QUEUE_U8, s, ws.data_ptr())
-    os.environ.pop("RSS_BALANCE", None)
+        # launches 6..8: static ones (hooks build) on the same workspace in between
+        with hooks(balance=0) if 6 <= i < 9 else contextlib.nullcontext():
+            native.hash_device(key, t.data_ptr(), n, H, Q, hashes.data_ptr(), queues.data_ptr(),
+                               outs[i].data_ptr(), native.FLAG_QUEUE_U8, s, ws.data_ptr())
     torch.cuda.synchronize()
     np.testing.assert_array_equal(hashes.cpu().numpy().view(np.uint32), h_want)
     np.testing.assert_array_equal(queues.cpu().numpy(), q_want.astype(np.uint8))
@@ -407,8 +347,7 @@ def test_balanced_tail_counts_only(native, oracle_lib, example_key, n):
     """Counts-only single-pass launches (the register-table kernel, two workgroups per CU)
     keep the static walk (the balanced tail measured 5 % slower there): counts exact over
     40 launches on one workspace of a workspace that full-output launches also use for their
-    tail counter, with RSS_BALANCE toggled in between."""
-    import os
+    tail counter, with static launches (the hooks build's balance=0) in between."""
     H, Q = 128, 24
     key = native.prepare_key(example_key)
     s = torch.cuda.current_stream().cuda_stream
@@ -418,16 +357,10 @@ def test_balanced_tail_counts_only(native, oracle_lib, example_key, n):
     t = torch.from_numpy(host.view(np.int32).reshape(-1)).to(DEV)
     ws = _ws(native, H, Q)
     outs = torch.zeros((40, Q), dtype=torch.int64, device=DEV)
-    try:
-        for i in range(40):
-            if i % 10 == 5:
-                os.environ["RSS_BALANCE"] = "0"
-            elif i % 10 == 8:
-                os.environ.pop("RSS_BALANCE", None)
+    for i in range(40):
+        with hooks(balance=0) if 5 <= i % 10 < 8 else contextlib.nullcontext():
             native.hash_device(key, t.data_ptr(), n, H, Q, None, None, outs[i].data_ptr(), 0, s,
                                ws.data_ptr())
-    finally:
-        os.environ.pop("RSS_BALANCE", None)
     got = outs.cpu().numpy().view(np.uint64)
     for i in range(40):
         np.testing.assert_array_equal(got[i], want)

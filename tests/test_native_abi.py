@@ -175,3 +175,37 @@ def test_copy_out_is_an_exact_owned_copy(n):
     b = _native._copy_out(a)
     assert b.dtype == np.uint8 and b.shape == a.shape and np.array_equal(a, b)
     assert n == 0 or b.ctypes.data != a.ctypes.data
+
+
+def _strings(path):
+    with open(path, "rb") as f:
+        return set(re.findall(rb"[\x20-\x7e]{4,}", f.read()))
+
+
+def test_product_library_reads_no_switches(lib):
+    """The product library takes every launch's path from its arguments: it names none of
+    the rounds-2..4 environment switches (RSS_RANGE8_DEBUG and the like), exports no test
+    hook, and the hooks build (tests only) exports them and is a separate file."""
+    import hooks as hk
+    text = b"\n".join(_strings(_native.LIB_PATH))
+    for name in (b"RSS_RANGE8", b"RSS_WS_ORDER", b"RSS_FOLD", b"RSS_RESID", b"RSS_WIDE_HIST",
+                 b"RSS_TAIL_DIV", b"RSS_COUNTS_PERM", b"RSS_OFF32", b"RSS_PREFETCH",
+                 b"RSS_BALANCE", b"RSS_SMALL_LUT", b"rss_test_set_option"):
+        assert name not in text, name
+    assert not hasattr(lib, "rss_test_set_option")
+    h = hk.load_hooks()
+    assert os.path.abspath(hk.HOOKS_PATH) != os.path.abspath(_native.LIB_PATH)
+    for sym in ("rss_test_set_option", "rss_test_reset_options", "rss_test_guard_margin"):
+        assert hasattr(h, sym)
+    assert all(hasattr(h, s) for s in _native.EXPORTED_SYMBOLS)
+
+
+def test_hook_options_validate_and_restore(lib):
+    """Unknown hook options are refused; the context restores the product library."""
+    import hooks as hk
+    with pytest.raises(ValueError):
+        with hk.hooks(no_such_option=1):
+            pass
+    with hk.hooks(recount=1, range8=0) as h:
+        assert _native.load() is h
+    assert _native.load() is lib

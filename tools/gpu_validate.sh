@@ -2,9 +2,8 @@
 # GPU box: the round's one final validation of the last tree, in two stages that each fit one
 # call -- `tests`: the full -m gpu suite and smoke(); `perf`: the driver's bench command, a
 # rocprofv3 kernel trace of the same command (+ its timed-launch summary), the FETCH_SIZE /
-# WRITE_SIZE passes of the bench's step, the same-buffer A/B of the step's variants, the
-# many-queues probe, the (H, Q) sweep and the distributed bench lines (world-1 RCCL, 8-rank
-# gloo rehearsal).
+# WRITE_SIZE passes of the bench's step and the distributed bench lines (world-1 RCCL,
+# 8-rank gloo rehearsal).
 # usage: tools/gpu_validate.sh TAG [tests|perf|all]     (outputs under gpurun_out/TAG/)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -34,10 +33,6 @@ if [ "$STAGE" = perf ] || [ "$STAGE" = all ]; then
   cat $O/prof_timed.json
   mkdir -p $O/pmc && bash $R/tools/pmc_traffic.sh $TAG/pmc > $O/pmc.log 2>&1
   cd $R
-  for p in 1 2; do timeout -k 10 200 python tools/ws_order_ab.py 6 > $O/ab_$p.json 2> $O/ab_$p.err; done
-  timeout -k 10 300 python tools/range8_probe.py 65536 131072 161144 262144 1000000 \
-      > $O/range8_probe.jsonl 2> $O/range8.err
-  timeout -k 10 600 python tools/config_sweep_probe.py > $O/config_sweep.jsonl 2> $O/sweep.err
   bash tools/gpu_dist_lines.sh $TAG/dist > $O/dist.log 2>&1
 fi
 echo "validate done"
