@@ -339,6 +339,84 @@ def gather_rows(torch, dist, row, device, distributed, world):
     return [o.tolist() for o in out]
 
 
+def max_over_ranks(torch, dist, values, device, distributed):
+    """Element-wise max of ``values`` (floats) over the ranks (rank-local without a group)."""
+    t = torch.tensor(values, dtype=torch.float64, device=device)
+    if distributed:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(x) for x in t.tolist()]
+
+
+def verified_of(rows, has_configs3):
+    """True: every rank's checks passed; False: any failed; None: nothing was checkable."""
+    codes = [r[7] for r in rows] + ([r[8] for r in rows] if has_configs3 else [])
+    return False if 0.0 in codes else (True if 1.0 in codes and -1.0 not in codes else None)
+
+
+def run_bucketed(pipe, launch, steps, warmup, barrier, sync, reduce_max, n, world, Q):
+    """The labelled secondary block at N > 1: the main line's steps with B = ``pipe.bucket``
+    steps' count rows per collective (CountsPipeline(bucket=B)) -- fewer exchanges than the
+    reference's one histogram per batch, so never the ``value``.  ``reduce_max`` = max over
+    ranks of a list of floats; the last reduced row must hold n * world tuples."""
+    for _ in range(warmup):
+        pipe.step(launch)
+    pipe.drain()
+    barrier()
+    sync()
+    tb = time.perf_counter()
+    for _ in range(steps):
+        pipe.step(launch)
+    blast = pipe.drain()
+    sync()
+    barrier()
+    b_elapsed = reduce_max([time.perf_counter() - tb])[0]
+    if int(blast.sum().item()) != n * world:
+        raise SystemExit("bench: bucketed counts sum to %d, expected %d"
+                         % (int(blast.sum().item()), n * world))
+    return {"steps_per_collective": pipe.bucket,
+            "collectives": -(-steps // pipe.bucket),
+            "value": n * world * steps / b_elapsed,
+            "ms_per_step": b_elapsed * 1e3 / steps,
+            "note": "secondary: the main line's steps with %d steps' count rows per "
+                    "collective (rows of a [%d, %d] bucket; every row is still its own "
+                    "batch's reduced histogram) -- not the reference's one exchange per "
+                    "batch, so not `value`" % (pipe.bucket, pipe.bucket, Q)}
+
+
+def configs3_block(total, world, H, Q, steps, allreduce, distributed, stats_max, qw):
+    """The ``configs3`` block from the slowest rank's [elapsed s, step ms, kernel ms, shard
+    tuples] (``stats_max``)."""
+    elapsed_max, step_max, kernel_max, n3_max = stats_max
+    write_bytes = HASH_BYTES + QUEUE_BYTES[qw]
+    achieved = n3_max * (READ_BYTES + write_bytes) / (kernel_max / 1e3) / 1e9
+    return {
+        "workload": "configs[3]: %d global synthetic 4-tuples split over %d rank(s) by "
+                    "sharding.shard_range (contiguous shards), htable=%d, queues=%d; one batch "
+                    "= one rss_hash_device_ws launch per rank + ONE %s of the batch's uint64[%d] "
+                    "counts" % (total, world, H, Q,
+                                {"rccl": "ncclAllReduce (rccl.RcclComm, launch stream)",
+                                 "overlap": "torch.distributed all-reduce" if distributed
+                                 else "local histogram (no process group)",
+                                 "stream": "torch.distributed all-reduce"}[allreduce], Q),
+        "global_tuples": total,
+        "tuples_per_rank_max": int(n3_max),
+        "steps": steps,
+        "scaling": "strong",
+        "ms_per_batch": elapsed_max * 1e3 / steps,
+        "tuples_per_s": total * steps / elapsed_max,
+        "step_ms_max_rank": step_max,
+        "kernel_ms_max_rank": kernel_max,
+        "exchange_ms_est": step_max - kernel_max,
+        "timing": "ms_per_batch = wall time of the timed batches (barrier + synchronize on "
+                  "both sides, slowest rank) / steps; step_ms = one HIP event pair on the "
+                  "launch stream around the timed batches (launch + all-reduce); kernel_ms = "
+                  "the same number of launches without the collective, after the region",
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "bytes_per_tuple": READ_BYTES + write_bytes},
+    }
+
+
 def run_configs3(args, torch, dist, _native, dev, stream, key, comm, rank, world, distributed,
                  barrier, qw, probe, gold):
     """BASELINE configs[3] as a strong-scaling batch: ``--configs3-tuples`` global tuples of
@@ -396,11 +474,8 @@ def run_configs3(args, torch, dist, _native, dev, stream, key, comm, rank, world
     ev[3].record(stream)
     torch.cuda.synchronize()
     kernel_ms = ev[2].elapsed_time(ev[3]) / steps
-    stats = torch.tensor([elapsed, step_ms, kernel_ms, float(n3)], dtype=torch.float64,
-                         device=dev if args.dist_backend == "nccl" else "cpu")
-    if distributed:
-        dist.all_reduce(stats, op=dist.ReduceOp.MAX)
-    elapsed_max, step_max, kernel_max, n3_max = (float(x) for x in stats.tolist())
+    stats_max = max_over_ranks(torch, dist, [elapsed, step_ms, kernel_ms, float(n3)],
+                               dev if args.dist_backend == "nccl" else "cpu", distributed)
     counts = [int(x) & ((1 << 64) - 1) for x in last.tolist()]
     if sum(counts) != total:
         raise SystemExit("bench: configs[3] counts sum to %d, expected %d" % (sum(counts), total))
@@ -409,39 +484,14 @@ def run_configs3(args, torch, dist, _native, dev, stream, key, comm, rank, world
         verified = verify_outputs(torch, gold, batch.hashes, batch.queue_view(), first, n3)
         want = golden_counts(gold, 0, total)
         verified["counts_ok"] = None if want is None else counts[:len(want)] == want
-    write_bytes = HASH_BYTES + QUEUE_BYTES[qw]
-    achieved = n3_max * (READ_BYTES + write_bytes) / (kernel_max / 1e3) / 1e9
-    out = {
-        "workload": "configs[3]: %d global synthetic 4-tuples split over %d rank(s) by "
-                    "sharding.shard_range (contiguous shards), htable=%d, queues=%d; one batch "
-                    "= one rss_hash_device_ws launch per rank + ONE %s of the batch's uint64[%d] "
-                    "counts" % (total, world, H, Q,
-                                {"rccl": "ncclAllReduce (rccl.RcclComm, launch stream)",
-                                 "overlap": "torch.distributed all-reduce" if distributed
-                                 else "local histogram (no process group)",
-                                 "stream": "torch.distributed all-reduce"}[allreduce], Q),
-        "global_tuples": total,
-        "tuples_per_rank_max": int(n3_max),
-        "steps": steps,
-        "scaling": "strong",
-        "ms_per_batch": elapsed_max * 1e3 / steps,
-        "tuples_per_s": total * steps / elapsed_max,
-        "step_ms_max_rank": step_max,
-        "kernel_ms_max_rank": kernel_max,
-        "exchange_ms_est": step_max - kernel_max,
-        "timing": "ms_per_batch = wall time of the timed batches (barrier + synchronize on "
-                  "both sides, slowest rank) / steps; step_ms = one HIP event pair on the "
-                  "launch stream around the timed batches (launch + all-reduce); kernel_ms = "
-                  "the same number of launches without the collective, after the region",
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS,
-                     "bytes_per_tuple": READ_BYTES + write_bytes},
+    out = configs3_block(total, world, H, Q, steps, allreduce, distributed, stats_max, qw)
+    out.update({
         "placement_rank0": dict(batch.report),
         "verified": verified,
         "kernel_ms_rank": kernel_ms,
         "placement_rank": {"chosen_ms": batch.report["chosen_ms"],
                            "first_allocation_ms": batch.report["first_allocation_ms"]},
-    }
+    })
     del batch, pipe, local
     torch.cuda.empty_cache()
     return out
@@ -542,6 +592,151 @@ def extra_lines(torch, _native, dev, stream, key_bytes):
                                        "1024 SIMDs / (4 x 99) per 512 evaluations, LDS 256 CUs / "
                                        "58 per 512"}
     return out
+
+
+def build_line(args, m):
+    """Rank 0's JSON line from the measurements ``m`` (every rank's reduced / gathered
+    values, rank 0's secondary timings); DESIGN.md §5 documents every field."""
+    n, world, H, Q, qw = m["n"], m["world"], args.htable, args.queues, m["qw"]
+    distributed, rows, c3 = m["distributed"], m["rows"], m["c3"]
+    kernel_ms_max, launch_ms, bucket = m["kernel_ms_max"], m["launch_ms"], m["bucket"]
+    co_ms, u32_ms, flow_ms = m["co_ms"], m["u32_ms"], m["flow_ms"]
+    value = n * world * args.steps / m["elapsed"]
+    # the slowest rank's mean launch time: at N > 1 the fraction is the worst rank's
+    write_bytes = m["write_bytes"]
+    achieved = n * (READ_BYTES + write_bytes) / (kernel_ms_max / 1e3) / 1e9
+    line = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "tuples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": m["elapsed"] * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": ("synthetic: splitmix64 IPv4 4-tuples generated on device, resident in HBM"
+                 if args.distribution == "uniform" else
+                 "synthetic flow-like IPv4 4-tuples (example_input/ips.csv shape: one IP "
+                 "pair, sequential source ports) generated on device, resident in HBM"),
+        "config": {
+            "workload": "configs[2]: %d synthetic 4-tuples per GPU (x%d GPUs), key "
+                        "example_input/hash_key.txt (40 B), htable=%d, queues=%d; outputs "
+                        "hash_result (u32) + queue_number (%s) + per-queue counts (u64)"
+                        % (n, world, H, Q, qw),
+            "distribution": args.distribution,
+            "tuples_per_gpu": n,
+            "global_tuples": n * world,
+            "htable": H,
+            "queues": Q,
+            "queue_width": qw,
+            "collectives_per_batch": (1.0 / bucket) if distributed else 0,
+            "parallelism": ("tuple-sharded x%d, %s all-reduce of every step's uint64[%d] "
+                            "counts, %s %s"
+                            % (world, "RCCL" if args.dist_backend == "nccl" else "gloo", Q,
+                               "one collective per batch" if bucket == 1 else
+                               "%d steps per collective (rows of a [%d, %d] bucket)"
+                               % (bucket, bucket, Q),
+                               {"overlap": "(torch.distributed async, overlapped with the "
+                                           "next step)",
+                                "stream": "(torch.distributed, stream-ordered after the "
+                                          "launch)",
+                                "rccl": "(ncclAllReduce via rccl.RcclComm, stream-ordered "
+                                        "after the launch)"}[args.allreduce]))
+                           if distributed else "single process, one GPU (no process group)",
+            "step": ("zero counts + " if args.zero_counts else
+                     "single-pass counts (rss_hash_device_ws): ") +
+                    ("hash kernel (hipGraph replay)" if m["graph"]
+                     else "hash kernel (eager launches)"),
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": m["traffic"],
+            "kernel": "rss_toeplitz_kernel",
+            "bytes_per_tuple": READ_BYTES + write_bytes,
+            "kernel_ms": kernel_ms_max,
+            "kernel_ms_rank0": m["kernel_ms"],
+            "kernel_ms_max_rank": kernel_ms_max,
+            "kernel_ms_min_max": [launch_ms[0], launch_ms[-1]],
+            "kernel_ms_median": launch_ms[len(launch_ms) // 2],
+            "kernel_ms_events_mean": sum(launch_ms) / len(launch_ms),
+            "timing": "kernel_ms = GPU time per step on the launch stream: one pair of HIP "
+                      "events around the %d timed launches (launches + the gaps between "
+                      "them), slowest rank (kernel_ms_max_rank); min_max / median / "
+                      "events_mean: %d launches each bracketed by HIP events, after the "
+                      "timed region (RSS_FLAG_ADDR64: the 64-bit instance, like the probe, "
+                      "settle and flow-like launches; the step's 32-bit instance runs only "
+                      "the warmup and timed launches)"
+                      % (args.steps, args.steps),
+        },
+        # SURVEY.md 8(d): the HBM-read roofline is the counts-only mode's bound (12 B read
+        # per tuple, 666.7 G tuples/s per GPU); the full-output `value` also writes
+        # write_bytes per tuple, so its share of that read-only bound understates its
+        # HBM use (roofline.frac is its own algorithmic-byte fraction)
+        "hbm_read_roofline": {
+            "bound_tuples_per_s_per_gpu": HBM_PEAK_GBS * 1e9 / READ_BYTES,
+            "counts_only_frac": n / (co_ms / 1e3) / (HBM_PEAK_GBS * 1e9 / READ_BYTES),
+            "full_value_frac": value / (world * HBM_PEAK_GBS * 1e9 / READ_BYTES),
+            # the same for the full-output kernel alone (slowest rank's mean launch), i.e.
+            # without the per-step counts zeroing, event records and launch gaps
+            "full_kernel_frac": n / (kernel_ms_max / 1e3) / (HBM_PEAK_GBS * 1e9 / READ_BYTES),
+        },
+        "counts_only": {
+            "kernel_ms": co_ms,
+            "input_probe_ms": m["co_probe"],
+            "tuples_per_s_per_gpu": n / (co_ms / 1e3),
+            "hbm_read_GBs": n * READ_BYTES / (co_ms / 1e3) / 1e9,
+            "hbm_read_frac": n * READ_BYTES / (co_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
+        },
+        "queue_u32": {
+            "kernel_ms": u32_ms,
+            "queue_buffer_probe_ms": m["u32_probe"],
+            "tuples_per_s_per_gpu": n / (u32_ms / 1e3),
+            "achieved_GBs": n * 20 / (u32_ms / 1e3) / 1e9,
+        },
+        "cpu_baseline": m["baseline"],
+    }
+    line["secondary_min_median_max_ms"] = m["secondary_spread"]
+    line["settle"] = {"launches": m["settle_launches"], "s": round(m["settle_s"], 3),
+                      "note": "untimed launches of the step before the warmup steps "
+                              "(--settle-ms; clock settle, rank-local)"}
+    line["placement"] = dict(m["placement"], first_allocation_tuples_per_s_per_gpu=n / (
+        m["placement"]["first_allocation_ms"] / 1e3), probe_addr64=True,
+        note="resident buffers chosen among the probed candidate allocations before the "
+             "timed region (ResidentBatch); first_allocation_* = the unplaced allocation's "
+             "kernel-only rate")
+    line["per_rank"] = [
+        {"rank": int(r[0]), "kernel_ms": r[1], "chosen_ms": r[2], "first_allocation_ms": r[3],
+         "configs3_kernel_ms": r[4] if c3 else None,
+         "configs3_chosen_ms": r[5] if c3 else None,
+         "configs3_first_allocation_ms": r[6] if c3 else None,
+         "verified_main": {1.0: True, 0.0: False}.get(r[7]),
+         "verified_configs3": {1.0: True, 0.0: False}.get(r[8])} for r in rows]
+    if m["bucketed"] is not None:
+        line["bucketed"] = m["bucketed"]
+    if c3 is not None:
+        c3.pop("kernel_ms_rank", None)
+        c3.pop("placement_rank", None)
+        line["configs3"] = c3
+    line["verification"] = dict(m["verified"], source="tests/golden/bench_digest.npz (C oracle, "
+                                "tests/golden/make_bench_digest.py): per-2^20-block hash / "
+                                "queue digests of every rank's resident outputs + the "
+                                "reduced counts, checked after the timed region")
+    line["verified"] = m["verified_all"]
+    if flow_ms is not None:
+        line["flow_like"] = {
+            "kernel_ms": flow_ms, "tuples_per_s_per_gpu": n / (flow_ms / 1e3),
+            "note": "same outputs on flow-like input (one IP pair, sequential source ports; "
+                    "--distribution flow), timed after the uniform run"}
+    if m["extras"] is not None:
+        line["row_f_kernels"] = m["extras"]
+    return line
 
 
 # rss_key_search_packed_kernel's bounds (DESIGN.md §7), per wave-step of 64 tuples x 8 keys
@@ -774,10 +969,12 @@ def main():
         e[1].record(stream)
     torch.cuda.synchronize()
     launch_ms = sorted(a.elapsed_time(b) for a, b in spread_ev)
-    stats = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
-    if distributed:
-        dist.all_reduce(stats, op=dist.ReduceOp.MAX)
-    elapsed, kernel_ms_max = float(stats[0]), float(stats[1])
+    red_dev = dev if args.dist_backend == "nccl" else "cpu"
+
+    def reduce_max(values):
+        return max_over_ranks(torch, dist, values, red_dev, distributed)
+
+    elapsed, kernel_ms_max = reduce_max([elapsed, kernel_ms])
 
     # The timed work itself, checked after the timed region (untimed): the resident outputs
     # of this rank's shard against the C oracle's per-block digests and the reduced counts
@@ -799,31 +996,8 @@ def main():
     if distributed and args.secondary_bucket > 1:
         bpipe = CountsPipeline(Q, dev, single_pass=not args.zero_counts, htable=H,
                                allreduce=args.allreduce, comm=comm, bucket=args.secondary_bucket)
-        for _ in range(args.warmup):
-            bpipe.step(launch)
-        bpipe.drain()
-        barrier()
-        torch.cuda.synchronize()
-        tb = time.perf_counter()
-        for _ in range(args.steps):
-            bpipe.step(launch)
-        blast = bpipe.drain()
-        torch.cuda.synchronize()
-        barrier()
-        bstats = torch.tensor([time.perf_counter() - tb], dtype=torch.float64, device=dev)
-        dist.all_reduce(bstats, op=dist.ReduceOp.MAX)
-        b_elapsed = float(bstats[0])
-        if int(blast.sum().item()) != n * world:
-            raise SystemExit("bench: bucketed counts sum to %d, expected %d"
-                             % (int(blast.sum().item()), n * world))
-        bucketed = {"steps_per_collective": bpipe.bucket,
-                    "collectives": -(-args.steps // bpipe.bucket),
-                    "value": n * world * args.steps / b_elapsed,
-                    "ms_per_step": b_elapsed * 1e3 / args.steps,
-                    "note": "secondary: the main line's steps with %d steps' count rows per "
-                            "collective (rows of a [%d, %d] bucket; every row is still its own "
-                            "batch's reduced histogram) -- not the reference's one exchange per "
-                            "batch, so not `value`" % (bpipe.bucket, bpipe.bucket, Q)}
+        bucketed = run_bucketed(bpipe, launch, args.steps, args.warmup, barrier,
+                                torch.cuda.synchronize, reduce_max, n, world, Q)
         del bpipe
 
     # BASELINE configs[3]: 2^30 global tuples split over the ranks (sharding.shard_range),
@@ -841,12 +1015,8 @@ def main():
            c3["kernel_ms_rank"] if c3 else -1.0, c3["placement_rank"]["chosen_ms"] if c3 else -1.0,
            c3["placement_rank"]["first_allocation_ms"] if c3 else -1.0,
            _okcode(verified["main"]), _okcode(verified["configs3"])]
-    rows = gather_rows(torch, dist, row, dev if args.dist_backend == "nccl" else "cpu",
-                       distributed, world)
-    # True: every rank's checks passed; False: any failed; None: nothing was checkable
-    codes = [r[7] for r in rows] + ([r[8] for r in rows] if c3 is not None else [])
-    verified_all = False if 0.0 in codes else (True if 1.0 in codes and -1.0 not in codes
-                                               else None)
+    rows = gather_rows(torch, dist, row, red_dev, distributed, world)
+    verified_all = verified_of(rows, c3 is not None)
 
     # secondary lines (rank 0, after the timed region): counts-only mode (12 B/tuple,
     # the HBM-read roofline) and u32 queue outputs (20 B/tuple)
@@ -911,141 +1081,15 @@ def main():
         extras = extra_lines(torch, _native, dev, stream, key_bytes)
 
     if rank == 0:
-        value = n * world * args.steps / elapsed
-        # the slowest rank's mean launch time: at N > 1 the fraction is the worst rank's
-        achieved = n * (READ_BYTES + write_bytes) / (kernel_ms_max / 1e3) / 1e9
-        traffic = load_traffic(args.profile_dir, n, H, Q, qw)
-        line = {
-            "metric": METRIC,
-            "value": value,
-            "unit": "tuples/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed * 1e3 / args.steps,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u32",
-            "data": ("synthetic: splitmix64 IPv4 4-tuples generated on device, resident in HBM"
-                     if args.distribution == "uniform" else
-                     "synthetic flow-like IPv4 4-tuples (example_input/ips.csv shape: one IP "
-                     "pair, sequential source ports) generated on device, resident in HBM"),
-            "config": {
-                "workload": "configs[2]: %d synthetic 4-tuples per GPU (x%d GPUs), key "
-                            "example_input/hash_key.txt (40 B), htable=%d, queues=%d; outputs "
-                            "hash_result (u32) + queue_number (%s) + per-queue counts (u64)"
-                            % (n, world, H, Q, qw),
-                "distribution": args.distribution,
-                "tuples_per_gpu": n,
-                "global_tuples": n * world,
-                "htable": H,
-                "queues": Q,
-                "queue_width": qw,
-                "collectives_per_batch": (1.0 / pipeline.bucket) if distributed else 0,
-                "parallelism": ("tuple-sharded x%d, %s all-reduce of every step's uint64[%d] "
-                                "counts, %s %s"
-                                % (world, "RCCL" if args.dist_backend == "nccl" else "gloo", Q,
-                                   "one collective per batch" if pipeline.bucket == 1 else
-                                   "%d steps per collective (rows of a [%d, %d] bucket)"
-                                   % (pipeline.bucket, pipeline.bucket, Q),
-                                   {"overlap": "(torch.distributed async, overlapped with the "
-                                               "next step)",
-                                    "stream": "(torch.distributed, stream-ordered after the "
-                                              "launch)",
-                                    "rccl": "(ncclAllReduce via rccl.RcclComm, stream-ordered "
-                                            "after the launch)"}[args.allreduce]))
-                               if distributed else "single process, one GPU (no process group)",
-                "step": ("zero counts + " if args.zero_counts else
-                         "single-pass counts (rss_hash_device_ws): ") +
-                        ("hash kernel (hipGraph replay)" if graphs is not None
-                         else "hash kernel (eager launches)"),
-            },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": traffic,
-                "kernel": "rss_toeplitz_kernel",
-                "bytes_per_tuple": READ_BYTES + write_bytes,
-                "kernel_ms": kernel_ms_max,
-                "kernel_ms_rank0": kernel_ms,
-                "kernel_ms_max_rank": kernel_ms_max,
-                "kernel_ms_min_max": [launch_ms[0], launch_ms[-1]],
-                "kernel_ms_median": launch_ms[len(launch_ms) // 2],
-                "kernel_ms_events_mean": sum(launch_ms) / len(launch_ms),
-                "timing": "kernel_ms = GPU time per step on the launch stream: one pair of HIP "
-                          "events around the %d timed launches (launches + the gaps between "
-                          "them), slowest rank (kernel_ms_max_rank); min_max / median / "
-                          "events_mean: %d launches each bracketed by HIP events, after the "
-                          "timed region (RSS_FLAG_ADDR64: the 64-bit instance, like the probe, "
-                          "settle and flow-like launches; the step's 32-bit instance runs only "
-                          "the warmup and timed launches)"
-                          % (args.steps, args.steps),
-            },
-            # the HBM-read roofline is the counts-only mode's bound (12 B read
-            # per tuple, 666.7 G tuples/s per GPU); the full-output `value` also writes
-            # write_bytes per tuple, so its share of that read-only bound understates its
-            # HBM use (roofline.frac is its own algorithmic-byte fraction)
-            "hbm_read_roofline": {
-                "bound_tuples_per_s_per_gpu": HBM_PEAK_GBS * 1e9 / READ_BYTES,
-                "counts_only_frac": n / (co_ms / 1e3) / (HBM_PEAK_GBS * 1e9 / READ_BYTES),
-                "full_value_frac": value / (world * HBM_PEAK_GBS * 1e9 / READ_BYTES),
-                # the same for the full-output kernel alone (slowest rank's mean launch), i.e.
-                # without the per-step counts zeroing, event records and launch gaps
-                "full_kernel_frac": n / (kernel_ms_max / 1e3) / (HBM_PEAK_GBS * 1e9 / READ_BYTES),
-            },
-            "counts_only": {
-                "kernel_ms": co_ms,
-                "input_probe_ms": co_probe,
-                "tuples_per_s_per_gpu": n / (co_ms / 1e3),
-                "hbm_read_GBs": n * READ_BYTES / (co_ms / 1e3) / 1e9,
-                "hbm_read_frac": n * READ_BYTES / (co_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
-            },
-            "queue_u32": {
-                "kernel_ms": u32_ms,
-                "queue_buffer_probe_ms": u32_probe,
-                "tuples_per_s_per_gpu": n / (u32_ms / 1e3),
-                "achieved_GBs": n * 20 / (u32_ms / 1e3) / 1e9,
-            },
-            "cpu_baseline": baseline,
-        }
-        line["secondary_min_median_max_ms"] = secondary_spread
-        line["settle"] = {"launches": settle_launches, "s": round(settle_s, 3),
-                          "note": "untimed launches of the step before the warmup steps "
-                                  "(--settle-ms; clock settle, rank-local)"}
-        line["placement"] = dict(placement, first_allocation_tuples_per_s_per_gpu=n / (
-            placement["first_allocation_ms"] / 1e3), probe_addr64=True,
-            note="resident buffers chosen among the probed candidate allocations before the "
-                 "timed region (ResidentBatch); first_allocation_* = the unplaced allocation's "
-                 "kernel-only rate")
-        line["per_rank"] = [
-            {"rank": int(r[0]), "kernel_ms": r[1], "chosen_ms": r[2], "first_allocation_ms": r[3],
-             "configs3_kernel_ms": r[4] if c3 else None,
-             "configs3_chosen_ms": r[5] if c3 else None,
-             "configs3_first_allocation_ms": r[6] if c3 else None,
-             "verified_main": {1.0: True, 0.0: False}.get(r[7]),
-             "verified_configs3": {1.0: True, 0.0: False}.get(r[8])} for r in rows]
-        if bucketed is not None:
-            line["bucketed"] = bucketed
-        if c3 is not None:
-            c3.pop("kernel_ms_rank", None)
-            c3.pop("placement_rank", None)
-            line["configs3"] = c3
-        line["verification"] = dict(verified, source="tests/golden/bench_digest.npz (C oracle, "
-                                    "tests/golden/make_bench_digest.py): per-2^20-block hash / "
-                                    "queue digests of every rank's resident outputs + the "
-                                    "reduced counts, checked after the timed region")
-        line["verified"] = verified_all
-        if flow_ms is not None:
-            line["flow_like"] = {
-                "kernel_ms": flow_ms, "tuples_per_s_per_gpu": n / (flow_ms / 1e3),
-                "note": "same outputs on flow-like input (one IP pair, sequential source ports; "
-                        "--distribution flow), timed after the uniform run"}
-        if extras is not None:
-            line["row_f_kernels"] = extras
+        line = build_line(args, dict(
+            n=n, world=world, elapsed=elapsed, kernel_ms=kernel_ms, kernel_ms_max=kernel_ms_max,
+            launch_ms=launch_ms, write_bytes=write_bytes, qw=qw, distributed=distributed,
+            bucket=pipeline.bucket, graph=graphs is not None, co_ms=co_ms, co_probe=co_probe,
+            u32_ms=u32_ms, u32_probe=u32_probe, flow_ms=flow_ms, baseline=baseline,
+            secondary_spread=secondary_spread, settle_launches=settle_launches,
+            settle_s=settle_s, placement=placement, rows=rows, c3=c3, bucketed=bucketed,
+            verified=verified, verified_all=verified_all, extras=extras,
+            traffic=load_traffic(args.profile_dir, n, H, Q, qw)))
         print(json.dumps(line), flush=True)
     if verified_all is False:
         print("bench: the timed work does not match the oracle's digests (see `verification`)",

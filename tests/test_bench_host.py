@@ -170,3 +170,62 @@ def test_committed_bench_lines_do_one_exchange_per_batch():
         seen.add((line["n_gpus"], "gloo" if "gloo" in cfg["parallelism"] else
                   ("RCCL" if "RCCL" in cfg["parallelism"] else "none")))
     assert (1, "RCCL") in seen and (8, "gloo") in seen, seen
+
+
+def test_world8_rehearsal_line(tmp_path):
+    """bench.py's N > 1 machinery at world size 8 on CPU ranks (gloo,
+    tests/bench_rehearsal.py): one all-reduce per batch in the main line, 8 per-rank rows in
+    rank order, the configs[3] block over 8 contiguous shards and the labelled bucketed
+    block -- so the driver's 8-GPU run does not meet a path only world size 1 has run."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = tmp_path / "line.json"
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "8", "--master-addr", "127.0.0.1", "--master-port",
+                        str(port), os.path.join(root, "tests", "bench_rehearsal.py"), str(out)],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    line = json.loads(out.read_text())
+    assert line["n_gpus"] == 8 and line["scaling"] == "weak" and line["value"] > 0
+    cfg = line["config"]
+    assert cfg["collectives_per_batch"] == 1.0 and cfg["global_tuples"] == 8 * 4096
+    assert "one collective per batch" in cfg["parallelism"] and "gloo" in cfg["parallelism"]
+    rows = line["per_rank"]
+    assert [r["rank"] for r in rows] == list(range(8))
+    assert line["roofline"]["kernel_ms_max_rank"] >= max(r["kernel_ms"] for r in rows) * 0.999
+    c3 = line["configs3"]
+    assert c3["scaling"] == "strong" and c3["global_tuples"] == 1 << 16
+    assert c3["tuples_per_rank_max"] == (1 << 16) // 8
+    b = line["bucketed"]
+    assert b["steps_per_collective"] == 8 and b["collectives"] == -(-line["steps"] // 8)
+    assert line["verified"] is None and line["verification"]["main"] is None
+
+
+def test_relaunch_runs_torchrun_on_loopback(monkeypatch):
+    """`bench.py --gpus 8` outside a launcher re-runs itself under torch.distributed.run with
+    8 processes on 127.0.0.1, the same arguments, and returns the child's exit code."""
+    import subprocess
+    seen = {}
+
+    class Done:
+        returncode = 7
+
+    def fake_run(cmd, *a, **k):
+        seen["cmd"] = cmd
+        return Done()
+
+    monkeypatch.setattr(subprocess, "run", fake_run)
+    monkeypatch.setattr("sys.argv", ["bench.py", "--gpus", "8", "--steps", "3"])
+    assert bench.relaunch_distributed(8) == 7
+    cmd = seen["cmd"]
+    assert cmd[1:4] == ["-m", "torch.distributed.run", "--nnodes=1"]
+    assert cmd[cmd.index("--nproc-per-node") + 1] == "8"
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-4:] == ["--gpus", "8", "--steps", "3"]
