@@ -131,15 +131,18 @@ int rss_key_select_fields(rss_key* key, uint32_t fields);
  * thread's current device.  Any alignment works; 16-byte aligned tuples/hashes
  * (and 4/8/16-byte aligned u8/u16/u32 queues) take the 4-tuples-per-lane path.
  * Counts-only launches with a power-of-two htable <= 256 run a table-free kernel;
- * with more than 8192 queues the counts go to LDS bins of the hash pass itself -- u16 bins
- * for up to 16384 queues beside the 12-bit tables and up to 80572 beside the 2.6 KiB
- * small tables (4-tuple body, no indirection table), u8 bins for up to 161144 (a bin that
- * wraps poisons the pass and a gated recount replaces its counts) -- whose per-workgroup
- * rows a reduce launch sums; the queues past that are counted by wide passes (163840 queues
- * per pass in u8 bins, 65536 in u16) over d_queue when given, else -- counts only -- over
- * per-wave lists of the tuples whose queue lies past the LDS range (the queue minus 161144,
- * 2 bytes per entry for nqueues <= 226680, else 4; stream-ordered hipMallocAsync /
- * hipFreeAsync on `stream`, like the per-workgroup rows).
+ * with more than 8192 queues the counts go to guarded LDS bins of the hash pass itself --
+ * u16 bins for up to 16384 queues beside the 12-bit tables and up to 80572 beside the
+ * 2.6 KiB small tables (4-tuple body, no indirection table), u8 bins for up to 161144 --
+ * whose per-workgroup rows a reduce launch sums; the queues past that are counted by wide
+ * passes (163840 queues per pass in u8 bins, 65536 in u16) over d_queue when given, else --
+ * counts only -- over per-wave lists of the tuples whose queue lies past the LDS range (the
+ * queue minus 161144, 2 bytes per entry for nqueues <= 226680, else 4).  A guarded bin that
+ * wraps (a batch piling many tuples onto one queue at once) poisons its pass and a gated
+ * recount with u32 bins replaces that pass's counts: exact for any input.  Scratch for the
+ * rows, the lists and the passes is stream-ordered hipMallocAsync / hipFreeAsync on
+ * `stream`, all of it taken before the first pass touches d_counts (RSS_ENOMEM leaves
+ * accumulated counts as they were).
  */
 int rss_hash_device(const rss_key* key, const rss_tuple4* d_tuples, size_t n,
                     uint32_t htable, uint32_t nqueues, uint32_t* d_hash,
@@ -161,10 +164,7 @@ int rss_hash_device(const rss_key* key, const rss_tuple4* d_tuples, size_t n,
  * rss_hash_device's.  With d_counts NULL the workspace is not used (may be NULL).
  * Ordering: a queue's count travels in the atomics on its own word, and the balanced
  * tail's counter (below) is reset by the launch's final claim on it, so no fence is needed
- * (the memory model's single-location coherence).  RSS_FOLD=ticket selects rounds 2-3's
- * fold (sums, a ticket taken with an agent-scope release, the last workgroup's acquire and
- * exchanges: two more atomic round trips and the fences on the last workgroup's path);
- * RSS_WS_ORDER=relaxed drops that fold's release/acquire.  All are stress-tested in
+ * (the memory model's single-location coherence); stress-tested in
  * tests/test_gpu_single_pass.py.  Launches of >= 2^24 tuples
  * also take the last tenth of their work from a counter in the workspace (the balanced tail: the XCDs finish
  * together), so a workspace must never be shared by two launches in flight.
