@@ -362,7 +362,7 @@ __device__ __forceinline__ void record_margin(int kind, uint32_t at) {
 // Nothing bounds the adds that land on the bin between that add and the subtract: the
 // workgroup's other waves keep adding while the guard's wave waits for its returns, and wave
 // issue is not fair.  So a bin can pass 0xFFFF and carry into its neighbour (observed once in
-// a u16 wide pass, profiles/r04/u16_guard/).  Exactly the add that takes a field past 0xFFFF
+// a u16 wide pass, profiles/archive/r04/u16_guard/).  Exactly the add that takes a field past 0xFFFF
 // returns 0xFFFF, and it raises *p.poison: the launch's rows and moves are then discarded (the
 // reduce is gated on !poison) and rss_range_fallback_kernel / rss_range_fallback_col_kernel
 // recount the range with u32 bins (gated on poison) -- exact whatever the timing.
@@ -1258,7 +1258,7 @@ __global__ __launch_bounds__(kBlock, 2) void rss_counts_perm_kernel(const PermPa
 //     t0 w0[10:0]  t1 w0[21:11]  t2 w1[10:0]  t3 w2[15:11] | w2[31:27] << 5  t4 w0[31:22]
 //     t5 w1[21:11] t6 w2[10:0]   t7 w2[26:16] t8 w1[31:22]
 //   = 6 x 16 + 3 x 8 KiB = 120 KiB; on the small tables it ran 0.77 against 0.97 T
-//   evaluations/s at H = 100, Q = 24 (profiles/r04/small_tables/keysearch_configs.jsonl).
+//   evaluations/s at H = 100, Q = 24 (profiles/archive/r04/small_tables/keysearch_configs.jsonl).
 // blockIdx.y selects the pair; each workgroup histograms its grid-stride share of the
 // tuples into counts rows 2y, 2y+1.  With the tuples resident in the 256 MiB Infinity Cache
 // the re-reads stay on die.
@@ -2156,7 +2156,7 @@ constexpr Options g_opt{};
 // Small-table passes without per-tuple outputs (counts only, no scratch column) issue the
 // next group's loads before this group's LDS work: 0.62 vs 0.66 ms at Q = 65536 / 131072,
 // where with outputs it cost 1-2 % and the balanced tail gains 4 % instead
-// (profiles/r04/small_tables/prefetch_ab.jsonl).
+// (profiles/archive/r04/small_tables/prefetch_ab.jsonl).
 bool prefetch_for(bool has_outputs) {
     return g_opt.prefetch >= 0 ? g_opt.prefetch == 1 : !has_outputs;
 }
