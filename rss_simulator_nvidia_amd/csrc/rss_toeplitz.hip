@@ -1881,7 +1881,7 @@ using KernelFn = void (*)(const LaunchParams);
 // per lane on the small tables (kSmallLut; HIST_RANGE16 / HIST_RANGE8 only)
 enum VecMode { VM_SCALAR = 0, VM_VEC4 = 1, VM_OFF32 = 2, VM_SMALL_LUT = 3 };
 template <bool kHPow2, int kQMode, int kHist, int kQWidth>
-KernelFn pick_vec(int vec4) {
+KernelFn pick_vec_reachable(int vec4) {
     if constexpr (kHist == HIST_RANGE8) {  // small tables, u32 / u16-residual columns only
         if constexpr ((kQWidth == QW_U32 || kQWidth == QW_U16R) && kQMode != QM_FAST8 &&
                       kQMode != QM_TABLE)
@@ -1906,6 +1906,20 @@ KernelFn pick_vec(int vec4) {
     if (vec4 == VM_SMALL_LUT) return nullptr;
     return vec4 ? rss_toeplitz_kernel<kHPow2, kQMode, kHist, kQWidth, true>
                 : rss_toeplitz_kernel<kHPow2, kQMode, kHist, kQWidth, false>;
+}
+
+// No launch reaches these combinations, so they are not instantiated: more than 7168 queues
+// (the many-queues modes, setup_modes) never come with u8 queues (min(H, Q) <= 256) or
+// QM_FAST8 (H <= 256, no table), and u8 bins (past 80572 queues) never with QM_FAST16
+// (Q < H <= 65536)
+template <bool kHPow2, int kQMode, int kHist, int kQWidth>
+KernelFn pick_vec(int vec4) {
+    constexpr bool kMany = kHist == HIST_GLOBAL || kHist == HIST_RANGE16 || kHist == HIST_RANGE8;
+    if constexpr ((kMany && (kQWidth == QW_U8 || kQMode == QM_FAST8)) ||
+                  (kHist == HIST_RANGE8 && kQMode == QM_FAST16))
+        return nullptr;
+    else
+        return pick_vec_reachable<kHPow2, kQMode, kHist, kQWidth>(vec4);
 }
 
 template <bool kHPow2, int kQMode, int kHist>
@@ -2707,8 +2721,11 @@ using KernelFn6 = void (*)(const LaunchParams6);
 
 template <bool kHPow2, int kQMode, int kHist>
 KernelFn6 pick6_vec(bool vec4) {
-    return vec4 ? rss_toeplitz6_kernel<kHPow2, kQMode, kHist, true>
-                : rss_toeplitz6_kernel<kHPow2, kQMode, kHist, false>;
+    if constexpr (kQMode == QM_FAST8 && (kHist == HIST_GLOBAL || kHist == HIST_RANGE))
+        return nullptr;  // (H <= 256: never more queues than the LDS bins hold)
+    else
+        return vec4 ? rss_toeplitz6_kernel<kHPow2, kQMode, kHist, true>
+                    : rss_toeplitz6_kernel<kHPow2, kQMode, kHist, false>;
 }
 
 template <bool kHPow2, int kQMode>
