@@ -12,7 +12,9 @@ extern "C" {
 
 // name: "recount" (0 measured, 1 poison every guarded pass, 2 no gate / no recount),
 // "range8", "small_lut", "balance", "counts_perm", "resid", "wide" (0 / 1), "prefetch" (-1
-// by outputs, 0 / 1 forced).  RSS_EINVAL for an unknown name.
+// by outputs, 0 / 1 forced), "guard_sleep" (n: a u16 guard's wave sleeps n x s_sleep 127
+// before its subtract, so that a heavy-hitter batch really wraps its bin; set on the current
+// device).  RSS_EINVAL for an unknown name.
 int rss_test_set_option(const char* name, int value);
 void rss_test_reset_options(void);
 

@@ -351,8 +351,18 @@ __device__ __forceinline__ void record_margin(int kind, uint32_t at) {
                            __HIP_MEMORY_SCOPE_AGENT);
 }
 #define RSS_RECORD_MARGIN(bits, kind, at) record_margin<bits>(kind, at)
+// Test-hooks build only: before its subtract a u16 guard's wave sleeps g_guard_sleep times
+// s_sleep 127 (~3 us each), so that the workgroup's other waves carry the bin past 0xFFFF --
+// a real wrap, which the poison word must catch (rss_test_set_option "guard_sleep").
+__device__ uint32_t g_guard_sleep;
+__device__ __forceinline__ void guard_delay() {
+    const uint32_t n = *reinterpret_cast<volatile uint32_t*>(&g_guard_sleep);
+    for (uint32_t i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
+}
+#define RSS_GUARD_DELAY() guard_delay()
 #else
 #define RSS_RECORD_MARGIN(bits, kind, at) ((void)(at))
+#define RSS_GUARD_DELAY() ((void)0)
 #endif
 
 // HIST_RANGE16's two halves: the add (returns the dword's previous value, 0 out of range)
@@ -380,6 +390,7 @@ __device__ __forceinline__ void range16_guard(uint32_t* bins, uint32_t q, uint32
     const uint32_t sh = (r & 1u) * 16u;
     const uint32_t f = (old >> sh) & 0xFFFFu;
     if (f == 0x7FFFu) {
+        RSS_GUARD_DELAY();
         const uint32_t at = __hip_atomic_fetch_sub(&bins[r >> 1], 0x8000u << sh, __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_WORKGROUP);
         RSS_RECORD_MARGIN(16, kMarginHash16, (at >> sh) & 0xFFFFu);
@@ -935,6 +946,7 @@ __global__ __launch_bounds__(kBlock) void rss_queue_hist_wide_kernel(
         const uint32_t sh = (r % kPerWord) * kBits;
         const uint32_t f = (old >> sh) & kField;
         if (f == kHalf - 1u) {
+            if constexpr (kBits == 16) RSS_GUARD_DELAY();
             const uint32_t at = __hip_atomic_fetch_sub(&bins[r / kPerWord], kHalf << sh,
                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             RSS_RECORD_MARGIN(kBits, kBits == 16 ? kMarginWide16 : kMarginWide8, (at >> sh) & kField);
@@ -3518,6 +3530,10 @@ int rss_key_search_host(rss_ctx* ctx, const rss_key* keys, size_t nkeys,
 // ------------------------------------------------- test hooks (tests only) --
 // Exported by librss_toeplitz_hooks.so alone (rss_test_hooks.h): the product library has
 // neither these symbols nor the options they set.
+namespace {
+uint32_t g_guard_sleep_host = 0;  // the value last copied to g_guard_sleep
+}  // namespace
+
 extern "C" {
 
 int rss_test_set_option(const char* name, int value) {
@@ -3531,11 +3547,23 @@ int rss_test_set_option(const char* name, int value) {
     else if (n == "counts_perm") g_opt.counts_perm = value != 0;
     else if (n == "resid") g_opt.resid = value != 0;
     else if (n == "wide") g_opt.wide = value != 0;
-    else return set_error(RSS_EINVAL, "rss_test_set_option: unknown option '%s'", name);
+    else if (n == "guard_sleep") {
+        const uint32_t v = value > 0 ? (uint32_t)value : 0u;
+        RSS_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_guard_sleep), &v, sizeof v));
+        g_guard_sleep_host = v;
+    } else return set_error(RSS_EINVAL, "rss_test_set_option: unknown option '%s'", name);
     return RSS_OK;
 }
 
-void rss_test_reset_options(void) { g_opt = Options{}; }
+// (the device word only when it was set: a process without a GPU never touches HIP here)
+void rss_test_reset_options(void) {
+    g_opt = Options{};
+    if (g_guard_sleep_host) {
+        const uint32_t zero = 0;
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_guard_sleep), &zero, sizeof zero);
+        g_guard_sleep_host = 0;
+    }
+}
 
 int rss_test_guard_margin(uint32_t* out, int reset) {
     if (!out) return set_error(RSS_EINVAL, "rss_test_guard_margin: NULL out");

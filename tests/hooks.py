@@ -17,7 +17,8 @@ from rss_simulator_nvidia_amd import _native
 
 HOOKS_PATH = os.path.join(os.path.dirname(os.path.abspath(_native.LIB_PATH)),
                           "librss_toeplitz_hooks.so")
-OPTIONS = ("recount", "range8", "small_lut", "prefetch", "balance", "counts_perm", "resid", "wide")
+OPTIONS = ("recount", "range8", "small_lut", "prefetch", "balance", "counts_perm", "resid", "wide",
+           "guard_sleep")
 MARGINS = ("hash16", "wide16", "hash8", "wide8")
 _hooks = None
 

@@ -519,3 +519,30 @@ def test_guard_margin_readout(native, oracle_lib, example_key):
     print("guard margin", m)
     assert m["hash16"] > 0  # the guard fired (~65536 adds per workgroup on one bin)
     assert all(v == 0 for v in m2.values())
+
+
+@pytest.mark.parametrize("Q,lo,hi", [(50000, 0, 50000), (12000, 8192, 12000),
+                                     (170000, SPAN8, 170000)])
+def test_u16_real_wrap_is_caught(native, oracle_lib, example_key, Q, lo, hi):
+    """A REAL u16 wrap, forced: with the hooks build's guard_sleep the wave of a guard that
+    saw 0x7FFF sleeps (~1 ms) before its subtract while the workgroup's other waves keep
+    adding 2^25 copies of one tuple onto the same bin -- the hash pass's u16 bins (small
+    tables Q = 50000, 12-bit tables Q = 12000) or the u16 wide pass after the u8 hash pass
+    (Q = 170000).  The bin passes 0xFFFF: without the gate and the recount (recount=2) the
+    counts come out wrong -- the wrap happened -- and with them (the product's path) they
+    equal the oracle's."""
+    n_same, n_rand, H = 1 << 25, 4099, 1 << 30
+    rnd = oracle_lib.generate(39, 0, n_rand)
+    _, q_rnd, _ = oracle_lib.run(example_key, rnd, H, Q)
+    pick = int(np.flatnonzero((q_rnd >= lo) & (q_rnd < hi))[0])
+    host = np.concatenate([np.repeat(rnd[pick:pick + 1], n_same, axis=0), rnd])
+    tup = torch.from_numpy(host.view(np.int32).reshape(-1)).to("cuda:0")
+    want = oracle_lib.run(example_key, rnd, H, Q, want_hash=False, want_queue=False)[2]
+    want[int(q_rnd[pick])] += n_same
+    key = native.prepare_key(example_key)
+    with hooks(guard_sleep=300, recount=2):
+        _, _, bad = _launch(native, key, tup, len(host), H, Q, False)
+    with hooks(guard_sleep=300):
+        _, _, good = _launch(native, key, tup, len(host), H, Q, False)
+    assert not np.array_equal(bad.cpu().numpy().view(np.uint64), want), "no wrap was forced"
+    np.testing.assert_array_equal(good.cpu().numpy().view(np.uint64), want)
