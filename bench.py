@@ -512,6 +512,49 @@ def relaunch_distributed(n):
     return subprocess.run(cmd).returncode
 
 
+CONFIGS4 = [(H, Q) for H in (128, 512) for Q in (8, 16, 24, 64)]
+
+
+def configs4_block(torch, _native, key, tuples, hashes, queues, n, stream, warm, reps):
+    """BASELINE configs[4] timed on this GPU (rank 0, after the main measurement): the same
+    resident tuples and output buffers hashed under every (htable, num-queues) of the sweep
+    (H in {128, 512} x Q in {8, 16, 24, 64}), full outputs (hash u32 + queue u8 + counts,
+    17 B/tuple) and counts only (12 B/tuple), each the mean of `reps` launches bracketed by one
+    HIP event pair after `warm` untimed ones.  Its per-queue parity with simulator.py is
+    tests/test_gpu_parity.py::test_256M_sweep_counts_and_digest."""
+    sp = stream.cuda_stream
+    counts = torch.zeros(64, dtype=torch.int64, device=tuples.device)
+    acc = _native.FLAG_ACCUMULATE
+
+    def timed(fn):
+        for _ in range(warm):
+            fn()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for _ in range(reps):
+            fn()
+        b.record(stream)
+        torch.cuda.synchronize()
+        return a.elapsed_time(b) / reps
+
+    rows = []
+    for H, Q in CONFIGS4:
+        full = timed(lambda: _native.hash_device(key, tuples.data_ptr(), n, H, Q, hashes.data_ptr(),
+                                                 queues.data_ptr(), counts.data_ptr(),
+                                                 _native.FLAG_QUEUE_U8 | acc, sp))
+        co = timed(lambda: _native.hash_device(key, tuples.data_ptr(), n, H, Q, None, None,
+                                               counts.data_ptr(), acc, sp))
+        rows.append({"htable": H, "queues": Q, "full_ms": full,
+                     "full_tuples_per_s": n / (full / 1e3),
+                     "full_frac": n * (READ_BYTES + HASH_BYTES + 1) / (full / 1e3) / 1e9 / HBM_PEAK_GBS,
+                     "counts_only_ms": co, "counts_only_tuples_per_s": n / (co / 1e3),
+                     "counts_only_read_frac": n * READ_BYTES / (co / 1e3) / 1e9 / HBM_PEAK_GBS})
+    return {"tuples": n, "rows": rows,
+            "note": "BASELINE configs[4]: the sweep's (H, Q) on the main line's placed buffers "
+                    "(uniform input), full outputs (u8 queues) and counts only; mean of %d "
+                    "launches after %d untimed ones, one HIP event pair each" % (reps, warm)}
+
+
 def extra_lines(torch, _native, dev, stream, key_bytes):
     """Secondary timings of the row-f kernels on this GPU, after the main measurement
     (DESIGN.md §7-§8): the IPv6 kernel (2^26 uniform 36-byte tuples, u32 hash + u8 queue +
@@ -734,6 +777,8 @@ def build_line(args, m):
             "kernel_ms": flow_ms, "tuples_per_s_per_gpu": n / (flow_ms / 1e3),
             "note": "same outputs on flow-like input (one IP pair, sequential source ports; "
                     "--distribution flow), timed after the uniform run"}
+    if m.get("configs4") is not None:
+        line["configs4"] = m["configs4"]
     if m["extras"] is not None:
         line["row_f_kernels"] = m["extras"]
     return line
@@ -1020,7 +1065,7 @@ def main():
 
     # secondary lines (rank 0, after the timed region): counts-only mode (12 B/tuple,
     # the HBM-read roofline) and u32 queue outputs (20 B/tuple)
-    co_ms = u32_ms = flow_ms = None
+    co_ms = u32_ms = flow_ms = configs4 = None
     if rank == 0:
         reps = max(5, args.steps // 2)
         # counts only reads its input alone, and the read rate also depends a little on the
@@ -1071,6 +1116,9 @@ def main():
             queues32, u32_probe = choose_buffer(torch, dev, 4 * n, probe32, candidates=4)
         u32_ms = kernel_ms_of(hashes.data_ptr(), queues32.data_ptr(), 0, reps)
         del queues32
+        if not args.no_extras and n >= 1 << 20:
+            configs4 = configs4_block(torch, _native, key, tuples, hashes, queues, n, stream,
+                                      args.secondary_warmup, reps)
         if args.distribution == "uniform":  # same kernel on SURVEY.md 8(d)'s flow-like input
             flow_device(torch, tuples, 0, n, dev)
             flow_ms = kernel_ms_of(hashes.data_ptr(), queues.data_ptr(),
@@ -1088,7 +1136,7 @@ def main():
             u32_ms=u32_ms, u32_probe=u32_probe, flow_ms=flow_ms, baseline=baseline,
             secondary_spread=secondary_spread, settle_launches=settle_launches,
             settle_s=settle_s, placement=placement, rows=rows, c3=c3, bucketed=bucketed,
-            verified=verified, verified_all=verified_all, extras=extras,
+            verified=verified, verified_all=verified_all, extras=extras, configs4=configs4,
             traffic=load_traffic(args.profile_dir, n, H, Q, qw)))
         print(json.dumps(line), flush=True)
     if verified_all is False:

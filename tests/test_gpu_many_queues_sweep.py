@@ -51,7 +51,7 @@ def _config(seed):
                 misaligned=bool(rng.random() < 0.2), u16=bool(rng.random() < 0.5))
 
 
-@pytest.mark.parametrize("seed", range(32))
+@pytest.mark.parametrize("seed", range(64))
 def test_many_queues_paths_match_oracle(native, oracle_lib, example_key, seed):
     c = _config(seed)
     rng, n, H, Q = c["rng"], c["n"], c["H"], c["Q"]
