@@ -13,8 +13,8 @@ O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd $R
 if [ "$STAGE" = tests ] || [ "$STAGE" = all ]; then
-  timeout -k 10 1000 python -u -m pytest -q -m gpu --timeout 300 --timeout-method thread tests \
-      > $O/pytest_gpu.log 2>&1
+  RSS_MARGIN_LOG=$O/guard_margin.jsonl timeout -k 10 1000 python -u -m pytest -q -m gpu \
+      --timeout 300 --timeout-method thread tests > $O/pytest_gpu.log 2>&1
   rc=$?
   tail -3 $O/pytest_gpu.log
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
