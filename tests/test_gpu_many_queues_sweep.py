@@ -7,6 +7,8 @@ instead of wide passes (wide=0), the load prefetch forced on / off, the static w
 two halves of a guarded pass.  Random H (power of two or not, >= Q or not), Q from 8193 to
 ~1.2M, n up to 2^20 + ragged tails, outputs or counts only, u16 / u32 queues, accumulation,
 misaligned tuples.  Bar: bit-exact against the C oracle on every path."""
+import os
+
 import numpy as np
 import pytest
 
@@ -17,6 +19,9 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 OPTS = ("range8", "small_lut", "resid", "wide", "balance")
+# RSS_MQ_SWEEP_CASES / RSS_MQ_SWEEP_SEED0 widen the sweep for a one-off deep run
+CASES = int(os.environ.get("RSS_MQ_SWEEP_CASES", "64"))
+SEED0 = int(os.environ.get("RSS_MQ_SWEEP_SEED0", "0"))
 
 
 @pytest.fixture(scope="module")
@@ -51,7 +56,7 @@ def _config(seed):
                 misaligned=bool(rng.random() < 0.2), u16=bool(rng.random() < 0.5))
 
 
-@pytest.mark.parametrize("seed", range(64))
+@pytest.mark.parametrize("seed", range(SEED0, SEED0 + CASES))
 def test_many_queues_paths_match_oracle(native, oracle_lib, example_key, seed):
     c = _config(seed)
     rng, n, H, Q = c["rng"], c["n"], c["H"], c["Q"]
