@@ -204,11 +204,33 @@ def cpu_baseline(key, n_sample, procs, distribution="uniform"):
     dt = time.perf_counter() - t0
     assert sum(len(o) for o in out) == n_sample
     return {"value": n_sample / dt, "unit": "tuples/s", "cores": procs, "kind": "port",
+            "reference_equivalent": reference_equivalent(n_sample / dt),
             "optimised_c": optimised_c_baseline(key, procs, distribution),
             "procs": procs, "cpu_share": cpu_share(), "host_cores": os.cpu_count(),
             "sample": "first %d tuples of the bench stream, pure-Python restatement of "
                       "toeplitz.py:46-69 (rotating bit-string key) in %d processes (one per "
                       "core of this process's CPU share), %.2f s wall" % (n_sample, procs, dt)}
+
+
+CALIBRATION_PATH = os.path.join(ROOT, "tests", "golden", "cpu_calibration.json")
+
+
+def reference_equivalent(port_rate, path=CALIBRATION_PATH):
+    """The port's rate expressed in the reference's own: the reference
+    cannot run on the GPU box, so tests/golden/make_cpu_calibration.py timed it beside the
+    port on one core of the build container, on the same rows, and recorded their ratio
+    (cpu_calibration.json, data only).  None when that record is absent."""
+    try:
+        with open(path) as f:
+            cal = json.load(f)
+    except (OSError, ValueError):
+        return None
+    ratio = float(cal["port_over_reference"])
+    return {"value": port_rate / ratio, "unit": "tuples/s", "port_over_reference": ratio,
+            "calibration": "tests/golden/cpu_calibration.json: reference %.0f vs port %.0f "
+                           "tuples/s on one build-container core, %d tuples, identical hashes"
+                           % (cal["reference_tuples_per_s"], cal["port_tuples_per_s"],
+                              cal["tuples"])}
 
 
 def optimised_c_baseline(key, threads, distribution="uniform", n=1 << 24):

@@ -229,3 +229,15 @@ def test_relaunch_runs_torchrun_on_loopback(monkeypatch):
     assert cmd[cmd.index("--nproc-per-node") + 1] == "8"
     assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
     assert cmd[-4:] == ["--gpus", "8", "--steps", "3"]
+
+
+def test_cpu_baseline_reference_calibration(tmp_path):
+    """the port's GPU-box rate is also reported in the reference's own terms,
+    through the ratio tests/golden/make_cpu_calibration.py measured against the reference on
+    identical rows (hashes equal); absent record -> None."""
+    cal = json.loads(open(bench.CALIBRATION_PATH).read())
+    assert cal["hashes_equal"] is True and cal["tuples"] >= 1000
+    assert 0.5 < cal["port_over_reference"] < 3.0
+    eq = bench.reference_equivalent(1000.0)
+    assert abs(eq["value"] * cal["port_over_reference"] - 1000.0) < 1e-6
+    assert bench.reference_equivalent(1000.0, str(tmp_path / "none.json")) is None
