@@ -1,11 +1,15 @@
-"""Large queue counts: when nqueues' bins do not fit the LDS beside the tables, the hash
-kernel counts queues [0, span) in LDS and writes the queue column (the caller's, or a
-stream-ordered scratch column for counts-only launches); every further range of queues is
-histogrammed from that column (rss_queue_hist_kernel) instead of one global atomic per
-tuple.  Bar: hash / queue / counts bit-exact to the C oracle across range counts 2..33 (u16
-and u32 queue columns, caller-owned and scratch), the fallback to global atomics past 32
-u32 ranges, RETA tables (whose LDS copy shrinks the range), misaligned input (the
-one-tuple-per-lane body and unaligned queue columns), ragged n and accumulation."""
+"""Large queue counts (more than the u32 LDS bins beside the tables hold, DESIGN.md §3 "Many
+queues"): the hash pass counts the first range of queues in guarded u16 / u8 LDS bins (a bin
+that wraps poisons the pass and a recount replaces it) and writes the queue column (the
+caller's, a stream-ordered scratch column, or -- counts only past 161144 queues -- per-wave
+residual lists); every further range is histogrammed from that column by guarded wide passes
+(or, without scratch memory for them, u32 narrow passes).  Bar: hash / queue / counts
+bit-exact to the C oracle on every path -- the product launch and, through the tests'
+hooks build (tests/hooks.py), the paths a launch takes without scratch memory, a guarded
+pass's bins alone and its recount alone, and real u16 wraps forced by delaying the guard --
+across Q up to 10^6, u16 / u32 columns, caller-owned and scratch, RETA tables (whose LDS copy
+shrinks the range), misaligned input and unaligned columns, heavy hitters, Zipf traffic,
+ragged n and accumulation."""
 import numpy as np
 import pytest
 
