@@ -141,8 +141,9 @@ int rss_key_select_fields(rss_key* key, uint32_t fields);
  * wraps (a batch piling many tuples onto one queue at once) poisons its pass and a gated
  * recount with u32 bins replaces that pass's counts: exact for any input.  Scratch for the
  * rows, the lists and the passes is stream-ordered hipMallocAsync / hipFreeAsync on
- * `stream`, all of it taken before the first pass touches d_counts (RSS_ENOMEM leaves
- * accumulated counts as they were).
+ * `stream`, all of it taken before the first pass touches d_counts; a launch that cannot
+ * get it counts with one global atomic per tuple instead (same counts, slower), as it does
+ * when a guarded path would need more narrow passes than the atomics cost.
  */
 int rss_hash_device(const rss_key* key, const rss_tuple4* d_tuples, size_t n,
                     uint32_t htable, uint32_t nqueues, uint32_t* d_hash,
@@ -243,7 +244,17 @@ int rss_hash6_device_ws(const rss_key6* key, const rss_tuple6* d_tuples, size_t 
                         uint32_t htable, uint32_t nqueues, uint32_t* d_hash, void* d_queue,
                         uint64_t* d_counts, uint32_t flags, uint64_t* d_workspace, void* stream);
 
-/* Host-memory convenience path (CSV in -> CSV out): owns device buffers. */
+/*
+ * Host-memory convenience path (CSV in -> CSV out): owns device buffers.
+ * Thread safety: any number of host threads may call the entry points that take one
+ * context at once; each call holds the context's lock from entry to return, so calls on
+ * one context run one after another (each with its own results) and calls on different
+ * contexts run concurrently.  Replaces the reentrancy of the reference's per-call
+ * Toeplitz.compute_hash (rss_simulator/toeplitz.py:59 copies the key on every call).
+ * rss_ctx_destroy must not race a call on the same context.  Output that a call leaves in
+ * context-owned memory (rss_csv_hash_text's file image) is valid until the next call on
+ * that context, whichever thread makes it.
+ */
 typedef struct rss_ctx rss_ctx;
 
 int rss_ctx_create(int device, rss_ctx** out);

@@ -368,11 +368,19 @@ def _copy_out(image, chunk=64 << 20):
 
 
 class HostContext:
-    """Owns an ``rss_ctx`` (device buffers + streams) for host-memory batches."""
+    """Owns an ``rss_ctx`` (device buffers + streams) for host-memory batches.
+
+    Thread-safe: the library serialises the calls on one context (``struct rss_ctx``'s
+    lock, ``include/rss_toeplitz.h``), so the process-wide :func:`default_context` can
+    serve many threads at once, as the reference's per-call ``Toeplitz.compute_hash``
+    (``toeplitz.py:59``) can.  Calls on different contexts run concurrently."""
 
     def __init__(self, device=0):
         self._lib = load()
         self._ctx = ctypes.c_void_p()
+        # held across rss_csv_hash_text and the copy of its context-owned image, which the
+        # next call on the context (from any thread) may overwrite
+        self._image_lock = threading.Lock()
         _check(self._lib.rss_ctx_create(device, ctypes.byref(self._ctx)), "rss_ctx_create")
         self.device = device
 
@@ -446,23 +454,24 @@ class HostContext:
         out, out_len, n = ctypes.c_void_p(), ctypes.c_size_t(0), ctypes.c_size_t(0)
         table = _csv_reta(reta, htable)
         name = "rss_csv6_hash_text" if isinstance(key, RssKey6) else "rss_csv_hash_text"
-        rc = getattr(self._lib, name)(
-            self._ctx, ctypes.byref(key), buf.ctypes.data, len(buf), htable, nqueues,
-            table.ctypes.data if table is not None else None,
-            FLAG_CSV_COUNTS_ONLY if counts_only else 0, ctypes.byref(out), ctypes.byref(out_len),
-            counts.ctypes.data, ctypes.byref(n))
-        if rc == ENOTSUP:
-            return None
-        _check(rc, name)
-        image = None
-        if not counts_only:
-            if out_len.value:
-                image = np.ctypeslib.as_array(ctypes.cast(out, ctypes.POINTER(ctypes.c_uint8)),
-                                              shape=(out_len.value,))
-                if copy:
-                    image = _copy_out(image)
-            else:
-                image = np.empty(0, dtype=np.uint8)
+        with self._image_lock:
+            rc = getattr(self._lib, name)(
+                self._ctx, ctypes.byref(key), buf.ctypes.data, len(buf), htable, nqueues,
+                table.ctypes.data if table is not None else None,
+                FLAG_CSV_COUNTS_ONLY if counts_only else 0, ctypes.byref(out),
+                ctypes.byref(out_len), counts.ctypes.data, ctypes.byref(n))
+            if rc == ENOTSUP:
+                return None
+            _check(rc, name)
+            image = None
+            if not counts_only:
+                if out_len.value:
+                    image = np.ctypeslib.as_array(
+                        ctypes.cast(out, ctypes.POINTER(ctypes.c_uint8)), shape=(out_len.value,))
+                    if copy:
+                        image = _copy_out(image)
+                else:
+                    image = np.empty(0, dtype=np.uint8)
         return image, counts, n.value
 
     def csv_hash_file(self, key, in_path, out_path, htable, nqueues, reta=None):
@@ -531,6 +540,41 @@ class MultiHostContext:
                                              ptr(q), ptr(c), 0), "rss_hash_host_multi")
         return h, q, c
 
+    def hash6(self, key6, tuples6, htable, nqueues, want_hash=True, want_queue=True,
+              want_counts=True, reta=None):
+        """IPv6 counterpart of :meth:`hash`: the same contiguous ranges as
+        ``rss_hash_host_multi`` (``sharding.shard_range``), one host thread per context
+        (ctypes releases the GIL), counts summed here."""
+        arr = np.ascontiguousarray(tuples6)
+        if arr.dtype != TUPLE6_DTYPE:
+            arr = np.ascontiguousarray(arr, dtype=np.uint32).reshape(-1, 9)
+        n, k = len(arr), len(self.contexts)
+        base, extra = divmod(n, k)
+        bounds = [base * i + min(i, extra) for i in range(k + 1)]
+        parts = [None] * k
+        errors = []
+
+        def work(i):
+            try:
+                parts[i] = self.contexts[i].hash6(key6, arr[bounds[i]:bounds[i + 1]], htable,
+                                                  nqueues, want_hash, want_queue, want_counts,
+                                                  reta)
+            except Exception as err:  # re-raised on the calling thread
+                errors.append(err)
+
+        workers = [threading.Thread(target=work, args=(i,)) for i in range(1, k)]
+        for w in workers:
+            w.start()
+        work(0)
+        for w in workers:
+            w.join()
+        if errors:
+            raise errors[0]
+        h = np.concatenate([p[0] for p in parts]) if want_hash else None
+        q = np.concatenate([p[1] for p in parts]) if want_queue else None
+        c = np.sum([p[2] for p in parts], axis=0, dtype=np.uint64) if want_counts else None
+        return h, q, c
+
 
 def default_context():
     """Process-wide HostContext on device ``$RSS_DEVICE`` (default 0), created on first use."""
@@ -539,6 +583,25 @@ def default_context():
         if _default_ctx is None:
             _default_ctx = HostContext(int(os.environ.get("RSS_DEVICE", "0")))
         return _default_ctx
+
+
+_multi_ctx = {}
+
+
+def host_context(devices=None):
+    """The context a host batch runs on: :func:`default_context` for ``devices`` None,
+    else a process-wide :class:`MultiHostContext` over ``devices`` (a sequence of device
+    ids; one may repeat, for several contexts on one GPU), created on first use."""
+    if devices is None:
+        return default_context()
+    devs = tuple(int(d) for d in devices)
+    if not devs:
+        raise ValueError("devices must name at least one GPU")
+    with _ctx_lock:
+        ctx = _multi_ctx.get(devs)
+        if ctx is None:
+            ctx = _multi_ctx[devs] = MultiHostContext(devs)
+        return ctx
 
 
 # ------------------------------------------------------- device pointers ----

@@ -938,6 +938,7 @@ int csv_hash_text(const char* who, rss_ctx* ctx, const typename CsvJob<Rows>::Ke
     int rc = check_args(key, htable, nqueues);
     if (rc) return rc;
     *n_rows = 0;
+    std::lock_guard<std::mutex> lock(ctx->mu);  // (struct rss_ctx)
     rss_csv_layout layout;
     size_t body_off;
     if (!rss_csv_header(text, len, &layout, &body_off))
@@ -978,6 +979,7 @@ int csv_hash_file(const char* who, rss_ctx* ctx, const typename CsvJob<Rows>::Ke
     int rc = check_args(key, htable, nqueues);
     if (rc) return rc;
     *n_rows = 0;
+    std::lock_guard<std::mutex> lock(ctx->mu);  // (struct rss_ctx)
     PhaseTimer timer(who);
     CSV_HIP_CHECK(hipSetDevice(ctx->device));
     if ((rc = reserve_stage(ctx))) return rc;

@@ -3,6 +3,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <mutex>
 #include <utility>
 #include <vector>
 
@@ -17,7 +18,14 @@ typedef struct ihipEvent_t* hipEvent_t;
 
 // Host-pipeline context (rss_ctx_create): device, streams and staging buffers of
 // rss_hash_host, plus the host output buffer of rss_csv_hash_text.
+//
+// Every entry point that takes a context holds `mu` for the whole call (the staging
+// buffers, streams and scratch below are one caller's at a time): the reference-compatible
+// classes share one process-wide context, and a caller may drive them from many threads
+// as it could the reference's Toeplitz.compute_hash, which copies its key per call
+// (toeplitz.py:59) and so is reentrant.
 struct rss_ctx {
+    std::mutex mu;
     int device = 0;
     size_t chunk = 0;  // tuples per staging buffer
     hipStream_t stream[2] = {nullptr, nullptr};

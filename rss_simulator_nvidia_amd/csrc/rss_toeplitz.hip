@@ -2172,6 +2172,7 @@ struct Options {
     bool counts_perm = true;  // the register-table counts-only kernel
     bool resid = true;        // counts only past 161144 queues: residual lists (else a column)
     bool wide = true;         // wide passes over a queue column (else u32 passes of 16384)
+    int alloc_fail = 0;       // scratch kinds (AllocKind bits) whose allocation is made to fail
 };
 #ifdef RSS_TEST_HOOKS
 Options g_opt;
@@ -2235,6 +2236,13 @@ int launch_counts_perm(const uint32_t* window, const void* tuples, uint64_t n, u
 // Whether a many-queues launch counts its queues from the queue column (launch_queue_ranges)
 // rather than with one global atomic per tuple: up to 64 wide passes (4M queues).
 bool ranged_histogram_ok(uint32_t q_eff) { return (uint64_t)q_eff <= 64ull * kWideSpan; }
+// Without the wide passes' scratch, the most narrow passes (16384 queues each) a launch runs
+// over a queue column before one global atomic per tuple is cheaper: 64 over u16 columns,
+// 32 over u32 ones
+uint64_t narrow_passes_max(int qw) { return qw == QW_U32 ? 32 : 64; }
+// launch_hash's many-queues attempt: "count with the global-atomic kernel instead" (every
+// RSS_* code is <= 0)
+constexpr int kTakeAtomics = 1;
 
 // --------------------------------------------------------- guarded passes --
 // Scratch block of a guarded pass (u16 / u8 bins with guard moves and a poison word: the
@@ -2249,7 +2257,11 @@ size_t guard_ctr_offset(uint32_t q_span) { return (((size_t)q_span + 2) * 4 + 7)
 size_t guard_tail_bytes(uint32_t q_span) { return guard_ctr_offset(q_span) + 8; }
 uint32_t guard_words(int bits, uint32_t q_span) { return bits == 8 ? (q_span + 3) / 4 : (q_span + 1) / 2; }
 
-void* alloc_block(size_t bytes, hipStream_t stream) {
+// What a scratch block is for (the test hooks' alloc_fail bits name them)
+enum AllocKind { AK_ROWS = 1, AK_WIDE = 2, AK_COLUMN = 4, AK_LISTS = 8 };
+
+void* alloc_block(size_t bytes, hipStream_t stream, int kind) {
+    if (g_opt.alloc_fail & kind) return nullptr;
     void* buf = nullptr;
     if (hipMallocAsync(&buf, bytes, stream) != hipSuccess) {
         (void)hipGetLastError();
@@ -2259,7 +2271,7 @@ void* alloc_block(size_t bytes, hipStream_t stream) {
 }
 void* alloc_guarded(int bits, unsigned grid, uint32_t q_span, hipStream_t stream) {
     return alloc_block(guard_rows_bytes(grid, guard_words(bits, q_span)) + guard_tail_bytes(q_span),
-                       stream);
+                       stream, AK_ROWS);
 }
 
 // frees `buf` stream-ordered after its readers; the first error wins
@@ -2308,23 +2320,29 @@ void launch_recount_col(const T* col, uint64_t n, uint32_t q_lo, uint32_t q_span
 // stream-ordered, so each reuses the rows and re-zeroes the tail), allocated before the
 // launch's first pass touches the counts -- a launch that cannot get it takes the narrow
 // passes (or, for residual lists, the scratch column) with the counts untouched.
-constexpr uint32_t kWideRowWords = kWideSpan8 / 4;  // >= kWideSpan / 2 (u16 rows)
 struct WideScratch {
     void* buf = nullptr;
     unsigned grid = 0;
+    uint32_t row_words = 0;  // one row's dwords: the widest pass the launch runs
     uint32_t* partial() const { return static_cast<uint32_t*>(buf); }
     uint32_t* ovf() const {
-        return reinterpret_cast<uint32_t*>(static_cast<char*>(buf) + guard_rows_bytes(grid, kWideRowWords));
+        return reinterpret_cast<uint32_t*>(static_cast<char*>(buf) + guard_rows_bytes(grid, row_words));
     }
 };
 unsigned wide_grid(uint64_t n, int cu_count) {
     const uint64_t want = (n + 8ull * kBlock - 1) / (8ull * kBlock);
     return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, cu_count));
 }
-WideScratch alloc_wide(unsigned grid, hipStream_t stream) {
+// The scratch of the wide passes over `nranged` queues: rows for u8 bins (kWideSpan8 / 4
+// dwords) when launch_queue_ranges will run a u8 pass (more than kWideSpan queues left),
+// else for u16 bins (kWideSpan / 2)
+WideScratch alloc_wide(unsigned grid, uint32_t nranged, hipStream_t stream) {
+    const bool u8 = g_opt.range8 && nranged > kWideSpan;
+    const uint32_t span = u8 ? kWideSpan8 : kWideSpan;
     WideScratch s;
     s.grid = grid;
-    s.buf = alloc_block(guard_rows_bytes(grid, kWideRowWords) + guard_tail_bytes(kWideSpan8), stream);
+    s.row_words = guard_words(u8 ? 8 : 16, span);
+    s.buf = alloc_block(guard_rows_bytes(grid, s.row_words) + guard_tail_bytes(span), stream, AK_WIDE);
     return s;
 }
 // a wide pass costs about two narrow ones (2^28 tuples: ~0.2 vs ~0.1 ms over a u16 column,
@@ -2566,131 +2584,143 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
     const uint64_t want = (n + per_lane * kBlock - 1) / (per_lane * kBlock);
     const uint64_t cap = (uint64_t)info.cu_count * kBlocksPerCU;
     const unsigned grid = (unsigned)(want < cap ? want : cap);
+    // many queues: the guarded passes, or kTakeAtomics when the launch counts with one
+    // global atomic per tuple instead (no scratch memory for them, or a column would need
+    // more narrow passes than the atomics cost)
     if (hist == HIST_GLOBAL && d_counts) {
-        // More queues than u32 LDS bins (DESIGN.md §3 "Many queues").  Guarded u16 bins
-        // (HIST_RANGE16): twice the queues of u32 bins in the LDS the tables leave -- 16384
-        // beside the 12-bit tables and, on the small tables (4-tuple body, no indirection
-        // table), up to 80572 in one pass.  Up to 16384 the 12-bit tables stay: 8 lookups and
-        // 3 VALU per lookup fewer than the small tables' 21 when the bins fit beside them.
-        const uint32_t span12 = ((kBinBytesMax - reta_bytes) / 4) * 2;
-        const bool small_lut = q_eff > span12 && vec4 && !reta && qwidth != QW_U8 && g_opt.small_lut;
-        const uint32_t lut_bytes = small_lut ? kSmallStaticBytes : kLutBytes;
-        const uint32_t span = ((kLdsBytes - lut_bytes - reta_bytes) / 4) * 2;
-        const int vm = small_lut ? VM_SMALL_LUT : (vec4 ? VM_VEC4 : VM_SCALAR);
-        const uint32_t qbytes = q_eff <= 65536u ? 2 : 4;
-        FallbackFn fb = pick_fallback(h_pow2, qmode);
-        if (q_eff <= span) {
-            p.q_lo = 0;
-            p.q_span = q_eff;
-            KernelFn fn = h_pow2 ? pick_queue<true>(qmode, HIST_RANGE16, qwidth, vm)
-                                 : pick_queue<false>(qmode, HIST_RANGE16, qwidth, vm);
-            void* buf = alloc_guarded(16, grid, q_eff, stream);
-            if (!buf) return set_error(RSS_ENOMEM, "rss_hash_device: no memory for the u16 bins' rows");
-            return launch_guarded(fn, fb, 16, grid, info.cu_count, ((q_eff + 1) / 2) * 4 + reta_bytes, p,
-                                  d_queue, qwidth, buf, reta_bytes, stream);
-        }
-        // Past the u16 bins' reach: guarded u8 bins (HIST_RANGE8) hold span8 = 161144 queues
-        // beside the small tables -- one pass up to there, and the first range of a
-        // queue-column launch beyond.
-        const uint32_t span8 = kLdsBytes - kSmallStaticBytes;
-        void* r8buf = nullptr;  // the u8 pass's scratch block, when it runs
-        if (small_lut && g_opt.range8 && fb)
-            r8buf = alloc_guarded(8, grid, std::min(q_eff, span8), stream);
-        if (r8buf && q_eff <= span8) {
-            p.q_lo = 0;
-            p.q_span = q_eff;
-            KernelFn fn = h_pow2 ? pick_queue<true>(qmode, HIST_RANGE8, qwidth, VM_SMALL_LUT)
-                                 : pick_queue<false>(qmode, HIST_RANGE8, qwidth, VM_SMALL_LUT);
-            return launch_guarded(fn, fb, 8, grid, info.cu_count, guard_words(8, q_eff) * 4, p, d_queue,
-                                  qwidth, r8buf, 0, stream);
-        }
-        // Counts only past span8 (u8 hash pass + wide passes): the queues past the pass's LDS
-        // range go to per-wave residual lists (resid_append) instead of a queue column --
-        // only those tuples' queues are written and read again, not every tuple's.
-        if (r8buf && !d_queue && q_eff > span8 && g_opt.resid) {
-            // the static walk gives a wave at most `rows` groups of 4 tuples per lane, plus the
-            // < 4 tail tuples (wave 0 of workgroup 0); 8 entries more keep every list 16-B aligned
-            const uint64_t per_row = (uint64_t)grid * kBlock;
-            const uint64_t rows = (n / 4 + per_row - 1) / per_row;
-            const uint64_t lcap = (rows * 4 * 64 + 4 + 7) & ~7ull;
-            const uint32_t nres = q_eff - span8;
-            const size_t esize = nres <= 65536u ? 2 : 4;
-            const size_t nlists = (size_t)grid * kWavesPerBlock;
-            const size_t list_bytes = nlists * lcap * esize;
-            void* lists = alloc_block(list_bytes + nlists * 4, stream);
-            WideScratch wsc = lists ? alloc_wide(grid, stream) : WideScratch{};
-            if (lists && wsc.buf) {
-                uint32_t* list_counts = reinterpret_cast<uint32_t*>(static_cast<char*>(lists) + list_bytes);
-                p.queue_out = nullptr;
-                p.resid_out = lists;
-                p.resid_counts = list_counts;
-                p.resid_cap = lcap;
-                p.resid_u16 = esize == 2;
-                p.prefetch = prefetch_for(false);
+        const int mq = [&]() -> int {
+            // More queues than u32 LDS bins (DESIGN.md §3 "Many queues").  Guarded u16 bins
+            // (HIST_RANGE16): twice the queues of u32 bins in the LDS the tables leave -- 16384
+            // beside the 12-bit tables and, on the small tables (4-tuple body, no indirection
+            // table), up to 80572 in one pass.  Up to 16384 the 12-bit tables stay: 8 lookups and
+            // 3 VALU per lookup fewer than the small tables' 21 when the bins fit beside them.
+            const uint32_t span12 = ((kBinBytesMax - reta_bytes) / 4) * 2;
+            const bool small_lut = q_eff > span12 && vec4 && !reta && qwidth != QW_U8 && g_opt.small_lut;
+            const uint32_t lut_bytes = small_lut ? kSmallStaticBytes : kLutBytes;
+            const uint32_t span = ((kLdsBytes - lut_bytes - reta_bytes) / 4) * 2;
+            const int vm = small_lut ? VM_SMALL_LUT : (vec4 ? VM_VEC4 : VM_SCALAR);
+            const uint32_t qbytes = q_eff <= 65536u ? 2 : 4;
+            FallbackFn fb = pick_fallback(h_pow2, qmode);
+            if (q_eff <= span) {
                 p.q_lo = 0;
-                p.q_span = span8;
-                KernelFn fn = h_pow2 ? pick_queue<true>(qmode, HIST_RANGE8, QW_U32, VM_SMALL_LUT)
-                                     : pick_queue<false>(qmode, HIST_RANGE8, QW_U32, VM_SMALL_LUT);
-                rc = launch_guarded(fn, fb, 8, grid, info.cu_count, guard_words(8, span8) * 4, p, nullptr,
-                                    QW_U32, r8buf, 0, stream);
-                p.resid_out = nullptr;
-                if (rc == RSS_OK)
-                    rc = launch_queue_ranges(lists, esize == 2 ? QW_U16 : QW_U32, n, 0, nres,
-                                             p.counts + span8, info.cu_count, stream, &wsc, list_counts,
-                                             lcap);
-                rc = free_block(wsc.buf, rc, stream);
-                return free_block(lists, rc, stream);
+                p.q_span = q_eff;
+                KernelFn fn = h_pow2 ? pick_queue<true>(qmode, HIST_RANGE16, qwidth, vm)
+                                     : pick_queue<false>(qmode, HIST_RANGE16, qwidth, vm);
+                void* buf = alloc_guarded(16, grid, q_eff, stream);
+                if (!buf) return kTakeAtomics;  // no memory for the u16 bins' rows
+                return launch_guarded(fn, fb, 16, grid, info.cu_count, ((q_eff + 1) / 2) * 4 + reta_bytes, p,
+                                      d_queue, qwidth, buf, reta_bytes, stream);
             }
-            (void)free_block(wsc.buf, RSS_OK, stream);  // no room for the lists: the scratch
-            (void)free_block(lists, RSS_OK, stream);    // column below
-        }
-        if (ranged_histogram_ok(q_eff)) {
-            void* qcol = d_queue;
-            int qw = qwidth;
-            bool scratch = false, ranged = true;
-            // counts only past the small tables' range: a u16 column of q - span (QW_U16R) when
-            // the rest of the queues fit 16 bits, else the queues themselves
-            const uint32_t first_span = r8buf ? span8 : span;
-            const bool resid = !d_queue && small_lut && q_eff - first_span <= 0xFFFFu;
-            const uint32_t sbytes = resid ? 2 : qbytes;
-            if (!qcol || qwidth == QW_U8) {  // (u8 queues always fit the bins: q_eff <= 256)
-                qcol = alloc_block((size_t)n * sbytes, stream);
-                if (qcol) {
-                    scratch = true;
-                    qw = resid ? QW_U16R : (qbytes == 2 ? QW_U16 : QW_U32);
-                } else {
-                    ranged = false;  // no room for a scratch column: one global atomic per tuple
+            // Past the u16 bins' reach: guarded u8 bins (HIST_RANGE8) hold span8 = 161144 queues
+            // beside the small tables -- one pass up to there, and the first range of a
+            // queue-column launch beyond.
+            const uint32_t span8 = kLdsBytes - kSmallStaticBytes;
+            void* r8buf = nullptr;  // the u8 pass's scratch block, when it runs
+            if (small_lut && g_opt.range8 && fb)
+                r8buf = alloc_guarded(8, grid, std::min(q_eff, span8), stream);
+            if (r8buf && q_eff <= span8) {
+                p.q_lo = 0;
+                p.q_span = q_eff;
+                KernelFn fn = h_pow2 ? pick_queue<true>(qmode, HIST_RANGE8, qwidth, VM_SMALL_LUT)
+                                     : pick_queue<false>(qmode, HIST_RANGE8, qwidth, VM_SMALL_LUT);
+                return launch_guarded(fn, fb, 8, grid, info.cu_count, guard_words(8, q_eff) * 4, p, d_queue,
+                                      qwidth, r8buf, 0, stream);
+            }
+            // Counts only past span8 (u8 hash pass + wide passes): the queues past the pass's LDS
+            // range go to per-wave residual lists (resid_append) instead of a queue column --
+            // only those tuples' queues are written and read again, not every tuple's.
+            if (r8buf && !d_queue && q_eff > span8 && g_opt.resid) {
+                // the static walk gives a wave at most `rows` groups of 4 tuples per lane, plus the
+                // < 4 tail tuples (wave 0 of workgroup 0); 8 entries more keep every list 16-B aligned
+                const uint64_t per_row = (uint64_t)grid * kBlock;
+                const uint64_t rows = (n / 4 + per_row - 1) / per_row;
+                const uint64_t lcap = (rows * 4 * 64 + 4 + 7) & ~7ull;
+                const uint32_t nres = q_eff - span8;
+                const size_t esize = nres <= 65536u ? 2 : 4;
+                const size_t nlists = (size_t)grid * kWavesPerBlock;
+                const size_t list_bytes = nlists * lcap * esize;
+                void* lists = alloc_block(list_bytes + nlists * 4, stream, AK_LISTS);
+                WideScratch wsc = lists ? alloc_wide(grid, nres, stream) : WideScratch{};
+                if (lists && wsc.buf) {
+                    uint32_t* list_counts = reinterpret_cast<uint32_t*>(static_cast<char*>(lists) + list_bytes);
+                    p.queue_out = nullptr;
+                    p.resid_out = lists;
+                    p.resid_counts = list_counts;
+                    p.resid_cap = lcap;
+                    p.resid_u16 = esize == 2;
+                    p.prefetch = prefetch_for(false);
+                    p.q_lo = 0;
+                    p.q_span = span8;
+                    KernelFn fn = h_pow2 ? pick_queue<true>(qmode, HIST_RANGE8, QW_U32, VM_SMALL_LUT)
+                                         : pick_queue<false>(qmode, HIST_RANGE8, QW_U32, VM_SMALL_LUT);
+                    rc = launch_guarded(fn, fb, 8, grid, info.cu_count, guard_words(8, span8) * 4, p, nullptr,
+                                        QW_U32, r8buf, 0, stream);
+                    p.resid_out = nullptr;
+                    if (rc == RSS_OK)
+                        rc = launch_queue_ranges(lists, esize == 2 ? QW_U16 : QW_U32, n, 0, nres,
+                                                 p.counts + span8, info.cu_count, stream, &wsc, list_counts,
+                                                 lcap);
+                    rc = free_block(wsc.buf, rc, stream);
+                    return free_block(lists, rc, stream);
                 }
+                (void)free_block(wsc.buf, RSS_OK, stream);  // no room for the lists: the scratch
+                (void)free_block(lists, RSS_OK, stream);    // column below
             }
-            if (ranged) {
-                p.queue_out = qcol;
-                p.prefetch = prefetch_for(true);  // the pass writes a column
-                p.q_lo = 0;
-                const bool v4 = vec4 && ((uintptr_t)qcol % (qw == QW_U32 ? 16 : 8)) == 0;
-                // the first range: the bins the first pass's tables leave (small tables: 4-tuple
-                // body only; the caller's queue buffer may not be aligned for it)
-                const bool b1 = small_lut && v4 && qw != QW_U8;
-                const bool r8 = b1 && r8buf;  // (a caller's u32 column: b1 == small_lut)
-                if (!r8 && r8buf) {
-                    (void)free_block(r8buf, RSS_OK, stream);
+            if (ranged_histogram_ok(q_eff)) {
+                void* qcol = d_queue;
+                int qw = qwidth;
+                bool scratch = false, ranged = true;
+                // counts only past the small tables' range: a u16 column of q - span (QW_U16R) when
+                // the rest of the queues fit 16 bits, else the queues themselves
+                const uint32_t first_span = r8buf ? span8 : span;
+                const bool resid = !d_queue && small_lut && q_eff - first_span <= 0xFFFFu;
+                const uint32_t sbytes = resid ? 2 : qbytes;
+                if (!qcol || qwidth == QW_U8) {  // (u8 queues always fit the bins: q_eff <= 256)
+                    qcol = alloc_block((size_t)n * sbytes, stream, AK_COLUMN);
+                    if (qcol) {
+                        scratch = true;
+                        qw = resid ? QW_U16R : (qbytes == 2 ? QW_U16 : QW_U32);
+                    } else {
+                        ranged = false;  // no room for a scratch column: one global atomic per tuple
+                    }
+                }
+                if (ranged) {
+                    p.queue_out = qcol;
+                    p.prefetch = prefetch_for(true);  // the pass writes a column
+                    p.q_lo = 0;
+                    const bool v4 = vec4 && ((uintptr_t)qcol % (qw == QW_U32 ? 16 : 8)) == 0;
+                    // the first range: the bins the first pass's tables leave (small tables: 4-tuple
+                    // body only; the caller's queue buffer may not be aligned for it)
+                    const bool b1 = small_lut && v4 && qw != QW_U8;
+                    const bool r8 = b1 && r8buf;  // (a caller's u32 column: b1 == small_lut)
+                    if (!r8 && r8buf) {
+                        (void)free_block(r8buf, RSS_OK, stream);
+                        r8buf = nullptr;
+                    }
+                    const uint32_t span1 = b1 ? (r8 ? span8 : span) : span12;
+                    p.q_span = span1;  // < q_eff here
+                    const int vm1 = b1 ? VM_SMALL_LUT : (v4 ? VM_VEC4 : VM_SCALAR);
+                    const int bits1 = r8 ? 8 : 16;
+                    KernelFn fn = h_pow2 ? pick_queue<true>(qmode, r8 ? HIST_RANGE8 : HIST_RANGE16, qw, vm1)
+                                         : pick_queue<false>(qmode, r8 ? HIST_RANGE8 : HIST_RANGE16, qw, vm1);
+                    const unsigned g1 = v4 ? grid : (unsigned)std::min<uint64_t>((n + kBlock - 1) / kBlock, cap);
+                    // every scratch block before the first pass touches the counts
+                    void* buf1 = r8 ? r8buf : alloc_guarded(16, g1, span1, stream);
                     r8buf = nullptr;
-                }
-                const uint32_t span1 = b1 ? (r8 ? span8 : span) : span12;
-                p.q_span = span1;  // < q_eff here
-                const int vm1 = b1 ? VM_SMALL_LUT : (v4 ? VM_VEC4 : VM_SCALAR);
-                const int bits1 = r8 ? 8 : 16;
-                KernelFn fn = h_pow2 ? pick_queue<true>(qmode, r8 ? HIST_RANGE8 : HIST_RANGE16, qw, vm1)
-                                     : pick_queue<false>(qmode, r8 ? HIST_RANGE8 : HIST_RANGE16, qw, vm1);
-                const unsigned g1 = v4 ? grid : (unsigned)std::min<uint64_t>((n + kBlock - 1) / kBlock, cap);
-                // every scratch block before the first pass touches the counts
-                void* buf1 = r8 ? r8buf : alloc_guarded(16, g1, span1, stream);
-                r8buf = nullptr;
-                const uint32_t nranged = q_eff - span1;
-                WideScratch wsc = buf1 && wide_pays(nranged) ? alloc_wide(wide_grid(n, info.cu_count), stream)
-                                                             : WideScratch{};
-                if (!buf1) {
-                    rc = set_error(RSS_ENOMEM, "rss_hash_device: no memory for the first range's rows");
-                } else {
+                    const uint32_t nranged = q_eff - span1;
+                    WideScratch wsc = buf1 && wide_pays(nranged)
+                                          ? alloc_wide(wide_grid(n, info.cu_count), nranged, stream)
+                                          : WideScratch{};
+                    // no rows for the first range, or no wide scratch and more narrow passes
+                    // over the column than one atomic per tuple costs: the atomics (the counts
+                    // are untouched so far)
+                    const uint64_t narrow = ((uint64_t)nranged + kNarrowSpan - 1) / kNarrowSpan;
+                    if (!buf1 || (!wsc.buf && narrow > narrow_passes_max(qw))) {
+                        (void)free_block(buf1, RSS_OK, stream);
+                        (void)free_block(wsc.buf, RSS_OK, stream);
+                        (void)free_block(scratch ? qcol : nullptr, RSS_OK, stream);
+                        return kTakeAtomics;
+                    }
                     const uint32_t shmem1 = guard_words(bits1, span1) * 4 + (bits1 == 16 ? reta_bytes : 0);
                     rc = launch_guarded(fn, fb, bits1, g1, info.cu_count, shmem1, p, qcol, qw, buf1,
                                         reta_bytes, stream);
@@ -2700,13 +2730,18 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
                     else if (rc == RSS_OK)
                         rc = launch_queue_ranges(qcol, qw, n, span1, q_eff, p.counts, info.cu_count,
                                                  stream, &wsc);
+                    rc = free_block(wsc.buf, rc, stream);
+                    // the scratch column goes back on every path (stream-ordered after its readers)
+                    return free_block(scratch ? qcol : nullptr, rc, stream);
                 }
-                rc = free_block(wsc.buf, rc, stream);
-                // the scratch column goes back on every path (stream-ordered after its readers)
-                return free_block(scratch ? qcol : nullptr, rc, stream);
             }
-        }
-        (void)free_block(r8buf, RSS_OK, stream);  // unused: global atomics below
+            (void)free_block(r8buf, RSS_OK, stream);  // unused: global atomics below
+            return kTakeAtomics;
+        }();
+        if (mq != kTakeAtomics) return mq;
+        p.queue_out = d_queue;  // (a ranged attempt may have pointed them elsewhere)
+        p.prefetch = prefetch_for(d_hash || d_queue);
+        p.q_lo = p.q_span = 0;
     }
     // 32-bit byte offsets when every stream's bytes fit them (input 12 n B is the largest)
     const int vmode = vec4 ? (12ull * n < (1ull << 32) && !(flags & RSS_FLAG_ADDR64) ? 2 : 1) : 0;
@@ -2856,7 +2891,7 @@ int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint
             void* qcol = d_queue;
             bool scratch = false, ranged = true;
             if (!qcol || qwidth == QW_U8) {
-                qcol = alloc_block((size_t)n * qbytes, stream);
+                qcol = alloc_block((size_t)n * qbytes, stream, AK_COLUMN);
                 if (qcol) {
                     scratch = true;
                     p.qwidth = qbytes == 2 ? QW_U16 : QW_U32;
@@ -2872,18 +2907,28 @@ int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint
                 const bool v4 = vec4 && ((uintptr_t)qcol % (qw == QW_U32 ? 16 : 8)) == 0;
                 KernelFn6 fn = h_pow2 ? pick6<true>(qmode, HIST_RANGE, v4) : pick6<false>(qmode, HIST_RANGE, v4);
                 const unsigned g1 = v4 ? grid : (unsigned)std::min<uint64_t>((n + kBlock - 1) / kBlock, cap);
-                // the wide passes' scratch before the first pass touches the counts
-                WideScratch wsc = wide_pays(q_eff - span) ? alloc_wide(wide_grid(n, info.cu_count), stream)
-                                                          : WideScratch{};
-                hipLaunchKernelGGL(fn, dim3(g1), dim3(kBlock), span * 4 + reta_bytes, stream, p);
-                const hipError_t le = hipGetLastError();
-                rc = le == hipSuccess
-                         ? launch_queue_ranges(qcol, (int)qw, n, span, q_eff, p.counts, info.cu_count, stream,
-                                               &wsc)
-                         : set_error(RSS_EIO, "rss_hash6_device: range launch failed: %s",
-                                     hipGetErrorString(le));
-                rc = free_block(wsc.buf, rc, stream);
-                return free_block(scratch ? qcol : nullptr, rc, stream);
+                // the wide passes' scratch before the first pass touches the counts; without
+                // it, more narrow passes than the atomics cost take the atomics (as launch_hash)
+                const uint32_t nranged = q_eff - p.q_span;
+                WideScratch wsc = wide_pays(nranged) ? alloc_wide(wide_grid(n, info.cu_count), nranged, stream)
+                                                     : WideScratch{};
+                const uint64_t narrow = ((uint64_t)nranged + kNarrowSpan - 1) / kNarrowSpan;
+                if (!wsc.buf && narrow > narrow_passes_max((int)qw)) {
+                    (void)free_block(scratch ? qcol : nullptr, RSS_OK, stream);
+                    p.queue_out = d_queue;
+                    p.qwidth = qwidth;
+                    p.q_lo = p.q_span = 0;
+                } else {
+                    hipLaunchKernelGGL(fn, dim3(g1), dim3(kBlock), span * 4 + reta_bytes, stream, p);
+                    const hipError_t le = hipGetLastError();
+                    rc = le == hipSuccess
+                             ? launch_queue_ranges(qcol, (int)qw, n, span, q_eff, p.counts, info.cu_count, stream,
+                                                   &wsc)
+                             : set_error(RSS_EIO, "rss_hash6_device: range launch failed: %s",
+                                         hipGetErrorString(le));
+                    rc = free_block(wsc.buf, rc, stream);
+                    return free_block(scratch ? qcol : nullptr, rc, stream);
+                }
             }
         }
     }
@@ -3034,6 +3079,7 @@ static int hash6_host_impl(rss_ctx* ctx, const rss_key6* key, const rss_tuple6* 
                            uint64_t* h_counts, uint32_t flags, const uint32_t* reta) {
     if (!ctx) return set_error(RSS_EINVAL, "rss_hash6_host: ctx is NULL");
     if (n && !h_tuples) return set_error(RSS_EINVAL, "rss_hash6_host: tuples is NULL");
+    std::lock_guard<std::mutex> lock(ctx->mu);  // (struct rss_ctx)
     RSS_HIP_CHECK(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream[0];
     rss_tuple6* d_t = nullptr;
@@ -3387,6 +3433,7 @@ static int hash_host_impl(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_
     if (htable < 1 || nqueues < 1)
         return set_error(RSS_EINVAL, "rss_hash_host: htable (%u) and nqueues (%u) must be >= 1",
                          htable, nqueues);
+    std::lock_guard<std::mutex> lock(ctx->mu);  // (struct rss_ctx)
     RSS_HIP_CHECK(hipSetDevice(ctx->device));
     if (n > 0 && n <= kSmallBatch)
         return hash_host_small(ctx, key, h_tuples, n, htable, nqueues, h_hash, h_queue, h_counts,
@@ -3482,6 +3529,7 @@ int rss_key_search_host(rss_ctx* ctx, const rss_key* keys, size_t nkeys,
     if (!ctx || !keys || !h_counts || nkeys == 0)
         return set_error(RSS_EINVAL, "rss_key_search_host: NULL argument or no keys");
     if (n && !h_tuples) return set_error(RSS_EINVAL, "rss_key_search_host: tuples is NULL");
+    std::lock_guard<std::mutex> lock(ctx->mu);  // (struct rss_ctx)
     RSS_HIP_CHECK(hipSetDevice(ctx->device));
     std::vector<uint32_t> windows(nkeys * RSS_INPUT_BITS);
     for (size_t k = 0; k < nkeys; ++k) {
@@ -3547,6 +3595,7 @@ int rss_test_set_option(const char* name, int value) {
     else if (n == "counts_perm") g_opt.counts_perm = value != 0;
     else if (n == "resid") g_opt.resid = value != 0;
     else if (n == "wide") g_opt.wide = value != 0;
+    else if (n == "alloc_fail") g_opt.alloc_fail = value;  // AllocKind bits
     else if (n == "guard_sleep") {
         const uint32_t v = value > 0 ? (uint32_t)value : 0u;
         RSS_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_guard_sleep), &v, sizeof v));

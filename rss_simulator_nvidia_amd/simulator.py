@@ -36,16 +36,19 @@ class Simulator(object):
     """RSS simulator class (``simulator.py:26``)."""
 
     def __init__(self, hash_key, hash_table_size, queue_number, hash_fields=None, ipv6=False,
-                 reta=None):
+                 reta=None, devices=None):
         """Key as ``List[int]``, hash-table size and number of queues (both >= 1).
 
         Additive options: ``hash_fields`` (mask or ``'sdfn'``
         letters) selects the hashed fields; ``ipv6`` reads IPv6 address columns; ``reta``
-        (``hash_table_size`` queue ids) replaces ``bucket % queue_number``."""
+        (``hash_table_size`` queue ids) replaces ``bucket % queue_number``; ``devices``
+        (GPU ids) splits ``calc_hash``'s rows over several GPUs, one context each (the
+        default hashes on one GPU).  Results do not depend on ``devices``."""
         self.__ip_df = None
         self.__toeplitz = Toeplitz(hash_key, hash_fields or "sdfn")
         self.__ipv6 = ipv6
         self.__reta = reta
+        self.__devices = None if devices is None else tuple(devices)
         self.__hash_table_size = hash_table_size
         self.__queue_num = queue_number
         self.__queues = None
@@ -95,9 +98,11 @@ class Simulator(object):
         if sparse:  # H, Q >= 2**32: hash % H % Q = hash (simulator.py:97); hashes only
             H = Q = 1
         if self.__ipv6:
-            h, q, c = self.__toeplitz.compute_queues6(pack_frame6(df), H, Q, self.__reta)
+            h, q, c = self.__toeplitz.compute_queues6(pack_frame6(df), H, Q, self.__reta,
+                                                      self.__devices)
         else:
-            h, q, c = self.__toeplitz.compute_queues(pack_frame(df), H, Q, self.__reta)
+            h, q, c = self.__toeplitz.compute_queues(pack_frame(df), H, Q, self.__reta,
+                                                     self.__devices)
         df[_HASH] = h.astype(np.int64)
         self.__count_rows = None
         if sparse:  # a 2**32-entry histogram: the non-empty queues only (value_counts)

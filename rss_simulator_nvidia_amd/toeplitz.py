@@ -69,14 +69,17 @@ class Toeplitz(object):
                                                   want_queue=False, want_counts=False)
         return h
 
-    def compute_queues(self, tuples, hash_table_size, queue_number, reta=None):
+    def compute_queues(self, tuples, hash_table_size, queue_number, reta=None, devices=None):
         """Hash + ``hash % htable % queues`` (or ``reta[hash % htable]``) + per-queue counts
         in one kernel pass.  Returns ``(hash_u32[n], queue_u32[n], counts_u64[queue_number])``.
-        """
-        return _native.default_context().hash(self.prepared_key, np.asarray(tuples),
-                                              hash_table_size, queue_number, reta=reta)
 
-    def compute_queues6(self, tuples6, hash_table_size, queue_number, reta=None):
+        ``devices`` (additive): GPU ids to split the batch over (contiguous ranges, one
+        context each, counts summed); None = the default context's one GPU.
+        """
+        return _native.host_context(devices).hash(self.prepared_key, np.asarray(tuples),
+                                                  hash_table_size, queue_number, reta=reta)
+
+    def compute_queues6(self, tuples6, hash_table_size, queue_number, reta=None, devices=None):
         """IPv6 counterpart of :meth:`compute_queues` (``rss_tuple6`` rows)."""
-        return _native.default_context().hash6(self.prepared_key6, np.asarray(tuples6),
-                                               hash_table_size, queue_number, reta=reta)
+        return _native.host_context(devices).hash6(self.prepared_key6, np.asarray(tuples6),
+                                                   hash_table_size, queue_number, reta=reta)

@@ -35,6 +35,16 @@ def main():
     from rss_simulator_nvidia_amd.sharding import CountsPipeline, shard_range
     args = bench.parse_args()
     dist.init_process_group("gloo")
+    # count the all-reduces the pipelines issue (sharding.allreduce_counts calls
+    # dist.all_reduce through the module): one per batch is the contract
+    issued = {"n": 0}
+    all_reduce = dist.all_reduce
+
+    def counting_all_reduce(*a, **k):
+        issued["n"] += 1
+        return all_reduce(*a, **k)
+
+    dist.all_reduce = counting_all_reduce
     distributed = True
     n, H, Q = args.tuples_per_gpu, args.htable, args.queues
     qw = "u8"
@@ -58,6 +68,7 @@ def main():
         return bench.max_over_ranks(torch, dist, values, "cpu", distributed)
 
     # the main line: one collective per batch
+    issued["n"] = 0
     launch = launch_of(rank * n, n)
     pipeline = CountsPipeline(Q, "cpu", allreduce="overlap", bucket=args.allreduce_bucket)
     for _ in range(args.warmup):
@@ -71,6 +82,7 @@ def main():
     last = pipeline.drain()
     barrier()
     elapsed = time.perf_counter() - t0
+    main_collectives = issued["n"]
     kernel_ms = elapsed * 1e3 / args.steps
     total = int(last.sum().item())
     if total != n * world:
@@ -87,6 +99,7 @@ def main():
     first, n3 = shard_range(args.configs3_tuples, rank, world)
     pipe3 = CountsPipeline(Q, "cpu", allreduce="overlap", bucket=1)
     launch3 = launch_of(first, n3)
+    issued["n"] = 0
     barrier()
     t3 = time.perf_counter()
     for _ in range(args.configs3_steps):
@@ -94,6 +107,10 @@ def main():
     last3 = pipe3.drain()
     barrier()
     e3 = time.perf_counter() - t3
+    c3_collectives = issued["n"]
+    dist.all_reduce = all_reduce
+    shards = [None] * world
+    dist.all_gather_object(shards, [first, n3, main_collectives, c3_collectives])
     if int(last3.sum().item()) != args.configs3_tuples:
         raise SystemExit("rehearsal: configs[3] counts sum to %d" % int(last3.sum().item()))
     stats3 = reduce_max([e3, e3 * 1e3 / args.configs3_steps, e3 * 1e3 / args.configs3_steps,
@@ -115,6 +132,12 @@ def main():
             c3=c3, bucketed=bucketed, verified=verified, verified_all=verified_all, extras=None,
             traffic=None))
         line["data"] = "rehearsal: CPU ranks, a CPU histogram in place of the kernel (not a rate)"
+        line["rehearsal"] = {
+            "main_batches": args.warmup + args.steps,
+            "main_collectives": [s[2] for s in shards],
+            "configs3_batches": args.configs3_steps,
+            "configs3_collectives": [s[3] for s in shards],
+            "configs3_shards": [[s[0], s[1]] for s in shards]}
         with open(out_path, "w") as f:
             f.write(json.dumps(line) + "\n")
     dist.barrier()

@@ -3,6 +3,7 @@ forms agree and start at example_input/ips.csv's first row; PMC traffic lookup k
 import json
 
 import numpy as np
+import pytest
 import torch
 
 import bench
@@ -172,11 +173,14 @@ def test_committed_bench_lines_do_one_exchange_per_batch():
     assert (1, "RCCL") in seen and (8, "gloo") in seen, seen
 
 
-def test_world8_rehearsal_line(tmp_path):
-    """bench.py's N > 1 machinery at world size 8 on CPU ranks (gloo,
-    tests/bench_rehearsal.py): one all-reduce per batch in the main line, 8 per-rank rows in
-    rank order, the configs[3] block over 8 contiguous shards and the labelled bucketed
-    block -- so the driver's 8-GPU run does not meet a path only world size 1 has run."""
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_world_rehearsal_line(tmp_path, world):
+    """bench.py's N > 1 machinery at every N of the driver's
+    curve but 1 (BASELINE configs[3] "scaling curve 1/2/4/8") on CPU ranks (gloo,
+    tests/bench_rehearsal.py): one all-reduce per batch on every rank (counted), N per-rank
+    rows in rank order, the configs[3] block over N contiguous shard_range shards that tile
+    the global batch, and the labelled bucketed block -- so the driver's multi-GPU runs do not
+    meet a path only world size 1 has run."""
     import os
     import socket
     import subprocess
@@ -188,24 +192,43 @@ def test_world8_rehearsal_line(tmp_path):
     out = tmp_path / "line.json"
     env = dict(os.environ, OMP_NUM_THREADS="1")
     p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-                        "--nproc-per-node", "8", "--master-addr", "127.0.0.1", "--master-port",
-                        str(port), os.path.join(root, "tests", "bench_rehearsal.py"), str(out)],
+                        "--nproc-per-node", str(world), "--master-addr", "127.0.0.1",
+                        "--master-port", str(port),
+                        os.path.join(root, "tests", "bench_rehearsal.py"), str(out)],
                        capture_output=True, text=True, timeout=240, env=env)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
     line = json.loads(out.read_text())
-    assert line["n_gpus"] == 8 and line["scaling"] == "weak" and line["value"] > 0
+    assert line["n_gpus"] == world and line["scaling"] == "weak" and line["value"] > 0
     cfg = line["config"]
-    assert cfg["collectives_per_batch"] == 1.0 and cfg["global_tuples"] == 8 * 4096
+    assert cfg["collectives_per_batch"] == 1.0 and cfg["global_tuples"] == world * 4096
     assert "one collective per batch" in cfg["parallelism"] and "gloo" in cfg["parallelism"]
     rows = line["per_rank"]
-    assert [r["rank"] for r in rows] == list(range(8))
+    assert [r["rank"] for r in rows] == list(range(world))
     assert line["roofline"]["kernel_ms_max_rank"] >= max(r["kernel_ms"] for r in rows) * 0.999
+    reh = line["rehearsal"]
+    assert reh["main_collectives"] == [reh["main_batches"]] * world
+    assert reh["configs3_collectives"] == [reh["configs3_batches"]] * world
     c3 = line["configs3"]
     assert c3["scaling"] == "strong" and c3["global_tuples"] == 1 << 16
-    assert c3["tuples_per_rank_max"] == (1 << 16) // 8
+    shards = reh["configs3_shards"]
+    assert shards[0][0] == 0 and sum(n for _, n in shards) == 1 << 16
+    assert all(a + n == b for (a, n), (b, _) in zip(shards, shards[1:]))  # contiguous
+    assert c3["tuples_per_rank_max"] == max(n for _, n in shards) == -(-(1 << 16) // world)
     b = line["bucketed"]
     assert b["steps_per_collective"] == 8 and b["collectives"] == -(-line["steps"] // 8)
     assert line["verified"] is None and line["verification"]["main"] is None
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_configs3_shards_tile_the_full_batch(world):
+    """BASELINE configs[3] at its real size: 2^30 tuples over N ranks, contiguous
+    shard_range shards of 2^30 / N (the same ranges rss_hash_host_multi uses)."""
+    from rss_simulator_nvidia_amd.sharding import shard_range
+    total = 1 << 30
+    shards = [shard_range(total, r, world) for r in range(world)]
+    assert shards[0][0] == 0 and all(n == total // world for _, n in shards)
+    assert all(a + n == b for (a, n), (b, _) in zip(shards, shards[1:]))
+    assert sum(n for _, n in shards) == total
 
 
 def test_relaunch_runs_torchrun_on_loopback(monkeypatch):

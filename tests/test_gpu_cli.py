@@ -17,8 +17,40 @@ def test_edge_cases_gpu(name, case, tmp_path, capsys, monkeypatch):
     check_edge(name, case, tmp_path, capsys, monkeypatch)
 
 
-def test_fast_path_equals_pandas_path_large(tmp_path, monkeypatch, capsys):
-    """300K generated canonical rows: native CSV path == pandas path, byte for byte."""
+def _assert_written_table_is_oracles(out_bytes, src, H, Q, oracle_lib, key):
+    """The written statistics file against the C oracle, not against another product path:
+    the input rows packed by the oracle's own ``ip_to_u32`` / ``pack_ports`` (``toeplitz.py:
+    100-142``), hashed by ``oracle_run``; the table's ``hash_result`` / ``queue_number`` and
+    the counts section (``value_counts().sort_index()``, ``simulator.py:107-113``) must be its
+    results, and the table's 4-tuple columns the input's."""
+    import io
+
+    import numpy as np
+    import pandas as pd
+
+    from oracle import oracle as o
+    src_df = pd.read_csv(src)
+    tup = np.array([[o.ip_to_u32(a), o.ip_to_u32(b), o.pack_ports(int(c), int(d))]
+                    for a, b, c, d in zip(src_df["src_ip"], src_df["dst_ip"], src_df["src_port"],
+                                          src_df["dst_port"])], dtype=np.uint32).reshape(-1, 3)
+    ho, qo, co = oracle_lib.run(key, tup, H, Q)
+    head, rows = out_bytes.decode().split("src_ip,", 1)
+    table = pd.read_csv(io.StringIO("src_ip," + rows))
+    assert list(table.columns[:4]) == list(src_df.columns[:4])
+    for col in src_df.columns[:4]:
+        assert table[col].astype(str).tolist() == src_df[col].astype(str).tolist(), col
+    np.testing.assert_array_equal(table["hash_result"].to_numpy().astype(np.uint64), ho)
+    np.testing.assert_array_equal(table["queue_number"].to_numpy().astype(np.uint64), qo)
+    counts = pd.read_csv(io.StringIO(head))
+    nz = np.flatnonzero(co)
+    np.testing.assert_array_equal(counts["queue_number"].to_numpy(), nz)
+    np.testing.assert_array_equal(counts["counts"].to_numpy().astype(np.uint64), co[nz])
+
+
+def test_fast_path_equals_pandas_path_large(tmp_path, monkeypatch, capsys, oracle_lib,
+                                            example_key):
+    """300K generated canonical rows: native CSV path == pandas path, byte for byte, and
+    the table and counts are the oracle's."""
     import os
     import subprocess
 
@@ -40,12 +72,14 @@ def test_fast_path_equals_pandas_path_large(tmp_path, monkeypatch, capsys):
         outs[mode] = open(out, "rb").read()
     assert outs["1"] == outs["0"]
     assert outs["1"].count(b"\n") == 300000 + 1 + 24 + 1
+    _assert_written_table_is_oracles(outs["1"], src, 512, 24, oracle_lib, example_key)
 
 
 @pytest.mark.parametrize("device_csv", ["1", "0"])
-def test_many_queues_csv_paths_equal_pandas(tmp_path, monkeypatch, capsys, device_csv):
+def test_many_queues_csv_paths_equal_pandas(tmp_path, monkeypatch, capsys, device_csv, oracle_lib,
+                                            example_key):
     """--num-queues 20000 (the many-queues ranges on the device CSV path and on the host text
-    path) writes the same bytes as the pandas path."""
+    path) writes the same bytes as the pandas path, and they are the oracle's table."""
     import os
     import subprocess
 
@@ -82,3 +116,4 @@ def test_many_queues_csv_paths_equal_pandas(tmp_path, monkeypatch, capsys, devic
     bc = np.bincount(q, minlength=20000)
     np.testing.assert_array_equal(counts["counts"].to_numpy(), bc[counts["queue_number"].to_numpy()])
     assert int(counts["counts"].sum()) == len(q) == 50000
+    _assert_written_table_is_oracles(outs["1"], src, 1048576, 20000, oracle_lib, example_key)

@@ -2,7 +2,7 @@
 library AND on the tests' hooks build with random path options: u8 bins off (range8=0), the
 12-bit tables (small_lut=0), the scratch column instead of residual lists (resid=0), narrow
 instead of wide passes (wide=0), the load prefetch forced on / off, the static walk
-(balance=0), every guarded pass recounted (recount=1) or read from its bins and moves alone
+(balance=0), refused scratch allocations (alloc_fail), every guarded pass recounted (recount=1) or read from its bins and moves alone
 (recount=2) -- the alternative paths a launch takes when it gets no scratch memory, and the
 two halves of a guarded pass.  Random H (power of two or not, >= Q or not), Q from 8193 to
 ~1.2M, n up to 2^20 + ragged tails, outputs or counts only, u16 / u32 queues, accumulation,
@@ -51,6 +51,8 @@ def _config(seed):
         opts["recount"] = 2  # uniform input: no bin wraps, so the bins and moves alone are exact
     if rng.random() < 0.3:
         opts["prefetch"] = int(rng.integers(0, 2))
+    if rng.random() < 0.2:  # refused scratch blocks (AllocKind bits): the fallbacks down to atomics
+        opts["alloc_fail"] = int(rng.integers(1, 16))
     return dict(rng=rng, n=n, H=H, Q=Q, opts=opts, hooks=bool(opts) or rng.random() < 0.5,
                 outputs=bool(rng.random() < 0.5), accumulate=bool(rng.random() < 0.3),
                 misaligned=bool(rng.random() < 0.2), u16=bool(rng.random() < 0.5))

@@ -550,3 +550,67 @@ def test_u16_real_wrap_is_caught(native, oracle_lib, example_key, Q, lo, hi):
         _, _, good = _launch(native, key, tup, len(host), H, Q, False)
     assert not np.array_equal(bad.cpu().numpy().view(np.uint64), want), "no wrap was forced"
     np.testing.assert_array_equal(good.cpu().numpy().view(np.uint64), want)
+
+
+# the hooks build's alloc_fail bits (AllocKind, csrc/rss_toeplitz.hip): which scratch blocks
+# a launch is refused
+AK_ROWS, AK_WIDE, AK_COLUMN, AK_LISTS = 1, 2, 4, 8
+
+
+@pytest.mark.parametrize("Q,outputs,fail", [
+    (50000, False, AK_ROWS),                 # the single u16 pass: no rows -> atomics
+    (50000, True, AK_ROWS),
+    (120000, False, AK_ROWS),                # the single u8 pass and the first range: atomics
+    (300000, False, AK_LISTS),               # no residual lists -> the scratch column
+    (300000, False, AK_LISTS | AK_COLUMN),   # ... and no column -> atomics
+    (300000, False, AK_WIDE),                # no wide scratch -> 9 narrow passes
+    (300000, True, AK_WIDE),
+    (1000000, False, AK_WIDE),               # 52 narrow u32 passes > 32 -> atomics
+    (1000000, True, AK_WIDE),
+    (1000000, True, AK_ROWS | AK_WIDE | AK_COLUMN | AK_LISTS),
+])
+def test_scratch_allocation_failures_fall_back(native, oracle_lib, example_key, Q, outputs, fail):
+    """A launch refused a scratch block (hooks alloc_fail) still succeeds with the oracle's
+    counts, accumulated onto the caller's (the counts are untouched until the path that runs
+    is chosen): the u16 / u8 rows, the residual lists, the scratch column and the wide
+    passes' scratch each have a fallback, down to one global atomic per tuple."""
+    n, H = (1 << 20) + 5, 1 << 30
+    host = oracle_lib.generate(41, 0, n)
+    dev = torch.device("cuda:0")
+    tup = torch.from_numpy(host.view(np.int32).reshape(-1)).to(dev)
+    h = torch.empty(n, dtype=torch.int32, device=dev) if outputs else None
+    q = torch.empty(n, dtype=torch.int32, device=dev) if outputs else None
+    base = np.arange(Q, dtype=np.int64) % 7
+    c = torch.from_numpy(base).to(dev)
+    with hooks(alloc_fail=fail):
+        native.hash_device(native.prepare_key(example_key), tup.data_ptr(), n, H, Q,
+                           h.data_ptr() if outputs else None, q.data_ptr() if outputs else None,
+                           c.data_ptr(), native.FLAG_ACCUMULATE,
+                           torch.cuda.current_stream(dev).cuda_stream)
+        torch.cuda.synchronize()
+    ho, qo, co = oracle_lib.run(example_key, host, H, Q, threads=8)
+    np.testing.assert_array_equal(c.cpu().numpy().view(np.uint64), co + base.astype(np.uint64))
+    if outputs:
+        np.testing.assert_array_equal(h.cpu().numpy().view(np.uint32), ho)
+        np.testing.assert_array_equal(q.cpu().numpy().view(np.uint32), qo)
+
+
+@pytest.mark.parametrize("Q,fail", [(100000, AK_WIDE), (1000000, AK_WIDE), (100000, AK_COLUMN)])
+def test_ipv6_scratch_allocation_failures_fall_back(native, example_key, Q, fail):
+    """IPv6 many queues without wide scratch (narrow passes, or atomics past 32 u32 passes)
+    or without a scratch column: counts equal hash % H % Q of the kernel's own hashes."""
+    n, H = (1 << 18) + 3, 1 << 30
+    rng = np.random.default_rng(Q + fail)
+    words = torch.from_numpy(rng.integers(-2**31, 2**31, 9 * n, dtype=np.int64).astype(np.int32)).to("cuda:0")
+    key6 = native.prepare_key6(example_key)
+    s = torch.cuda.current_stream().cuda_stream
+    h = torch.empty(n, dtype=torch.int32, device="cuda:0")
+    native.hash6_device(key6, words.data_ptr(), n, 1, 1, h.data_ptr(), None, None, 0, s)
+    c = torch.zeros(Q, dtype=torch.int64, device="cuda:0")
+    with hooks(alloc_fail=fail):
+        native.hash6_device(key6, words.data_ptr(), n, H, Q, None, None, c.data_ptr(), 0, s)
+        torch.cuda.synchronize()
+    hv = h.cpu().numpy().view(np.uint32).astype(np.uint64)
+    want_q = (hv % np.uint64(H)) % np.uint64(Q)
+    np.testing.assert_array_equal(c.cpu().numpy().view(np.uint64),
+                                  np.bincount(want_q.astype(np.int64), minlength=Q).astype(np.uint64))
