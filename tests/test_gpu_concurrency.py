@@ -46,6 +46,12 @@ def _frame(tup):
                          "dst_port": (tup[:, 2] & 0xFFFF).astype(np.int64)})
 
 
+def _assert_counts(c, want):
+    """Counts are min(H, Q) long (queue_modulus): the oracle's Q-long vector is zero past it."""
+    np.testing.assert_array_equal(c, want[:len(c)])
+    assert not want[len(c):].any()
+
+
 def _jobs(oracle_lib, key):
     """(kind, args, expected) work items, expected results computed up front (serially)."""
     jobs = []
@@ -79,7 +85,7 @@ def _run_job(job, key, tz):
         h, q, c = tz.compute_queues(t, H, Q)
         np.testing.assert_array_equal(h, want[0])
         np.testing.assert_array_equal(q, want[1])
-        np.testing.assert_array_equal(c, want[2])
+        _assert_counts(c, want[2])
     else:
         sim = Simulator(key, 128, 24)
         sim.load_frame(_frame(args))
@@ -119,7 +125,7 @@ def test_eight_threads_grow_a_fresh_context(native, oracle_lib, example_key):
         h, q, c = ctx.hash(key, t, H, Q)
         np.testing.assert_array_equal(h, want[0])
         np.testing.assert_array_equal(q, want[1])
-        np.testing.assert_array_equal(c, want[2])
+        _assert_counts(c, want[2])
         return len(t)
 
     with cf.ThreadPoolExecutor(THREADS) as pool:
