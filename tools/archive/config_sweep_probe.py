@@ -6,6 +6,10 @@ run the Q <= H kernel.  For Q > 8192 the round-2 narrow range passes (RSS_WIDE_H
 timed beside the wide pass; the 12-bit tables (RSS_SMALL_LUT=0: 16384 queues in the
 hash pass) beside the small tables (up to 80572 in u16 bins, 161144 in u8) for Q > 8192.  ``many`` as the argument: the Q > 8192 rows
 only.  Prints one JSON line per configuration."""
+raise SystemExit("archived (round 5): this A/B probe set RSS_* environment switches that the "
+                 "product library no longer reads, so every variant would time the default "
+                 "path; the alternatives are reachable through tests/hooks.py only")
+
 import json
 import os
 import sys

@@ -5,6 +5,10 @@ launches after 5 warm ones, three alternating rounds, best kept.  Run it once pe
 (RSS_TOEPLITZ_LIB) to compare builds on one box.  One JSON line per Q.
 
 usage: python tools/fullout_ab.py [Q ...]"""
+raise SystemExit("archived (round 5): this A/B probe set RSS_* environment switches that the "
+                 "product library no longer reads, so every variant would time the default "
+                 "path; the alternatives are reachable through tests/hooks.py only")
+
 import json
 import os
 import sys

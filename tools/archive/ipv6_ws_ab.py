@@ -7,6 +7,10 @@ hash u32 + queue u8 + counts = 41 B per tuple.  Each variant: 20 warm launches, 
 event pair around 40 launches; the variants alternate for ``ROUNDS`` rounds.  Prints one JSON
 line.  usage: python tools/ipv6_ws_ab.py [ROUNDS]
 """
+raise SystemExit("archived (round 5): this A/B probe set RSS_* environment switches that the "
+                 "product library no longer reads, so every variant would time the default "
+                 "path; the alternatives are reachable through tests/hooks.py only")
+
 import json
 import os
 import sys

@@ -5,6 +5,10 @@ product): 2^28 uniform tuples, H = 2^30, full outputs (hash u32 + queue u32) and
 three alternating rounds, medians of 10 launches after 5 warm ones.  One JSON line per Q.
 
 usage: python tools/prefetch_ab.py [Q ...]"""
+raise SystemExit("archived (round 5): this A/B probe set RSS_* environment switches that the "
+                 "product library no longer reads, so every variant would time the default "
+                 "path; the alternatives are reachable through tests/hooks.py only")
+
 import json
 import os
 import sys

@@ -6,6 +6,10 @@ a batch that wraps a u8 bin costs); `column` = counts only through a scratch que
 instead of residual lists (RSS_RESID=0).  Prints one JSON line per Q.
 
 usage: python tools/range8_probe.py [Q ...]"""
+raise SystemExit("archived (round 5): this A/B probe set RSS_* environment switches that the "
+                 "product library no longer reads, so every variant would time the default "
+                 "path; the alternatives are reachable through tests/hooks.py only")
+
 import json
 import os
 import sys

@@ -5,6 +5,10 @@ prefetch), the lists on the static walk (RSS_PREFETCH=0) and the scratch column 
 One JSON line per Q.
 
 usage: python tools/resid_probe.py [Q ...]"""
+raise SystemExit("archived (round 5): this A/B probe set RSS_* environment switches that the "
+                 "product library no longer reads, so every variant would time the default "
+                 "path; the alternatives are reachable through tests/hooks.py only")
+
 import json
 import os
 import sys

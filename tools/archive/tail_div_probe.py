@@ -5,6 +5,10 @@ the many-queues full-output launch (H = 2^30, Q = 131072, hash u32 + queue u32);
 uniform tuples, medians of 10 launches after 5 warm ones, three alternating rounds, best kept.
 
 usage: python tools/tail_div_probe.py [div ...]"""
+raise SystemExit("archived (round 5): this A/B probe set RSS_* environment switches that the "
+                 "product library no longer reads, so every variant would time the default "
+                 "path; the alternatives are reachable through tests/hooks.py only")
+
 import json
 import os
 import sys

@@ -8,6 +8,10 @@ counts-only form; variants alternate in blocks of 50 launches.
 
     python tools/ws_fold_ab.py [rounds]
 """
+raise SystemExit("archived (round 5): this A/B probe set RSS_* environment switches that the "
+                 "product library no longer reads, so every variant would time the default "
+                 "path; the alternatives are reachable through tests/hooks.py only")
+
 import json
 import os
 import statistics

@@ -6,6 +6,10 @@ rss_hash_device_ws over 2^28 tuples, H=128, Q=24, u8 queues.
 
     python tools/ws_order_ab.py [rounds]
 """
+raise SystemExit("archived (round 5): this A/B probe set RSS_* environment switches that the "
+                 "product library no longer reads, so every variant would time the default "
+                 "path; the alternatives are reachable through tests/hooks.py only")
+
 import json
 import os
 import statistics
