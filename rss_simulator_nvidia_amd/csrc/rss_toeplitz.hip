@@ -1,4 +1,5 @@
-// rss_toeplitz.hip -- CDNA4 (gfx950) RSS Toeplitz engine: kernels + C ABI.
+// rss_toeplitz.hip -- CDNA4 (gfx950) RSS Toeplitz engine: the kernels and their launchers
+// (the C ABI and the host pipeline around them: rss_host.hip, through rss_engine.h).
 //
 // Hot path replaced (reference noamsto/rss_simulator_nvidia v0.0.2):
 //   Toeplitz.compute_hash            rss_simulator/toeplitz.py:46-69
@@ -32,35 +33,11 @@
 #include <thread>
 #include <vector>
 
+#include "rss_engine.h"
 #include "rss_internal.h"
 #include "rss_toeplitz.h"
 
 namespace {
-thread_local std::string g_last_error;
-}  // namespace
-
-int rss_set_error(int code, const char* fmt, ...) {
-    char buf[512];
-    va_list ap;
-    va_start(ap, fmt);
-    vsnprintf(buf, sizeof buf, fmt, ap);
-    va_end(ap);
-    g_last_error = buf;
-    return code;
-}
-
-namespace {
-
-// ---------------------------------------------------------------- errors ----
-#define set_error rss_set_error
-
-#define RSS_HIP_CHECK(expr)                                                        \
-    do {                                                                           \
-        hipError_t e_ = (expr);                                                    \
-        if (e_ != hipSuccess)                                                      \
-            return set_error(e_ == hipErrorOutOfMemory ? RSS_ENOMEM : RSS_EIO,     \
-                             "%s failed: %s", #expr, hipGetErrorString(e_));       \
-    } while (0)
 
 // ------------------------------------------------------------ constants -----
 constexpr int kBlock = 1024;            // threads per workgroup (16 waves)
@@ -2947,632 +2924,46 @@ int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint
     return RSS_OK;
 }
 
-// window remap for field selection over a tuple of `nfields` fields
-void remap_windows(uint32_t* window, int nbits, const int* start, const int* width, int nfields,
-                   uint32_t fields) {
-    std::vector<uint32_t> out(nbits, 0);
-    int pos = 0;
-    for (int f = 0; f < nfields; ++f) {
-        if (!(fields & (1u << f))) continue;
-        for (int b = 0; b < width[f]; ++b) out[start[f] + b] = window[pos + b];
-        pos += width[f];
-    }
-    memcpy(window, out.data(), sizeof(uint32_t) * nbits);
-}
-
-void rotation_windows(const uint8_t* key, size_t len, uint32_t* window, int nbits) {
-    // after i one-bit rotations of the whole key (toeplitz.py:83-98) its leftmost 32 bits
-    // are key bits (i + j) mod 8*len, j = 0..31
-    const uint64_t kbits = (uint64_t)len * 8;
-    for (int i = 0; i < nbits; ++i) {
-        uint32_t w = 0;
-        for (int j = 0; j < 32; ++j) {
-            const uint64_t b = ((uint64_t)i + j) % kbits;
-            w = (w << 1) | ((key[b >> 3] >> (7 - (b & 7))) & 1u);
-        }
-        window[i] = w;
-    }
-}
-
 }  // namespace
 
-// ------------------------------------------------------------ C ABI ---------
-// (struct rss_ctx: rss_internal.h)
+// ---------------------------------------------------- launchers (rss_engine.h) --
+// What the C ABI (rss_host.hip) calls; the launch logic above stays internal to this file.
+namespace rss {
 
-extern "C" {
-
-int rss_abi_version(void) { return RSS_ABI_VERSION; }
-
-const char* rss_last_error(void) { return g_last_error.c_str(); }
-
-int rss_key_prepare(const uint8_t* key, size_t len, rss_key* out) {
-    if (!key || !out) return set_error(RSS_EINVAL, "rss_key_prepare: NULL argument");
-    if (len < RSS_KEY_MIN_BYTES)
-        return set_error(RSS_EINVAL, "rss_key_prepare: key must hold >= %d bytes, got %zu",
-                         RSS_KEY_MIN_BYTES, len);
-    memset(out, 0, sizeof *out);
-    out->len = (uint32_t)len;
-    memcpy(out->bytes, key, len < RSS_KEY_MAX_BYTES ? len : RSS_KEY_MAX_BYTES);
-    // For len >= 16 bytes the rotation never wraps and only bytes 0..15 matter.
-    rotation_windows(key, len, out->window, RSS_INPUT_BITS);
-    return RSS_OK;
+int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32_t htable,
+                uint32_t nqueues, uint32_t* d_hash, void* d_queue, uint64_t* d_counts,
+                uint32_t flags, hipStream_t stream, const uint32_t* reta, uint64_t* ws) {
+    return ::launch_hash(key, d_tuples, n, htable, nqueues, d_hash, d_queue, d_counts, flags,
+                         stream, reta, ws);
 }
 
-int rss_key_select_fields(rss_key* key, uint32_t fields) {
-    if (!key || key->len < RSS_KEY_MIN_BYTES)
-        return set_error(RSS_EINVAL, "rss_key_select_fields: key not prepared");
-    if (fields == 0 || (fields & ~RSS_FIELDS_ALL))
-        return set_error(RSS_EINVAL, "rss_key_select_fields: bad field mask 0x%x", fields);
-    // field f spans input bits [start[f], start[f] + width[f]) of the full tuple
-    static const int kStart[4] = {0, 32, 64, 80}, kWidth[4] = {32, 32, 16, 16};
-    remap_windows(key->window, RSS_INPUT_BITS, kStart, kWidth, 4, fields);
-    return RSS_OK;
+int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint32_t htable,
+                 uint32_t nqueues, uint32_t* d_hash, void* d_queue, uint64_t* d_counts,
+                 uint32_t flags, hipStream_t stream, const uint32_t* reta, uint64_t* ws) {
+    return ::launch_hash6(key, d_tuples, n, htable, nqueues, d_hash, d_queue, d_counts, flags,
+                          stream, reta, ws);
 }
 
-int rss_key6_prepare(const uint8_t* key, size_t len, rss_key6* out) {
-    if (!key || !out) return set_error(RSS_EINVAL, "rss_key6_prepare: NULL argument");
-    if (len < RSS_KEY_MIN_BYTES)
-        return set_error(RSS_EINVAL, "rss_key6_prepare: key must hold >= %d bytes, got %zu",
-                         RSS_KEY_MIN_BYTES, len);
-    memset(out, 0, sizeof *out);
-    out->len = (uint32_t)len;
-    rotation_windows(key, len, out->window, RSS_INPUT6_BITS);
-    return RSS_OK;
+int launch_search(const uint32_t* d_windows, size_t nkeys, const rss_tuple4* d_tuples, size_t n,
+                  uint32_t htable, uint32_t nqueues, uint64_t* d_counts, hipStream_t stream) {
+    return ::launch_search(d_windows, nkeys, d_tuples, n, htable, nqueues, d_counts, stream);
 }
 
-int rss_key6_select_fields(rss_key6* key, uint32_t fields) {
-    if (!key || key->len < RSS_KEY_MIN_BYTES)
-        return set_error(RSS_EINVAL, "rss_key6_select_fields: key not prepared");
-    if (fields == 0 || (fields & ~RSS_FIELDS_ALL))
-        return set_error(RSS_EINVAL, "rss_key6_select_fields: bad field mask 0x%x", fields);
-    static const int kStart[4] = {0, 128, 256, 272}, kWidth[4] = {128, 128, 16, 16};
-    remap_windows(key->window, RSS_INPUT6_BITS, kStart, kWidth, 4, fields);
-    return RSS_OK;
-}
-
-int rss_hash6_device(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint32_t htable,
-                     uint32_t nqueues, uint32_t* d_hash, void* d_queue, uint64_t* d_counts,
-                     uint32_t flags, void* stream) {
-    return launch_hash6(key, d_tuples, n, htable, nqueues, d_hash, d_queue, d_counts, flags,
-                        static_cast<hipStream_t>(stream));
-}
-
-int rss_hash6_device_ws(const rss_key6* key, const rss_tuple6* d_tuples, size_t n,
-                        uint32_t htable, uint32_t nqueues, uint32_t* d_hash, void* d_queue,
-                        uint64_t* d_counts, uint32_t flags, uint64_t* d_workspace, void* stream) {
-    if (d_counts && (!d_workspace || ((uintptr_t)d_workspace & 7u)))
-        return set_error(RSS_EINVAL, "rss_hash6_device_ws: workspace NULL or not 8-byte aligned");
-    return launch_hash6(key, d_tuples, n, htable, nqueues, d_hash, d_queue, d_counts, flags,
-                        static_cast<hipStream_t>(stream), nullptr, d_workspace);
-}
-
-int rss_hash6_device_reta(const rss_key6* key, const rss_tuple6* d_tuples, size_t n,
-                          uint32_t htable, const uint32_t* reta, uint32_t nqueues,
-                          uint32_t* d_hash, void* d_queue, uint64_t* d_counts, uint32_t flags,
-                          void* stream) {
-    if (!reta) return set_error(RSS_EINVAL, "rss_hash6_device_reta: reta is NULL");
-    return launch_hash6(key, d_tuples, n, htable, nqueues, d_hash, d_queue, d_counts, flags,
-                        static_cast<hipStream_t>(stream), reta);
-}
-
-static int hash6_host_impl(rss_ctx* ctx, const rss_key6* key, const rss_tuple6* h_tuples, size_t n,
-                           uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
-                           uint64_t* h_counts, uint32_t flags, const uint32_t* reta);
-
-int rss_hash6_host(rss_ctx* ctx, const rss_key6* key, const rss_tuple6* h_tuples, size_t n,
-                   uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
-                   uint64_t* h_counts, uint32_t flags) {
-    return hash6_host_impl(ctx, key, h_tuples, n, htable, nqueues, h_hash, h_queue, h_counts,
-                           flags, nullptr);
-}
-
-int rss_hash6_host_reta(rss_ctx* ctx, const rss_key6* key, const rss_tuple6* h_tuples, size_t n,
-                        uint32_t htable, const uint32_t* reta, uint32_t nqueues, uint32_t* h_hash,
-                        uint32_t* h_queue, uint64_t* h_counts, uint32_t flags) {
-    if (!reta) return set_error(RSS_EINVAL, "rss_hash6_host_reta: reta is NULL");
-    return hash6_host_impl(ctx, key, h_tuples, n, htable, nqueues, h_hash, h_queue, h_counts,
-                           flags, reta);
-}
-
-static int hash6_host_impl(rss_ctx* ctx, const rss_key6* key, const rss_tuple6* h_tuples, size_t n,
-                           uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
-                           uint64_t* h_counts, uint32_t flags, const uint32_t* reta) {
-    if (!ctx) return set_error(RSS_EINVAL, "rss_hash6_host: ctx is NULL");
-    if (n && !h_tuples) return set_error(RSS_EINVAL, "rss_hash6_host: tuples is NULL");
-    std::lock_guard<std::mutex> lock(ctx->mu);  // (struct rss_ctx)
-    RSS_HIP_CHECK(hipSetDevice(ctx->device));
-    hipStream_t s = ctx->stream[0];
-    rss_tuple6* d_t = nullptr;
-    uint32_t *d_h = nullptr, *d_q = nullptr;
-    uint64_t* d_c = nullptr;
-    auto cleanup = [&] {
-        (void)hipFree(d_t);
-        (void)hipFree(d_h);
-        (void)hipFree(d_q);
-        (void)hipFree(d_c);
-    };
-    hipError_t e = hipSuccess;
-    if (n) e = hipMalloc(&d_t, n * sizeof(rss_tuple6));
-    if (e == hipSuccess && n && h_hash) e = hipMalloc(&d_h, n * 4);
-    if (e == hipSuccess && n && h_queue) e = hipMalloc(&d_q, n * 4);
-    if (e == hipSuccess && h_counts) e = hipMalloc(&d_c, nqueues * 8);
-    if (e == hipSuccess && n)
-        e = hipMemcpyAsync(d_t, h_tuples, n * sizeof(rss_tuple6), hipMemcpyHostToDevice, s);
-    if (e != hipSuccess) {
-        cleanup();
-        return set_error(e == hipErrorOutOfMemory ? RSS_ENOMEM : RSS_EIO, "rss_hash6_host: %s",
-                         hipGetErrorString(e));
-    }
-    int rc = launch_hash6(key, d_t, n, htable, nqueues, d_h, d_q, d_c,
-                          0u, s, reta);  // device counts start at 0; accumulation on the host
-    if (rc == RSS_OK) {
-        if (d_h) e = hipMemcpyAsync(h_hash, d_h, n * 4, hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess && d_q) e = hipMemcpyAsync(h_queue, d_q, n * 4, hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess && d_c) {
-            std::vector<uint64_t> tmp(nqueues);
-            e = hipMemcpyAsync(tmp.data(), d_c, nqueues * 8, hipMemcpyDeviceToHost, s);
-            if (e == hipSuccess) e = hipStreamSynchronize(s);
-            if (e == hipSuccess)
-                for (uint32_t q = 0; q < nqueues; ++q)
-                    h_counts[q] = (flags & RSS_FLAG_ACCUMULATE ? h_counts[q] : 0) + tmp[q];
-        }
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess) rc = set_error(RSS_EIO, "rss_hash6_host: %s", hipGetErrorString(e));
-    }
-    cleanup();
-    return rc;
-}
-
-int rss_device_count(int* out) {
-    if (!out) return set_error(RSS_EINVAL, "rss_device_count: NULL argument");
-    *out = 0;
-    int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess) {
-        (void)hipGetLastError();
-        return RSS_OK;
-    }
-    int count = 0;
-    for (int d = 0; d < n; ++d) {
-        hipDeviceProp_t prop;
-        if (hipGetDeviceProperties(&prop, d) != hipSuccess) continue;
-        if (strncmp(prop.gcnArchName, "gfx950", 6) == 0) ++count;
-    }
-    *out = count;
-    return RSS_OK;
-}
-
-int rss_hash_device(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32_t htable,
-                    uint32_t nqueues, uint32_t* d_hash, void* d_queue, uint64_t* d_counts,
-                    uint32_t flags, void* stream) {
-    return launch_hash(key, d_tuples, n, htable, nqueues, d_hash, d_queue, d_counts, flags,
-                       static_cast<hipStream_t>(stream));
-}
-
-int rss_counts_workspace_bytes(uint32_t nqueues, size_t* out) {
-    if (!out) return set_error(RSS_EINVAL, "rss_counts_workspace_bytes: NULL argument");
-    if (nqueues < 1) return set_error(RSS_EINVAL, "rss_counts_workspace_bytes: nqueues must be >= 1");
-    // a reserved word (ws[0], the rounds 2-3 fold's ticket; the size is ABI) + one arrival
-    // accumulator per queue + the balanced tail's unit counter (fold_counts, walk_rows)
-    *out = sizeof(uint64_t) * ((size_t)nqueues + 2);
-    return RSS_OK;
-}
-
-int rss_hash_device_ws(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32_t htable,
-                       uint32_t nqueues, uint32_t* d_hash, void* d_queue, uint64_t* d_counts,
-                       uint32_t flags, uint64_t* d_workspace, void* stream) {
-    if (d_counts && (!d_workspace || ((uintptr_t)d_workspace & 7u)))
-        return set_error(RSS_EINVAL, "rss_hash_device_ws: workspace NULL or not 8-byte aligned");
-    return launch_hash(key, d_tuples, n, htable, nqueues, d_hash, d_queue, d_counts, flags,
-                       static_cast<hipStream_t>(stream), nullptr, d_workspace);
-}
-
-int rss_hash_device_reta(const rss_key* key, const rss_tuple4* d_tuples, size_t n,
-                         uint32_t htable, const uint32_t* reta, uint32_t nqueues, uint32_t* d_hash,
-                         void* d_queue, uint64_t* d_counts, uint32_t flags, void* stream) {
-    if (!reta) return set_error(RSS_EINVAL, "rss_hash_device_reta: reta is NULL");
-    return launch_hash(key, d_tuples, n, htable, nqueues, d_hash, d_queue, d_counts, flags,
-                       static_cast<hipStream_t>(stream), reta);
-}
-
-int rss_key_search_device(const uint32_t* d_windows, size_t nkeys, const rss_tuple4* d_tuples,
-                          size_t n, uint32_t htable, uint32_t nqueues, uint64_t* d_counts,
-                          void* stream) {
-    return launch_search(d_windows, nkeys, d_tuples, n, htable, nqueues, d_counts,
-                         static_cast<hipStream_t>(stream));
-}
-
-int rss_generate_tuples(uint64_t seed, uint64_t first_index, size_t n, rss_tuple4* d_tuples,
-                        void* stream) {
-    if (n == 0) return RSS_OK;
-    if (!d_tuples) return set_error(RSS_EINVAL, "rss_generate_tuples: tuples is NULL");
+int launch_generate(uint64_t seed, uint64_t first_index, size_t n, rss_tuple4* d_tuples,
+                    hipStream_t stream) {
     DeviceInfo info;
     int rc = device_info(&info);
     if (rc) return rc;
     const uint64_t want = (n + 255) / 256;
     const uint64_t cap = (uint64_t)info.cu_count * 8;
     const unsigned grid = (unsigned)(want < cap ? want : cap);
-    hipLaunchKernelGGL(rss_generate_kernel, dim3(grid), dim3(256), 0,
-                       static_cast<hipStream_t>(stream), seed, first_index, (uint64_t)n,
-                       reinterpret_cast<uint32_t*>(d_tuples));
+    hipLaunchKernelGGL(rss_generate_kernel, dim3(grid), dim3(256), 0, stream, seed, first_index,
+                       (uint64_t)n, reinterpret_cast<uint32_t*>(d_tuples));
     RSS_HIP_CHECK(hipGetLastError());
     return RSS_OK;
 }
 
-void rss_ctx_destroy(rss_ctx* ctx) {
-    if (!ctx) return;
-    (void)hipSetDevice(ctx->device);
-    rss_csv_release(ctx);
-    for (int b = 0; b < 2; ++b) {
-        if (ctx->stream[b]) (void)hipStreamSynchronize(ctx->stream[b]);
-        (void)hipFree(ctx->d_in[b]);
-        (void)hipFree(ctx->d_hash[b]);
-        (void)hipFree(ctx->d_queue[b]);
-        (void)hipFree(ctx->d_counts[b]);
-        (void)hipHostFree(ctx->h_in[b]);
-        (void)hipHostFree(ctx->h_hash[b]);
-        (void)hipHostFree(ctx->h_queue[b]);
-        if (ctx->stream[b]) (void)hipStreamDestroy(ctx->stream[b]);
-    }
-    (void)hipHostFree(ctx->h_counts);
-    delete ctx;
-}
-
-int rss_ctx_create(int device, rss_ctx** out) {
-    if (!out) return set_error(RSS_EINVAL, "rss_ctx_create: NULL argument");
-    *out = nullptr;
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
-        (void)hipGetLastError();
-        return set_error(RSS_ENODEV, "rss_ctx_create: no HIP device visible");
-    }
-    if (device < 0 || device >= ndev)
-        return set_error(RSS_EINVAL, "rss_ctx_create: device %d out of range [0, %d)", device, ndev);
-    hipDeviceProp_t prop;
-    RSS_HIP_CHECK(hipGetDeviceProperties(&prop, device));
-    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
-        return set_error(RSS_ENODEV, "rss_ctx_create: device %d is %s, this build targets gfx950",
-                         device, prop.gcnArchName);
-    rss_ctx* ctx = new rss_ctx();
-    ctx->device = device;
-    hipError_t e = hipSetDevice(device);
-    for (int b = 0; b < 2 && e == hipSuccess; ++b)
-        e = hipStreamCreateWithFlags(&ctx->stream[b], hipStreamNonBlocking);
-    if (e != hipSuccess) {
-        rss_ctx_destroy(ctx);
-        return set_error(RSS_EIO, "rss_ctx_create: %s", hipGetErrorString(e));
-    }
-    *out = ctx;
-    return RSS_OK;
-}
-
-static int ctx_reserve(rss_ctx* ctx, size_t chunk, uint32_t nqueues) {
-    if (ctx->chunk < chunk) {
-        for (int b = 0; b < 2; ++b) {
-            (void)hipFree(ctx->d_in[b]);
-            (void)hipFree(ctx->d_hash[b]);
-            (void)hipFree(ctx->d_queue[b]);
-            (void)hipHostFree(ctx->h_in[b]);
-            (void)hipHostFree(ctx->h_hash[b]);
-            (void)hipHostFree(ctx->h_queue[b]);
-            ctx->d_in[b] = nullptr;
-            ctx->d_hash[b] = ctx->d_queue[b] = nullptr;
-            ctx->h_in[b] = nullptr;
-            ctx->h_hash[b] = ctx->h_queue[b] = nullptr;
-        }
-        ctx->chunk = 0;
-        for (int b = 0; b < 2; ++b) {
-            RSS_HIP_CHECK(hipMalloc(&ctx->d_in[b], chunk * sizeof(rss_tuple4)));
-            RSS_HIP_CHECK(hipMalloc(&ctx->d_hash[b], chunk * sizeof(uint32_t)));
-            RSS_HIP_CHECK(hipMalloc(&ctx->d_queue[b], chunk * sizeof(uint32_t)));
-            RSS_HIP_CHECK(hipHostMalloc(&ctx->h_in[b], chunk * sizeof(rss_tuple4), hipHostMallocDefault));
-            RSS_HIP_CHECK(hipHostMalloc(&ctx->h_hash[b], chunk * sizeof(uint32_t), hipHostMallocDefault));
-            RSS_HIP_CHECK(hipHostMalloc(&ctx->h_queue[b], chunk * sizeof(uint32_t), hipHostMallocDefault));
-        }
-        RSS_HIP_CHECK(hipHostGetDevicePointer(&ctx->alias_in, ctx->h_in[0], 0));
-        RSS_HIP_CHECK(hipHostGetDevicePointer(&ctx->alias_hash, ctx->h_hash[0], 0));
-        RSS_HIP_CHECK(hipHostGetDevicePointer(&ctx->alias_queue, ctx->h_queue[0], 0));
-        ctx->chunk = chunk;
-    }
-    if (ctx->counts_cap < nqueues) {
-        for (int b = 0; b < 2; ++b) {
-            (void)hipFree(ctx->d_counts[b]);
-            ctx->d_counts[b] = nullptr;
-        }
-        (void)hipHostFree(ctx->h_counts);
-        ctx->h_counts = nullptr;
-        ctx->counts_cap = 0;
-        for (int b = 0; b < 2; ++b)
-            RSS_HIP_CHECK(hipMalloc(&ctx->d_counts[b], sizeof(uint64_t) * nqueues));
-        RSS_HIP_CHECK(hipHostMalloc(&ctx->h_counts, sizeof(uint64_t) * nqueues, hipHostMallocDefault));
-        ctx->counts_cap = nqueues;
-    }
-    return RSS_OK;
-}
-
-// Small host batches -- a reference-style caller hashing one row per call
-// (Toeplitz.compute_hash from Simulator.__calc_entry_hash, simulator.py:80-92) -- are
-// bound by per-call overhead, not bytes: one stream, no pointer-attribute queries, the
-// kernel reading the tuples from and writing hash / queue straight into slot 0's pinned
-// staging (mapped into the device address space), the counts landing in pinned memory,
-// one synchronisation.  Same kernel and results as the pipelined path.
-constexpr size_t kSmallBatch = (size_t)1 << 14;
-
-static int hash_host_small(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples, size_t n,
-                           uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
-                           uint64_t* h_counts, uint32_t flags, const uint32_t* reta) {
-    int rc = ctx_reserve(ctx, std::max(ctx->chunk, kSmallBatch), h_counts ? nqueues : 1);
-    if (rc) return rc;
-    hipStream_t s = ctx->stream[0];
-    memcpy(ctx->h_in[0], h_tuples, n * sizeof(rss_tuple4));
-    rc = launch_hash(key, static_cast<const rss_tuple4*>(ctx->alias_in), n, htable, nqueues,
-                     h_hash ? static_cast<uint32_t*>(ctx->alias_hash) : nullptr,
-                     h_queue ? ctx->alias_queue : nullptr, h_counts ? ctx->d_counts[0] : nullptr,
-                     0, s, reta);
-    if (rc) return rc;
-    if (h_counts)
-        RSS_HIP_CHECK(hipMemcpyAsync(ctx->h_counts, ctx->d_counts[0], sizeof(uint64_t) * nqueues,
-                                     hipMemcpyDeviceToHost, s));
-    RSS_HIP_CHECK(hipStreamSynchronize(s));
-    if (h_hash) memcpy(h_hash, ctx->h_hash[0], n * 4);
-    if (h_queue) memcpy(h_queue, ctx->h_queue[0], n * 4);
-    if (h_counts) {
-        if (!(flags & RSS_FLAG_ACCUMULATE)) memset(h_counts, 0, sizeof(uint64_t) * nqueues);
-        for (uint32_t q = 0; q < nqueues; ++q) h_counts[q] += ctx->h_counts[q];
-    }
-    return RSS_OK;
-}
-
-static int hash_host_impl(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples, size_t n,
-                          uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
-                          uint64_t* h_counts, uint32_t flags, const uint32_t* reta);
-
-int rss_hash_host(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples, size_t n,
-                  uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
-                  uint64_t* h_counts, uint32_t flags) {
-    return hash_host_impl(ctx, key, h_tuples, n, htable, nqueues, h_hash, h_queue, h_counts, flags,
-                          nullptr);
-}
-
-int rss_hash_host_reta(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples, size_t n,
-                       uint32_t htable, const uint32_t* reta, uint32_t nqueues, uint32_t* h_hash,
-                       uint32_t* h_queue, uint64_t* h_counts, uint32_t flags) {
-    if (!reta) return set_error(RSS_EINVAL, "rss_hash_host_reta: reta is NULL");
-    return hash_host_impl(ctx, key, h_tuples, n, htable, nqueues, h_hash, h_queue, h_counts, flags,
-                          reta);
-}
-
-int rss_hash_host_multi(rss_ctx* const* ctxs, int nctx, const rss_key* key,
-                        const rss_tuple4* h_tuples, size_t n, uint32_t htable,
-                        const uint32_t* reta, uint32_t nqueues, uint32_t* h_hash,
-                        uint32_t* h_queue, uint64_t* h_counts, uint32_t flags) {
-    if (!ctxs || nctx < 1 || !key)
-        return set_error(RSS_EINVAL, "rss_hash_host_multi: NULL argument or no contexts");
-    for (int i = 0; i < nctx; ++i) {
-        if (!ctxs[i]) return set_error(RSS_EINVAL, "rss_hash_host_multi: context %d is NULL", i);
-        for (int j = 0; j < i; ++j)
-            if (ctxs[j] == ctxs[i])
-                return set_error(RSS_EINVAL, "rss_hash_host_multi: contexts %d and %d are the same",
-                                 j, i);
-    }
-    if (n && !h_tuples) return set_error(RSS_EINVAL, "rss_hash_host_multi: tuples is NULL");
-    if (htable < 1 || nqueues < 1)
-        return set_error(RSS_EINVAL, "rss_hash_host_multi: htable (%u) and nqueues (%u) must be >= 1",
-                         htable, nqueues);
-    // contiguous ranges, exactly sharding.shard_range's: n / nctx each, the first n % nctx
-    // ranges one longer
-    const size_t base = n / (size_t)nctx, extra = n % (size_t)nctx;
-    std::vector<std::vector<uint64_t>> part(nctx, std::vector<uint64_t>(h_counts ? nqueues : 0));
-    std::vector<int> rcs(nctx, RSS_OK);
-    std::vector<std::string> errs(nctx);
-    auto work = [&](int i) {
-        const size_t a = base * (size_t)i + std::min((size_t)i, extra);
-        const size_t b = a + base + ((size_t)i < extra ? 1 : 0);
-        const int rc = hash_host_impl(ctxs[i], key, h_tuples ? h_tuples + a : nullptr, b - a, htable,
-                                      nqueues, h_hash ? h_hash + a : nullptr,
-                                      h_queue ? h_queue + a : nullptr,
-                                      h_counts ? part[i].data() : nullptr, 0, reta);
-        if (rc) {
-            rcs[i] = rc;
-            errs[i] = g_last_error;  // thread-local: carried back to the calling thread
-        }
-    };
-    std::vector<std::thread> pool;
-    for (int i = 1; i < nctx; ++i) pool.emplace_back(work, i);
-    work(0);
-    for (auto& t : pool) t.join();
-    for (int i = 0; i < nctx; ++i)
-        if (rcs[i]) return set_error(rcs[i], "rss_hash_host_multi: context %d: %s", i, errs[i].c_str());
-    if (h_counts) {
-        if (!(flags & RSS_FLAG_ACCUMULATE)) memset(h_counts, 0, sizeof(uint64_t) * nqueues);
-        for (int i = 0; i < nctx; ++i)
-            for (uint32_t q = 0; q < nqueues; ++q) h_counts[q] += part[i][q];
-    }
-    return RSS_OK;
-}
-
-// memcpy split over up to 8 threads: the pinned staging copies, not PCIe or the kernel,
-// bound rss_hash_host (one thread moves ~10 GB/s; a 4M-tuple slot is 80 MB each way)
-static void par_memcpy(void* dst, const void* src, size_t bytes) {
-    constexpr size_t kPerThread = (size_t)4 << 20;
-    const size_t nt = std::min<size_t>(8, bytes / kPerThread);
-    if (nt <= 1) {
-        memcpy(dst, src, bytes);
-        return;
-    }
-    std::vector<std::thread> pool;
-    for (size_t k = 1; k < nt; ++k)
-        pool.emplace_back([=] {
-            const size_t a = bytes * k / nt, b = bytes * (k + 1) / nt;
-            memcpy(static_cast<char*>(dst) + a, static_cast<const char*>(src) + a, b - a);
-        });
-    memcpy(dst, src, bytes / nt);
-    for (auto& t : pool) t.join();
-}
-
-// Whether [p, p + bytes) is page-locked host memory (rss_host_alloc, hipHostMalloc,
-// hipHostRegister) that the copy engines can read / write directly.
-static bool host_pinned(const void* p, size_t bytes) {
-    if (!p || !bytes) return true;
-    const char* ends[2] = {static_cast<const char*>(p), static_cast<const char*>(p) + bytes - 1};
-    for (const char* q : ends) {
-        hipPointerAttribute_t a;
-        if (hipPointerGetAttributes(&a, q) != hipSuccess) {
-            (void)hipGetLastError();
-            return false;
-        }
-        if (a.type != hipMemoryTypeHost) return false;
-    }
-    return true;
-}
-
-static int hash_host_impl(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples, size_t n,
-                          uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
-                          uint64_t* h_counts, uint32_t flags, const uint32_t* reta) {
-    if (!ctx) return set_error(RSS_EINVAL, "rss_hash_host: ctx is NULL");
-    if (n && !h_tuples) return set_error(RSS_EINVAL, "rss_hash_host: tuples is NULL");
-    if (htable < 1 || nqueues < 1)
-        return set_error(RSS_EINVAL, "rss_hash_host: htable (%u) and nqueues (%u) must be >= 1",
-                         htable, nqueues);
-    std::lock_guard<std::mutex> lock(ctx->mu);  // (struct rss_ctx)
-    RSS_HIP_CHECK(hipSetDevice(ctx->device));
-    if (n > 0 && n <= kSmallBatch)
-        return hash_host_small(ctx, key, h_tuples, n, htable, nqueues, h_hash, h_queue, h_counts,
-                               flags, reta);
-    constexpr size_t kChunkMax = (size_t)1 << 22;  // 4M tuples: 48 MB in + 32 MB out per slot
-    const size_t chunk = n < kChunkMax ? (n ? n : 1) : kChunkMax;
-    int rc = ctx_reserve(ctx, chunk, nqueues);
-    if (rc) return rc;
-    for (int b = 0; b < 2; ++b)
-        RSS_HIP_CHECK(hipMemsetAsync(ctx->d_counts[b], 0, sizeof(uint64_t) * nqueues, ctx->stream[b]));
-
-    // Double-buffered pipeline: while slot b runs H2D -> kernel -> D2H on its
-    // stream, the host fills the other slot's pinned input and drains its output.
-    // Caller buffers that are already page-locked skip the staging copy: the copy
-    // engines move them directly, so only PCIe bounds the pipeline.
-    const bool in_direct = host_pinned(h_tuples, n * sizeof(rss_tuple4));
-    const bool hash_direct = host_pinned(h_hash, h_hash ? n * 4 : 0);
-    const bool queue_direct = host_pinned(h_queue, h_queue ? n * 4 : 0);
-    const size_t nchunks = (n + chunk - 1) / chunk;
-    size_t pending_off[2] = {0, 0}, pending_len[2] = {0, 0};
-    auto drain = [&](int b) -> int {
-        RSS_HIP_CHECK(hipStreamSynchronize(ctx->stream[b]));
-        if (pending_len[b]) {
-            if (h_hash && !hash_direct)
-                par_memcpy(h_hash + pending_off[b], ctx->h_hash[b], pending_len[b] * 4);
-            if (h_queue && !queue_direct)
-                par_memcpy(h_queue + pending_off[b], ctx->h_queue[b], pending_len[b] * 4);
-            pending_len[b] = 0;
-        }
-        return RSS_OK;
-    };
-    for (size_t c = 0; c < nchunks; ++c) {
-        const int b = (int)(c & 1);
-        const size_t off = c * chunk;
-        const size_t len = (n - off) < chunk ? (n - off) : chunk;
-        hipStream_t s = ctx->stream[b];
-        // staged slots are reused only after the host has drained them; direct copies
-        // are ordered behind the slot's previous chunk by the stream itself
-        if (!(in_direct && hash_direct && queue_direct)) {
-            rc = drain(b);
-            if (rc) return rc;
-        }
-        const rss_tuple4* up = h_tuples + off;
-        if (!in_direct) {
-            par_memcpy(ctx->h_in[b], up, len * sizeof(rss_tuple4));
-            up = ctx->h_in[b];
-        }
-        RSS_HIP_CHECK(hipMemcpyAsync(ctx->d_in[b], up, len * sizeof(rss_tuple4),
-                                     hipMemcpyHostToDevice, s));
-        rc = launch_hash(key, ctx->d_in[b], len, htable, nqueues, h_hash ? ctx->d_hash[b] : nullptr,
-                         h_queue ? ctx->d_queue[b] : nullptr, ctx->d_counts[b],
-                         RSS_FLAG_ACCUMULATE, s, reta);  // u32 queues on the host path
-        if (rc) return rc;
-        if (h_hash)
-            RSS_HIP_CHECK(hipMemcpyAsync(hash_direct ? h_hash + off : ctx->h_hash[b],
-                                         ctx->d_hash[b], len * 4, hipMemcpyDeviceToHost, s));
-        if (h_queue)
-            RSS_HIP_CHECK(hipMemcpyAsync(queue_direct ? h_queue + off : ctx->h_queue[b],
-                                         ctx->d_queue[b], len * 4, hipMemcpyDeviceToHost, s));
-        pending_off[b] = off;
-        pending_len[b] = len;
-    }
-    for (int b = 0; b < 2; ++b) {
-        rc = drain(b);
-        if (rc) return rc;
-    }
-    if (h_counts) {
-        std::vector<uint64_t> tmp(nqueues);
-        if (!(flags & RSS_FLAG_ACCUMULATE)) memset(h_counts, 0, sizeof(uint64_t) * nqueues);
-        for (int b = 0; b < 2; ++b) {
-            RSS_HIP_CHECK(hipMemcpy(tmp.data(), ctx->d_counts[b], sizeof(uint64_t) * nqueues,
-                                    hipMemcpyDeviceToHost));
-            for (uint32_t q = 0; q < nqueues; ++q) h_counts[q] += tmp[q];
-        }
-    }
-    return RSS_OK;
-}
-
-int rss_host_alloc(size_t bytes, void** out) {
-    if (!out) return set_error(RSS_EINVAL, "rss_host_alloc: NULL argument");
-    *out = nullptr;
-    RSS_HIP_CHECK(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
-    return RSS_OK;
-}
-
-void rss_host_free(void* p) {
-    if (p) (void)hipHostFree(p);
-}
-
-int rss_key_search_host(rss_ctx* ctx, const rss_key* keys, size_t nkeys,
-                        const rss_tuple4* h_tuples, size_t n, uint32_t htable, uint32_t nqueues,
-                        uint64_t* h_counts) {
-    if (!ctx || !keys || !h_counts || nkeys == 0)
-        return set_error(RSS_EINVAL, "rss_key_search_host: NULL argument or no keys");
-    if (n && !h_tuples) return set_error(RSS_EINVAL, "rss_key_search_host: tuples is NULL");
-    std::lock_guard<std::mutex> lock(ctx->mu);  // (struct rss_ctx)
-    RSS_HIP_CHECK(hipSetDevice(ctx->device));
-    std::vector<uint32_t> windows(nkeys * RSS_INPUT_BITS);
-    for (size_t k = 0; k < nkeys; ++k) {
-        if (keys[k].len < RSS_KEY_MIN_BYTES)
-            return set_error(RSS_EINVAL, "rss_key_search_host: key %zu not prepared", k);
-        memcpy(&windows[k * RSS_INPUT_BITS], keys[k].window, sizeof keys[k].window);
-    }
-    uint32_t* d_w = nullptr;
-    rss_tuple4* d_t = nullptr;
-    uint64_t* d_c = nullptr;
-    hipStream_t s = ctx->stream[0];
-    auto cleanup = [&] {
-        (void)hipFree(d_w);
-        (void)hipFree(d_t);
-        (void)hipFree(d_c);
-    };
-    int rc = RSS_OK;
-    hipError_t e = hipMalloc(&d_w, windows.size() * sizeof(uint32_t));
-    if (e == hipSuccess && n) e = hipMalloc(&d_t, n * sizeof(rss_tuple4));
-    if (e == hipSuccess) e = hipMalloc(&d_c, nkeys * nqueues * sizeof(uint64_t));
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(d_w, windows.data(), windows.size() * sizeof(uint32_t),
-                           hipMemcpyHostToDevice, s);
-    if (e == hipSuccess && n)
-        e = hipMemcpyAsync(d_t, h_tuples, n * sizeof(rss_tuple4), hipMemcpyHostToDevice, s);
-    if (e != hipSuccess) {
-        cleanup();
-        return set_error(e == hipErrorOutOfMemory ? RSS_ENOMEM : RSS_EIO, "rss_key_search_host: %s",
-                         hipGetErrorString(e));
-    }
-    rc = launch_search(d_w, nkeys, d_t, n, htable, nqueues, d_c, s);
-    if (rc == RSS_OK) {
-        e = hipMemcpyAsync(h_counts, d_c, nkeys * nqueues * sizeof(uint64_t),
-                           hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess)
-            rc = set_error(RSS_EIO, "rss_key_search_host: %s", hipGetErrorString(e));
-    }
-    cleanup();
-    return rc;
-}
-
-}  // extern "C"
+}  // namespace rss
 
 #ifdef RSS_TEST_HOOKS
 // ------------------------------------------------- test hooks (tests only) --
