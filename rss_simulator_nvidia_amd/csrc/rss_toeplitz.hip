@@ -1,5 +1,8 @@
-// rss_toeplitz.hip -- CDNA4 (gfx950) RSS Toeplitz engine: the kernels and their launchers
-// (the C ABI and the host pipeline around them: rss_host.hip, through rss_engine.h).
+// rss_toeplitz.hip -- CDNA4 (gfx950) RSS Toeplitz engine: the IPv4 and IPv6 hash kernels, the
+// many-queues passes, the counts-only register-table kernel, the synthetic-input generator and
+// their launchers.  Shared device code and launch setup: rss_kernel_common.h; key search:
+// rss_keysearch.hip; the C ABI and the host pipeline around them: rss_host.hip (all three
+// through rss_engine.h).  The only file compiled twice (product, -DRSS_TEST_HOOKS).
 //
 // Hot path replaced (reference noamsto/rss_simulator_nvidia v0.0.2):
 //   Toeplitz.compute_hash            rss_simulator/toeplitz.py:46-69
@@ -14,11 +17,9 @@
 // 12-bit slice of the input selects, 128 KiB, built per workgroup from the 96
 // windows; slices cut field-LSB first so structured flows spread over the LDS
 // banks): 8 ds_read_b32 + ~31 VALU per tuple instead of the reference's 96-step
-// bit-serial loop (XOR trees as three-input v_bitop3).  Key search packs the low
-// bucket bits of 8 (H <= 256) or 4 (H <= 65536) keys, else the full hashes of 2 keys,
-// into each 8-byte table entry (ds_read_b64); IPv6 uses 29 word-aligned 11/11/10-bit
-// and byte tables.  The per-queue histogram is privatised per lane column in LDS and
-// folded into global uint64 counts once per workgroup.
+// bit-serial loop (XOR trees as three-input v_bitop3).  IPv6 uses 29 word-aligned
+// 11/11/10-bit and byte tables.  The per-queue histogram is privatised per lane column in
+// LDS and folded into global uint64 counts once per workgroup.
 // tools/kbench.hip holds the measured design space (4/6/8/12-bit tables).
 #include <hip/hip_runtime.h>
 
@@ -35,593 +36,10 @@
 
 #include "rss_engine.h"
 #include "rss_internal.h"
+#include "rss_kernel_common.h"
 #include "rss_toeplitz.h"
 
 namespace {
-
-// ------------------------------------------------------------ constants -----
-constexpr int kBlock = 1024;            // threads per workgroup (16 waves)
-constexpr int kBlocksPerCU = 1;         // the 128 KiB LUT admits one workgroup per CU
-constexpr int kChunkBits = 12;          // input bits per table lookup
-constexpr int kTables = RSS_INPUT_BITS / kChunkBits;        // 8
-constexpr uint32_t kTableEntries = 1u << kChunkBits;        // 4096
-constexpr uint32_t kLutDwords = kTables * kTableEntries;    // 32768
-constexpr uint32_t kLutBytes = kLutDwords * 4;              // 128 KiB
-constexpr uint32_t kLdsBytes = 160 * 1024;                  // gfx950 LDS per CU
-constexpr uint32_t kBinBytesMax = kLdsBytes - kLutBytes;    // 32 KiB for histogram bins
-constexpr int kBinCols = 32;            // private histogram columns (one per bank)
-static_assert(kLutBytes == 128 * 1024, "LUT layout: 8 tables x 4096 x u32");
-static_assert(kBlock * 4 == (int)kTableEntries, "LUT build maps 4 entries per thread per table");
-
-enum QueueMode { QM_MASK = 0, QM_FAST16 = 1, QM_FAST32 = 2, QM_TABLE = 3, QM_FAST8 = 4 };
-constexpr uint32_t kRetaMax = 1024;  // indirection-table entries carried in the kernarg
-enum HistMode { HIST_PRIVATE = 0, HIST_SHARED = 1, HIST_GLOBAL = 2, HIST_NONE = 3, HIST_RANGE = 4,
-                HIST_RANGE16 = 5, HIST_RANGE8 = 6 };
-// HIST_RANGE8 (IPv4 small-table kernel, past the u16 bins' reach): u8 bins, four per dword, a
-// guard at 0x80 and a poison word for a bin that wraps (range8_guard) -- 161144 queues in the
-// LDS beside the small tables, one pass.
-// HIST_RANGE16 (IPv4 kernel): HIST_RANGE with u16 bins, two per dword, twice the queues in the
-// same LDS -- a guard at 0x8000 and a poison word like HIST_RANGE8's (range16_guard).
-// HIST_RANGE: shared u32 LDS bins for queues [q_lo, q_lo + q_span) only -- the IPv6 kernel's
-// first range of a multi-pass launch for nqueues whose bins do not fit the LDS beside its
-// tables (launch_hash6), instead of one global atomic per tuple (13x slower).
-enum QueueWidth { QW_U32 = 0, QW_U16 = 1, QW_U8 = 2, QW_U16R = 3 };
-// QW_U16R: a counts-only many-queues launch's scratch column (launch_hash): u16 q - q_span for
-// the queues past the hash pass's LDS range [0, q_span), 0xFFFF (never counted) for the rest --
-// half the bytes of a u32 column for the wide pass that counts [q_span, q_eff).
-
-// Everything a launch needs, passed by value in the kernarg segment.
-struct LaunchParams {
-    uint32_t window[RSS_INPUT_BITS];  // rss_key::window
-    const rss_tuple4* tuples;
-    uint32_t* hash_out;
-    void* queue_out;
-    unsigned long long* counts;
-    unsigned long long* ws;       // single-pass counts workspace (rss_hash_device_ws) or NULL
-    uint32_t accumulate;          // with ws: fold mode (kFoldAccumulate)
-    uint64_t n;
-    uint64_t h_m64;     // ceil(2^64 / H) for the non-power-of-two htable path
-    uint32_t h_mask;    // H - 1 when H is a power of two
-    uint32_t H;
-    uint32_t Q;
-    uint32_t q_mask;    // Q - 1 (power of two) or ~0u when Q >= H (identity)
-    uint32_t q_m32;     // ceil(2^32 / Q): exact b % Q for b, Q < 2^16
-    uint32_t nkeys;     // key search: keys in this launch
-    uint64_t q_m64;     // ceil(2^64 / Q): exact b % Q for any 32-bit b, Q
-    uint32_t q_m16;     // ceil(2^16 / Q): exact b % Q for b < 256 (QM_FAST8, packed search)
-    const uint32_t* key_windows;  // key search: nkeys x 96 windows in device memory
-    uint32_t q_lo, q_span;        // HIST_RANGE: the queues this pass counts
-    uint32_t* partial;            // HIST_RANGE16 / RANGE8: u16 / u8 [grid][partial_stride] rows;
-    uint32_t partial_stride;      //   dwords per row
-    uint32_t q_stride;            // key search: row stride of the [keys, nqueues] counts (>= Q)
-    uint32_t tail_rows;           // balanced tail: rows handed out as units (0 = static grid-stride)
-    uint32_t bal_off;             // balanced tail: byte offset of its LDS slot (dynamic LDS)
-    uint32_t* ovf;                // HIST_RANGE16 / RANGE8: u32 [q_span] guard moves (2^15 / 128)
-    uint32_t* poison;             //   set when a bin wrapped (rows and moves discarded)
-    uint32_t fb_span;             // the recount's queues per slice (its u32 bins in the LDS)
-    uint32_t prefetch;            // small-table passes: next group's loads before this group's LDS work
-    unsigned long long* tail_ctr; // balanced tail's unit counter when the launch has no ws (HIST_RANGE8)
-    void* resid_out;              // HIST_RANGE8 counts only: per-wave lists of q - q_span for the
-    uint32_t* resid_counts;       //   tuples past the LDS range (u16 when resid_u16, else u32), wave
-    uint64_t resid_cap;           //   v of workgroup x's at resid_out + (16 x + v) * resid_cap entries,
-    uint32_t resid_u16;           //   its length in resid_counts[16 x + v] (no queue column)
-    uint16_t reta[kRetaMax];      // QM_TABLE: queue of bucket b (ethtool -X indirection)
-};
-
-// ------------------------------------------------------------- device -------
-// LUT: eight tables, each indexed by 12 of the 96 input bits; entry v of table t
-// holds the XOR of the key windows of the input bits set in v -- the reference's
-// inner loop (toeplitz.py:65-68) pre-summed over 12 bits.  Toeplitz is linear in
-// the input bits, so any partition of the 96 bits into tables gives the exact hash.
-// Entry (t, v) lives at LDS byte t*16384 + v*4.  One hash = 8 ds_read_b32 + 7 XOR.
-//
-// Partition (words w0 = src ip, w1 = dst ip, w2 = sport << 16 | dport, bit 0 = LSB):
-//   t0: w0[31:24] | w2[15:12] << 8     t1: w1[31:24] | w2[31:28] << 8
-//   t2: w0[11:0]   t3: w1[11:0]   t4: w0[23:12]   t5: w1[23:12]
-//   t6: w2[11:0] (dport)          t7: w2[27:16] (sport)
-// Every field's least significant bits -- the ones that vary from flow to flow in
-// real traffic (sequential ports, neighbouring hosts) -- are the LOW bits of a table
-// index, i.e. they select the LDS bank ((addr/4) mod 32 for ds_read_b32).  Slicing
-// the MSB-first bit string in order instead puts e.g. sport[7:0] at index bits 4..11:
-// on flow-like input (one IP pair, sequential source ports) every lane of a wave
-// then reads a different entry of ONE bank, a 32-way conflict (measured: 55 % more
-// SQ_LDS_BANK_CONFLICT cycles and 16 % longer counts-only launches than uniform input).
-
-// Input bit (toeplitz.py:65-68 order: 0 = MSB of the source ip) that feeds bit b of
-// table t's index.  Word k bit i is input bit 32k + 31 - i.
-__host__ __device__ constexpr int slice_bit(int t, int b) {
-    return t == 0 ? (b < 8 ? 7 - b : 91 - b)      // w0[24+b] ; w2[4+b]
-         : t == 1 ? (b < 8 ? 39 - b : 75 - b)     // w1[24+b] ; w2[20+b]
-         : t == 2 ? 31 - b                        // w0[b]
-         : t == 3 ? 63 - b                        // w1[b]
-         : t == 4 ? 19 - b                        // w0[12+b]
-         : t == 5 ? 51 - b                        // w1[12+b]
-         : t == 6 ? 95 - b                        // w2[b]
-                  : 79 - b;                       // w2[16+b]
-}
-
-// Build: thread `tid` owns v = hi*1024 + tid (hi = 0..3) of every table: the low
-// ten bits of v are its thread id, so it XORs their windows once per table and
-// derives the four entries from the two top-bit windows.
-__device__ __forceinline__ void build_lut(uint32_t* lut, const uint32_t* __restrict__ window,
-                                          uint32_t tid) {
-#pragma unroll
-    for (int t = 0; t < kTables; ++t) {
-        uint32_t base = 0;
-#pragma unroll
-        for (int b = 0; b < 10; ++b) base ^= ((tid >> b) & 1u) ? window[slice_bit(t, b)] : 0u;
-        const uint32_t w10 = window[slice_bit(t, 10)], w11 = window[slice_bit(t, 11)];
-        uint32_t* dst = lut + t * kTableEntries + tid;
-        dst[0 * kBlock] = base;
-        dst[1 * kBlock] = base ^ w10;
-        dst[2 * kBlock] = base ^ w11;
-        dst[3 * kBlock] = base ^ w10 ^ w11;
-    }
-}
-
-// Byte address of table t's entry for (w0, w1, w2): the index moved to bits 2..13 and
-// masked -- 2 VALU ops for the one-field tables 2..7, 4 for the two-field tables 0..1.
-// Tables 4..7 sit above the 16-bit ds_read immediate, so their base 0x10000 is ORed
-// in by the same v_and_or_b32 from `hi` -- an opaque register holding 0x10000 (a
-// literal would cost a separate v_or).
-template <int kT>
-__device__ __forceinline__ uint32_t chunk_offset(uint32_t w0, uint32_t w1, uint32_t w2,
-                                                 uint32_t hi) {
-    constexpr uint32_t kMask = (kTableEntries - 1) << 2;  // 0x3FFC
-    if constexpr (kT == 0) return ((w0 >> 22) & 0x3FCu) | ((w2 >> 2) & 0x3C00u);
-    if constexpr (kT == 1) return ((w1 >> 22) & 0x3FCu) | ((w2 >> 18) & 0x3C00u);
-    if constexpr (kT == 2) return (w0 << 2) & kMask;
-    if constexpr (kT == 3) return (w1 << 2) & kMask;
-    if constexpr (kT == 4) return ((w0 >> 10) & kMask) | hi;
-    if constexpr (kT == 5) return ((w1 >> 10) & kMask) | hi;
-    if constexpr (kT == 6) return ((w2 << 2) & kMask) | hi;
-    return ((w2 >> 14) & kMask) | hi;
-}
-
-template <int kT>
-__device__ __forceinline__ uint32_t lut_term(const char* lut, uint32_t w0, uint32_t w1, uint32_t w2,
-                                             uint32_t hi) {
-    constexpr uint32_t kImm = (kT & 3) * (kTableEntries * 4);  // fits the 16-bit offset
-    return *reinterpret_cast<const uint32_t*>(lut + kImm + chunk_offset<kT>(w0, w1, w2, hi));
-}
-
-// a ^ b ^ c in one VALU op (v_bitop3_b32, truth table 0x96)
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
-}
-
-// Toeplitz hash of one 96-bit input (toeplitz.py:46-69 over the bytes of :113-142).
-__device__ __forceinline__ uint32_t toeplitz_hash(const uint32_t* __restrict__ lut, uint32_t w0,
-                                                  uint32_t w1, uint32_t w2, uint32_t hi) {
-    const char* base = reinterpret_cast<const char*>(lut);
-    return xor3(xor3(lut_term<0>(base, w0, w1, w2, hi), lut_term<1>(base, w0, w1, w2, hi),
-                     lut_term<2>(base, w0, w1, w2, hi)),
-                xor3(lut_term<3>(base, w0, w1, w2, hi), lut_term<4>(base, w0, w1, w2, hi),
-                     lut_term<5>(base, w0, w1, w2, hi)),
-                lut_term<6>(base, w0, w1, w2, hi) ^ lut_term<7>(base, w0, w1, w2, hi));
-}
-
-// Small tables (many-queues launches, DESIGN.md §3 "Many queues"): 21 tables of at most 32
-// entries -- word k (w0, w1, w2) cut LSB first into fields of 5, 5, 5, 5, 5, 5 and 2 bits,
-// table 7k + j indexed by field j -- 2688 bytes instead of the 12-bit tables' 128 KiB, so the
-// LDS left for histogram bins grows from 16384 u16 queues to 80572 u16 / 161144 u8 queues.
-// Each table starts on a 128-byte (32-bank) boundary and has at most 32 entries, so entry v
-// is alone on bank v: lanes that hit one bank read one address and broadcast -- a random
-// index can never conflict.  21 conflict-free ds_read_b32 (2 LDS cycles each) per tuple
-// replace 8 random 12-bit reads (2 + ~4.5 conflict cycles each on uniform input) or 12
-// random byte-table reads (the round-3 form, ~7 cycles each).  Entry (t, v) lives at LDS
-// byte t*128 + v*4.
-constexpr int kSmallFields = 7;                                  // per 32-bit word
-constexpr int kSmallTables = 3 * kSmallFields;                   // 21
-constexpr uint32_t kSmallLutDwords = kSmallTables * 32;          // 672
-constexpr uint32_t kSmallLutBytes = kSmallLutDwords * 4;         // 2688
-constexpr uint32_t kSmallStaticBytes = kSmallLutBytes + 8;      // + the balanced tail's LDS slot
-__host__ __device__ constexpr int small_width(int j) { return j < 6 ? 5 : 2; }
-// input bit (toeplitz.py:65-68 order) of bit b of table t's index: word t/7, bit 5 (t%7) + b
-__host__ __device__ constexpr int small_slice_bit(int t, int b) {
-    return 32 * (t / kSmallFields) + 31 - 5 * (t % kSmallFields) - b;
-}
-
-__device__ __forceinline__ void build_small_lut(uint32_t* lut, const uint32_t* __restrict__ window,
-                                                uint32_t tid) {
-    for (uint32_t e = tid; e < kSmallLutDwords; e += kBlock) {
-        const int t = (int)(e >> 5);
-        const uint32_t v = e & 31u;
-        const int width = small_width(t % kSmallFields);
-        uint32_t x = 0;
-#pragma unroll
-        for (int b = 0; b < 5; ++b)
-            x ^= (b < width && ((v >> b) & 1u)) ? window[small_slice_bit(t, b)] : 0u;
-        lut[e] = (v >> width) ? 0u : x;  // entries past a 2-bit table's 4 are never read
-    }
-}
-
-// table 7k + j's term for word w (= word k): the field moved to byte offset 4 * field
-template <int kT>
-__device__ __forceinline__ uint32_t small_term(const char* lut, uint32_t w) {
-    constexpr int j = kT % kSmallFields, o = 5 * j;
-    uint32_t off;
-    if constexpr (j == 0)
-        off = (w << 2) & 0x7Cu;
-    else if constexpr (j == 6)
-        off = (w >> 28) & 0x0Cu;
-    else
-        off = (w >> (o - 2)) & 0x7Cu;
-    return *reinterpret_cast<const uint32_t*>(lut + kT * 128 + off);
-}
-
-template <int kBase>
-__device__ __forceinline__ uint32_t small_word(const char* lut, uint32_t w) {  // 7 terms
-    return xor3(xor3(small_term<kBase + 0>(lut, w), small_term<kBase + 1>(lut, w),
-                     small_term<kBase + 2>(lut, w)),
-                xor3(small_term<kBase + 3>(lut, w), small_term<kBase + 4>(lut, w),
-                     small_term<kBase + 5>(lut, w)),
-                small_term<kBase + 6>(lut, w));
-}
-
-__device__ __forceinline__ uint32_t toeplitz_hash_small(const uint32_t* __restrict__ lut, uint32_t w0,
-                                                        uint32_t w1, uint32_t w2) {
-    const char* b = reinterpret_cast<const char*>(lut);
-    return xor3(small_word<0>(b, w0), small_word<7>(b, w1), small_word<14>(b, w2));
-}
-
-template <bool kSmallLut>
-__device__ __forceinline__ uint32_t hash_of(const uint32_t* lut, uint32_t w0, uint32_t w1,
-                                            uint32_t w2, uint32_t hi) {
-    if constexpr (kSmallLut) return toeplitz_hash_small(lut, w0, w1, w2);
-    return toeplitz_hash(lut, w0, w1, w2, hi);
-}
-
-// hash % htable  (simulator.py:97, first modulo)
-template <bool kHPow2>
-__device__ __forceinline__ uint32_t bucket_of(uint32_t h, const LaunchParams& p) {
-    if constexpr (kHPow2) {
-        return h & p.h_mask;
-    } else {
-        // Lemire-Kaser-Kurz direct remainder, exact for all 32-bit h and H.
-        const uint64_t low = p.h_m64 * (uint64_t)h;
-        return (uint32_t)__umul64hi(low, (uint64_t)p.H);
-    }
-}
-
-// bucket % nqueues  (simulator.py:97, second modulo)
-template <int kQMode>
-__device__ __forceinline__ uint32_t queue_of(uint32_t b, const LaunchParams& p) {
-    if constexpr (kQMode == QM_MASK) {
-        return b & p.q_mask;
-    } else if constexpr (kQMode == QM_FAST8) {
-        // b < 256, Q < 256: b - Q * ((b * ceil(2^16 / Q)) >> 16), exact (checked for every
-        // b, Q), with full-rate 24-bit multiplies instead of FAST16's two quarter-rate ones
-        const uint32_t d = __umul24(b, p.q_m16) >> 16;
-        return b - __umul24(d, p.Q);
-    } else if constexpr (kQMode == QM_FAST16) {
-        return __umulhi(p.q_m32 * b, p.Q);  // b < 2^16, Q < 2^16
-    } else {
-        const uint64_t low = p.q_m64 * (uint64_t)b;
-        return (uint32_t)__umul64hi(low, (uint64_t)p.Q);
-    }
-}
-
-// queue of a bucket: the modulo modes above, or the indirection table copied to LDS
-template <int kQMode>
-__device__ __forceinline__ uint32_t queue_lookup(uint32_t b, const LaunchParams& p,
-                                                 const uint32_t* reta_lds) {
-    if constexpr (kQMode == QM_TABLE) {
-        return reta_lds[b];
-    } else {
-        return queue_of<kQMode>(b, p);
-    }
-}
-
-#ifdef RSS_TEST_HOOKS
-// Test-hooks build only: the largest number of adds that landed on a guarded bin between the
-// add that took it to half range and the guard's subtract, per guard kind (kMarginHash16: the
-// hash pass's u16 bins, kMarginWide16: the u16 wide passes, kMarginHash8 / kMarginWide8: the
-// u8 ones, modulo 256) -- read by rss_test_guard_margin.
-enum { kMarginHash16 = 0, kMarginWide16 = 1, kMarginHash8 = 2, kMarginWide8 = 3, kMargins = 4 };
-__device__ uint32_t g_guard_margin[kMargins];
-// `at`: the field's value when the subtract landed = half + the adds in between (mod 2^bits)
-template <int kBits>
-__device__ __forceinline__ void record_margin(int kind, uint32_t at) {
-    constexpr uint32_t kHalf = 1u << (kBits - 1), kField = (1u << kBits) - 1u;
-    __hip_atomic_fetch_max(&g_guard_margin[kind], (at - kHalf) & kField, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-}
-#define RSS_RECORD_MARGIN(bits, kind, at) record_margin<bits>(kind, at)
-// Test-hooks build only: before its subtract a u16 guard's wave sleeps g_guard_sleep times
-// s_sleep 127 (~3 us each), so that the workgroup's other waves carry the bin past 0xFFFF --
-// a real wrap, which the poison word must catch (rss_test_set_option "guard_sleep").
-__device__ uint32_t g_guard_sleep;
-__device__ __forceinline__ void guard_delay() {
-    const uint32_t n = *reinterpret_cast<volatile uint32_t*>(&g_guard_sleep);
-    for (uint32_t i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
-}
-#define RSS_GUARD_DELAY() guard_delay()
-#else
-#define RSS_RECORD_MARGIN(bits, kind, at) ((void)(at))
-#define RSS_GUARD_DELAY() ((void)0)
-#endif
-
-// HIST_RANGE16's two halves: the add (returns the dword's previous value, 0 out of range)
-// and the guard (the add that returned 0x7FFF, so that its bin now holds 0x8000, subtracts
-// 0x8000 from the bin and counts one move of 2^15 in p.ovf[r]).  The 4-tuple body issues its
-// four adds before the four guards, so they do not wait for each other.
-// Nothing bounds the adds that land on the bin between that add and the subtract: the
-// workgroup's other waves keep adding while the guard's wave waits for its returns, and wave
-// issue is not fair.  So a bin can pass 0xFFFF and carry into its neighbour (observed once in
-// a u16 wide pass, profiles/archive/r04/u16_guard/).  Exactly the add that takes a field past 0xFFFF
-// returns 0xFFFF, and it raises *p.poison: the launch's rows and moves are then discarded (the
-// reduce is gated on !poison) and rss_range_fallback_kernel / rss_range_fallback_col_kernel
-// recount the range with u32 bins (gated on poison) -- exact whatever the timing.
-__device__ __forceinline__ uint32_t range16_add(uint32_t* bins, uint32_t q, const LaunchParams& p) {
-    const uint32_t r = q - p.q_lo;  // wraps for q < q_lo
-    if (r >= p.q_span) return 0u;
-    return __hip_atomic_fetch_add(&bins[r >> 1], 1u << ((r & 1u) * 16u), __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-__device__ __forceinline__ void range16_guard(uint32_t* bins, uint32_t q, uint32_t old,
-                                              const LaunchParams& p) {
-    const uint32_t r = q - p.q_lo;
-    if (r >= p.q_span) return;
-    const uint32_t sh = (r & 1u) * 16u;
-    const uint32_t f = (old >> sh) & 0xFFFFu;
-    if (f == 0x7FFFu) {
-        RSS_GUARD_DELAY();
-        const uint32_t at = __hip_atomic_fetch_sub(&bins[r >> 1], 0x8000u << sh, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-        RSS_RECORD_MARGIN(16, kMarginHash16, (at >> sh) & 0xFFFFu);
-        atomicAdd(&p.ovf[r], 1u);
-    } else if (f == 0xFFFFu) {
-        __hip_atomic_store(p.poison, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-// HIST_RANGE8's halves.  u8 bins, four per dword: the add that returns 0x7F (its bin now
-// holds 0x80) subtracts 0x80 from the bin and counts one move of 128 in p.ovf (a u32 per
-// queue, summed by the partial reduce).  Unlike u16 bins, the adds in flight while that
-// subtract is pending are not bounded below the field's headroom: a workgroup can hold 4096
-// adds on one bin (every lane's four tuples in one queue), and a field that passes 0xFF
-// carries into its neighbour.  Exactly the add that takes a field past 0xFF sees 0xFF, so
-// that add raises *p.poison: the launch's bins are then discarded -- the partial reduce is
-// gated on !poison and rss_range8_fallback_kernel (gated on poison) recounts the range with
-// u32 bins.  Uniform and flow-like input stay far from it (a bin meets ~8 adds per workgroup
-// at 131072 queues); a batch of one repeated tuple takes the fallback.
-__device__ __forceinline__ uint32_t range8_add(uint32_t* bins, uint32_t q, const LaunchParams& p) {
-    const uint32_t r = q - p.q_lo;  // wraps for q < q_lo
-    if (r >= p.q_span) return 0u;
-    return __hip_atomic_fetch_add(&bins[r >> 2], 1u << ((r & 3u) * 8u), __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-__device__ __forceinline__ void range8_guard(uint32_t* bins, uint32_t q, uint32_t old,
-                                             const LaunchParams& p) {
-    const uint32_t r = q - p.q_lo;
-    if (r >= p.q_span) return;
-    const uint32_t sh = (r & 3u) * 8u;
-    const uint32_t f = (old >> sh) & 0xFFu;
-    if (f == 0x7Fu) {
-        const uint32_t at = __hip_atomic_fetch_sub(&bins[r >> 2], 0x80u << sh, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-        RSS_RECORD_MARGIN(8, kMarginHash8, (at >> sh) & 0xFFu);
-        atomicAdd(&p.ovf[r], 1u);
-    } else if (f == 0xFFu) {
-        __hip_atomic_store(p.poison, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-template <int kHist>
-__device__ __forceinline__ void count_queue(uint32_t* bins, uint32_t q, uint32_t col,
-                                            const LaunchParams& p) {
-    if constexpr (kHist == HIST_PRIVATE) {
-        __hip_atomic_fetch_add(&bins[q * kBinCols + col], 1u, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
-    } else if constexpr (kHist == HIST_SHARED) {
-        __hip_atomic_fetch_add(&bins[q], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    } else if constexpr (kHist == HIST_GLOBAL) {
-        atomicAdd(&p.counts[q], 1ull);
-    } else if constexpr (kHist == HIST_RANGE) {
-        const uint32_t r = q - p.q_lo;  // wraps for q < q_lo
-        if (r < p.q_span)
-            __hip_atomic_fetch_add(&bins[r], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    } else if constexpr (kHist == HIST_RANGE16) {
-        range16_guard(bins, q, range16_add(bins, q, p), p);
-    } else if constexpr (kHist == HIST_RANGE8) {
-        range8_guard(bins, q, range8_add(bins, q, p), p);
-    }
-}
-
-
-
-// Streaming outputs are written once and never re-read by this kernel: use
-// nontemporal stores so they do not displace the input stream in L2.
-template <typename T>
-__device__ __forceinline__ void stream_store(T* dst, T v) {
-    __builtin_nontemporal_store(v, dst);
-}
-
-// the value a queue column of width kQWidth holds for queue q (QW_U16R: see QueueWidth)
-template <int kQWidth>
-__device__ __forceinline__ uint32_t column_queue(uint32_t q, const LaunchParams& p) {
-    if constexpr (kQWidth == QW_U16R) return min(q - p.q_span, 0xFFFFu);  // q < q_span wraps
-    return q;
-}
-template <int kQWidth>
-constexpr int kStoreWidth = kQWidth == QW_U16R ? QW_U16 : kQWidth;
-
-template <int kQWidth>
-__device__ __forceinline__ void store_queue1(void* out, uint64_t i, uint32_t q) {
-    if constexpr (kQWidth == QW_U8) {
-        stream_store(static_cast<uint8_t*>(out) + i, (uint8_t)q);
-    } else if constexpr (kQWidth == QW_U16) {
-        stream_store(static_cast<uint16_t*>(out) + i, (uint16_t)q);
-    } else {
-        stream_store(static_cast<uint32_t*>(out) + i, q);
-    }
-}
-
-// four consecutive queues of group g (tuples 4g .. 4g+3) as one 4/8/16-byte store
-template <int kQWidth, typename Idx>
-__device__ __forceinline__ void store_queue4(void* out, Idx g, uint32_t q0, uint32_t q1,
-                                             uint32_t q2, uint32_t q3) {
-    if constexpr (kQWidth == QW_U8) {
-        stream_store(static_cast<uint32_t*>(out) + g, q0 | q1 << 8 | q2 << 16 | q3 << 24);
-    } else if constexpr (kQWidth == QW_U16) {
-        uint32_t* o = static_cast<uint32_t*>(out) + 2 * g;
-        stream_store(o, q0 | q1 << 16);
-        stream_store(o + 1, q2 | q3 << 16);
-    } else {
-        uint32_t* o = static_cast<uint32_t*>(out) + 4 * g;
-        stream_store(o, q0);
-        stream_store(o + 1, q1);
-        stream_store(o + 2, q2);
-        stream_store(o + 3, q3);
-    }
-}
-
-// Fold a workgroup's per-queue totals (`sum_of(q)`, q < Q) into the global uint64 counts.
-// Without a workspace: one atomicAdd per non-zero total (counts zeroed by the caller or by
-// a hipMemsetAsync before the launch).  With one (rss_hash_device_ws, single-pass counts) the
-// launch writes the batch's counts itself (overwriting, or adding when `mode &
-// kFoldAccumulate`) and leaves the workspace zero for the next launch -- so a batch's counts
-// need no zeroing launch before it.  Arrival fold: each workgroup adds (1 << kArrivalShift) |
-// total into ws[1 + q] for every queue; the add whose returned arrival count is gridDim.x - 1
-// is the queue's last, so its workgroup writes counts[q] = old sum + its own and resets
-// ws[1 + q].  Every queue is finalised by one atomic round trip and needs no release/acquire:
-// its count travels in the atomics on one location (the balanced tail's unit counter is
-// reset in walk_rows by the launch's final claim, also one location).  Stress-tested in
-// tests/test_gpu_single_pass.py.  (Rounds 2-3 used a ticket fold -- totals, a ticket, the
-// last workgroup's exchanges: three serialised round trips on the last workgroup's path.)
-constexpr uint32_t kFoldAccumulate = 1u;
-// ws[1 + q] = (arrivals << kArrivalShift) | sum.  Sums stay below 2^44 (a launch is < 2^44
-// tuples) and arrivals below 2^20 workgroups.
-constexpr uint32_t kArrivalShift = 44;
-constexpr unsigned long long kArrivalOne = 1ull << kArrivalShift;
-constexpr unsigned long long kSumMask = kArrivalOne - 1;
-// the balanced tail's unit counter: ws[Q + 1]
-__host__ __device__ __forceinline__ unsigned long long* ws_tail_counter(unsigned long long* ws,
-                                                                        uint32_t Q) {
-    return ws + Q + 1;
-}
-
-template <typename SumOf>
-__device__ __forceinline__ void fold_counts(SumOf sum_of, uint32_t Q, unsigned long long* counts,
-                                            unsigned long long* ws, uint32_t mode) {
-    const uint32_t tid = threadIdx.x;
-    if (!ws) {
-        for (uint32_t q = tid; q < Q; q += blockDim.x) {
-            const uint32_t s = sum_of(q);
-            if (s) atomicAdd(&counts[q], (unsigned long long)s);
-        }
-        return;
-    }
-    const bool accumulate = (mode & kFoldAccumulate) != 0;
-    const unsigned long long last = (unsigned long long)gridDim.x - 1;
-    for (uint32_t q = tid; q < Q; q += blockDim.x) {
-        const unsigned long long add = kArrivalOne | sum_of(q);
-        // the sums travel in the atomics on one word each: no fence is needed
-        const unsigned long long old = atomicAdd(&ws[1 + q], add);
-        if ((old >> kArrivalShift) == last) {  // every other workgroup's add is in `old`
-            const unsigned long long total = (old & kSumMask) + (add & kSumMask);
-            counts[q] = accumulate ? counts[q] + total : total;
-            atomicExch(&ws[1 + q], 0ull);  // after every add of this launch to it
-        }
-    }
-}
-
-// The grid's walk over `ngroups` groups of 4 tuples (`group(g)`), one grid-stride row at a
-// time: row r = groups [r * gstride, (r + 1) * gstride), workgroup w takes slot w of it.
-// With `tail_rows` (single-pass launches, DESIGN.md §3 "Balanced tail") rows [0, srows) go
-// statically and the last tail_rows rows are handed out in order as units of one workgroup
-// slot (kBlock groups) through the workspace counter `next`, one claim per workgroup in
-// flight (issued one unit ahead, broadcast through the LDS word `slot`), so the workgroups
-// -- the XCDs -- that stream faster (measured: even XCDs finish ~4 % before odd ones) take
-// more of the tail and every XCD ends together, while the whole grid still sweeps one
-// window of the arrays at a time.  `next` is reset by the launch's final claim (below).
-template <typename Group>
-__device__ __forceinline__ void walk_rows(Group group, uint64_t ngroups, uint32_t tail_rows,
-                                          unsigned long long* next, unsigned long long* slot) {
-    const uint32_t tid = threadIdx.x;
-    const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
-    const uint64_t gstride = (uint64_t)gridDim.x * kBlock;
-    if (!tail_rows) {
-        for (uint64_t g = gtid; g < ngroups; g += gstride) group(g);
-        return;
-    }
-    const uint64_t nrows = (ngroups + gstride - 1) / gstride;
-    const uint64_t srows = nrows - tail_rows;  // the launcher keeps tail_rows < nrows
-    // Every workgroup claims until a claim fails (returns >= the tail's units), so a launch
-    // makes exactly tail units + gridDim.x claims; the one that returns the last of them is the
-    // final RMW of the launch on `next` and resets it -- one location, so no fence is needed.
-    const unsigned long long last_claim = (unsigned long long)tail_rows * gridDim.x + gridDim.x - 1;
-    auto publish = [&](unsigned long long c) {  // tid 0
-        if (c == last_claim) atomicExch(next, 0ull);
-        *slot = c;
-    };
-    unsigned long long claim = 0;
-    if (tid == 0) claim = atomicAdd(next, 1ull);  // the first tail unit, in flight meanwhile
-    for (uint64_t row = 0; row < srows; ++row) group(row * gstride + gtid);  // full rows
-    if (tid == 0) publish(claim);
-    __syncthreads();
-    const uint64_t first = srows * gridDim.x, nunits = nrows * gridDim.x;
-    uint64_t u = first + *slot;
-    while (u < nunits) {
-        __syncthreads();  // every lane has read the slot
-        if (tid == 0) claim = atomicAdd(next, 1ull);  // the next unit, during this one
-        const uint64_t g = (u / gridDim.x) * gstride + (u % gridDim.x) * kBlock + tid;
-        if (g < ngroups) group(g);
-        if (tid == 0) publish(claim);
-        __syncthreads();
-        u = first + *slot;
-    }
-}
-
-// Rows of a launch of `ngroups` groups on `grid` workgroups, and the tail a single-pass
-// launch hands out (about a tenth; none below 16 rows, where the spread is a few us)
-inline uint32_t balanced_tail_rows(uint64_t ngroups, unsigned grid) {
-    const uint64_t per_row = (uint64_t)grid * kBlock;
-    const uint64_t rows = (ngroups + per_row - 1) / per_row;
-    return rows >= 16 ? (uint32_t)std::max<uint64_t>(1, rows / 10) : 0u;
-}
-
-// HIST_RANGE8 counts only, queues past the pass's LDS range (q >= q_span): instead of a queue
-// column with every tuple's queue, each wave appends r = q - q_span to a list of its own (K
-// queues per lane): a ballot per slot, the entries at the wave's running length `count` plus
-// the lanes below (mbcnt), stored at 32-bit offsets from the wave's list (`list`, uniform).
-// No atomic: the length is the same in every lane (sums of ballot popcounts), and a wave's
-// list never exceeds its tuples (the launcher sizes resid_cap for the static walk's share of a
-// wave).  The entries are exact whether or not the bins are poisoned.
-constexpr uint32_t kWavesPerBlock = kBlock / 64;
-__device__ __forceinline__ char* resid_list(const LaunchParams& p) {
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    return static_cast<char*>(p.resid_out) +
-           ((uint64_t)blockIdx.x * kWavesPerBlock + wave) * p.resid_cap * (p.resid_u16 ? 2 : 4);
-}
-template <int K>
-__device__ __forceinline__ void resid_append(const LaunchParams& p, char* list, uint32_t& count,
-                                             const uint32_t* q) {
-    // The first active lane took part in every earlier append of its wave (lanes leave the
-    // walk from the top, and the < 4 tail tuples are lanes 0..2): its length is the wave's.
-    // Per slot: the ballot's compare, two mbcnt and one shift-add for the address (the
-    // length's byte offset stays scalar), one subtract for the entry.
-    const uint32_t sh = p.resid_u16 ? 1u : 2u;
-    uint32_t at = __builtin_amdgcn_readfirstlane(count) << sh;  // byte offset of the next entry
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const uint64_t m = __ballot(q[k] >= p.q_span);
-        if (q[k] >= p.q_span) {
-            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            char* dst = list + (at + (below << sh));
-            if (p.resid_u16)
-                *reinterpret_cast<uint16_t*>(dst) = (uint16_t)(q[k] - p.q_span);
-            else
-                *reinterpret_cast<uint32_t*>(dst) = q[k] - p.q_span;
-        }
-        at += (uint32_t)__popcll(m) << sh;
-    }
-    count = at >> sh;
-}
 
 template <bool kHPow2, int kQMode, int kHist, int kQWidth, bool kSmallLut>
 __device__ __forceinline__ void one_tuple(const uint32_t* lut, uint32_t* bins, uint64_t i,
@@ -1228,343 +646,6 @@ __global__ __launch_bounds__(kBlock, 2) void rss_counts_perm_kernel(const PermPa
     }, p.Q, p.counts, p.ws, p.accumulate);
 }
 
-// Key search: per-queue counts of the same tuples under many
-// keys.  A table index depends only on the tuple, so one table can serve two keys: entry
-// v holds (key A's XOR of windows, key B's) as 8 bytes and ONE ds_read_b64 -- 64 banks,
-// 256 B/clk (twice ds_read_b32's rate) -- fetches both keys' terms.  Two table sets:
-// * the packed kernel (power-of-two H, several keys' low bits per entry) reads the small
-//   tables' 21 fields (5, 5, 5, 5, 5, 5, 2 bits of each word, LSB first; kSmallLut) with
-//   8-byte entries: 32 entries x 8 B = 256 B cover the 64 banks exactly once, so every entry
-//   sits on its own bank pair and a random index never conflicts -- 21 conflict-free reads
-//   (2 LDS cycles each) per tuple against 9 random reads at ~7 cycles each on the wide
-//   tables below (PMC: 0 against 44 of 80 LDS cycles per 64 tuples x 8 keys in bank
-//   conflicts, profiles/r04/pmc_keysearch*/); at Q = 24 the two run equal (the small tables'
-//   extra address VALU makes it VALU-bound instead), but 5.25 KiB of tables leave ~155 KiB to
-//   the bins: 8 keys per workgroup up to Q = 154 (wide tables: 40) and 4 up to 309 (80);
-// * the pair kernel (any H: two full 32-bit hashes, their Lemire remainders and two adds per
-//   tuple) keeps the nine wide tables of 2048 / 1024 entries (11 / 10 input bits, field LSBs
-//   first as in the hash kernel's partition), whose 9 lookups cost less VALU than 21:
-//     t0 w0[10:0]  t1 w0[21:11]  t2 w1[10:0]  t3 w2[15:11] | w2[31:27] << 5  t4 w0[31:22]
-//     t5 w1[21:11] t6 w2[10:0]   t7 w2[26:16] t8 w1[31:22]
-//   = 6 x 16 + 3 x 8 KiB = 120 KiB; on the small tables it ran 0.77 against 0.97 T
-//   evaluations/s at H = 100, Q = 24 (profiles/archive/r04/small_tables/keysearch_configs.jsonl).
-// blockIdx.y selects the pair; each workgroup histograms its grid-stride share of the
-// tuples into counts rows 2y, 2y+1.  With the tuples resident in the 256 MiB Infinity Cache
-// the re-reads stay on die.
-constexpr uint32_t kPairLutBytes = kSmallTables * 256;            // 5376 (packed kernel)
-constexpr uint32_t kPackedBinBytesMax = kLdsBytes - kPairLutBytes;  // 154.75 KiB for the bins
-constexpr uint32_t kWidePairLutBytes = 6 * 16384 + 3 * 8192;     // 122880 (pair kernel)
-constexpr uint32_t kWidePairBinBytesMax = kLdsBytes - kWidePairLutBytes;  // 40 KiB, 2 x Q bins
-
-__host__ __device__ constexpr int wide_pair_width(int t) {
-    return (t == 3 || t == 4 || t == 8) ? 10 : 11;
-}
-__host__ __device__ constexpr uint32_t wide_pair_table(int t) {  // byte offset
-    return t == 0 ? 0u : t == 1 ? 16384u : t == 2 ? 32768u : t == 3 ? 49152u : t == 4 ? 57344u
-         : t == 5 ? 65536u : t == 6 ? 81920u : t == 7 ? 98304u : 114688u;
-}
-// input bit (0 = MSB of the source ip) feeding bit b of table t's index
-__host__ __device__ constexpr int wide_pair_bit(int t, int b) {
-    return t == 0 ? 31 - b : t == 1 ? 20 - b : t == 2 ? 63 - b
-         : t == 3 ? (b < 5 ? 84 - b : 73 - b)
-         : t == 4 ? 9 - b : t == 5 ? 52 - b : t == 6 ? 95 - b : t == 7 ? 79 - b : 41 - b;
-}
-
-template <int kT>
-__device__ __forceinline__ void build_wide_pair_table(uint2* lut, const uint32_t* __restrict__ wa,
-                                                      const uint32_t* __restrict__ wb, uint32_t tid) {
-    uint32_t a = 0, b = 0;
-#pragma unroll
-    for (int j = 0; j < 10; ++j) {
-        const bool set = (tid >> j) & 1u;
-        a ^= set ? wa[wide_pair_bit(kT, j)] : 0u;
-        b ^= set ? wb[wide_pair_bit(kT, j)] : 0u;
-    }
-    uint2* dst = lut + wide_pair_table(kT) / 8;
-    dst[tid] = make_uint2(a, b);
-    if constexpr (wide_pair_width(kT) == 11)
-        dst[tid + 1024] = make_uint2(a ^ wa[wide_pair_bit(kT, 10)], b ^ wb[wide_pair_bit(kT, 10)]);
-}
-
-// byte address of wide table t's entry: 2 VALU (4 for the two-field t3); tables 5..8 take
-// their 64 KiB base from the opaque register `hi`
-template <int kT>
-__device__ __forceinline__ uint32_t wide_pair_offset(uint32_t w0, uint32_t w1, uint32_t w2,
-                                                     uint32_t hi) {
-    if constexpr (kT == 0) return (w0 << 3) & 0x3FF8u;
-    if constexpr (kT == 1) return (w0 >> 8) & 0x3FF8u;
-    if constexpr (kT == 2) return (w1 << 3) & 0x3FF8u;
-    if constexpr (kT == 3) return ((w2 >> 8) & 0xF8u) | ((w2 >> 19) & 0x1F00u);
-    if constexpr (kT == 4) return (w0 >> 19) & 0x1FF8u;
-    if constexpr (kT == 5) return ((w1 >> 8) & 0x3FF8u) | hi;
-    if constexpr (kT == 6) return ((w2 << 3) & 0x3FF8u) | hi;
-    if constexpr (kT == 7) return ((w2 >> 13) & 0x3FF8u) | hi;
-    return ((w1 >> 19) & 0x1FF8u) | hi;
-}
-
-template <int kT>
-__device__ __forceinline__ uint2 wide_pair_term(const char* lut, uint32_t w0, uint32_t w1,
-                                                uint32_t w2, uint32_t hi) {
-    constexpr uint32_t kImm = wide_pair_table(kT) & 0xFFFFu;
-    return *reinterpret_cast<const uint2*>(lut + kImm + wide_pair_offset<kT>(w0, w1, w2, hi));
-}
-
-// (hash under key A, hash under key B) of one tuple on the wide tables
-__device__ __forceinline__ uint2 toeplitz_hash_wide_pair(const uint2* __restrict__ lut, uint32_t w0,
-                                                         uint32_t w1, uint32_t w2, uint32_t hi) {
-    const char* base = reinterpret_cast<const char*>(lut);
-    const uint2 t0 = wide_pair_term<0>(base, w0, w1, w2, hi), t1 = wide_pair_term<1>(base, w0, w1, w2, hi);
-    const uint2 t2 = wide_pair_term<2>(base, w0, w1, w2, hi), t3 = wide_pair_term<3>(base, w0, w1, w2, hi);
-    const uint2 t4 = wide_pair_term<4>(base, w0, w1, w2, hi), t5 = wide_pair_term<5>(base, w0, w1, w2, hi);
-    const uint2 t6 = wide_pair_term<6>(base, w0, w1, w2, hi), t7 = wide_pair_term<7>(base, w0, w1, w2, hi);
-    const uint2 t8 = wide_pair_term<8>(base, w0, w1, w2, hi);
-    return make_uint2(xor3(xor3(t0.x, t1.x, t2.x), xor3(t3.x, t4.x, t5.x), xor3(t6.x, t7.x, t8.x)),
-                      xor3(xor3(t0.y, t1.y, t2.y), xor3(t3.y, t4.y, t5.y), xor3(t6.y, t7.y, t8.y)));
-}
-
-// entry e = 32 t + v of the 21 pair tables: (XOR of key A's windows, of key B's) over the
-// input bits set in v; `win(i)` gives the two keys' window i as a uint2
-template <typename Win>
-__device__ __forceinline__ void build_small_pair_lut(uint2* lut, Win win, uint32_t tid) {
-    for (uint32_t e = tid; e < kSmallLutDwords; e += kBlock) {
-        const int t = (int)(e >> 5);
-        const uint32_t v = e & 31u;
-        const int width = small_width(t % kSmallFields);
-        uint32_t a = 0, b = 0;
-#pragma unroll
-        for (int j = 0; j < 5; ++j) {
-            if (j < width && ((v >> j) & 1u)) {
-                const uint2 w = win(small_slice_bit(t, j));
-                a ^= w.x;
-                b ^= w.y;
-            }
-        }
-        lut[e] = (v >> width) ? make_uint2(0u, 0u) : make_uint2(a, b);
-    }
-}
-
-// table 7k + j's 8-byte term for word w (= word k): the field moved to byte offset 8 * field
-template <int kT>
-__device__ __forceinline__ uint2 small_pair_term(const char* lut, uint32_t w) {
-    constexpr int j = kT % kSmallFields, o = 5 * j;
-    uint32_t off;
-    if constexpr (j == 0)
-        off = (w << 3) & 0xF8u;
-    else if constexpr (j == 6)
-        off = (w >> 27) & 0x18u;
-    else
-        off = (w >> (o - 3)) & 0xF8u;
-    return *reinterpret_cast<const uint2*>(lut + kT * 256 + off);
-}
-
-template <int kBase>
-__device__ __forceinline__ uint2 small_pair_word(const char* lut, uint32_t w) {  // 7 terms
-    const uint2 t0 = small_pair_term<kBase + 0>(lut, w), t1 = small_pair_term<kBase + 1>(lut, w);
-    const uint2 t2 = small_pair_term<kBase + 2>(lut, w), t3 = small_pair_term<kBase + 3>(lut, w);
-    const uint2 t4 = small_pair_term<kBase + 4>(lut, w), t5 = small_pair_term<kBase + 5>(lut, w);
-    const uint2 t6 = small_pair_term<kBase + 6>(lut, w);
-    return make_uint2(xor3(xor3(t0.x, t1.x, t2.x), xor3(t3.x, t4.x, t5.x), t6.x),
-                      xor3(xor3(t0.y, t1.y, t2.y), xor3(t3.y, t4.y, t5.y), t6.y));
-}
-
-// (hash under key A, hash under key B) of one tuple (packed kernel: 8 / 4 keys' low bits)
-__device__ __forceinline__ uint2 toeplitz_hash_pair(const uint2* __restrict__ lut, uint32_t w0,
-                                                    uint32_t w1, uint32_t w2) {
-    const char* base = reinterpret_cast<const char*>(lut);
-    const uint2 a = small_pair_word<0>(base, w0), b = small_pair_word<7>(base, w1);
-    const uint2 c = small_pair_word<14>(base, w2);
-    return make_uint2(xor3(a.x, b.x, c.x), xor3(a.y, b.y, c.y));
-}
-
-template <bool kHPow2, int kQMode, int kHist>
-__device__ __forceinline__ void count_pair(uint32_t* bins_a, uint32_t* bins_b, uint2 h,
-                                           uint32_t col, const LaunchParams& qa,
-                                           const LaunchParams& qb) {
-    count_queue<kHist>(bins_a, queue_of<kQMode>(bucket_of<kHPow2>(h.x, qa), qa), col, qa);
-    count_queue<kHist>(bins_b, queue_of<kQMode>(bucket_of<kHPow2>(h.y, qb), qb), col, qb);
-}
-
-template <int kHist>
-__device__ __forceinline__ void flush_bins(const uint32_t* bins, unsigned long long* counts,
-                                           uint32_t Q, uint32_t tid) {
-    for (uint32_t k = tid; k < Q; k += kBlock) {
-        uint32_t s;
-        if constexpr (kHist == HIST_PRIVATE) {
-            s = 0;
-            for (uint32_t c = 0; c < kBinCols; ++c) s += bins[k * kBinCols + ((c + k) & (kBinCols - 1))];
-        } else {
-            s = bins[k];
-        }
-        if (s) atomicAdd(&counts[k], (unsigned long long)s);
-    }
-}
-
-template <bool kHPow2, int kQMode, int kHist, bool kVec4>
-__global__ __launch_bounds__(kBlock) void rss_key_search_kernel(const LaunchParams p) {
-    __shared__ uint2 lut[kWidePairLutBytes / 8];
-    extern __shared__ uint32_t bins[];
-    const uint32_t tid = threadIdx.x;
-    // keys 2y and 2y+1; an odd last key is paired with itself and its copy discarded
-    const uint32_t key_a = 2 * blockIdx.y;
-    const bool has_b = key_a + 1 < p.nkeys;
-    const uint32_t key_b = has_b ? key_a + 1 : key_a;
-    const uint32_t* wa = p.key_windows + (size_t)RSS_INPUT_BITS * key_a;
-    const uint32_t* wb = p.key_windows + (size_t)RSS_INPUT_BITS * key_b;
-    build_wide_pair_table<0>(lut, wa, wb, tid);
-    build_wide_pair_table<1>(lut, wa, wb, tid);
-    build_wide_pair_table<2>(lut, wa, wb, tid);
-    build_wide_pair_table<3>(lut, wa, wb, tid);
-    build_wide_pair_table<4>(lut, wa, wb, tid);
-    build_wide_pair_table<5>(lut, wa, wb, tid);
-    build_wide_pair_table<6>(lut, wa, wb, tid);
-    build_wide_pair_table<7>(lut, wa, wb, tid);
-    build_wide_pair_table<8>(lut, wa, wb, tid);
-    const uint32_t per_key =
-        kHist == HIST_PRIVATE ? p.Q * kBinCols : (kHist == HIST_SHARED ? p.Q : 0u);
-    for (uint32_t e = tid; e < 2 * per_key; e += kBlock) bins[e] = 0;
-    __syncthreads();
-
-    LaunchParams qa = p, qb = p;  // per-key counts rows
-    qa.counts = p.counts + (size_t)key_a * p.q_stride;
-    qb.counts = p.counts + (size_t)key_b * p.q_stride;
-    uint32_t* bins_a = bins;
-    uint32_t* bins_b = bins + per_key;
-    const uint32_t col = tid & (kBinCols - 1);
-    uint32_t hi = 65536u;
-    asm volatile("" : "+v"(hi));
-    const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
-    const uint64_t gstride = (uint64_t)gridDim.x * kBlock;
-    uint64_t tail_begin = 0;
-    if constexpr (kVec4) {
-        const uint4* __restrict__ src = reinterpret_cast<const uint4*>(p.tuples);
-        const uint64_t ngroups = p.n >> 2;
-        for (uint64_t g = gtid; g < ngroups; g += gstride) {
-            const uint4 a = src[3 * g + 0];
-            const uint4 b = src[3 * g + 1];
-            const uint4 c = src[3 * g + 2];
-            count_pair<kHPow2, kQMode, kHist>(bins_a, bins_b, toeplitz_hash_wide_pair(lut, a.x, a.y, a.z, hi), col, qa, qb);
-            count_pair<kHPow2, kQMode, kHist>(bins_a, bins_b, toeplitz_hash_wide_pair(lut, a.w, b.x, b.y, hi), col, qa, qb);
-            count_pair<kHPow2, kQMode, kHist>(bins_a, bins_b, toeplitz_hash_wide_pair(lut, b.z, b.w, c.x, hi), col, qa, qb);
-            count_pair<kHPow2, kQMode, kHist>(bins_a, bins_b, toeplitz_hash_wide_pair(lut, c.y, c.z, c.w, hi), col, qa, qb);
-        }
-        tail_begin = ngroups << 2;
-    }
-    for (uint64_t i = tail_begin + gtid; i < p.n; i += gstride) {
-        const uint32_t* t = reinterpret_cast<const uint32_t*>(p.tuples) + 3 * i;
-        count_pair<kHPow2, kQMode, kHist>(bins_a, bins_b, toeplitz_hash_wide_pair(lut, t[0], t[1], t[2], hi), col, qa, qb);
-    }
-    if constexpr (kHist == HIST_PRIVATE || kHist == HIST_SHARED) {
-        __syncthreads();
-        flush_bins<kHist>(bins_a, qa.counts, p.Q, tid);
-        if (has_b) flush_bins<kHist>(bins_b, qb.counts, p.Q, tid);
-    }
-}
-
-// Packed-bucket key search.  For a power-of-two H the bucket (simulator.py:97,
-// `hash % htable`) is the low log2(H) bits of the hash, and the low bits of a XOR are
-// the XOR of the low bits: a table term needs only those bits of each key.  With
-// H <= 256 an 8-byte entry holds the low BYTE of 8 keys' terms (H <= 65536: the low
-// half-word of 4 keys'), so the same 21 conflict-free ds_read_b64 of the pair kernel
-// serve 8 (4) keys and the per-key work is a bit-field extract, the queue step and one
-// LDS add.
-// Bins are [q][key][lane column]: the key's offset is a ds_add immediate and every
-// half-wave's adds stay conflict-free.
-constexpr uint32_t kPackedPrepBytes = RSS_INPUT_BITS * 8;  // packed windows, before the bins
-
-template <int kLaneBits, int kQMode, bool kVec4>
-__global__ __launch_bounds__(kBlock) void rss_key_search_packed_kernel(const LaunchParams p) {
-    constexpr uint32_t kKeys = 64 / kLaneBits;
-    __shared__ uint2 lut[kPairLutBytes / 8];
-    extern __shared__ uint32_t bins[];
-    const uint32_t tid = threadIdx.x;
-    const uint32_t key0 = kKeys * blockIdx.y;
-
-    // 1. pack: lane k of packed[i] = low kLaneBits of key (key0 + k)'s window i (a key
-    //    past the end repeats the last key; its counts are discarded)
-    uint2* packed = reinterpret_cast<uint2*>(bins);
-    if (tid < RSS_INPUT_BITS) {
-        uint32_t lo = 0, hi = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < kKeys; ++k) {
-            const uint32_t key = min(key0 + k, p.nkeys - 1);
-            const uint32_t w = p.key_windows[(size_t)RSS_INPUT_BITS * key + tid] &
-                               ((1u << kLaneBits) - 1);
-            const uint32_t shift = k * kLaneBits;
-            if (shift < 32) lo |= w << shift;
-            else hi |= w << (shift - 32);
-        }
-        packed[tid] = make_uint2(lo, hi);
-    }
-    __syncthreads();
-    build_small_pair_lut(lut, [&](int i) { return packed[i]; }, tid);
-    __syncthreads();  // packed windows are dead: the region becomes bins
-    const uint32_t nbins = p.Q * kKeys * kBinCols;
-    for (uint32_t e = tid; e < nbins; e += kBlock) bins[e] = 0;
-    __syncthreads();
-
-    uint32_t* bins_col = bins + (tid & (kBinCols - 1));
-    char* bins_colb = reinterpret_cast<char*>(bins_col);
-    const uint32_t hbits = 31 - __clz(p.H);  // log2(H)
-    constexpr uint32_t kRowShift = kLaneBits == 8 ? 10 : 9;  // log2(kKeys * kBinCols * 4)
-    // byte-lane queue step folded into the bin address: q * 2^kRowShift =
-    // (b << kRowShift) - d * (Q << kRowShift), d = floor(b / Q) (as QM_FAST8): two
-    // full-rate 24-bit multiplies, the second a v_mad_i32_i24
-    const int neg_q_row = -(int)(p.Q << kRowShift);
-    // byte lanes: mask every lane to the bucket bits at once, then each key's bucket is
-    // a plain byte select (which the multiplies and shifts take as an SDWA operand)
-    const uint32_t lane_mask4 = (p.H - 1) * 0x01010101u;
-    auto count = [&](uint2 x) {
-        if constexpr (kLaneBits == 8) {
-            x.x &= lane_mask4;
-            x.y &= lane_mask4;
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < kKeys; ++k) {
-            const uint32_t word = (k * kLaneBits) < 32 ? x.x : x.y;
-            const uint32_t b = kLaneBits == 8 ? (word >> ((k * 8) & 31)) & 0xFFu
-                                              : __builtin_amdgcn_ubfe(word, (k * kLaneBits) & 31, hbits);
-            uint32_t row;
-            if constexpr (kLaneBits == 8 && kQMode == QM_FAST16) {
-                const uint32_t d = __umul24(b, p.q_m16) >> 16;
-                row = (uint32_t)__mul24((int)d, neg_q_row) + (b << kRowShift);
-            } else {
-                row = queue_of<kQMode>(b, p) << kRowShift;
-            }
-            __hip_atomic_fetch_add(reinterpret_cast<uint32_t*>(bins_colb + row) + k * kBinCols, 1u,
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-    };
-    const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
-    const uint64_t gstride = (uint64_t)gridDim.x * kBlock;
-    uint64_t tail_begin = 0;
-    if constexpr (kVec4) {
-        const uint4* __restrict__ src = reinterpret_cast<const uint4*>(p.tuples);
-        const uint64_t ngroups = p.n >> 2;
-        for (uint64_t g = gtid; g < ngroups; g += gstride) {
-            const uint4 a = src[3 * g + 0];
-            const uint4 b = src[3 * g + 1];
-            const uint4 c = src[3 * g + 2];
-            count(toeplitz_hash_pair(lut, a.x, a.y, a.z));
-            count(toeplitz_hash_pair(lut, a.w, b.x, b.y));
-            count(toeplitz_hash_pair(lut, b.z, b.w, c.x));
-            count(toeplitz_hash_pair(lut, c.y, c.z, c.w));
-        }
-        tail_begin = ngroups << 2;
-    }
-    for (uint64_t i = tail_begin + gtid; i < p.n; i += gstride) {
-        const uint32_t* t = reinterpret_cast<const uint32_t*>(p.tuples) + 3 * i;
-        count(toeplitz_hash_pair(lut, t[0], t[1], t[2]));
-    }
-    __syncthreads();
-    for (uint32_t e = tid; e < p.Q * kKeys; e += kBlock) {
-        const uint32_t q = e / kKeys, k = e % kKeys;
-        if (key0 + k >= p.nkeys) continue;
-        uint32_t s = 0;
-        for (uint32_t c = 0; c < kBinCols; ++c) s += bins[e * kBinCols + ((c + e) & (kBinCols - 1))];
-        if (s) atomicAdd(&p.counts[(size_t)(key0 + k) * p.q_stride + q], (unsigned long long)s);
-    }
-}
-
 // ------------------------------------------------------------- IPv6 -------
 // 36-byte input: nine big-endian words, 288 bits (w0..w3 src
 // address, w4..w7 dst address, w8 ports).  12-bit tables would need 384 KiB, so the
@@ -1841,29 +922,6 @@ __global__ __launch_bounds__(256) void rss_generate_kernel(uint64_t seed, uint64
     }
 }
 
-// --------------------------------------------------------------- host -------
-struct DeviceInfo {
-    int cu_count = 0;
-};
-
-std::mutex g_dev_mutex;
-std::vector<DeviceInfo> g_devices;
-
-int device_info(DeviceInfo* out) {
-    int dev = 0;
-    RSS_HIP_CHECK(hipGetDevice(&dev));
-    std::lock_guard<std::mutex> lock(g_dev_mutex);
-    if ((int)g_devices.size() <= dev) g_devices.resize(dev + 1);
-    if (g_devices[dev].cu_count == 0) {
-        int cus = 0;
-        RSS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-        g_devices[dev].cu_count = cus > 0 ? cus : 1;
-    }
-    *out = g_devices[dev];
-    return RSS_OK;
-}
-
-using KernelFn = void (*)(const LaunchParams);
 
 // vec4: 0 = one tuple per lane, 1 = four per lane, 2 = four per lane with 32-bit byte offsets
 // (kOff32; instantiated for the single-pass histogram modes only, the bench's step), 3 = four
@@ -1943,194 +1001,6 @@ KernelFn pick_queue(int qmode, int hist, int qwidth, int vec4) {
         case QM_TABLE: return pick_hist<kHPow2, QM_TABLE>(hist, qwidth, vec4);
         default: return pick_hist<kHPow2, QM_FAST32>(hist, qwidth, vec4);
     }
-}
-
-bool is_pow2(uint32_t x) { return x && !(x & (x - 1)); }
-bool aligned16(const void* ptr) { return ((uintptr_t)ptr & 15u) == 0; }
-
-// ceil(2^64 / d) as Lemire's M = floor((2^64 - 1) / d) + 1 (wraps to 0 for d = 1,
-// which still yields the correct remainder 0).
-uint64_t magic64(uint32_t d) { return UINT64_MAX / d + 1; }
-uint32_t magic32(uint32_t d) { return UINT32_MAX / d + 1; }
-
-// The queues a launch can produce.  Without an indirection table queue = bucket % Q with
-// bucket < H (simulator.py:96-98), so every queue is < min(H, Q); with one, < max(reta) + 1.
-// Bins, the queue-width check and the counts the kernels write are sized by this; counts
-// [q_eff, nqueues) of the caller's vector are always zero (zero_counts_tail).
-uint32_t effective_queues(uint32_t htable, uint32_t nqueues, const uint32_t* reta) {
-    if (reta) {
-        uint32_t m = 0;
-        for (uint32_t b = 0; b < htable; ++b) m = std::max(m, reta[b]);
-        return m + 1;  // <= nqueues (check_reta)
-    }
-    return nqueues < htable ? nqueues : htable;
-}
-
-// counts[q_eff, nqueues) of a non-accumulating launch: queues no tuple can have
-int zero_counts_tail(uint64_t* d_counts, uint32_t q_eff, uint32_t nqueues, uint32_t flags,
-                     hipStream_t stream) {
-    if (d_counts && q_eff < nqueues && !(flags & RSS_FLAG_ACCUMULATE))
-        RSS_HIP_CHECK(hipMemsetAsync(d_counts + q_eff, 0, sizeof(uint64_t) * (nqueues - q_eff),
-                                     stream));
-    return RSS_OK;
-}
-
-// Modulo strategy (mask / exact 16-bit magic / exact 64-bit magic) and histogram
-// placement (private LDS columns / shared LDS bins / global atomics) for H and Q.
-// Returns whether H is a power of two.
-bool setup_modes(LaunchParams* p, uint32_t htable, uint32_t nqueues, bool want_counts, int* qmode,
-                 int* hist, uint32_t* bin_bytes, uint32_t bin_budget = kBinBytesMax,
-                 bool allow_fast8 = true) {
-    p->H = htable;
-    p->Q = nqueues;
-    p->h_mask = htable - 1;
-    p->h_m64 = magic64(htable);
-    if (nqueues >= htable) {  // bucket < htable <= nqueues: remainder is the bucket itself
-        *qmode = QM_MASK;
-        p->q_mask = 0xFFFFFFFFu;
-    } else if (is_pow2(nqueues)) {
-        *qmode = QM_MASK;
-        p->q_mask = nqueues - 1;
-    } else if (htable <= 65536u) {  // bucket < 2^16 and nqueues < htable <= 2^16
-        *qmode = htable <= 256u && allow_fast8 ? QM_FAST8 : QM_FAST16;
-        p->q_m32 = magic32(nqueues);
-        p->q_m16 = 65536u / nqueues + (65536u % nqueues != 0);
-    } else {
-        *qmode = QM_FAST32;
-        p->q_m64 = magic64(nqueues);
-    }
-    *bin_bytes = 0;
-    if (!want_counts) {
-        *hist = HIST_NONE;
-    } else if ((uint64_t)nqueues * kBinCols * 4 <= bin_budget) {
-        *hist = HIST_PRIVATE;
-        *bin_bytes = nqueues * kBinCols * 4;
-    } else if ((uint64_t)nqueues * 4 <= bin_budget) {
-        *hist = HIST_SHARED;
-        *bin_bytes = nqueues * 4;
-    } else {
-        *hist = HIST_GLOBAL;
-    }
-    return is_pow2(htable);
-}
-
-template <bool kHPow2, int kQMode, int kHist>
-KernelFn pick_search_vec(bool vec4) {
-    return vec4 ? rss_key_search_kernel<kHPow2, kQMode, kHist, true>
-                : rss_key_search_kernel<kHPow2, kQMode, kHist, false>;
-}
-
-template <bool kHPow2, int kQMode>
-KernelFn pick_search_hist(int hist, bool vec4) {
-    switch (hist) {
-        case HIST_PRIVATE: return pick_search_vec<kHPow2, kQMode, HIST_PRIVATE>(vec4);
-        case HIST_SHARED: return pick_search_vec<kHPow2, kQMode, HIST_SHARED>(vec4);
-        default: return pick_search_vec<kHPow2, kQMode, HIST_GLOBAL>(vec4);
-    }
-}
-
-template <bool kHPow2>
-KernelFn pick_search(int qmode, int hist, bool vec4) {
-    switch (qmode) {
-        case QM_MASK: return pick_search_hist<kHPow2, QM_MASK>(hist, vec4);
-        case QM_FAST16: return pick_search_hist<kHPow2, QM_FAST16>(hist, vec4);
-        default: return pick_search_hist<kHPow2, QM_FAST32>(hist, vec4);
-    }
-}
-
-// ~256K tuples per workgroup amortise its 120 KiB table build
-unsigned search_grid_x(size_t n, int cu_count) {
-    const uint64_t slices = (n + (1u << 18) - 1) >> 18;
-    return (unsigned)(slices < (uint64_t)cu_count ? slices : cu_count);
-}
-
-template <int kLaneBits, int kQMode>
-KernelFn pick_packed_vec(bool vec4) {
-    return vec4 ? rss_key_search_packed_kernel<kLaneBits, kQMode, true>
-                : rss_key_search_packed_kernel<kLaneBits, kQMode, false>;
-}
-
-KernelFn pick_packed(int lane_bits, int qmode, bool vec4) {
-    if (lane_bits == 8)
-        return qmode == QM_MASK ? pick_packed_vec<8, QM_MASK>(vec4) : pick_packed_vec<8, QM_FAST16>(vec4);
-    return qmode == QM_MASK ? pick_packed_vec<16, QM_MASK>(vec4) : pick_packed_vec<16, QM_FAST16>(vec4);
-}
-
-int launch_search(const uint32_t* d_windows, size_t nkeys, const rss_tuple4* d_tuples, size_t n,
-                  uint32_t htable, uint32_t nqueues, uint64_t* d_counts, hipStream_t stream) {
-    if (!d_windows || !d_counts || nkeys == 0)
-        return set_error(RSS_EINVAL, "rss_key_search_device: windows/counts NULL or no keys");
-    if (htable < 1 || nqueues < 1)
-        return set_error(RSS_EINVAL,
-                         "rss_key_search_device: htable (%u) and nqueues (%u) must be >= 1",
-                         htable, nqueues);
-    if (n && !d_tuples) return set_error(RSS_EINVAL, "rss_key_search_device: tuples is NULL");
-    RSS_HIP_CHECK(hipMemsetAsync(d_counts, 0, sizeof(uint64_t) * nqueues * nkeys, stream));
-    if (n == 0) return RSS_OK;
-    LaunchParams p;
-    memset(&p, 0, sizeof p);
-    p.tuples = d_tuples;
-    p.n = n;
-    p.q_stride = nqueues;  // rows keep the caller's nqueues; queues >= min(H, Q) stay zero
-    const uint32_t q_eff = effective_queues(htable, nqueues, nullptr);
-    int qmode, hist;
-    uint32_t bin_bytes;  // per key; a workgroup holds the bins of its two keys
-    const bool h_pow2 = setup_modes(&p, htable, q_eff, true, &qmode, &hist, &bin_bytes,
-                                    kWidePairBinBytesMax / 2, false);
-    const bool vec4 = aligned16(d_tuples);
-    DeviceInfo info;
-    int rc = device_info(&info);
-    if (rc) return rc;
-    // packed buckets (8 keys per table entry for H <= 256, 4 for H <= 65536) whenever
-    // their private bins fit (8 keys: Q <= 154, 4 keys: Q <= 309); else pairs of full hashes
-    const bool bytes_fit = (uint64_t)q_eff * 8 * kBinCols * 4 <= kPackedBinBytesMax;
-    const int lane_bits = htable <= 256u && bytes_fit ? 8 : 16;
-    const uint32_t keys_per_wg = 64 / lane_bits;
-    const uint64_t packed_bins = (uint64_t)q_eff * keys_per_wg * kBinCols * 4;
-    if (h_pow2 && htable <= 65536u && packed_bins <= kPackedBinBytesMax) {
-        p.q_m16 = 65536u / q_eff + (65536u % q_eff != 0);
-        KernelFn fn = pick_packed(lane_bits, qmode, vec4);
-        const unsigned gx = search_grid_x(n, info.cu_count);
-        const uint32_t shmem = (uint32_t)std::max<uint64_t>(packed_bins, kPackedPrepBytes);
-        const size_t max_keys = (size_t)keys_per_wg * 65535;  // grid.y limit
-        for (size_t k0 = 0; k0 < nkeys; k0 += max_keys) {
-            const size_t kn = nkeys - k0 < max_keys ? nkeys - k0 : max_keys;
-            p.key_windows = d_windows + k0 * RSS_INPUT_BITS;
-            p.counts = reinterpret_cast<unsigned long long*>(d_counts + k0 * nqueues);
-            p.nkeys = (uint32_t)kn;
-            hipLaunchKernelGGL(fn, dim3(gx, (unsigned)((kn + keys_per_wg - 1) / keys_per_wg)),
-                               dim3(kBlock), shmem, stream, p);
-            RSS_HIP_CHECK(hipGetLastError());
-        }
-        return RSS_OK;
-    }
-    KernelFn fn = h_pow2 ? pick_search<true>(qmode, hist, vec4) : pick_search<false>(qmode, hist, vec4);
-    const unsigned gx = search_grid_x(n, info.cu_count);
-    constexpr size_t kMaxKeysPerLaunch = 2 * 65535;  // grid.y (key pairs) limit
-    for (size_t k0 = 0; k0 < nkeys; k0 += kMaxKeysPerLaunch) {
-        const size_t kn = nkeys - k0 < kMaxKeysPerLaunch ? nkeys - k0 : kMaxKeysPerLaunch;
-        p.key_windows = d_windows + k0 * RSS_INPUT_BITS;
-        p.counts = reinterpret_cast<unsigned long long*>(d_counts + k0 * nqueues);
-        p.nkeys = (uint32_t)kn;
-        hipLaunchKernelGGL(fn, dim3(gx, (unsigned)((kn + 1) / 2)), dim3(kBlock), 2 * bin_bytes,
-                           stream, p);
-        RSS_HIP_CHECK(hipGetLastError());
-    }
-    return RSS_OK;
-}
-
-// An indirection table travels in the kernel arguments as u16[htable <= kRetaMax].
-int check_reta(const uint32_t* reta, uint32_t htable, uint32_t nqueues, const char* who) {
-    if (htable > kRetaMax)
-        return set_error(RSS_EINVAL, "%s: htable %u exceeds %u entries", who, htable, kRetaMax);
-    for (uint32_t b = 0; b < htable; ++b) {
-        if (reta[b] >= nqueues)
-            return set_error(RSS_EINVAL, "%s: reta[%u] = %u >= nqueues %u", who, b, reta[b],
-                             nqueues);
-        if (reta[b] > 0xFFFFu)
-            return set_error(RSS_EINVAL, "%s: reta[%u] = %u exceeds 65535", who, b, reta[b]);
-    }
-    return RSS_OK;
 }
 
 // ---------------------------------------------------------- path options ----
@@ -2942,11 +1812,6 @@ int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint
                  uint32_t flags, hipStream_t stream, const uint32_t* reta, uint64_t* ws) {
     return ::launch_hash6(key, d_tuples, n, htable, nqueues, d_hash, d_queue, d_counts, flags,
                           stream, reta, ws);
-}
-
-int launch_search(const uint32_t* d_windows, size_t nkeys, const rss_tuple4* d_tuples, size_t n,
-                  uint32_t htable, uint32_t nqueues, uint64_t* d_counts, hipStream_t stream) {
-    return ::launch_search(d_windows, nkeys, d_tuples, n, htable, nqueues, d_counts, stream);
 }
 
 int launch_generate(uint64_t seed, uint64_t first_index, size_t n, rss_tuple4* d_tuples,
