@@ -148,15 +148,15 @@ def test_default_exchange_is_one_collective_per_batch(monkeypatch):
 
 def test_committed_bench_lines_do_one_exchange_per_batch():
     """The world-size-1 RCCL run (torchrun --nproc-per-node 1) and the 8-rank gloo rehearsal
-    on one GPU (RSS_BENCH_DEVICE=0), as committed under profiles/r05/: the configs[3] and
+    on one GPU (RSS_BENCH_DEVICE=0), as committed under profiles/r06/: the configs[3] and
     per-rank blocks, ONE all-reduce per batch in the main line (VERDICT r03 item 2:
     simulator.py:100-116 makes one histogram per batch) and the 8-steps-per-collective form
     only as the labelled `bucketed` block."""
     import glob
     import os
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    paths = sorted(glob.glob(os.path.join(root, "profiles", "r05", "bench_lines", "*.json")))
-    assert paths, "no committed round-5 bench lines"
+    paths = sorted(glob.glob(os.path.join(root, "profiles", "r06", "bench_lines", "*.json")))
+    assert paths, "no committed round-6 bench lines"
     seen = set()
     for p in paths:
         with open(p) as f:
