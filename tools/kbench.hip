@@ -92,6 +92,55 @@ __global__ __launch_bounds__(1024) void mem_ceiling6_q8(Params p) {
     }
 }
 
+// the same IPv6 byte mix with lane-contiguous loads: instruction k of a wave reads bytes
+// [1024 k, 1024 k + 1024) of the wave's 9 KiB block (256 tuples), 16 B per lane -- the shape a
+// kernel that reassembled tuples across lanes would read; kRead = read-only (36 R)
+template <bool kRead>
+__global__ __launch_bounds__(1024) void mem_ceiling6_contig(Params p) {
+    const uint4* src = reinterpret_cast<const uint4*>(p.tuples);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t wave = ((uint64_t)blockIdx.x * 1024 + threadIdx.x) >> 6;
+    const uint64_t nwaves = ((uint64_t)gridDim.x * 1024) >> 6;
+    const uint64_t nblocks = p.n >> 8;  // 256 tuples = 576 uint4 per block
+    uint32_t keep = 0;
+    for (uint64_t b = wave; b < nblocks; b += nwaves) {
+        const uint4* blk = src + b * 576;
+        uint32_t acc[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            const uint4 x = blk[64 * k + lane];
+            acc[k & 3] ^= x.x ^ x.y ^ x.z ^ x.w;
+        }
+        if constexpr (kRead) {
+            keep ^= acc[0] ^ acc[1] ^ acc[2] ^ acc[3];
+        } else {
+            const uint64_t g = b * 64 + lane;  // the lane's 4 tuples' outputs, as the product
+            uint32_t* o = p.hash_out + 4 * g;
+            __builtin_nontemporal_store(acc[0], o);
+            __builtin_nontemporal_store(acc[1], o + 1);
+            __builtin_nontemporal_store(acc[2], o + 2);
+            __builtin_nontemporal_store(acc[3], o + 3);
+            __builtin_nontemporal_store((acc[0] ^ acc[3]) & 0x17171717u, p.queue_out + g);
+        }
+    }
+    if (kRead && keep == 0x12345678u) p.counts[0] = keep;
+}
+
+// IPv6 read-only stream in the product's shape (9 x 16-B loads per lane at a 144-B stride)
+__global__ __launch_bounds__(1024) void mem_ceiling6_read(Params p) {
+    const uint4* src = reinterpret_cast<const uint4*>(p.tuples);
+    const uint64_t ng = p.n >> 2;
+    uint32_t keep = 0;
+    for (uint64_t g = (uint64_t)blockIdx.x * 1024 + threadIdx.x; g < ng; g += (uint64_t)gridDim.x * 1024) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            const uint4 x = src[9 * g + k];
+            keep ^= x.x ^ x.y ^ x.z ^ x.w;
+        }
+    }
+    if (keep == 0x12345678u) p.counts[0] = keep;
+}
+
 typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
 // practical HBM ceilings for other read / write mixes on the same box: a float4 copy
 // (1 R : 1 W, the microarch guide's 6.29 TB/s shape) and a write-only fill
@@ -1019,6 +1068,25 @@ int main(int argc, char** argv) {
                    "stream 36R+5W %.3f ms (%.0f GB/s)  read-only 12n %.3f ms (%.0f GB/s)\n",
                    tk, n6 * 41e-9 / tk * 1e3, tc, n6 * 36e-9 / tc * 1e3, ts, n6 * 41e-9 / ts * 1e3,
                    tr, n * 12e-9 / tr * 1e3);
+        }
+    }
+
+    if (strstr("ipv6shape", filter)) {
+        // IPv6's load shape: the product's lane-owned 144 B (9 x 16-B loads at a 144-B stride)
+        // against lane-contiguous 1 KiB wave loads, 36 R + 5 W and read-only, same buffers
+        Params pp = p;
+        pp.n = (n / 3) & ~255ull;
+        pp.hash_out = h1;
+        pp.queue_out = q1;
+        const double gbw = pp.n * 41e-9, gbr = pp.n * 36e-9;
+        for (int round = 0; round < 3; ++round) {
+            const float s0 = time_ms([&] { hipLaunchKernelGGL(mem_ceiling6_q8, dim3(g_cus), dim3(1024), 0, 0, pp); }, reps);
+            const float s1 = time_ms([&] { hipLaunchKernelGGL(mem_ceiling6_contig<false>, dim3(g_cus), dim3(1024), 0, 0, pp); }, reps);
+            const float r0 = time_ms([&] { hipLaunchKernelGGL(mem_ceiling6_read, dim3(g_cus), dim3(1024), 0, 0, pp); }, reps);
+            const float r1 = time_ms([&] { hipLaunchKernelGGL(mem_ceiling6_contig<true>, dim3(g_cus), dim3(1024), 0, 0, pp); }, reps);
+            printf("ipv6shape  36R+5W strided %.3f ms (%.0f GB/s)  contiguous %.3f ms (%.0f GB/s)  "
+                   "36R strided %.3f ms (%.0f GB/s)  contiguous %.3f ms (%.0f GB/s)\n",
+                   s0, gbw / s0 * 1e3, s1, gbw / s1 * 1e3, r0, gbr / r0 * 1e3, r1, gbr / r1 * 1e3);
         }
     }
 
