@@ -237,3 +237,60 @@ def test_compute_queues6_devices_option(native, oracle_lib, example_key):
         assert int(h2[i]) == oracle_lib.hash_bytes(example_key, o.words_to_bytes(words[i]))
     np.testing.assert_array_equal(q2, h2 % 512 % 100)
     np.testing.assert_array_equal(c2, np.bincount(q2, minlength=100).astype(np.uint64))
+
+
+def test_every_context_entry_point_from_threads(native, oracle_lib, example_key, tmp_path):
+    """Every entry point that takes a context, interleaved from 8 threads on ONE context:
+    rss_hash_host, rss_hash6_host, rss_key_search_host, rss_csv_hash_text and
+    rss_csv_hash_file.  Each result equals the same call made alone (and the IPv4 / key-search
+    ones the oracle; the IPv6 ones the oracle on a sample)."""
+    from oracle import oracle as o
+    ctx = native.HostContext(0)
+    key = native.prepare_key(example_key)
+    key6 = native.prepare_key6(example_key)
+    rng = np.random.default_rng(61)
+    t4 = oracle_lib.generate(800, 0, 300000)
+    w6 = rng.integers(0, 2**32, size=(70001, 9), dtype=np.uint64).astype(np.uint32)
+    keys = [[int(b) for b in rng.permutation(256)[:40]] for _ in range(5)]
+    ks_tuples = oracle_lib.generate(801, 0, 50000)
+    text = _frame(oracle_lib.generate(802, 0, 20000)).to_csv(index=False).encode()
+    src = tmp_path / "in.csv"
+    src.write_bytes(text)
+
+    want4 = oracle_lib.run(example_key, t4, 512, 24)
+    want6 = ctx.hash6(key6, w6, 128, 24)
+    for i in rng.integers(0, len(w6), size=32):
+        assert int(want6[0][i]) == oracle_lib.hash_bytes(example_key, o.words_to_bytes(w6[i]))
+    want_ks = np.stack([oracle_lib.run(k, ks_tuples, 128, 24, want_hash=False,
+                                       want_queue=False)[2] for k in keys])
+    img, want_txt_counts, _ = ctx.csv_hash_text(key, text, 128, 24)
+    want_txt = img.tobytes()
+
+    def one(i):
+        kind = i % 5
+        if kind == 0:
+            h, q, c = ctx.hash(key, t4, 512, 24)
+            np.testing.assert_array_equal(h, want4[0])
+            np.testing.assert_array_equal(q, want4[1])
+            np.testing.assert_array_equal(c, want4[2])
+        elif kind == 1:
+            h, q, c = ctx.hash6(key6, w6, 128, 24)
+            for got, ref in zip((h, q, c), want6):
+                np.testing.assert_array_equal(got, ref)
+        elif kind == 2:
+            got = ctx.key_search([native.prepare_key(k) for k in keys], ks_tuples, 128, 24)
+            np.testing.assert_array_equal(got, want_ks)
+        elif kind == 3:
+            img, c, _ = ctx.csv_hash_text(key, text, 128, 24)
+            assert img.tobytes() == want_txt
+            np.testing.assert_array_equal(c, want_txt_counts)
+        else:
+            out = tmp_path / ("out%d.csv" % i)
+            c, n = ctx.csv_hash_file(key, str(src), str(out), 128, 24)
+            assert n == 20000 and out.read_bytes() == want_txt
+            np.testing.assert_array_equal(c, want_txt_counts)
+        return kind
+
+    with cf.ThreadPoolExecutor(THREADS) as pool:
+        assert sorted(set(pool.map(one, range(40)))) == [0, 1, 2, 3, 4]
+    ctx.close()
