@@ -929,30 +929,37 @@ __global__ __launch_bounds__(256) void rss_generate_kernel(uint64_t seed, uint64
 enum VecMode { VM_SCALAR = 0, VM_VEC4 = 1, VM_OFF32 = 2, VM_SMALL_LUT = 3 };
 template <bool kHPow2, int kQMode, int kHist, int kQWidth>
 KernelFn pick_vec_reachable(int vec4) {
+    // (an else-chain: a statement after an `if constexpr` block that returns is still
+    // instantiated, so every branch below is one alternative of the chain -- round 5's flat
+    // form instantiated 148 unreachable kernels)
     if constexpr (kHist == HIST_RANGE8) {  // small tables, u32 / u16-residual columns only
         if constexpr ((kQWidth == QW_U32 || kQWidth == QW_U16R) && kQMode != QM_FAST8 &&
-                      kQMode != QM_TABLE)
+                      kQMode != QM_TABLE) {
             if (vec4 == VM_SMALL_LUT)
                 return rss_toeplitz_kernel<kHPow2, kQMode, kHist, kQWidth, true, false, true>;
+        }
         return nullptr;
-    }
-    if constexpr (kQWidth == QW_U16R) {  // the small-table HIST_RANGE16 / RANGE8 bodies only
-        if constexpr (kHist == HIST_RANGE16 && kQMode != QM_FAST8 && kQMode != QM_TABLE)
+    } else if constexpr (kQWidth == QW_U16R) {  // the small-table HIST_RANGE16 / RANGE8 bodies only
+        if constexpr (kHist == HIST_RANGE16 && kQMode != QM_FAST8 && kQMode != QM_TABLE) {
             if (vec4 == VM_SMALL_LUT)
                 return rss_toeplitz_kernel<kHPow2, kQMode, kHist, kQWidth, true, false, true>;
+        }
         return nullptr;
+    } else {
+        if constexpr (kHist == HIST_PRIVATE || kHist == HIST_SHARED) {
+            if (vec4 == VM_OFF32) return rss_toeplitz_kernel<kHPow2, kQMode, kHist, kQWidth, true, true>;
+        }
+        if constexpr (kHist == HIST_RANGE16 && kQWidth != QW_U8 && kQMode != QM_FAST8 &&
+                      kQMode != QM_TABLE) {  // (H <= 1024 with those: never this many queues)
+            if (vec4 == VM_SMALL_LUT)
+                return rss_toeplitz_kernel<kHPow2, kQMode, kHist, kQWidth, true, false, true>;
+        }
+        // a small-table request with no small-table instance must not fall back to the 12-bit
+        // tables: the launcher sized the dynamic LDS for the small-table span
+        if (vec4 == VM_SMALL_LUT) return nullptr;
+        return vec4 ? rss_toeplitz_kernel<kHPow2, kQMode, kHist, kQWidth, true>
+                    : rss_toeplitz_kernel<kHPow2, kQMode, kHist, kQWidth, false>;
     }
-    if constexpr (kHist == HIST_PRIVATE || kHist == HIST_SHARED)
-        if (vec4 == VM_OFF32) return rss_toeplitz_kernel<kHPow2, kQMode, kHist, kQWidth, true, true>;
-    if constexpr (kHist == HIST_RANGE16 && kQWidth != QW_U8 && kQMode != QM_FAST8 &&
-                  kQMode != QM_TABLE)  // (H <= 1024 with those: never this many queues)
-        if (vec4 == VM_SMALL_LUT)
-            return rss_toeplitz_kernel<kHPow2, kQMode, kHist, kQWidth, true, false, true>;
-    // a small-table request with no small-table instance must not fall back to the 12-bit
-    // tables: the launcher sized the dynamic LDS for the small-table span
-    if (vec4 == VM_SMALL_LUT) return nullptr;
-    return vec4 ? rss_toeplitz_kernel<kHPow2, kQMode, kHist, kQWidth, true>
-                : rss_toeplitz_kernel<kHPow2, kQMode, kHist, kQWidth, false>;
 }
 
 // No launch reaches these combinations, so they are not instantiated: more than 7168 queues
