@@ -10,15 +10,13 @@
 #include "rss_internal.h"
 #include "rss_toeplitz.h"
 
-#define set_error rss_set_error
-
 // return the failing HIP call as RSS_ENOMEM / RSS_EIO with rss_last_error() set
 #define RSS_HIP_CHECK(expr)                                                        \
     do {                                                                           \
         hipError_t e_ = (expr);                                                    \
         if (e_ != hipSuccess)                                                      \
-            return set_error(e_ == hipErrorOutOfMemory ? RSS_ENOMEM : RSS_EIO,     \
-                             "%s failed: %s", #expr, hipGetErrorString(e_));       \
+            return rss_set_error(e_ == hipErrorOutOfMemory ? RSS_ENOMEM : RSS_EIO, \
+                                 "%s failed: %s", #expr, hipGetErrorString(e_));   \
     } while (0)
 
 namespace rss {

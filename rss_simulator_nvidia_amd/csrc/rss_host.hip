@@ -79,10 +79,10 @@ int rss_abi_version(void) { return RSS_ABI_VERSION; }
 const char* rss_last_error(void) { return g_last_error.c_str(); }
 
 int rss_key_prepare(const uint8_t* key, size_t len, rss_key* out) {
-    if (!key || !out) return set_error(RSS_EINVAL, "rss_key_prepare: NULL argument");
+    if (!key || !out) return rss_set_error(RSS_EINVAL, "rss_key_prepare: NULL argument");
     if (len < RSS_KEY_MIN_BYTES)
-        return set_error(RSS_EINVAL, "rss_key_prepare: key must hold >= %d bytes, got %zu",
-                         RSS_KEY_MIN_BYTES, len);
+        return rss_set_error(RSS_EINVAL, "rss_key_prepare: key must hold >= %d bytes, got %zu",
+                             RSS_KEY_MIN_BYTES, len);
     memset(out, 0, sizeof *out);
     out->len = (uint32_t)len;
     memcpy(out->bytes, key, len < RSS_KEY_MAX_BYTES ? len : RSS_KEY_MAX_BYTES);
@@ -93,9 +93,9 @@ int rss_key_prepare(const uint8_t* key, size_t len, rss_key* out) {
 
 int rss_key_select_fields(rss_key* key, uint32_t fields) {
     if (!key || key->len < RSS_KEY_MIN_BYTES)
-        return set_error(RSS_EINVAL, "rss_key_select_fields: key not prepared");
+        return rss_set_error(RSS_EINVAL, "rss_key_select_fields: key not prepared");
     if (fields == 0 || (fields & ~RSS_FIELDS_ALL))
-        return set_error(RSS_EINVAL, "rss_key_select_fields: bad field mask 0x%x", fields);
+        return rss_set_error(RSS_EINVAL, "rss_key_select_fields: bad field mask 0x%x", fields);
     // field f spans input bits [start[f], start[f] + width[f]) of the full tuple
     static const int kStart[4] = {0, 32, 64, 80}, kWidth[4] = {32, 32, 16, 16};
     remap_windows(key->window, RSS_INPUT_BITS, kStart, kWidth, 4, fields);
@@ -103,10 +103,10 @@ int rss_key_select_fields(rss_key* key, uint32_t fields) {
 }
 
 int rss_key6_prepare(const uint8_t* key, size_t len, rss_key6* out) {
-    if (!key || !out) return set_error(RSS_EINVAL, "rss_key6_prepare: NULL argument");
+    if (!key || !out) return rss_set_error(RSS_EINVAL, "rss_key6_prepare: NULL argument");
     if (len < RSS_KEY_MIN_BYTES)
-        return set_error(RSS_EINVAL, "rss_key6_prepare: key must hold >= %d bytes, got %zu",
-                         RSS_KEY_MIN_BYTES, len);
+        return rss_set_error(RSS_EINVAL, "rss_key6_prepare: key must hold >= %d bytes, got %zu",
+                             RSS_KEY_MIN_BYTES, len);
     memset(out, 0, sizeof *out);
     out->len = (uint32_t)len;
     rotation_windows(key, len, out->window, RSS_INPUT6_BITS);
@@ -115,9 +115,9 @@ int rss_key6_prepare(const uint8_t* key, size_t len, rss_key6* out) {
 
 int rss_key6_select_fields(rss_key6* key, uint32_t fields) {
     if (!key || key->len < RSS_KEY_MIN_BYTES)
-        return set_error(RSS_EINVAL, "rss_key6_select_fields: key not prepared");
+        return rss_set_error(RSS_EINVAL, "rss_key6_select_fields: key not prepared");
     if (fields == 0 || (fields & ~RSS_FIELDS_ALL))
-        return set_error(RSS_EINVAL, "rss_key6_select_fields: bad field mask 0x%x", fields);
+        return rss_set_error(RSS_EINVAL, "rss_key6_select_fields: bad field mask 0x%x", fields);
     static const int kStart[4] = {0, 128, 256, 272}, kWidth[4] = {128, 128, 16, 16};
     remap_windows(key->window, RSS_INPUT6_BITS, kStart, kWidth, 4, fields);
     return RSS_OK;
@@ -134,7 +134,7 @@ int rss_hash6_device_ws(const rss_key6* key, const rss_tuple6* d_tuples, size_t 
                         uint32_t htable, uint32_t nqueues, uint32_t* d_hash, void* d_queue,
                         uint64_t* d_counts, uint32_t flags, uint64_t* d_workspace, void* stream) {
     if (d_counts && (!d_workspace || ((uintptr_t)d_workspace & 7u)))
-        return set_error(RSS_EINVAL, "rss_hash6_device_ws: workspace NULL or not 8-byte aligned");
+        return rss_set_error(RSS_EINVAL, "rss_hash6_device_ws: workspace NULL or not 8-byte aligned");
     return rss::launch_hash6(key, d_tuples, n, htable, nqueues, d_hash, d_queue, d_counts, flags,
                              static_cast<hipStream_t>(stream), nullptr, d_workspace);
 }
@@ -143,7 +143,7 @@ int rss_hash6_device_reta(const rss_key6* key, const rss_tuple6* d_tuples, size_
                           uint32_t htable, const uint32_t* reta, uint32_t nqueues,
                           uint32_t* d_hash, void* d_queue, uint64_t* d_counts, uint32_t flags,
                           void* stream) {
-    if (!reta) return set_error(RSS_EINVAL, "rss_hash6_device_reta: reta is NULL");
+    if (!reta) return rss_set_error(RSS_EINVAL, "rss_hash6_device_reta: reta is NULL");
     return rss::launch_hash6(key, d_tuples, n, htable, nqueues, d_hash, d_queue, d_counts, flags,
                              static_cast<hipStream_t>(stream), reta);
 }
@@ -162,7 +162,7 @@ int rss_hash6_host(rss_ctx* ctx, const rss_key6* key, const rss_tuple6* h_tuples
 int rss_hash6_host_reta(rss_ctx* ctx, const rss_key6* key, const rss_tuple6* h_tuples, size_t n,
                         uint32_t htable, const uint32_t* reta, uint32_t nqueues, uint32_t* h_hash,
                         uint32_t* h_queue, uint64_t* h_counts, uint32_t flags) {
-    if (!reta) return set_error(RSS_EINVAL, "rss_hash6_host_reta: reta is NULL");
+    if (!reta) return rss_set_error(RSS_EINVAL, "rss_hash6_host_reta: reta is NULL");
     return hash6_host_impl(ctx, key, h_tuples, n, htable, nqueues, h_hash, h_queue, h_counts,
                            flags, reta);
 }
@@ -170,8 +170,8 @@ int rss_hash6_host_reta(rss_ctx* ctx, const rss_key6* key, const rss_tuple6* h_t
 static int hash6_host_impl(rss_ctx* ctx, const rss_key6* key, const rss_tuple6* h_tuples, size_t n,
                            uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
                            uint64_t* h_counts, uint32_t flags, const uint32_t* reta) {
-    if (!ctx) return set_error(RSS_EINVAL, "rss_hash6_host: ctx is NULL");
-    if (n && !h_tuples) return set_error(RSS_EINVAL, "rss_hash6_host: tuples is NULL");
+    if (!ctx) return rss_set_error(RSS_EINVAL, "rss_hash6_host: ctx is NULL");
+    if (n && !h_tuples) return rss_set_error(RSS_EINVAL, "rss_hash6_host: tuples is NULL");
     std::lock_guard<std::mutex> lock(ctx->mu);  // (struct rss_ctx)
     RSS_HIP_CHECK(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream[0];
@@ -193,8 +193,8 @@ static int hash6_host_impl(rss_ctx* ctx, const rss_key6* key, const rss_tuple6* 
         e = hipMemcpyAsync(d_t, h_tuples, n * sizeof(rss_tuple6), hipMemcpyHostToDevice, s);
     if (e != hipSuccess) {
         cleanup();
-        return set_error(e == hipErrorOutOfMemory ? RSS_ENOMEM : RSS_EIO, "rss_hash6_host: %s",
-                         hipGetErrorString(e));
+        return rss_set_error(e == hipErrorOutOfMemory ? RSS_ENOMEM : RSS_EIO, "rss_hash6_host: %s",
+                             hipGetErrorString(e));
     }
     int rc = rss::launch_hash6(key, d_t, n, htable, nqueues, d_h, d_q, d_c,
                                0u, s, reta);  // device counts start at 0; accumulation on the host
@@ -210,14 +210,14 @@ static int hash6_host_impl(rss_ctx* ctx, const rss_key6* key, const rss_tuple6* 
                     h_counts[q] = (flags & RSS_FLAG_ACCUMULATE ? h_counts[q] : 0) + tmp[q];
         }
         if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess) rc = set_error(RSS_EIO, "rss_hash6_host: %s", hipGetErrorString(e));
+        if (e != hipSuccess) rc = rss_set_error(RSS_EIO, "rss_hash6_host: %s", hipGetErrorString(e));
     }
     cleanup();
     return rc;
 }
 
 int rss_device_count(int* out) {
-    if (!out) return set_error(RSS_EINVAL, "rss_device_count: NULL argument");
+    if (!out) return rss_set_error(RSS_EINVAL, "rss_device_count: NULL argument");
     *out = 0;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) {
@@ -242,8 +242,8 @@ int rss_hash_device(const rss_key* key, const rss_tuple4* d_tuples, size_t n, ui
 }
 
 int rss_counts_workspace_bytes(uint32_t nqueues, size_t* out) {
-    if (!out) return set_error(RSS_EINVAL, "rss_counts_workspace_bytes: NULL argument");
-    if (nqueues < 1) return set_error(RSS_EINVAL, "rss_counts_workspace_bytes: nqueues must be >= 1");
+    if (!out) return rss_set_error(RSS_EINVAL, "rss_counts_workspace_bytes: NULL argument");
+    if (nqueues < 1) return rss_set_error(RSS_EINVAL, "rss_counts_workspace_bytes: nqueues must be >= 1");
     // a reserved word (ws[0], the rounds 2-3 fold's ticket; the size is ABI) + one arrival
     // accumulator per queue + the balanced tail's unit counter (fold_counts, walk_rows)
     *out = sizeof(uint64_t) * ((size_t)nqueues + 2);
@@ -254,7 +254,7 @@ int rss_hash_device_ws(const rss_key* key, const rss_tuple4* d_tuples, size_t n,
                        uint32_t nqueues, uint32_t* d_hash, void* d_queue, uint64_t* d_counts,
                        uint32_t flags, uint64_t* d_workspace, void* stream) {
     if (d_counts && (!d_workspace || ((uintptr_t)d_workspace & 7u)))
-        return set_error(RSS_EINVAL, "rss_hash_device_ws: workspace NULL or not 8-byte aligned");
+        return rss_set_error(RSS_EINVAL, "rss_hash_device_ws: workspace NULL or not 8-byte aligned");
     return rss::launch_hash(key, d_tuples, n, htable, nqueues, d_hash, d_queue, d_counts, flags,
                             static_cast<hipStream_t>(stream), nullptr, d_workspace);
 }
@@ -262,7 +262,7 @@ int rss_hash_device_ws(const rss_key* key, const rss_tuple4* d_tuples, size_t n,
 int rss_hash_device_reta(const rss_key* key, const rss_tuple4* d_tuples, size_t n,
                          uint32_t htable, const uint32_t* reta, uint32_t nqueues, uint32_t* d_hash,
                          void* d_queue, uint64_t* d_counts, uint32_t flags, void* stream) {
-    if (!reta) return set_error(RSS_EINVAL, "rss_hash_device_reta: reta is NULL");
+    if (!reta) return rss_set_error(RSS_EINVAL, "rss_hash_device_reta: reta is NULL");
     return rss::launch_hash(key, d_tuples, n, htable, nqueues, d_hash, d_queue, d_counts, flags,
                             static_cast<hipStream_t>(stream), reta);
 }
@@ -277,7 +277,7 @@ int rss_key_search_device(const uint32_t* d_windows, size_t nkeys, const rss_tup
 int rss_generate_tuples(uint64_t seed, uint64_t first_index, size_t n, rss_tuple4* d_tuples,
                         void* stream) {
     if (n == 0) return RSS_OK;
-    if (!d_tuples) return set_error(RSS_EINVAL, "rss_generate_tuples: tuples is NULL");
+    if (!d_tuples) return rss_set_error(RSS_EINVAL, "rss_generate_tuples: tuples is NULL");
     return rss::launch_generate(seed, first_index, n, d_tuples, static_cast<hipStream_t>(stream));
 }
 
@@ -301,20 +301,20 @@ void rss_ctx_destroy(rss_ctx* ctx) {
 }
 
 int rss_ctx_create(int device, rss_ctx** out) {
-    if (!out) return set_error(RSS_EINVAL, "rss_ctx_create: NULL argument");
+    if (!out) return rss_set_error(RSS_EINVAL, "rss_ctx_create: NULL argument");
     *out = nullptr;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
         (void)hipGetLastError();
-        return set_error(RSS_ENODEV, "rss_ctx_create: no HIP device visible");
+        return rss_set_error(RSS_ENODEV, "rss_ctx_create: no HIP device visible");
     }
     if (device < 0 || device >= ndev)
-        return set_error(RSS_EINVAL, "rss_ctx_create: device %d out of range [0, %d)", device, ndev);
+        return rss_set_error(RSS_EINVAL, "rss_ctx_create: device %d out of range [0, %d)", device, ndev);
     hipDeviceProp_t prop;
     RSS_HIP_CHECK(hipGetDeviceProperties(&prop, device));
     if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
-        return set_error(RSS_ENODEV, "rss_ctx_create: device %d is %s, this build targets gfx950",
-                         device, prop.gcnArchName);
+        return rss_set_error(RSS_ENODEV, "rss_ctx_create: device %d is %s, this build targets gfx950",
+                             device, prop.gcnArchName);
     rss_ctx* ctx = new rss_ctx();
     ctx->device = device;
     hipError_t e = hipSetDevice(device);
@@ -322,7 +322,7 @@ int rss_ctx_create(int device, rss_ctx** out) {
         e = hipStreamCreateWithFlags(&ctx->stream[b], hipStreamNonBlocking);
     if (e != hipSuccess) {
         rss_ctx_destroy(ctx);
-        return set_error(RSS_EIO, "rss_ctx_create: %s", hipGetErrorString(e));
+        return rss_set_error(RSS_EIO, "rss_ctx_create: %s", hipGetErrorString(e));
     }
     *out = ctx;
     return RSS_OK;
@@ -419,7 +419,7 @@ int rss_hash_host(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples, 
 int rss_hash_host_reta(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples, size_t n,
                        uint32_t htable, const uint32_t* reta, uint32_t nqueues, uint32_t* h_hash,
                        uint32_t* h_queue, uint64_t* h_counts, uint32_t flags) {
-    if (!reta) return set_error(RSS_EINVAL, "rss_hash_host_reta: reta is NULL");
+    if (!reta) return rss_set_error(RSS_EINVAL, "rss_hash_host_reta: reta is NULL");
     return hash_host_impl(ctx, key, h_tuples, n, htable, nqueues, h_hash, h_queue, h_counts, flags,
                           reta);
 }
@@ -429,18 +429,18 @@ int rss_hash_host_multi(rss_ctx* const* ctxs, int nctx, const rss_key* key,
                         const uint32_t* reta, uint32_t nqueues, uint32_t* h_hash,
                         uint32_t* h_queue, uint64_t* h_counts, uint32_t flags) {
     if (!ctxs || nctx < 1 || !key)
-        return set_error(RSS_EINVAL, "rss_hash_host_multi: NULL argument or no contexts");
+        return rss_set_error(RSS_EINVAL, "rss_hash_host_multi: NULL argument or no contexts");
     for (int i = 0; i < nctx; ++i) {
-        if (!ctxs[i]) return set_error(RSS_EINVAL, "rss_hash_host_multi: context %d is NULL", i);
+        if (!ctxs[i]) return rss_set_error(RSS_EINVAL, "rss_hash_host_multi: context %d is NULL", i);
         for (int j = 0; j < i; ++j)
             if (ctxs[j] == ctxs[i])
-                return set_error(RSS_EINVAL, "rss_hash_host_multi: contexts %d and %d are the same",
-                                 j, i);
+                return rss_set_error(RSS_EINVAL, "rss_hash_host_multi: contexts %d and %d are the same",
+                                     j, i);
     }
-    if (n && !h_tuples) return set_error(RSS_EINVAL, "rss_hash_host_multi: tuples is NULL");
+    if (n && !h_tuples) return rss_set_error(RSS_EINVAL, "rss_hash_host_multi: tuples is NULL");
     if (htable < 1 || nqueues < 1)
-        return set_error(RSS_EINVAL, "rss_hash_host_multi: htable (%u) and nqueues (%u) must be >= 1",
-                         htable, nqueues);
+        return rss_set_error(RSS_EINVAL, "rss_hash_host_multi: htable (%u) and nqueues (%u) must be >= 1",
+                             htable, nqueues);
     // contiguous ranges, exactly sharding.shard_range's: n / nctx each, the first n % nctx
     // ranges one longer
     const size_t base = n / (size_t)nctx, extra = n % (size_t)nctx;
@@ -464,7 +464,7 @@ int rss_hash_host_multi(rss_ctx* const* ctxs, int nctx, const rss_key* key,
     work(0);
     for (auto& t : pool) t.join();
     for (int i = 0; i < nctx; ++i)
-        if (rcs[i]) return set_error(rcs[i], "rss_hash_host_multi: context %d: %s", i, errs[i].c_str());
+        if (rcs[i]) return rss_set_error(rcs[i], "rss_hash_host_multi: context %d: %s", i, errs[i].c_str());
     if (h_counts) {
         if (!(flags & RSS_FLAG_ACCUMULATE)) memset(h_counts, 0, sizeof(uint64_t) * nqueues);
         for (int i = 0; i < nctx; ++i)
@@ -511,11 +511,11 @@ static bool host_pinned(const void* p, size_t bytes) {
 static int hash_host_impl(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples, size_t n,
                           uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
                           uint64_t* h_counts, uint32_t flags, const uint32_t* reta) {
-    if (!ctx) return set_error(RSS_EINVAL, "rss_hash_host: ctx is NULL");
-    if (n && !h_tuples) return set_error(RSS_EINVAL, "rss_hash_host: tuples is NULL");
+    if (!ctx) return rss_set_error(RSS_EINVAL, "rss_hash_host: ctx is NULL");
+    if (n && !h_tuples) return rss_set_error(RSS_EINVAL, "rss_hash_host: tuples is NULL");
     if (htable < 1 || nqueues < 1)
-        return set_error(RSS_EINVAL, "rss_hash_host: htable (%u) and nqueues (%u) must be >= 1",
-                         htable, nqueues);
+        return rss_set_error(RSS_EINVAL, "rss_hash_host: htable (%u) and nqueues (%u) must be >= 1",
+                             htable, nqueues);
     std::lock_guard<std::mutex> lock(ctx->mu);  // (struct rss_ctx)
     RSS_HIP_CHECK(hipSetDevice(ctx->device));
     if (n > 0 && n <= kSmallBatch)
@@ -596,7 +596,7 @@ static int hash_host_impl(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_
 }
 
 int rss_host_alloc(size_t bytes, void** out) {
-    if (!out) return set_error(RSS_EINVAL, "rss_host_alloc: NULL argument");
+    if (!out) return rss_set_error(RSS_EINVAL, "rss_host_alloc: NULL argument");
     *out = nullptr;
     RSS_HIP_CHECK(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
     return RSS_OK;
@@ -610,14 +610,14 @@ int rss_key_search_host(rss_ctx* ctx, const rss_key* keys, size_t nkeys,
                         const rss_tuple4* h_tuples, size_t n, uint32_t htable, uint32_t nqueues,
                         uint64_t* h_counts) {
     if (!ctx || !keys || !h_counts || nkeys == 0)
-        return set_error(RSS_EINVAL, "rss_key_search_host: NULL argument or no keys");
-    if (n && !h_tuples) return set_error(RSS_EINVAL, "rss_key_search_host: tuples is NULL");
+        return rss_set_error(RSS_EINVAL, "rss_key_search_host: NULL argument or no keys");
+    if (n && !h_tuples) return rss_set_error(RSS_EINVAL, "rss_key_search_host: tuples is NULL");
     std::lock_guard<std::mutex> lock(ctx->mu);  // (struct rss_ctx)
     RSS_HIP_CHECK(hipSetDevice(ctx->device));
     std::vector<uint32_t> windows(nkeys * RSS_INPUT_BITS);
     for (size_t k = 0; k < nkeys; ++k) {
         if (keys[k].len < RSS_KEY_MIN_BYTES)
-            return set_error(RSS_EINVAL, "rss_key_search_host: key %zu not prepared", k);
+            return rss_set_error(RSS_EINVAL, "rss_key_search_host: key %zu not prepared", k);
         memcpy(&windows[k * RSS_INPUT_BITS], keys[k].window, sizeof keys[k].window);
     }
     uint32_t* d_w = nullptr;
@@ -640,8 +640,8 @@ int rss_key_search_host(rss_ctx* ctx, const rss_key* keys, size_t nkeys,
         e = hipMemcpyAsync(d_t, h_tuples, n * sizeof(rss_tuple4), hipMemcpyHostToDevice, s);
     if (e != hipSuccess) {
         cleanup();
-        return set_error(e == hipErrorOutOfMemory ? RSS_ENOMEM : RSS_EIO, "rss_key_search_host: %s",
-                         hipGetErrorString(e));
+        return rss_set_error(e == hipErrorOutOfMemory ? RSS_ENOMEM : RSS_EIO, "rss_key_search_host: %s",
+                             hipGetErrorString(e));
     }
     rc = rss::launch_search(d_w, nkeys, d_t, n, htable, nqueues, d_c, s);
     if (rc == RSS_OK) {
@@ -649,7 +649,7 @@ int rss_key_search_host(rss_ctx* ctx, const rss_key* keys, size_t nkeys,
                            hipMemcpyDeviceToHost, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess)
-            rc = set_error(RSS_EIO, "rss_key_search_host: %s", hipGetErrorString(e));
+            rc = rss_set_error(RSS_EIO, "rss_key_search_host: %s", hipGetErrorString(e));
     }
     cleanup();
     return rc;

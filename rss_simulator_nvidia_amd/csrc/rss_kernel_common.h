@@ -701,13 +701,13 @@ inline bool setup_modes(LaunchParams* p, uint32_t htable, uint32_t nqueues, bool
 // An indirection table travels in the kernel arguments as u16[htable <= kRetaMax].
 inline int check_reta(const uint32_t* reta, uint32_t htable, uint32_t nqueues, const char* who) {
     if (htable > kRetaMax)
-        return set_error(RSS_EINVAL, "%s: htable %u exceeds %u entries", who, htable, kRetaMax);
+        return rss_set_error(RSS_EINVAL, "%s: htable %u exceeds %u entries", who, htable, kRetaMax);
     for (uint32_t b = 0; b < htable; ++b) {
         if (reta[b] >= nqueues)
-            return set_error(RSS_EINVAL, "%s: reta[%u] = %u >= nqueues %u", who, b, reta[b],
-                             nqueues);
+            return rss_set_error(RSS_EINVAL, "%s: reta[%u] = %u >= nqueues %u", who, b, reta[b],
+                                 nqueues);
         if (reta[b] > 0xFFFFu)
-            return set_error(RSS_EINVAL, "%s: reta[%u] = %u exceeds 65535", who, b, reta[b]);
+            return rss_set_error(RSS_EINVAL, "%s: reta[%u] = %u exceeds 65535", who, b, reta[b]);
     }
     return RSS_OK;
 }

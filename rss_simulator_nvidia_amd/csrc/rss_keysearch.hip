@@ -397,12 +397,12 @@ KernelFn pick_packed(int lane_bits, int qmode, bool vec4) {
 int launch_search(const uint32_t* d_windows, size_t nkeys, const rss_tuple4* d_tuples, size_t n,
                   uint32_t htable, uint32_t nqueues, uint64_t* d_counts, hipStream_t stream) {
     if (!d_windows || !d_counts || nkeys == 0)
-        return set_error(RSS_EINVAL, "rss_key_search_device: windows/counts NULL or no keys");
+        return rss_set_error(RSS_EINVAL, "rss_key_search_device: windows/counts NULL or no keys");
     if (htable < 1 || nqueues < 1)
-        return set_error(RSS_EINVAL,
-                         "rss_key_search_device: htable (%u) and nqueues (%u) must be >= 1",
-                         htable, nqueues);
-    if (n && !d_tuples) return set_error(RSS_EINVAL, "rss_key_search_device: tuples is NULL");
+        return rss_set_error(RSS_EINVAL,
+                             "rss_key_search_device: htable (%u) and nqueues (%u) must be >= 1",
+                             htable, nqueues);
+    if (n && !d_tuples) return rss_set_error(RSS_EINVAL, "rss_key_search_device: tuples is NULL");
     RSS_HIP_CHECK(hipMemsetAsync(d_counts, 0, sizeof(uint64_t) * nqueues * nkeys, stream));
     if (n == 0) return RSS_OK;
     LaunchParams p;

@@ -1133,7 +1133,7 @@ int free_block(void* buf, int rc, hipStream_t stream) {
     if (!buf) return rc;
     const hipError_t fe = hipFreeAsync(buf, stream);
     if (fe != hipSuccess && rc == RSS_OK)
-        rc = set_error(RSS_EIO, "hipFreeAsync failed: %s", hipGetErrorString(fe));
+        rc = rss_set_error(RSS_EIO, "hipFreeAsync failed: %s", hipGetErrorString(fe));
     return rc;
 }
 
@@ -1257,13 +1257,13 @@ int launch_queue_ranges(const void* qcol, int qw, uint64_t n, uint32_t first, ui
                                                            region_counts, region_cap);
             }
             if (e != hipSuccess)
-                return set_error(RSS_EIO, "wide queue histogram launch failed: %s", hipGetErrorString(e));
+                return rss_set_error(RSS_EIO, "wide queue histogram launch failed: %s", hipGetErrorString(e));
             lo += sp;
         }
         return RSS_OK;
     }
     if (region_counts)
-        return set_error(RSS_EIO, "rss_hash_device: residual lists without the wide passes' scratch");
+        return rss_set_error(RSS_EIO, "rss_hash_device: residual lists without the wide passes' scratch");
     const uint32_t span = kNarrowSpan;
     const uint64_t qwant = (n + 8ull * kBlock - 1) / (8ull * kBlock);
     const unsigned qgrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(qwant, (uint64_t)cu_count * 2));
@@ -1307,7 +1307,7 @@ int launch_guarded(KernelFn fn, FallbackFn fallback, int bits, unsigned grid, in
     const bool col = qcol && (qw == QW_U32 || qw == QW_U16);
     if (!fn || (!col && !fallback)) {
         (void)hipFreeAsync(buf, stream);
-        return set_error(RSS_EIO, "rss_hash_device: no kernel instance for this launch");
+        return rss_set_error(RSS_EIO, "rss_hash_device: no kernel instance for this launch");
     }
     const uint32_t words = guard_words(bits, p.q_span);
     uint32_t* tail = reinterpret_cast<uint32_t*>(static_cast<char*>(buf) + guard_rows_bytes(grid, words));
@@ -1346,7 +1346,7 @@ int launch_guarded(KernelFn fn, FallbackFn fallback, int bits, unsigned grid, in
         e = hipGetLastError();
     }
     int rc = e == hipSuccess ? RSS_OK
-                             : set_error(RSS_EIO, "rss_hash_device: launch failed: %s", hipGetErrorString(e));
+                             : rss_set_error(RSS_EIO, "rss_hash_device: launch failed: %s", hipGetErrorString(e));
     rc = free_block(buf, rc, stream);
     p.partial = nullptr;
     p.ovf = p.poison = nullptr;
@@ -1362,13 +1362,13 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
                 uint32_t nqueues, uint32_t* d_hash, void* d_queue, uint64_t* d_counts,
                 uint32_t flags, hipStream_t stream, const uint32_t* reta = nullptr,
                 uint64_t* ws = nullptr) {
-    if (!key) return set_error(RSS_EINVAL, "rss_hash_device: key is NULL");
+    if (!key) return rss_set_error(RSS_EINVAL, "rss_hash_device: key is NULL");
     if (key->len < RSS_KEY_MIN_BYTES)
-        return set_error(RSS_EINVAL, "rss_hash_device: key not prepared (len=%u)", key->len);
+        return rss_set_error(RSS_EINVAL, "rss_hash_device: key not prepared (len=%u)", key->len);
     if (htable < 1 || nqueues < 1)
-        return set_error(RSS_EINVAL, "rss_hash_device: htable (%u) and nqueues (%u) must be >= 1",
-                         htable, nqueues);
-    if (n && !d_tuples) return set_error(RSS_EINVAL, "rss_hash_device: tuples is NULL");
+        return rss_set_error(RSS_EINVAL, "rss_hash_device: htable (%u) and nqueues (%u) must be >= 1",
+                             htable, nqueues);
+    if (n && !d_tuples) return rss_set_error(RSS_EINVAL, "rss_hash_device: tuples is NULL");
     if (reta) {
         const int rc = check_reta(reta, htable, nqueues, "rss_hash_device_reta");
         if (rc) return rc;
@@ -1378,12 +1378,12 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
     int qwidth = QW_U32;
     if (flags & RSS_FLAG_QUEUE_U8) {
         if (q_eff > 256)
-            return set_error(RSS_EINVAL, "rss_hash_device: RSS_FLAG_QUEUE_U8 needs min(htable, nqueues) <= 256 "
+            return rss_set_error(RSS_EINVAL, "rss_hash_device: RSS_FLAG_QUEUE_U8 needs min(htable, nqueues) <= 256 "
                                          "(got %u)", q_eff);
         qwidth = QW_U8;
     } else if (flags & RSS_FLAG_QUEUE_U16) {
         if (q_eff > 65536)
-            return set_error(RSS_EINVAL, "rss_hash_device: RSS_FLAG_QUEUE_U16 needs min(htable, nqueues) <= 65536 "
+            return rss_set_error(RSS_EINVAL, "rss_hash_device: RSS_FLAG_QUEUE_U16 needs min(htable, nqueues) <= 65536 "
                                          "(got %u)", q_eff);
         qwidth = QW_U16;
     }
@@ -1601,7 +1601,7 @@ int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32
     const int vmode = vec4 ? (12ull * n < (1ull << 32) && !(flags & RSS_FLAG_ADDR64) ? 2 : 1) : 0;
     KernelFn fn = h_pow2 ? pick_queue<true>(qmode, hist, qwidth, vmode)
                          : pick_queue<false>(qmode, hist, qwidth, vmode);
-    if (!fn) return set_error(RSS_EIO, "rss_hash_device: no kernel instance for this launch");
+    if (!fn) return rss_set_error(RSS_EIO, "rss_hash_device: no kernel instance for this launch");
     uint32_t shmem = bin_bytes + reta_bytes;  // dynamic part; the 128 KiB LUT is static
     // Balanced tail (single-pass launches: the workspace holds its unit counter and is used
     // by one launch at a time): the last ~1/10 of the grid-stride rows handed out per
@@ -1656,11 +1656,11 @@ int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint
                  uint32_t flags, hipStream_t stream, const uint32_t* reta = nullptr,
                  uint64_t* ws = nullptr) {
     if (!key || key->len < RSS_KEY_MIN_BYTES)
-        return set_error(RSS_EINVAL, "rss_hash6_device: key NULL or not prepared");
+        return rss_set_error(RSS_EINVAL, "rss_hash6_device: key NULL or not prepared");
     if (htable < 1 || nqueues < 1)
-        return set_error(RSS_EINVAL, "rss_hash6_device: htable (%u) and nqueues (%u) must be >= 1",
-                         htable, nqueues);
-    if (n && !d_tuples) return set_error(RSS_EINVAL, "rss_hash6_device: tuples is NULL");
+        return rss_set_error(RSS_EINVAL, "rss_hash6_device: htable (%u) and nqueues (%u) must be >= 1",
+                             htable, nqueues);
+    if (n && !d_tuples) return rss_set_error(RSS_EINVAL, "rss_hash6_device: tuples is NULL");
     if (reta) {
         const int rc = check_reta(reta, htable, nqueues, "rss_hash6_device_reta");
         if (rc) return rc;
@@ -1669,12 +1669,12 @@ int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint
     uint32_t qwidth = QW_U32;
     if (flags & RSS_FLAG_QUEUE_U8) {
         if (q_eff > 256)
-            return set_error(RSS_EINVAL, "rss_hash6_device: RSS_FLAG_QUEUE_U8 needs min(htable, nqueues) <= 256 "
+            return rss_set_error(RSS_EINVAL, "rss_hash6_device: RSS_FLAG_QUEUE_U8 needs min(htable, nqueues) <= 256 "
                                          "(got %u)", q_eff);
         qwidth = QW_U8;
     } else if (flags & RSS_FLAG_QUEUE_U16) {
         if (q_eff > 65536)
-            return set_error(RSS_EINVAL, "rss_hash6_device: RSS_FLAG_QUEUE_U16 needs min(htable, nqueues) <= 65536 "
+            return rss_set_error(RSS_EINVAL, "rss_hash6_device: RSS_FLAG_QUEUE_U16 needs min(htable, nqueues) <= 65536 "
                                          "(got %u)", q_eff);
         qwidth = QW_U16;
     }
@@ -1778,8 +1778,8 @@ int launch_hash6(const rss_key6* key, const rss_tuple6* d_tuples, size_t n, uint
                     rc = le == hipSuccess
                              ? launch_queue_ranges(qcol, (int)qw, n, span, q_eff, p.counts, info.cu_count, stream,
                                                    &wsc)
-                             : set_error(RSS_EIO, "rss_hash6_device: range launch failed: %s",
-                                         hipGetErrorString(le));
+                             : rss_set_error(RSS_EIO, "rss_hash6_device: range launch failed: %s",
+                                             hipGetErrorString(le));
                     rc = free_block(wsc.buf, rc, stream);
                     return free_block(scratch ? qcol : nullptr, rc, stream);
                 }
@@ -1848,7 +1848,7 @@ uint32_t g_guard_sleep_host = 0;  // the value last copied to g_guard_sleep
 extern "C" {
 
 int rss_test_set_option(const char* name, int value) {
-    if (!name) return set_error(RSS_EINVAL, "rss_test_set_option: NULL name");
+    if (!name) return rss_set_error(RSS_EINVAL, "rss_test_set_option: NULL name");
     const std::string n(name);
     if (n == "recount") g_opt.recount = value;
     else if (n == "range8") g_opt.range8 = value != 0;
@@ -1863,7 +1863,7 @@ int rss_test_set_option(const char* name, int value) {
         const uint32_t v = value > 0 ? (uint32_t)value : 0u;
         RSS_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_guard_sleep), &v, sizeof v));
         g_guard_sleep_host = v;
-    } else return set_error(RSS_EINVAL, "rss_test_set_option: unknown option '%s'", name);
+    } else return rss_set_error(RSS_EINVAL, "rss_test_set_option: unknown option '%s'", name);
     return RSS_OK;
 }
 
@@ -1878,7 +1878,7 @@ void rss_test_reset_options(void) {
 }
 
 int rss_test_guard_margin(uint32_t* out, int reset) {
-    if (!out) return set_error(RSS_EINVAL, "rss_test_guard_margin: NULL out");
+    if (!out) return rss_set_error(RSS_EINVAL, "rss_test_guard_margin: NULL out");
     RSS_HIP_CHECK(hipDeviceSynchronize());
     RSS_HIP_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_guard_margin), sizeof(uint32_t) * kMargins));
     if (reset) {
