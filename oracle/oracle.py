@@ -20,7 +20,8 @@ Contents (each restates noamsto/rss_simulator_nvidia v0.0.2):
 * :func:`hash_batch_np` -- vectorised closed form (window i = key bits [i, i+32)),
   numpy, for mid-size checks.
 * :class:`OracleLib` -- ctypes binding of ``oracle/liboracle.so`` (the C restatement
-  with the literal rotating key, ``oracle/toeplitz_oracle.c``) for large-N checks.
+  with the literal rotating key, ``oracle/toeplitz_oracle.c``) for large-N checks, incl.
+  ``run_words`` for tuples of any number of words (the 9-word IPv6 tuple).
 * :func:`generate_np` -- the splitmix64 synthetic-tuple generator of
   ``include/rss_toeplitz.h`` (``rss_generate_tuples``).
 * :func:`queue_and_counts` -- ``simulator.py:94-98`` and the ``value_counts`` of
@@ -192,6 +193,10 @@ class OracleLib:
         lib.oracle_windows_n.restype = ctypes.c_int
         lib.oracle_hash_bytes.argtypes = [u8p, ctypes.c_size_t, u8p, ctypes.c_size_t]
         lib.oracle_hash_bytes.restype = ctypes.c_uint32
+        lib.oracle_run_words.argtypes = [u8p, ctypes.c_size_t, u32p, ctypes.c_int, ctypes.c_size_t,
+                                         ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, u64p,
+                                         ctypes.c_int]
+        lib.oracle_run_words.restype = ctypes.c_int
         lib.oracle_generate.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t, u32p]
         lib.oracle_generate.restype = None
         self._lib = lib
@@ -244,6 +249,24 @@ class OracleLib:
             c.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), threads or os.cpu_count() or 1)
         if rc:
             raise ValueError("%s failed (%d)" % (fn, rc))
+        return h, q, c
+
+    def run_words(self, key, words, htable, nqueues, threads=None):
+        """(hash, queue, counts) for tuples of big-endian-valued uint32 words, shape (n, W):
+        W = 9 is the 36-byte IPv6 tuple (``oracle_run_words``, the literal loop's windows)."""
+        words = np.ascontiguousarray(words, dtype=np.uint32)
+        n, nw = words.shape
+        k, klen = self._key(key)
+        h = np.empty(n, dtype=np.uint32)
+        q = np.empty(n, dtype=np.uint32)
+        c = np.zeros(nqueues, dtype=np.uint64)
+        u32p = ctypes.POINTER(ctypes.c_uint32)
+        rc = self._lib.oracle_run_words(k, klen, words.ctypes.data_as(u32p), nw, n, htable, nqueues,
+                                        h.ctypes.data_as(u32p), q.ctypes.data_as(u32p),
+                                        c.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                        threads or os.cpu_count() or 1)
+        if rc:
+            raise ValueError("oracle_run_words failed (%d)" % rc)
         return h, q, c
 
     def generate(self, seed, first_index, n):

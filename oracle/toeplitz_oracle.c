@@ -236,6 +236,51 @@ int oracle_run_tables(const uint8_t* key, size_t len, const uint32_t* tuples, si
     return 0;
 }
 
+/*
+ * Batch form over tuples of `nwords` big-endian-valued uint32 words each (the input bytes
+ * are the words' big-endian bytes: nwords = 3 is oracle_run's packed IPv4 tuple, 9 the
+ * 36-byte IPv6 tuple -- src 16 B, dst 16 B, sport << 16 | dport).  The same literal loop as
+ * oracle_hash_bytes, with the rotations precomputed as the 32 * nwords windows
+ * (oracle_windows_n); hash % htable % nqueues and the histogram as oracle_run.  Any output
+ * may be NULL; counts (nqueues entries) is overwritten.  Returns 0 or -22.
+ */
+int oracle_run_words(const uint8_t* key, size_t len, const uint32_t* words, int nwords, size_t n,
+                     uint32_t htable, uint32_t nqueues, uint32_t* hash_out, uint32_t* queue_out,
+                     uint64_t* counts, int threads) {
+    if (nwords < 1 || nwords > 16 || htable < 1 || nqueues < 1) return -22;
+    uint32_t w[32 * 16];
+    if (oracle_windows_n(key, len, 32 * nwords, w)) return -22;
+    if (counts) memset(counts, 0, sizeof(uint64_t) * nqueues);
+#ifdef _OPENMP
+    if (threads < 1) threads = 1;
+#pragma omp parallel num_threads(threads)
+#endif
+    {
+        uint64_t* local = counts ? calloc(nqueues, sizeof(uint64_t)) : NULL;
+#ifdef _OPENMP
+#pragma omp for schedule(static)
+#endif
+        for (int64_t i = 0; i < (int64_t)n; ++i) {
+            const uint32_t* t = words + (size_t)nwords * i;
+            uint32_t h = 0;
+            for (int b = 0; b < 32 * nwords; ++b)  /* input bit b: MSB first, word by word */
+                if ((t[b >> 5] >> (31 - (b & 31))) & 1) h ^= w[b];
+            const uint32_t q = (h % htable) % nqueues;
+            if (hash_out) hash_out[i] = h;
+            if (queue_out) queue_out[i] = q;
+            if (local) ++local[q];
+        }
+        if (local) {
+#ifdef _OPENMP
+#pragma omp critical
+#endif
+            for (uint32_t q = 0; q < nqueues; ++q) counts[q] += local[q];
+            free(local);
+        }
+    }
+    return 0;
+}
+
 /* splitmix64 finaliser; the synthetic generator of include/rss_toeplitz.h. */
 static inline uint64_t mix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;

@@ -122,3 +122,34 @@ def test_table_form_equals_window_form(random_golden, oracle_lib):
             np.testing.assert_array_equal(a[0], g["hashes"][k])
             for x, y in zip(a, b):
                 np.testing.assert_array_equal(x, y)
+
+
+def test_word_tuple_batch_pinned(random_golden, golden_dir, oracle_lib):
+    """oracle_run_words (the IPv6 checker of tests/test_gpu_ipv6_oracle.py): with 3 words per
+    tuple it is oracle_run on the reference-made F3 hashes, all four keys; with 9 words it is
+    the literal rotating loop over the 36 input bytes (oracle_hash_bytes) and the Microsoft
+    IPv6 KAT."""
+    tup = random_golden["tuples"]
+    for k, key in enumerate(random_golden["key_list"]):
+        h, q, c = oracle_lib.run_words(key, tup, 128, 24)
+        np.testing.assert_array_equal(h, random_golden["hashes"][k].astype(np.uint32))
+        ho, qo, co = oracle_lib.run(key, tup, 128, 24)
+        np.testing.assert_array_equal(q, qo)
+        np.testing.assert_array_equal(c, co)
+    rng = np.random.default_rng(9)
+    for key in random_golden["key_list"]:
+        words = rng.integers(0, 2**32, (300, 9), dtype=np.uint64).astype(np.uint32)
+        h, q, c = oracle_lib.run_words(key, words, 1000, 77)
+        want = np.array([oracle_lib.hash_bytes(key, o.words_to_bytes(r)) for r in words],
+                        dtype=np.uint32)
+        np.testing.assert_array_equal(h, want)
+        np.testing.assert_array_equal(q, want % 1000 % 77)
+        np.testing.assert_array_equal(c, np.bincount(q, minlength=77).astype(np.uint64))
+    from rss_simulator_nvidia_amd.ingest import ipv6_words
+    kat = json.load(open(os.path.join(golden_dir, "ms_kat_ipv6.json")))
+    key = [int(x, 16) for x in kat["key"].split(":")]
+    words = np.array([ipv6_words(v["src_ip"]) + ipv6_words(v["dst_ip"]) +
+                      [(v["src_port"] << 16) | v["dst_port"]] for v in kat["vectors"]],
+                     dtype=np.uint32)
+    h, _, _ = oracle_lib.run_words(key, words, 1, 1)
+    assert [int(x) for x in h] == [int(v["hash_hex"], 16) for v in kat["vectors"]]
