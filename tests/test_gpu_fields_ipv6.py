@@ -1,6 +1,7 @@
 """GPU parity for field selection (IPv4 kernel with remapped windows) and the IPv6 kernel:
 bit-exact against the literal rotating-key oracle over the selected bytes and the
-Microsoft verification-suite vectors."""
+Microsoft verification-suite vectors; at scale (2^20 tuples per mask) against
+oracle_run_words over the selected, zero-padded bytes."""
 import json
 import os
 
@@ -242,3 +243,62 @@ def test_cli_ipv6_csv_fast_path_equals_pandas_path(tmp_path, golden_dir, monkeyp
         assert status == 0, exc
         outs.append(out.read_bytes())
     assert outs[0] == outs[1]
+
+
+def _selected_words(words, spans, mask):
+    """The bytes of the selected fields (spans: (bit, first byte, length) of the big-endian
+    input), concatenated and zero-padded to whole words: zero bits add nothing to a Toeplitz
+    hash, so oracle_run_words over them is the literal loop over the selected bytes."""
+    raw = words.astype(">u4").view(np.uint8).reshape(len(words), -1)
+    cols = [raw[:, a:a + n] for bit, a, n in spans if mask & bit]
+    sel = np.concatenate(cols, axis=1)
+    pad = (-sel.shape[1]) % 4
+    if pad:
+        sel = np.concatenate([sel, np.zeros((len(sel), pad), np.uint8)], axis=1)
+    return np.ascontiguousarray(sel).view(">u4").astype(np.uint32)
+
+
+@pytest.mark.parametrize("mask", [1, 2, 3, 4, 5, 8, 10, 12, 14, 15])
+def test_ipv4_field_masks_at_scale(native, oracle_lib, example_key, mask):
+    """2^20 + 3 tuples per field mask through the device API, element by element against
+    oracle_run_words over the selected bytes (tests/test_oracle.py pins it to the literal
+    loop); the 15-mask row is the reference's whole-tuple hash."""
+    n = (1 << 20) + 3
+    host = oracle_lib.generate(90 + mask, 0, n)
+    spans = [(1, 0, 4), (2, 4, 4), (4, 8, 2), (8, 10, 2)]
+    ho, qo, co = oracle_lib.run_words(example_key, _selected_words(host, spans, mask), 512, 24)
+    dev = torch.device("cuda:0")
+    t = torch.from_numpy(host.view(np.int32).reshape(-1)).to(dev)
+    h = torch.empty(n, dtype=torch.int32, device=dev)
+    q = torch.empty(n, dtype=torch.int32, device=dev)
+    c = torch.empty(24, dtype=torch.int64, device=dev)
+    native.hash_device(native.prepare_key(example_key, mask), t.data_ptr(), n, 512, 24,
+                       h.data_ptr(), q.data_ptr(), c.data_ptr(), 0,
+                       torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(h.cpu().numpy().view(np.uint32), ho)
+    np.testing.assert_array_equal(q.cpu().numpy().view(np.uint32), qo)
+    np.testing.assert_array_equal(c.cpu().numpy().view(np.uint64), co)
+
+
+@pytest.mark.parametrize("mask", [3, 12, 1, 15])
+def test_ipv6_field_masks_at_scale(native, oracle_lib, example_key, mask):
+    """The IPv6 kernel with remapped windows: 2^20 + 1 tuples per mask ("sd" = the IPv6-only
+    hash) against oracle_run_words over the selected bytes."""
+    n = (1 << 20) + 1
+    rng = np.random.default_rng(mask)
+    host = rng.integers(0, 2**32, size=(n, 9), dtype=np.uint64).astype(np.uint32)
+    spans = [(1, 0, 16), (2, 16, 16), (4, 32, 2), (8, 34, 2)]
+    ho, qo, co = oracle_lib.run_words(example_key, _selected_words(host, spans, mask), 128, 24)
+    dev = torch.device("cuda:0")
+    t = torch.from_numpy(host.view(np.int32).reshape(-1)).to(dev)
+    h = torch.empty(n, dtype=torch.int32, device=dev)
+    q = torch.empty(n, dtype=torch.uint8, device=dev)
+    c = torch.empty(24, dtype=torch.int64, device=dev)
+    native.hash6_device(native.prepare_key6(example_key, mask), t.data_ptr(), n, 128, 24,
+                        h.data_ptr(), q.data_ptr(), c.data_ptr(), native.FLAG_QUEUE_U8,
+                        torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(h.cpu().numpy().view(np.uint32), ho)
+    np.testing.assert_array_equal(q.cpu().numpy().astype(np.uint32), qo)
+    np.testing.assert_array_equal(c.cpu().numpy().view(np.uint64), co)
