@@ -92,3 +92,28 @@ def test_key_search_odd_key_counts_flow_input(native, oracle_lib, nkeys, H, Q):
         c = oracle_lib.run(key, tuples, H, Q)[2]
         assert not c[qn:].any()
         np.testing.assert_array_equal(counts[k], c[:qn])
+
+
+def test_bench_key_search_launch_matches_oracle(native, oracle_lib):
+    """The bench's row_f_kernels.key_search launch exactly (bench.py extra_lines): 1024 random
+    keys (keysearch.random_keys seed 0) x 2^20 device-generated tuples (seed 1), H = 128,
+    Q = 24, one rss_key_search_device launch -- every key's 24 counts against the oracle."""
+    from rss_simulator_nvidia_amd import keysearch
+    nk, nt = 1024, 1 << 20
+    keys = keysearch.random_keys(nk, seed=0)
+    dev = torch.device("cuda:0")
+    sp = torch.cuda.current_stream(dev).cuda_stream
+    win = np.stack([np.ctypeslib.as_array(native.prepare_key(k).window) for k in keys])
+    windows = torch.from_numpy(win.astype(np.uint32).view(np.int32)).to(dev)
+    tup = torch.empty(3 * nt, dtype=torch.int32, device=dev)
+    native.generate_device(1, 0, nt, tup.data_ptr(), sp)
+    kc = torch.empty((nk, 24), dtype=torch.int64, device=dev)
+    native.key_search_device(windows.data_ptr(), nk, tup.data_ptr(), nt, 128, 24, kc.data_ptr(), sp)
+    torch.cuda.synchronize()
+    got = kc.cpu().numpy().view(np.uint64)
+    host = oracle_lib.generate(1, 0, nt)
+    np.testing.assert_array_equal(tup.cpu().numpy().view(np.uint32).reshape(nt, 3), host)
+    for k in range(nk):
+        _, _, c = oracle_lib.run(keys[k], host, 128, 24, threads=16, want_hash=False,
+                                 want_queue=False)
+        np.testing.assert_array_equal(got[k], c, err_msg="key %d" % k)
