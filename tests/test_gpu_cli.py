@@ -117,3 +117,45 @@ def test_many_queues_csv_paths_equal_pandas(tmp_path, monkeypatch, capsys, devic
     np.testing.assert_array_equal(counts["counts"].to_numpy(), bc[counts["queue_number"].to_numpy()])
     assert int(counts["counts"].sum()) == len(q) == 50000
     _assert_written_table_is_oracles(outs["1"], src, 1048576, 20000, oracle_lib, example_key)
+
+
+@pytest.mark.parametrize("H,Q", [(128, 24), (1 << 20, 20000)])
+def test_csv_device_path_4m_rows_vs_oracle(tmp_path, capsys, oracle_lib, example_key, H, Q):
+    """4M canonical rows (tools/gen_csv.c: row i is the splitmix64 tuple i of the seed, i.e.
+    exactly oracle_generate's) through the CLI's default device CSV path; the written table's
+    hash_result / queue_number columns and the counts section against oracle_run on the same
+    tuples, the 4-tuple text of the first and last rows against the input."""
+    import os
+    import subprocess
+
+    import numpy as np
+    import pandas as pd
+
+    from cli_cases import GOLDEN, run_main
+    root = os.path.dirname(GOLDEN.rstrip("/").rsplit("/", 1)[0])
+    gen = str(tmp_path / "gen_csv")
+    subprocess.run(["gcc", "-O2", "-o", gen, os.path.join(root, "tools", "gen_csv.c")], check=True)
+    n, seed = 4_000_000, 4711
+    src, out = str(tmp_path / "in.csv"), str(tmp_path / "out.csv")
+    subprocess.run([gen, str(n), str(seed), src], check=True)
+    status, so, _, exc = run_main(
+        ["--key-file", os.path.join(GOLDEN, "example_input", "hash_key.txt"), "--ips-file", src,
+         "--htable-size", str(H), "--num-queues", str(Q), "--csv", out], capsys)
+    assert status == 0, exc
+    ho, qo, co = oracle_lib.run(example_key, oracle_lib.generate(seed, 0, n), H, Q, threads=16)
+    with open(out, "rb") as f:
+        data = f.read()
+    head, rows = data.split(b"src_ip,dst_ip,src_port,dst_port,hash_result,queue_number\n", 1)
+    counts = np.loadtxt(head.decode().splitlines()[1:], delimiter=",", dtype=np.uint64, ndmin=2)
+    nz = np.flatnonzero(co)
+    np.testing.assert_array_equal(counts[:, 0], nz)
+    np.testing.assert_array_equal(counts[:, 1], co[nz])
+    table = pd.read_csv(out, skiprows=len(head.decode().splitlines()) + 1, header=None,
+                        usecols=[4, 5], names=["h", "q"], dtype=np.uint64)
+    np.testing.assert_array_equal(table["h"].to_numpy(), ho.astype(np.uint64))
+    np.testing.assert_array_equal(table["q"].to_numpy(), qo.astype(np.uint64))
+    lines = rows.split(b"\n")
+    with open(src, "rb") as f:
+        src_lines = f.read().split(b"\n")
+    for i in (0, 1, n // 2, n - 1):
+        assert lines[i].rsplit(b",", 2)[0] == src_lines[i + 1]
