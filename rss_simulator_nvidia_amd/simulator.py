@@ -48,7 +48,9 @@ class Simulator(object):
         self.__toeplitz = Toeplitz(hash_key, hash_fields or "sdfn")
         self.__ipv6 = ipv6
         self.__reta = reta
-        self.__devices = None if devices is None else tuple(devices)
+        self.__devices = None if devices is None else tuple(int(d) for d in devices)
+        if self.__devices == ():
+            raise ValueError("devices must name at least one GPU")
         self.__hash_table_size = hash_table_size
         self.__queue_num = queue_number
         self.__queues = None

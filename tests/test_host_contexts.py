@@ -103,3 +103,9 @@ def test_simulator_passes_devices_through(monkeypatch, example_key):
         sim.load_frame(df.copy())
         sim.calc_hash()
         assert seen[-1] == want
+
+
+def test_simulator_rejects_an_empty_device_list(example_key):
+    from rss_simulator_nvidia_amd.simulator import Simulator
+    with pytest.raises(ValueError):
+        Simulator(example_key, 128, 24, devices=[])
