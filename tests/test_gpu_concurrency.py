@@ -294,3 +294,32 @@ def test_every_context_entry_point_from_threads(native, oracle_lib, example_key,
     with cf.ThreadPoolExecutor(THREADS) as pool:
         assert sorted(set(pool.map(one, range(40)))) == [0, 1, 2, 3, 4]
     ctx.close()
+
+
+def test_multi_context_batches_sharing_contexts_from_threads(native, oracle_lib, example_key):
+    """rss_hash_host_multi from 8 threads over two context lists that share their contexts
+    in opposite orders ([a, b] and [b, a]): each worker holds one context's lock at a time,
+    so the calls interleave without deadlock and every batch equals the oracle."""
+    a, b = native.HostContext(0), native.HostContext(0)
+
+    def multi(ctxs):
+        m = object.__new__(native.MultiHostContext)
+        m.contexts, m._lib = ctxs, native.load()
+        return m
+
+    ab, ba = multi([a, b]), multi([b, a])
+    key = native.prepare_key(example_key)
+    batches = [oracle_lib.generate(900 + i, 0, n) for i, n in enumerate([3, 40000, 1 << 20, 77777])]
+    want = [oracle_lib.run(example_key, t, 128, 24) for t in batches]
+
+    def one(i):
+        m = ab if i % 2 else ba
+        h, q, c = m.hash(key, batches[i % 4], 128, 24)
+        for got, ref in zip((h, q, c), want[i % 4]):
+            np.testing.assert_array_equal(got, ref)
+        return i
+
+    with cf.ThreadPoolExecutor(THREADS) as pool:
+        assert sorted(pool.map(one, range(32))) == list(range(32))
+    a.close()
+    b.close()
