@@ -196,6 +196,11 @@ def cpu_baseline(key, n_sample, procs, distribution="uniform"):
     dotted = lambda v: "%d.%d.%d.%d" % ((v >> 24) & 255, (v >> 16) & 255, (v >> 8) & 255, v & 255)  # noqa
     rows = [(dotted(int(s)), dotted(int(d)), int(p) >> 16, int(p) & 0xFFFF) for s, d, p in tup]
     procs = max(1, min(procs, n_sample))
+    # one core, in this process, as the calibration against the reference was measured
+    n1 = min(1000, n_sample)
+    t1 = time.perf_counter()
+    assert len(_port_worker((key, rows[:n1]))) == n1
+    single = n1 / (time.perf_counter() - t1)
     chunks = [rows[i::procs] for i in range(procs)]
     ctx = mp.get_context("fork")
     t0 = time.perf_counter()
@@ -204,7 +209,9 @@ def cpu_baseline(key, n_sample, procs, distribution="uniform"):
     dt = time.perf_counter() - t0
     assert sum(len(o) for o in out) == n_sample
     return {"value": n_sample / dt, "unit": "tuples/s", "cores": procs, "kind": "port",
-            "reference_equivalent": reference_equivalent(n_sample / dt),
+            "single_core": {"value": single, "unit": "tuples/s", "sample": "first %d tuples, one "
+                            "process, no pool" % n1},
+            "reference_equivalent": reference_equivalent(n_sample / dt, single_core_rate=single),
             "optimised_c": optimised_c_baseline(key, procs, distribution),
             "procs": procs, "cpu_share": cpu_share(), "host_cores": os.cpu_count(),
             "sample": "first %d tuples of the bench stream, pure-Python restatement of "
@@ -215,11 +222,14 @@ def cpu_baseline(key, n_sample, procs, distribution="uniform"):
 CALIBRATION_PATH = os.path.join(ROOT, "tests", "golden", "cpu_calibration.json")
 
 
-def reference_equivalent(port_rate, path=CALIBRATION_PATH):
+def reference_equivalent(port_rate, path=CALIBRATION_PATH, single_core_rate=None):
     """The port's rate expressed in the reference's own: the reference
     cannot run on the GPU box, so tests/golden/make_cpu_calibration.py timed it beside the
     port on one core of the build container, on the same rows, and recorded their ratio
-    (cpu_calibration.json, data only).  None when that record is absent."""
+    (cpu_calibration.json, data only).  None when that record is absent.  With
+    ``single_core_rate`` (the port timed on one core of this host, in process, as the ratio
+    was measured) the line also carries that rate converted the same way: the like-for-like
+    figure, one core against one core."""
     try:
         with open(path) as f:
             cal = json.load(f)
@@ -235,7 +245,8 @@ def reference_equivalent(port_rate, path=CALIBRATION_PATH):
             "mismatch": "the ratio was measured single-core on the build container (its CPU and "
                         "Python build), the port's rate here is a multi-process pool timing on "
                         "the GPU box's host including pool start-up: an approximate conversion, "
-                        "not a measurement of the reference"}
+                        "not a measurement of the reference",
+            "single_core_value": (single_core_rate / ratio if single_core_rate else None)}
 
 
 def optimised_c_baseline(key, threads, distribution="uniform", n=1 << 24):
