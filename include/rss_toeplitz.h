@@ -305,6 +305,18 @@ int rss_csv_parse(const char* data, size_t len, rss_tuple4* tuples, size_t cap,
 size_t rss_csv_format_bound(size_t n, uint32_t nqueues);
 
 /*
+ * An address column of a DataFrame (Simulator.calc_hash on pandas data, whatever file or
+ * frame it came from): `text` holds its n cells joined by '\n'.  Cell i that is a plain
+ * quad -- four dot-separated runs of 1-3 ASCII digits, nothing else -- gets ok[i] = 1 and
+ * out[i] = (o0 << 24 | o1 << 16 | o2 << 8 | o3) mod 2^32 with the octets NOT range-checked
+ * and OR-combined, exactly __ip_to_int + the byte masks of __prepare_input_bytes
+ * (rss_simulator/toeplitz.py:100-111, :127-137); any other cell gets ok[i] = 0 and the caller
+ * converts it with the reference's own rules (whitespace, extra octets, errors).  RSS_EINVAL
+ * when the text does not hold exactly n cells (a cell containing '\n').
+ */
+int rss_parse_dotted(const char* text, size_t len, size_t n, uint32_t* out, uint8_t* ok);
+
+/*
  * Write the statistics file of write_statistics (simulator.py:100-115): the
  * "queue_number,counts" rows of the non-empty queues, then the table with the
  * input columns in input order plus hash_result,queue_number.  `cap` must be

@@ -39,6 +39,7 @@ EXPORTED_SYMBOLS = (
     "rss_pcap_parse6", "rss_hash6_device_reta", "rss_hash6_host_reta", "rss_csv_parse6",
     "rss_csv_format6_bound", "rss_csv_format6", "rss_csv6_hash_text", "rss_csv6_hash_file",
     "rss_counts_workspace_bytes", "rss_hash_device_ws", "rss_hash6_device_ws",
+    "rss_parse_dotted",
 )
 FIELD_SRC_IP, FIELD_DST_IP, FIELD_SRC_PORT, FIELD_DST_PORT = 1, 2, 4, 8
 FIELDS_IP, FIELDS_ALL = 3, 15
@@ -145,6 +146,7 @@ def _bind(lib):
         "rss_host_free": ([vp], None),
         "rss_hash_host_multi": ([ctypes.POINTER(vp), ctypes.c_int, key_p, vp, sz, u32, vp, u32,
                                  vp, vp, vp, u32], ctypes.c_int),
+        "rss_parse_dotted": ([vp, sz, sz, vp, vp], ctypes.c_int),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(lib, name)
@@ -683,6 +685,24 @@ def generate_device(seed, first_index, n, tuples_ptr, stream=None):
 
 
 # ------------------------------------------------------------ CSV fast path --
+def parse_dotted(cells):
+    """``(ok, value)`` for a sequence of ``str`` cells (``rss_parse_dotted``): ``ok[i]``
+    whether cell i is a plain ``d.d.d.d`` quad (1-3 digits per octet), ``value[i]`` its
+    ``__ip_to_int`` value mod 2**32; None when the cells cannot be joined into one
+    '\n'-separated UTF-8 text of exactly ``len(cells)`` cells (the caller then converts
+    them one by one)."""
+    n = len(cells)
+    try:
+        text = "\n".join(cells).encode("utf-8")
+    except (TypeError, UnicodeEncodeError):
+        return None
+    out = np.empty(n, dtype=np.uint32)
+    ok = np.empty(n, dtype=np.uint8)
+    if load().rss_parse_dotted(text, len(text), n, out.ctypes.data, ok.ctypes.data) != 0:
+        return None  # a cell holding '\n'
+    return ok.astype(bool), out
+
+
 def csv_parse(data, threads=0):
     """Parse a canonical 4-tuple CSV image (bytes / uint8 array).
 

@@ -328,6 +328,40 @@ size_t rss_csv_format_prefix(const uint64_t* counts, uint32_t nqueues,
 
 extern "C" {
 
+int rss_parse_dotted(const char* text, size_t len, size_t n, uint32_t* out, uint8_t* ok) {
+    if ((n && (!out || !ok)) || (len && !text)) return RSS_EINVAL;
+    const char* p = text;
+    const char* const end = text + len;
+    for (size_t i = 0; i < n; ++i) {
+        const char* eol = static_cast<const char*>(memchr(p, '\n', (size_t)(end - p)));
+        if (i + 1 < n ? !eol : eol != nullptr) return RSS_EINVAL;  // exactly n cells
+        const char* const cell_end = eol ? eol : end;
+        uint64_t value = 0;
+        int octets = 0, digits = 0;
+        uint32_t octet = 0;
+        bool good = true;
+        for (const char* c = p; c < cell_end && good; ++c) {
+            if (*c >= '0' && *c <= '9') {
+                octet = octet * 10 + (uint32_t)(*c - '0');
+                good = ++digits <= 3;
+            } else if (*c == '.') {
+                good = digits > 0 && octets < 3;
+                value |= (uint64_t)octet << (24 - 8 * octets);  // (no range check: OR)
+                ++octets;
+                octet = 0;
+                digits = 0;
+            } else {
+                good = false;
+            }
+        }
+        good = good && octets == 3 && digits > 0;
+        ok[i] = good ? 1 : 0;
+        out[i] = good ? (uint32_t)(value | octet) : 0u;
+        p = eol ? eol + 1 : end;
+    }
+    return RSS_OK;
+}
+
 size_t rss_csv_format_bound(size_t n, uint32_t nqueues) {
     return rss_csv_prefix_bound(nqueues) + n * kMaxRowBytes;
 }

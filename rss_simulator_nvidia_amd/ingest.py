@@ -19,7 +19,7 @@ by column, so with several bad cells the reported one may differ (same exit).
 import numpy as np
 import pandas as pd
 
-from rss_simulator_nvidia_amd._native import TUPLE6_DTYPE, TUPLE_DTYPE
+from rss_simulator_nvidia_amd._native import TUPLE6_DTYPE, TUPLE_DTYPE, parse_dotted
 from rss_simulator_nvidia_amd.column_names import ColumnNames
 
 _DOTTED = r"[0-9]{1,3}\.[0-9]{1,3}\.[0-9]{1,3}\.[0-9]{1,3}"
@@ -38,24 +38,34 @@ def port_to_u16(port):
 
 
 def ip_column(series):
-    """uint32 array for an address column (pandas Series)."""
+    """uint32 array for an address column (pandas Series).
+
+    Cells that are plain ``d.d.d.d`` quads (``_DOTTED``) are converted in one native pass
+    (``rss_parse_dotted`` over the column joined by newlines, 1M cells in ~0.1 s against
+    ~4 s for pandas' regex + split); every other cell -- whitespace, 5 octets, non-strings,
+    anything the reference's ``int()`` might still accept or reject -- goes through
+    :func:`ip_to_u32`, the literal restatement, which raises what the reference raises."""
     n = len(series)
     out = np.empty(n, dtype=np.uint32)
     if n == 0:
         return out
-    if series.dtype == object or pd.api.types.is_string_dtype(series.dtype):
+    values = series.to_numpy()
+    fast = None
+    if pd.api.types.infer_dtype(values, skipna=False) == "string":  # every cell a str
+        parsed = parse_dotted(values.tolist())
+        if parsed is not None:
+            fast, vals = parsed
+            out[fast] = vals[fast]
+    if fast is None and (series.dtype == object or pd.api.types.is_string_dtype(series.dtype)):
         try:
-            fast = series.str.fullmatch(_DOTTED).fillna(False).to_numpy(dtype=bool)
+            fast = series.str.fullmatch(_DOTTED).eq(True).to_numpy(dtype=bool)  # NaN: False
         except AttributeError:  # the .str accessor refuses this column
-            fast = np.zeros(n, dtype=bool)
-        if fast.any():
+            fast = None
+        if fast is not None and fast.any():
             parts = series[fast].str.split(".", expand=True).to_numpy(dtype=np.int64)
             vals = (parts[:, 0] << 24) | (parts[:, 1] << 16) | (parts[:, 2] << 8) | parts[:, 3]
             out[fast] = (vals & 0xFFFFFFFF).astype(np.uint32)
-        slow = np.flatnonzero(~fast)
-    else:
-        slow = np.arange(n)
-    values = series.to_numpy()
+    slow = np.arange(n) if fast is None else np.flatnonzero(~fast)
     for i in slow:
         out[i] = ip_to_u32(values[i])
     return out

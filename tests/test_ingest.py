@@ -1,0 +1,84 @@
+"""Address-column ingest (``ingest.ip_column``) against the literal restatement of the
+reference's ``__ip_to_int`` + byte masks (``ingest.ip_to_u32``, ``toeplitz.py:100-111`` /
+``:127-137``) cell by cell: the native quad parser (``rss_parse_dotted``) must take exactly
+the plain ``d.d.d.d`` cells and give their reference values, and every other cell -- which the
+reference may still accept (whitespace, extra octets, octets > 255, signs, underscores,
+non-ASCII digits) or reject -- must come out as the literal path gives it, exceptions
+included.  CPU only (the library loads without a GPU)."""
+import numpy as np
+import pandas as pd
+import pytest
+
+from rss_simulator_nvidia_amd import _native
+from rss_simulator_nvidia_amd.ingest import ip_column, ip_to_u32, pack_frame
+
+ACCEPTED = ["1.2.3.4", "0.0.0.0", "255.255.255.255", "999.999.999.999", "010.001.0.9",
+            "1.2.3.4.5", "1.2.3.4.x", " 1.2.3.4", "1.2.3.4 ", "1.2.3.4\r", "+1.2.3.4",
+            "1_0.2.3.4", "１.2.3.4", "1.2.3.0004", "4294.1.1.1", "1.2.3.-4", "-1.2.3.4"]
+REJECTED = ["1.2.3", "", "a.b.c.d", "1..2.3", "1.2.3.", ".1.2.3", "1.2.3.4/24", "1,2,3,4",
+            "1 .2.3.4x"]
+
+
+def _literal(cell):
+    try:
+        return ip_to_u32(cell), None
+    except Exception as err:  # the type the reference raises
+        return None, type(err)
+
+
+def test_native_parser_takes_exactly_the_plain_quads():
+    cells = ACCEPTED + REJECTED + ["12.34.56.78", "1.22.333.4", "1234.1.1.1", "1.2.3.4\n5"]
+    ok, val = _native.parse_dotted(["1.2.3.4", "9.8.7.6"])
+    assert ok.tolist() == [True, True] and val.tolist() == [0x01020304, 0x09080706]
+    assert _native.parse_dotted(["1.2.3.4\n5", "1.2.3.4"]) is None  # a cell holding '\n'
+    got = _native.parse_dotted([c for c in cells if "\n" not in c])
+    assert got is not None
+    import re
+    plain = re.compile(r"[0-9]{1,3}\.[0-9]{1,3}\.[0-9]{1,3}\.[0-9]{1,3}")
+    for c, o, v in zip([c for c in cells if "\n" not in c], *got):
+        assert bool(o) == bool(plain.fullmatch(c)), c
+        if o:
+            assert int(v) == ip_to_u32(c), c
+
+
+def test_random_columns_equal_the_literal_path():
+    rng = np.random.default_rng(12)
+    pool = ACCEPTED + ["%d.%d.%d.%d" % tuple(rng.integers(0, 1000, 4)) for _ in range(200)]
+    for trial in range(20):
+        cells = [pool[i] for i in rng.integers(0, len(pool), 5000)]
+        got = ip_column(pd.Series(cells, dtype=object))
+        want = np.array([ip_to_u32(c) for c in cells], dtype=np.uint32)
+        np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("bad", REJECTED + [None, 1.5, float("nan"), b"1.2.3.4", 16909060])
+def test_a_rejected_cell_raises_what_the_literal_path_raises(bad):
+    cells = ["1.2.3.4"] * 10 + [bad] + ["5.6.7.8"] * 5
+    _, err = _literal(bad)
+    if err is None:  # (an int cell: the reference raises on .split too)
+        pytest.skip("accepted by the literal path")
+    with pytest.raises(err):
+        ip_column(pd.Series(cells, dtype=object))
+
+
+def test_string_dtype_and_ports_through_pack_frame():
+    df = pd.DataFrame({"src_ip": pd.Series(["1.2.3.4", " 10.0.0.1"], dtype="string"),
+                       "dst_ip": ["255.255.255.255", "1.2.3.4.5"],
+                       "src_port": [65536 + 7, -1], "dst_port": [80, 443]})
+    t = pack_frame(df)
+    assert t["sip"].tolist() == [0x01020304, 0x0A000001]
+    assert t["dip"].tolist() == [0xFFFFFFFF, 0x01020304]
+    assert t["ports"].tolist() == [(7 << 16) | 80, (0xFFFF << 16) | 443]
+
+
+def test_million_row_column_is_fast():
+    import time
+    rng = np.random.default_rng(3)
+    v = rng.integers(0, 2**32, 1_000_000, dtype=np.uint64).tolist()
+    cells = ["%d.%d.%d.%d" % (x >> 24, (x >> 16) & 255, (x >> 8) & 255, x & 255) for x in v]
+    s = pd.Series(cells, dtype=object)
+    t0 = time.perf_counter()
+    got = ip_column(s)
+    dt = time.perf_counter() - t0
+    np.testing.assert_array_equal(got, np.array(v, dtype=np.uint64).astype(np.uint32))
+    assert dt < 2.0, dt  # native pass: ~0.1 s here; pandas' regex + split took ~4 s
