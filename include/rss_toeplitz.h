@@ -317,6 +317,14 @@ size_t rss_csv_format_bound(size_t n, uint32_t nqueues);
 int rss_parse_dotted(const char* text, size_t len, size_t n, uint32_t* out, uint8_t* ok);
 
 /*
+ * The same for an IPv6 address column (the additive --ipv6 input): cell i that is RFC 4291
+ * text without an embedded IPv4 part or zone (1-4 hex digits per group, at most one '::';
+ * the CSV path's canonical IPv6 form) gets ok[i] = 1 and out[4i..4i+3] = its 128 bits as four
+ * big-endian-valued words, as ipaddress.IPv6Address reads it; any other cell ok[i] = 0.
+ */
+int rss_parse_ipv6(const char* text, size_t len, size_t n, uint32_t* out, uint8_t* ok);
+
+/*
  * Write the statistics file of write_statistics (simulator.py:100-115): the
  * "queue_number,counts" rows of the non-empty queues, then the table with the
  * input columns in input order plus hash_result,queue_number.  `cap` must be

@@ -39,7 +39,7 @@ EXPORTED_SYMBOLS = (
     "rss_pcap_parse6", "rss_hash6_device_reta", "rss_hash6_host_reta", "rss_csv_parse6",
     "rss_csv_format6_bound", "rss_csv_format6", "rss_csv6_hash_text", "rss_csv6_hash_file",
     "rss_counts_workspace_bytes", "rss_hash_device_ws", "rss_hash6_device_ws",
-    "rss_parse_dotted",
+    "rss_parse_dotted", "rss_parse_ipv6",
 )
 FIELD_SRC_IP, FIELD_DST_IP, FIELD_SRC_PORT, FIELD_DST_PORT = 1, 2, 4, 8
 FIELDS_IP, FIELDS_ALL = 3, 15
@@ -147,6 +147,7 @@ def _bind(lib):
         "rss_hash_host_multi": ([ctypes.POINTER(vp), ctypes.c_int, key_p, vp, sz, u32, vp, u32,
                                  vp, vp, vp, u32], ctypes.c_int),
         "rss_parse_dotted": ([vp, sz, sz, vp, vp], ctypes.c_int),
+        "rss_parse_ipv6": ([vp, sz, sz, vp, vp], ctypes.c_int),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(lib, name)
@@ -700,6 +701,22 @@ def parse_dotted(cells):
     ok = np.empty(n, dtype=np.uint8)
     if load().rss_parse_dotted(text, len(text), n, out.ctypes.data, ok.ctypes.data) != 0:
         return None  # a cell holding '\n'
+    return ok.astype(bool), out
+
+
+def parse_ipv6(cells):
+    """``(ok, words)`` for a sequence of ``str`` IPv6 cells (``rss_parse_ipv6``): ``ok[i]``
+    whether cell i is plain RFC 4291 text (no embedded IPv4 part, no zone), ``words[i]`` its
+    four big-endian-valued words; None as :func:`parse_dotted`."""
+    n = len(cells)
+    try:
+        text = "\n".join(cells).encode("utf-8")
+    except (TypeError, UnicodeEncodeError):
+        return None
+    out = np.empty((n, 4), dtype=np.uint32)
+    ok = np.empty(n, dtype=np.uint8)
+    if load().rss_parse_ipv6(text, len(text), n, out.ctypes.data, ok.ctypes.data) != 0:
+        return None
     return ok.astype(bool), out
 
 

@@ -362,6 +362,24 @@ int rss_parse_dotted(const char* text, size_t len, size_t n, uint32_t* out, uint
     return RSS_OK;
 }
 
+int rss_parse_ipv6(const char* text, size_t len, size_t n, uint32_t* out, uint8_t* ok) {
+    if ((n && (!out || !ok)) || (len && !text)) return RSS_EINVAL;
+    const char* p = text;
+    const char* const end = text + len;
+    for (size_t i = 0; i < n; ++i) {
+        const char* eol = static_cast<const char*>(memchr(p, '\n', (size_t)(end - p)));
+        if (i + 1 < n ? !eol : eol != nullptr) return RSS_EINVAL;  // exactly n cells
+        const char* const cell_end = eol ? eol : end;
+        const char* q = p;
+        // the row scanner's address rules (scan_ip6), and nothing after the address
+        const bool good = q < cell_end && scan_ip6(q, cell_end, out + 4 * i) && q == cell_end;
+        ok[i] = good ? 1 : 0;
+        if (!good) memset(out + 4 * i, 0, 16);
+        p = eol ? eol + 1 : end;
+    }
+    return RSS_OK;
+}
+
 size_t rss_csv_format_bound(size_t n, uint32_t nqueues) {
     return rss_csv_prefix_bound(nqueues) + n * kMaxRowBytes;
 }

@@ -82,3 +82,37 @@ def test_million_row_column_is_fast():
     dt = time.perf_counter() - t0
     np.testing.assert_array_equal(got, np.array(v, dtype=np.uint64).astype(np.uint32))
     assert dt < 2.0, dt  # native pass: ~0.1 s here; pandas' regex + split took ~4 s
+
+
+def _v6_forms(rng, k):
+    import ipaddress
+    out = []
+    for _ in range(k):
+        hi = int(rng.integers(0, 2**63)) << 1 | int(rng.integers(0, 2))
+        lo = int(rng.integers(0, 2**16)) if rng.random() < 0.4 else int(rng.integers(0, 2**63))
+        a = ipaddress.IPv6Address((hi << 64 | lo) if rng.random() < 0.7 else lo)
+        form = int(rng.integers(0, 4))
+        out.append(str(a) if form == 0 else a.exploded if form == 1 else
+                   str(a).upper() if form == 2 else a.exploded.replace(":0000", ":0"))
+    return out
+
+
+def test_ipv6_columns_equal_ipaddress():
+    from rss_simulator_nvidia_amd.ingest import ipv6_column, ipv6_words
+    rng = np.random.default_rng(6)
+    odd = ["::", "::1", "1::", "::ffff:1.2.3.4", "fe80::1%eth0", " ::1 ", "::1\r", "0:0:0:0:0:0:0:0",
+           "FFFF:ffff:FfFf:ffff:ffff:ffff:ffff:ffff"]
+    cells = _v6_forms(rng, 3000) + odd
+    rng.shuffle(cells)
+    got = ipv6_column(pd.Series(cells, dtype=object))
+    want = np.array([ipv6_words(c) for c in cells], dtype=np.uint32)
+    np.testing.assert_array_equal(got, want)
+    ok, _ = _native.parse_ipv6(["::ffff:1.2.3.4", "::1", " ::1", "1:2:3:4:5:6:7:8:9"])
+    assert ok.tolist() == [False, True, False, False]  # the odd forms take ipaddress
+
+
+@pytest.mark.parametrize("bad", [":::", "1:2:3:4:5:6:7:8:9", "12345::", "g::1", "1.2.3.4", ""])
+def test_ipv6_bad_cells_raise_like_ipaddress(bad):
+    from rss_simulator_nvidia_amd.ingest import ipv6_column
+    with pytest.raises(ValueError):
+        ipv6_column(pd.Series(["::1"] * 5 + [bad], dtype=object))
