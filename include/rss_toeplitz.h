@@ -307,7 +307,9 @@ size_t rss_csv_format_bound(size_t n, uint32_t nqueues);
 /*
  * An address column of a DataFrame (Simulator.calc_hash on pandas data, whatever file or
  * frame it came from): `text` holds its n cells joined by '\n'.  Cell i that is a plain
- * quad -- four dot-separated runs of 1-3 ASCII digits, nothing else -- gets ok[i] = 1 and
+ * quad -- four dot-separated runs of 1-3 ASCII digits, nothing else -- gets ok[i] = 1 (2 when
+ * it is also canonical: octets 0..255 without leading zeros, the text rss_csv_format writes
+ * back, so a write_statistics of such cells may take the native formatter) and
  * out[i] = (o0 << 24 | o1 << 16 | o2 << 8 | o3) mod 2^32 with the octets NOT range-checked
  * and OR-combined, exactly __ip_to_int + the byte masks of __prepare_input_bytes
  * (rss_simulator/toeplitz.py:100-111, :127-137); any other cell gets ok[i] = 0 and the caller

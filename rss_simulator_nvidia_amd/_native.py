@@ -686,12 +686,13 @@ def generate_device(seed, first_index, n, tuples_ptr, stream=None):
 
 
 # ------------------------------------------------------------ CSV fast path --
-def parse_dotted(cells):
+def parse_dotted(cells, canonical=False):
     """``(ok, value)`` for a sequence of ``str`` cells (``rss_parse_dotted``): ``ok[i]``
-    whether cell i is a plain ``d.d.d.d`` quad (1-3 digits per octet), ``value[i]`` its
-    ``__ip_to_int`` value mod 2**32; None when the cells cannot be joined into one
-    '\n'-separated UTF-8 text of exactly ``len(cells)`` cells (the caller then converts
-    them one by one)."""
+    whether cell i is a plain ``d.d.d.d`` quad (1-3 digits per octet) -- with
+    ``canonical``, whether it is also canonical (octets 0..255, no leading zeros) --
+    ``value[i]`` its ``__ip_to_int`` value mod 2**32; None when the cells cannot be joined
+    into one '\n'-separated UTF-8 text of exactly ``len(cells)`` cells (the caller then
+    converts them one by one)."""
     n = len(cells)
     try:
         text = "\n".join(cells).encode("utf-8")
@@ -701,7 +702,7 @@ def parse_dotted(cells):
     ok = np.empty(n, dtype=np.uint8)
     if load().rss_parse_dotted(text, len(text), n, out.ctypes.data, ok.ctypes.data) != 0:
         return None  # a cell holding '\n'
-    return ok.astype(bool), out
+    return (ok == 2 if canonical else ok > 0), out
 
 
 def parse_ipv6(cells):

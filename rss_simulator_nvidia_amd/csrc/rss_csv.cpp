@@ -339,13 +339,15 @@ int rss_parse_dotted(const char* text, size_t len, size_t n, uint32_t* out, uint
         uint64_t value = 0;
         int octets = 0, digits = 0;
         uint32_t octet = 0;
-        bool good = true;
+        bool good = true, canonical = true;
         for (const char* c = p; c < cell_end && good; ++c) {
             if (*c >= '0' && *c <= '9') {
+                canonical = canonical && !(digits == 1 && octet == 0);  // no leading zero
                 octet = octet * 10 + (uint32_t)(*c - '0');
                 good = ++digits <= 3;
             } else if (*c == '.') {
                 good = digits > 0 && octets < 3;
+                canonical = canonical && octet <= 255;
                 value |= (uint64_t)octet << (24 - 8 * octets);  // (no range check: OR)
                 ++octets;
                 octet = 0;
@@ -355,7 +357,8 @@ int rss_parse_dotted(const char* text, size_t len, size_t n, uint32_t* out, uint
             }
         }
         good = good && octets == 3 && digits > 0;
-        ok[i] = good ? 1 : 0;
+        canonical = good && canonical && octet <= 255;
+        ok[i] = canonical ? 2 : (good ? 1 : 0);
         out[i] = good ? (uint32_t)(value | octet) : 0u;
         p = eol ? eol + 1 : end;
     }

@@ -129,13 +129,55 @@ class Simulator(object):
         return [(int(q), int(counts[q])) for q in nz]
 
     def write_statistics(self, output):
-        """Write counts then the full table to ``output`` (``simulator.py:100-116``)."""
-        with open(output, "w") as f:
-            f.write("{},counts\n".format(_QUEUE))
-            for q, c in self.queue_count_rows():
-                f.write("{},{}\n".format(q, c))
-        self.__ip_df.to_csv(output, mode="a", index=False)
+        """Write counts then the full table to ``output`` (``simulator.py:100-116``).
+
+        A frame of exactly the four input columns (any order) + ``hash_result`` +
+        ``queue_number`` whose cells are canonical (quads with octets 0..255 and no leading
+        zeros, integer ports 0..65535 -- text pandas writes back unchanged) is written by the
+        native formatter (``rss_csv_format``, the bytes ``to_csv`` would write, ~8x faster);
+        any other frame by pandas, as the reference."""
+        if not self.__write_native(output):
+            with open(output, "w") as f:
+                f.write("{},counts\n".format(_QUEUE))
+                for q, c in self.queue_count_rows():
+                    f.write("{},{}\n".format(q, c))
+            self.__ip_df.to_csv(output, mode="a", index=False)
         print("Wrote statistics to {csv}.".format(csv=output))
+
+    def __write_native(self, output):
+        """The canonical-frame path of :meth:`write_statistics`; False when it does not apply."""
+        df, counts = self.__ip_df, self.__counts
+        names = [c.value for c in INPUT_COLUMNS]
+        cols = list(df.columns)
+        if (counts is None or self.__count_rows is not None or len(df) == 0 or len(cols) != 6
+                or sorted(cols[:4]) != sorted(names) or cols[4:] != [_HASH, _QUEUE]):
+            return False
+        packed = {}
+        for name in names[:2]:
+            values = df[name].to_numpy()
+            if pd.api.types.infer_dtype(values, skipna=False) != "string":
+                return False
+            parsed = _native.parse_dotted(values.tolist(), canonical=True)
+            if parsed is None or not parsed[0].all():
+                return False
+            packed[name] = parsed[1]
+        for name in names[2:] + [_HASH, _QUEUE]:
+            col = df[name]
+            top = 0xFFFF if name in names[2:] else 0xFFFFFFFF
+            if col.dtype.kind not in "iu" or col.min() < 0 or col.max() > top:
+                return False
+            packed[name] = col.to_numpy().astype(np.uint32)
+        tuples = np.empty(len(df), dtype=_native.TUPLE_DTYPE)
+        tuples["sip"], tuples["dip"] = packed[names[0]], packed[names[1]]
+        tuples["ports"] = (packed[names[2]] << np.uint32(16)) | packed[names[3]]
+        layout = _native.RssCsvLayout()
+        for f, name in enumerate(cols[:4]):
+            layout.field_column[f] = names.index(name)
+        image = _native.csv_format(tuples, packed[_HASH], packed[_QUEUE],
+                                   np.asarray(counts, dtype=np.uint64), layout)
+        with open(output, "wb") as f:
+            f.write(memoryview(image))
+        return True
 
     def histogram_caption(self):
         """The caption lines of ``simulator.py:160-169``."""

@@ -116,3 +116,80 @@ def test_ipv6_bad_cells_raise_like_ipaddress(bad):
     from rss_simulator_nvidia_amd.ingest import ipv6_column
     with pytest.raises(ValueError):
         ipv6_column(pd.Series(["::1"] * 5 + [bad], dtype=object))
+
+
+# ---------------------------------------------------------------- write_statistics ----
+def _pandas_statistics(df, counts, path):
+    """write_statistics' bytes the reference way (simulator.py:100-116)."""
+    with open(path, "w") as f:
+        f.write("queue_number,counts\n")
+        for q in np.flatnonzero(counts):
+            f.write("{},{}\n".format(int(q), int(counts[q])))
+    df.to_csv(path, mode="a", index=False)
+    with open(path, "rb") as f:
+        return f.read()
+
+
+def _simulator_with(df, counts):
+    from rss_simulator_nvidia_amd.simulator import Simulator
+    sim = Simulator([0] * 40, 128, 24)
+    sim.load_frame(df)
+    sim._Simulator__counts = counts  # (what calc_hash leaves)
+    return sim
+
+
+def _frame(rng, n, order):
+    v = rng.integers(0, 2**32, (2, n), dtype=np.uint64)
+    quad = lambda u: ["%d.%d.%d.%d" % (x >> 24, (x >> 16) & 255, (x >> 8) & 255, x & 255)  # noqa: E731
+                      for x in u.tolist()]
+    cols = {"src_ip": quad(v[0]), "dst_ip": quad(v[1]),
+            "src_port": rng.integers(0, 65536, n), "dst_port": rng.integers(0, 65536, n)}
+    df = pd.DataFrame({c: cols[c] for c in order})
+    df["hash_result"] = rng.integers(0, 2**32, n).astype(np.int64)
+    df["queue_number"] = (df["hash_result"] % 128 % 24).astype(np.int64)
+    counts = np.bincount(df["queue_number"], minlength=24).astype(np.uint64)
+    return df, counts
+
+
+@pytest.mark.parametrize("order", [["src_ip", "dst_ip", "src_port", "dst_port"],
+                                   ["dst_port", "src_ip", "src_port", "dst_ip"]])
+def test_write_statistics_native_bytes_equal_pandas(tmp_path, capsys, order):
+    """A canonical frame takes the native formatter: the file is byte for byte what the
+    reference's to_csv writes, the stdout line unchanged."""
+    df, counts = _frame(np.random.default_rng(len(order[0])), 50000, order)
+    want = _pandas_statistics(df, counts, tmp_path / "ref.csv")
+    sim = _simulator_with(df, counts)
+    calls = []
+    orig = _native.csv_format
+    try:
+        _native.csv_format = lambda *a, **k: calls.append(1) or orig(*a, **k)
+        sim.write_statistics(str(tmp_path / "out.csv"))
+    finally:
+        _native.csv_format = orig
+    assert calls, "the canonical frame did not take the native formatter"
+    assert (tmp_path / "out.csv").read_bytes() == want
+    assert capsys.readouterr().out == "Wrote statistics to %s.\n" % (tmp_path / "out.csv")
+
+
+@pytest.mark.parametrize("spoil", ["leading_zero", "octet_256", "extra_column", "no_queue",
+                                   "negative_port", "float_port", "space"])
+def test_write_statistics_non_canonical_frames_take_pandas(tmp_path, capsys, spoil):
+    df, counts = _frame(np.random.default_rng(3), 2000, ["src_ip", "dst_ip", "src_port",
+                                                         "dst_port"])
+    if spoil == "leading_zero":
+        df.loc[7, "src_ip"] = "01.2.3.4"
+    elif spoil == "octet_256":
+        df.loc[7, "dst_ip"] = "1.2.3.256"
+    elif spoil == "extra_column":
+        df["note"] = "x"
+    elif spoil == "no_queue":
+        df = df.drop(columns=["queue_number"])
+    elif spoil == "negative_port":
+        df.loc[7, "src_port"] = -1
+    elif spoil == "float_port":
+        df["dst_port"] = df["dst_port"].astype(float)
+    else:
+        df.loc[7, "src_ip"] = " 1.2.3.4"
+    want = _pandas_statistics(df, counts, tmp_path / "ref.csv")
+    _simulator_with(df, counts).write_statistics(str(tmp_path / "out.csv"))
+    assert (tmp_path / "out.csv").read_bytes() == want
