@@ -32,6 +32,32 @@ _HASH = ColumnNames.HASH_RESULT.value
 _QUEUE = ColumnNames.QUEUE_NUMBER.value
 
 
+def _read_canonical_csv(path):
+    """The DataFrame ``pd.read_csv(path)`` would build, for a canonical 4-tuple file (header =
+    the four input columns in any order, dotted quads, decimal ports: ``rss_csv_parse``),
+    read by pyarrow; None for anything else (unreadable, not canonical, no pyarrow), which
+    the caller hands to pandas."""
+    try:
+        import pyarrow as pa
+        import pyarrow.csv as pacsv
+        with open(path, "rb") as f:
+            data = f.read()
+    except (ImportError, OSError, TypeError, ValueError):
+        return None
+    if _native.csv_parse(data) is None:  # not canonical
+        return None
+    try:
+        df = pacsv.read_csv(pa.BufferReader(data)).to_pandas()
+    except Exception:  # (pandas then reads it -- and raises -- as the reference)
+        return None
+    names = {c.value for c in INPUT_COLUMNS}
+    if set(df.columns) != names or len(df.columns) != 4 or any(
+            df[c.value].dtype != (object if c.value.endswith("_ip") else np.int64)
+            for c in INPUT_COLUMNS):
+        return None
+    return df
+
+
 class Simulator(object):
     """RSS simulator class (``simulator.py:26``)."""
 
@@ -68,7 +94,16 @@ class Simulator(object):
         return self.__counts
 
     def load_ips_from_csv(self, csv_path):
-        """Read the 4-tuple CSV; raise ParseException like ``simulator.py:54-71``."""
+        """Read the 4-tuple CSV; raise ParseException like ``simulator.py:54-71``.
+
+        A canonical file (the CSV fast path's format, checked by ``rss_csv_parse``) is read by
+        pyarrow's multi-threaded reader into the same DataFrame ``pd.read_csv`` builds (str
+        address columns, int64 ports, header order) in ~half the time; any other file, and
+        every error, takes ``pd.read_csv`` as the reference does."""
+        df = _read_canonical_csv(csv_path)
+        if df is not None:
+            self.load_frame(df)
+            return
         try:
             df = pd.read_csv(csv_path)
         except (UnicodeDecodeError, IOError, pd_ParserError):

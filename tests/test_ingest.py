@@ -193,3 +193,49 @@ def test_write_statistics_non_canonical_frames_take_pandas(tmp_path, capsys, spo
     want = _pandas_statistics(df, counts, tmp_path / "ref.csv")
     _simulator_with(df, counts).write_statistics(str(tmp_path / "out.csv"))
     assert (tmp_path / "out.csv").read_bytes() == want
+
+
+# ---------------------------------------------------------------- load_ips_from_csv ----
+@pytest.mark.parametrize("variant", ["plain", "reordered", "crlf", "blank_lines", "no_final_newline"])
+def test_canonical_csv_frame_equals_pandas(tmp_path, variant):
+    """load_ips_from_csv of a canonical file (pyarrow reader) builds exactly pd.read_csv's
+    DataFrame: values, dtypes, column order."""
+    from rss_simulator_nvidia_amd.simulator import Simulator
+    rng = np.random.default_rng(len(variant))
+    df, _ = _frame(rng, 3000, ["dst_port", "src_ip", "dst_ip", "src_port"] if variant == "reordered"
+                   else ["src_ip", "dst_ip", "src_port", "dst_port"])
+    text = df.drop(columns=["hash_result", "queue_number"]).to_csv(index=False)
+    if variant == "crlf":
+        text = text.replace("\n", "\r\n")
+    elif variant == "blank_lines":
+        lines = text.split("\n")
+        text = "\n".join(lines[:10] + [""] + lines[10:20] + ["", ""] + lines[20:])
+    elif variant == "no_final_newline":
+        text = text.rstrip("\n")
+    path = tmp_path / "in.csv"
+    path.write_bytes(text.encode())
+    want = pd.read_csv(path)
+    sim = Simulator([0] * 40, 128, 24)
+    calls = []
+    import rss_simulator_nvidia_amd.simulator as simmod
+    orig = simmod._read_canonical_csv
+    simmod._read_canonical_csv = lambda p: calls.append(1) or orig(p)
+    try:
+        sim.load_ips_from_csv(str(path))
+    finally:
+        simmod._read_canonical_csv = orig
+    got = sim.data_frame
+    assert calls and orig(str(path)) is not None, "the canonical file did not take pyarrow"
+    assert list(got.columns) == list(want.columns)
+    assert got.dtypes.tolist() == want.dtypes.tolist()
+    assert got.equals(want)
+
+
+def test_non_canonical_csv_keeps_pandas(tmp_path):
+    from rss_simulator_nvidia_amd.simulator import _read_canonical_csv
+    path = tmp_path / "in.csv"
+    path.write_text("src_ip,dst_ip,src_port,dst_port\n01.2.3.4,1.2.3.4,1,2\n")
+    assert _read_canonical_csv(str(path)) is None  # leading zero: not canonical
+    path.write_text("src_ip,dst_ip,src_port,dst_port,extra\n1.2.3.4,1.2.3.4,1,2,x\n")
+    assert _read_canonical_csv(str(path)) is None
+    assert _read_canonical_csv(str(tmp_path / "missing.csv")) is None
