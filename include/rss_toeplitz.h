@@ -253,7 +253,8 @@ int rss_hash6_device_ws(const rss_key6* key, const rss_tuple6* d_tuples, size_t 
  * Toeplitz.compute_hash (rss_simulator/toeplitz.py:59 copies the key on every call).
  * rss_ctx_destroy must not race a call on the same context.  Output that a call leaves in
  * context-owned memory (rss_csv_hash_text's file image) is valid until the next call on
- * that context, whichever thread makes it.
+ * that context, whichever thread makes it.  A call that fails returns only after every
+ * copy and kernel it queued has finished: the caller's buffers are its own again.
  */
 typedef struct rss_ctx rss_ctx;
 

@@ -926,10 +926,10 @@ struct Fd {
 };
 
 template <class Rows>
-int csv_hash_text(const char* who, rss_ctx* ctx, const typename CsvJob<Rows>::Key* key,
-                  const char* text, size_t len, uint32_t htable, uint32_t nqueues,
-                  const uint32_t* reta, uint32_t flags, const char** out, size_t* out_len,
-                  uint64_t* counts, size_t* n_rows) {
+int csv_hash_text_locked(const char* who, rss_ctx* ctx, const typename CsvJob<Rows>::Key* key,
+                         const char* text, size_t len, uint32_t htable, uint32_t nqueues,
+                         const uint32_t* reta, uint32_t flags, const char** out, size_t* out_len,
+                         uint64_t* counts, size_t* n_rows) {
     if (!ctx || !text || !counts || !n_rows)
         return rss_set_error(RSS_EINVAL, "%s: NULL argument", who);
     const bool want_file = !(flags & RSS_CSV_COUNTS_ONLY);
@@ -938,7 +938,6 @@ int csv_hash_text(const char* who, rss_ctx* ctx, const typename CsvJob<Rows>::Ke
     int rc = check_args(key, htable, nqueues);
     if (rc) return rc;
     *n_rows = 0;
-    std::lock_guard<std::mutex> lock(ctx->mu);  // (struct rss_ctx)
     rss_csv_layout layout;
     size_t body_off;
     if (!rss_csv_header(text, len, &layout, &body_off))
@@ -968,9 +967,9 @@ int csv_hash_text(const char* who, rss_ctx* ctx, const typename CsvJob<Rows>::Ke
 }
 
 template <class Rows>
-int csv_hash_file(const char* who, rss_ctx* ctx, const typename CsvJob<Rows>::Key* key,
-                  const char* in_path, const char* out_path, uint32_t htable, uint32_t nqueues,
-                  const uint32_t* reta, uint32_t flags, uint64_t* counts, size_t* n_rows) {
+int csv_hash_file_locked(const char* who, rss_ctx* ctx, const typename CsvJob<Rows>::Key* key,
+                         const char* in_path, const char* out_path, uint32_t htable, uint32_t nqueues,
+                         const uint32_t* reta, uint32_t flags, uint64_t* counts, size_t* n_rows) {
     if (!ctx || !in_path || !counts || !n_rows)
         return rss_set_error(RSS_EINVAL, "%s: NULL argument", who);
     const bool want_file = !(flags & RSS_CSV_COUNTS_ONLY);
@@ -979,7 +978,6 @@ int csv_hash_file(const char* who, rss_ctx* ctx, const typename CsvJob<Rows>::Ke
     int rc = check_args(key, htable, nqueues);
     if (rc) return rc;
     *n_rows = 0;
-    std::lock_guard<std::mutex> lock(ctx->mu);  // (struct rss_ctx)
     PhaseTimer timer(who);
     CSV_HIP_CHECK(hipSetDevice(ctx->device));
     if ((rc = reserve_stage(ctx))) return rc;
@@ -1113,6 +1111,33 @@ int csv_hash_file(const char* who, rss_ctx* ctx, const typename CsvJob<Rows>::Ke
     outf.fd = -1;
     timer.mark("close");
     return RSS_OK;
+}
+
+// Every entry point holds the context's lock for the whole call (struct rss_ctx) and, when
+// the call fails, waits out what it left in flight before the lock is released.
+template <class Rows>
+int csv_hash_text(const char* who, rss_ctx* ctx, const typename CsvJob<Rows>::Key* key,
+                  const char* text, size_t len, uint32_t htable, uint32_t nqueues,
+                  const uint32_t* reta, uint32_t flags, const char** out, size_t* out_len,
+                  uint64_t* counts, size_t* n_rows) {
+    if (!ctx) return rss_set_error(RSS_EINVAL, "%s: NULL argument", who);
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    const int rc = csv_hash_text_locked<Rows>(who, ctx, key, text, len, htable, nqueues, reta,
+                                              flags, out, out_len, counts, n_rows);
+    if (rc != RSS_OK) rss_ctx_quiesce(ctx);
+    return rc;
+}
+
+template <class Rows>
+int csv_hash_file(const char* who, rss_ctx* ctx, const typename CsvJob<Rows>::Key* key,
+                  const char* in_path, const char* out_path, uint32_t htable, uint32_t nqueues,
+                  const uint32_t* reta, uint32_t flags, uint64_t* counts, size_t* n_rows) {
+    if (!ctx) return rss_set_error(RSS_EINVAL, "%s: NULL argument", who);
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    const int rc = csv_hash_file_locked<Rows>(who, ctx, key, in_path, out_path, htable, nqueues,
+                                              reta, flags, counts, n_rows);
+    if (rc != RSS_OK) rss_ctx_quiesce(ctx);
+    return rc;
 }
 
 }  // namespace

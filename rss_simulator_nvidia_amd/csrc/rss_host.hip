@@ -72,6 +72,16 @@ void rotation_windows(const uint8_t* key, size_t len, uint32_t* window, int nbit
 // ------------------------------------------------------------ C ABI ---------
 // (struct rss_ctx: rss_internal.h)
 
+// (rss_internal.h) A host call that fails part-way may have left copies in flight -- an
+// earlier chunk's H2D from the caller's tuples, its D2H into the caller's outputs or the
+// staging.  Waiting them out before the lock is released keeps the caller's buffers and the
+// next call's staging untouched once the error is reported.  Errors here are ignored: the
+// first one is already in rss_last_error.
+void rss_ctx_quiesce(rss_ctx* ctx) {
+    for (int b = 0; b < 2; ++b)
+        if (ctx->stream[b]) (void)hipStreamSynchronize(ctx->stream[b]);
+}
+
 extern "C" {
 
 int rss_abi_version(void) { return RSS_ABI_VERSION; }
@@ -179,6 +189,7 @@ static int hash6_host_impl(rss_ctx* ctx, const rss_key6* key, const rss_tuple6* 
     uint32_t *d_h = nullptr, *d_q = nullptr;
     uint64_t* d_c = nullptr;
     auto cleanup = [&] {
+        (void)hipStreamSynchronize(s);  // nothing in flight may touch the freed buffers
         (void)hipFree(d_t);
         (void)hipFree(d_h);
         (void)hipFree(d_q);
@@ -408,6 +419,9 @@ static int hash_host_small(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h
 static int hash_host_impl(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples, size_t n,
                           uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
                           uint64_t* h_counts, uint32_t flags, const uint32_t* reta);
+static int hash_host_pipeline(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples, size_t n,
+                              uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
+                              uint64_t* h_counts, uint32_t flags, const uint32_t* reta);
 
 int rss_hash_host(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples, size_t n,
                   uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
@@ -518,9 +532,18 @@ static int hash_host_impl(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_
                              htable, nqueues);
     std::lock_guard<std::mutex> lock(ctx->mu);  // (struct rss_ctx)
     RSS_HIP_CHECK(hipSetDevice(ctx->device));
-    if (n > 0 && n <= kSmallBatch)
-        return hash_host_small(ctx, key, h_tuples, n, htable, nqueues, h_hash, h_queue, h_counts,
-                               flags, reta);
+    const int rc = n > 0 && n <= kSmallBatch
+                       ? hash_host_small(ctx, key, h_tuples, n, htable, nqueues, h_hash, h_queue,
+                                         h_counts, flags, reta)
+                       : hash_host_pipeline(ctx, key, h_tuples, n, htable, nqueues, h_hash, h_queue,
+                                            h_counts, flags, reta);
+    if (rc != RSS_OK) rss_ctx_quiesce(ctx);
+    return rc;
+}
+
+static int hash_host_pipeline(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples, size_t n,
+                              uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
+                              uint64_t* h_counts, uint32_t flags, const uint32_t* reta) {
     constexpr size_t kChunkMax = (size_t)1 << 22;  // 4M tuples: 48 MB in + 32 MB out per slot
     const size_t chunk = n < kChunkMax ? (n ? n : 1) : kChunkMax;
     int rc = ctx_reserve(ctx, chunk, nqueues);
@@ -625,6 +648,7 @@ int rss_key_search_host(rss_ctx* ctx, const rss_key* keys, size_t nkeys,
     uint64_t* d_c = nullptr;
     hipStream_t s = ctx->stream[0];
     auto cleanup = [&] {
+        (void)hipStreamSynchronize(s);
         (void)hipFree(d_w);
         (void)hipFree(d_t);
         (void)hipFree(d_c);

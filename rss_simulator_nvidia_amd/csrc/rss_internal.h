@@ -56,6 +56,11 @@ struct rss_ctx {
 // rss_csv_device.hip: release the CSV device path's staging and pooled blocks of a context
 RSS_HIDDEN void rss_csv_release(rss_ctx* ctx);
 
+// rss_host.hip: wait out whatever a failed call left in flight on the context's streams
+// (copies from or into the caller's buffers and the staging), called under `mu` before an
+// entry point returns an error.
+RSS_HIDDEN void rss_ctx_quiesce(rss_ctx* ctx);
+
 // Record the thread's rss_last_error() message; returns `code`.
 RSS_HIDDEN int rss_set_error(int code, const char* fmt, ...)
     __attribute__((format(printf, 2, 3)));

@@ -14,7 +14,9 @@ extern "C" {
 // "range8", "small_lut", "balance", "counts_perm", "resid", "wide" (0 / 1), "prefetch" (-1
 // by outputs, 0 / 1 forced), "guard_sleep" (n: a u16 guard's wave sleeps n x s_sleep 127
 // before its subtract, so that a heavy-hitter batch really wraps its bin; set on the current
-// device).  RSS_EINVAL for an unknown name.
+// device), "alloc_fail" (AllocKind bits: those scratch blocks are refused), "fail_launch"
+// (k > 0: the k-th IPv4 hash launch from now returns RSS_EIO, e.g. a later chunk of a
+// host-memory call).  RSS_EINVAL for an unknown name.
 int rss_test_set_option(const char* name, int value);
 void rss_test_reset_options(void);
 

@@ -1027,6 +1027,7 @@ struct Options {
     bool resid = true;        // counts only past 161144 queues: residual lists (else a column)
     bool wide = true;         // wide passes over a queue column (else u32 passes of 16384)
     int alloc_fail = 0;       // scratch kinds (AllocKind bits) whose allocation is made to fail
+    int fail_launch = 0;      // k > 0: the k-th rss::launch_hash from now returns RSS_EIO
 };
 #ifdef RSS_TEST_HOOKS
 Options g_opt;
@@ -1810,6 +1811,10 @@ namespace rss {
 int launch_hash(const rss_key* key, const rss_tuple4* d_tuples, size_t n, uint32_t htable,
                 uint32_t nqueues, uint32_t* d_hash, void* d_queue, uint64_t* d_counts,
                 uint32_t flags, hipStream_t stream, const uint32_t* reta, uint64_t* ws) {
+#ifdef RSS_TEST_HOOKS
+    if (g_opt.fail_launch > 0 && --g_opt.fail_launch == 0)
+        return rss_set_error(RSS_EIO, "rss_hash_device: launch failed (test hook fail_launch)");
+#endif
     return ::launch_hash(key, d_tuples, n, htable, nqueues, d_hash, d_queue, d_counts, flags,
                          stream, reta, ws);
 }
@@ -1859,6 +1864,7 @@ int rss_test_set_option(const char* name, int value) {
     else if (n == "resid") g_opt.resid = value != 0;
     else if (n == "wide") g_opt.wide = value != 0;
     else if (n == "alloc_fail") g_opt.alloc_fail = value;  // AllocKind bits
+    else if (n == "fail_launch") g_opt.fail_launch = value;
     else if (n == "guard_sleep") {
         const uint32_t v = value > 0 ? (uint32_t)value : 0u;
         RSS_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_guard_sleep), &v, sizeof v));

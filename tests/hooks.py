@@ -3,8 +3,9 @@
 ``csrc/rss_test_hooks.h``).  The product library reads no environment and exports no
 switches; these tests force the paths a launch takes when scratch memory runs short (u16
 bins instead of u8, the 12-bit tables, the scratch column instead of residual lists, the
-narrow passes, the static walk, a refused scratch block: alloc_fail) and the recount of a
-guarded pass through this build, and read the guarded bins' in-flight margin from it.
+narrow passes, the static walk, a refused scratch block: alloc_fail), the recount of a
+guarded pass and a launch that fails part-way through a host call (fail_launch) through this
+build, and read the guarded bins' in-flight margin from it.
 
 ``with hooks(recount=1): ...`` points ``_native``'s library handle at the hooks build for the
 duration (every ``_native`` entry point then calls it), sets the options and resets them on
@@ -18,7 +19,7 @@ from rss_simulator_nvidia_amd import _native
 HOOKS_PATH = os.path.join(os.path.dirname(os.path.abspath(_native.LIB_PATH)),
                           "librss_toeplitz_hooks.so")
 OPTIONS = ("recount", "range8", "small_lut", "prefetch", "balance", "counts_perm", "resid", "wide",
-           "guard_sleep", "alloc_fail")
+           "guard_sleep", "alloc_fail", "fail_launch")
 MARGINS = ("hash16", "wide16", "hash8", "wide8")
 _hooks = None
 

@@ -3,6 +3,7 @@ formats on the device must be byte-identical to the reference's golden outputs a
 the host path (rss_csv_parse + oracle hashes + rss_csv_format, itself pinned to pandas
 and the reference by tests/test_fastcsv.py); it must refuse exactly what the host
 scanner refuses."""
+import functools
 import os
 import random
 
@@ -215,6 +216,37 @@ def test_file_to_file_in_segments(native, ctx, oracle_lib, example_key, tmp_path
     c2, n2 = ctx.csv_hash_file(key, str(src), None, 128, 24)  # counts only, segmented too
     np.testing.assert_array_equal(c2, want[1])
     assert n2 == n
+
+
+@functools.lru_cache(maxsize=1)
+def _segmented_text():
+    return _random_canonical(random.Random(5), 2_400_000, [0, 1, 2, 3], crlf=False,
+                             blank_lines=False, trailing_nl=True)
+
+
+@pytest.mark.parametrize("where", ["first", "last"])
+def test_refusal_inside_a_segmented_file_then_recovery(native, ctx, oracle_lib, example_key,
+                                                       tmp_path, monkeypatch, where):
+    """A non-canonical row in the first or the last of a file's segments: the call refuses
+    part-way through the streaming (no output file), and the next call on the same context
+    streams the good file exactly."""
+    monkeypatch.setenv("RSS_CSV_SEGMENT_BYTES", str((64 << 20) + 4096))
+    text = _segmented_text()
+    header, body = text.split("\n", 1)
+    bad_row = "3.3.3.300,1.1.1.1,1,1\n"
+    bad_text = header + "\n" + (bad_row + body if where == "first" else body + bad_row)
+    src, bad, dst = tmp_path / "in.csv", tmp_path / "bad.csv", tmp_path / "out.csv"
+    src.write_bytes(text.encode())
+    bad.write_bytes(bad_text.encode())
+    assert src.stat().st_size > (64 << 20) + 4096
+    key = native.prepare_key(example_key)
+    assert ctx.csv_hash_file(key, str(bad), str(dst), 128, 24) is None
+    assert not dst.exists()
+    counts, n = ctx.csv_hash_file(key, str(src), str(dst), 128, 24)
+    want = host_image(native, oracle_lib, text, example_key, 128, 24)
+    assert n == want[2]
+    np.testing.assert_array_equal(counts, want[1])
+    assert dst.read_bytes() == want[0]
 
 
 def test_default_image_is_an_owned_copy(native, ctx, example_key):

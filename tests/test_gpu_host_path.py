@@ -1,8 +1,14 @@
 """rss_hash_host on page-locked buffers: the direct-DMA pipeline (no staging copies)
 must give exactly what the staged pipeline and the oracle give, for every mix of
-pinned / pageable input and outputs, over several 4M-tuple chunks with a ragged tail."""
+pinned / pageable input and outputs, over several 4M-tuple chunks with a ragged tail; and a call whose launch fails part-way
+leaves nothing in flight."""
+import time
+
 import numpy as np
 import pytest
+from hooks import hooks
+
+from rss_simulator_nvidia_amd.exceptions import DeviceError
 
 pytestmark = pytest.mark.gpu
 
@@ -117,3 +123,50 @@ def test_multi_context_small_and_ragged(native, oracle_lib, example_key, n):
     np.testing.assert_array_equal(q, reta[eh % 64])
     np.testing.assert_array_equal(c, np.bincount(reta[eh % 64], minlength=5).astype(np.uint64))
     multi.close()
+
+
+@pytest.mark.parametrize("fail_at", [1, 2, 3])
+@pytest.mark.parametrize("pinned", [True, False])
+def test_failed_chunk_leaves_nothing_in_flight(native, example_key, expected, fail_at, pinned):
+    """A launch that fails part-way through a host call (hooks fail_launch: the first, second
+    or third 4M-tuple chunk) reports the error, and the call has waited out the earlier
+    chunks' copies before returning: the caller's page-locked outputs stop changing the
+    moment it returns, and the next call on the same context gives the oracle's results."""
+    tup, ho, qo, co = expected
+    key = native.prepare_key(example_key)
+    if pinned:
+        src = native.pinned_empty(tup.shape, np.uint32)
+        src[:] = tup
+        out = (native.pinned_empty(N, np.uint32), native.pinned_empty(N, np.uint32))
+    else:
+        src, out = tup, (np.empty(N, np.uint32), np.empty(N, np.uint32))
+    with hooks(fail_launch=fail_at):
+        hctx = native.HostContext(0)
+        out[0].fill(0xDEADBEEF)
+        with pytest.raises(DeviceError, match="fail_launch"):
+            hctx.hash(key, src, 128, 24, out=out)
+        snap = out[0].copy()
+        time.sleep(0.05)
+        np.testing.assert_array_equal(out[0], snap)
+        if pinned and fail_at > 1:  # chunks before the failed one were written directly
+            np.testing.assert_array_equal(out[0][:4 << 20], ho[:4 << 20])
+        h, q, c = hctx.hash(key, src, 128, 24, out=out)
+        np.testing.assert_array_equal(h, ho)
+        np.testing.assert_array_equal(q, qo)
+        np.testing.assert_array_equal(c, co)
+        hctx.close()
+
+
+def test_failed_small_batch_then_recovers(native, example_key, expected):
+    """The small-batch path (<= 16384 tuples) after a failed launch on the same context."""
+    tup, ho, qo, _ = expected
+    key = native.prepare_key(example_key)
+    with hooks(fail_launch=1):
+        hctx = native.HostContext(0)
+        with pytest.raises(DeviceError, match="fail_launch"):
+            hctx.hash(key, tup[:1000], 128, 24)
+        h, q, c = hctx.hash(key, tup[:1000], 128, 24)
+        np.testing.assert_array_equal(h, ho[:1000])
+        np.testing.assert_array_equal(q, qo[:1000])
+        assert int(c.sum()) == 1000
+        hctx.close()
