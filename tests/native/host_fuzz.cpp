@@ -106,7 +106,7 @@ void mutate(Bytes& b, const std::vector<Bytes>& seeds, std::mt19937_64& rng) {
 }
 
 struct Stats {
-    size_t pcap4 = 0, pcap6 = 0, csv4 = 0, csv6 = 0;
+    size_t pcap4 = 0, pcap6 = 0, csv4 = 0, csv6 = 0, dotted = 0, ipv6 = 0;
 };
 
 void run_one(const Bytes& img, Stats& st) {
@@ -174,6 +174,28 @@ void run_one(const Bytes& img, Stats& st) {
             if (threads == 1) ++st.csv6;
         }
     }
+    // the DataFrame address-column parsers: the image as '\n'-joined cells
+    size_t cells = 1;
+    for (size_t i = 0; i < len; ++i) cells += text[i] == '\n';
+    std::vector<uint32_t> addr(4 * cells);
+    std::vector<uint8_t> ok(cells);
+    if (rss_parse_dotted(text, len, cells, addr.data(), ok.data()) != RSS_OK) abort();
+    if (rss_parse_dotted(text, len, cells + 1, addr.data(), ok.data()) != RSS_EINVAL) abort();
+    for (size_t i = 0, a = 0; i < cells; ++i) {  // a canonical cell is what formatting writes
+        size_t b = a;
+        while (b < len && text[b] != '\n') ++b;
+        if (ok[i] == 2) {
+            char buf[16];
+            const uint32_t v = addr[i];
+            const int k = snprintf(buf, sizeof buf, "%u.%u.%u.%u", v >> 24, (v >> 16) & 255u,
+                                   (v >> 8) & 255u, v & 255u);
+            if ((size_t)k != b - a || memcmp(buf, text + a, b - a) != 0) abort();
+            ++st.dotted;
+        }
+        a = b + 1;
+    }
+    if (rss_parse_ipv6(text, len, cells, addr.data(), ok.data()) != RSS_OK) abort();
+    for (size_t i = 0; i < cells; ++i) st.ipv6 += ok[i];
     free(data);
 }
 
@@ -195,7 +217,8 @@ int main(int argc, char** argv) {
         mutate(b, seeds, rng);
         run_one(b, st);
     }
-    printf("fuzz ok: %ld images, accepted pcap4 %zu pcap6 %zu csv4 %zu csv6 %zu\n",
-           iters + (long)seeds.size(), st.pcap4, st.pcap6, st.csv4, st.csv6);
+    printf("fuzz ok: %ld images, accepted pcap4 %zu pcap6 %zu csv4 %zu csv6 %zu dotted %zu "
+           "ipv6 %zu\n",
+           iters + (long)seeds.size(), st.pcap4, st.pcap6, st.csv4, st.csv6, st.dotted, st.ipv6);
     return 0;
 }
