@@ -1,3 +1,5 @@
+# The bench step 50,000 times back to back (no extras): sustained rate, per-launch spread.
+# GPU box: bash tools/sustained.sh  (writes gpurun_out/sustained/; a heartbeat file while it runs)
 mkdir -p gpurun_out/sustained || exit 1
 python -c "import torch; print('torch', torch.__version__, flush=True)" || exit 1
 ( for i in $(seq 1 22); do sleep 20; echo "bench running $((i*20)) s" >> gpurun_out/sustained/heartbeat.txt; done ) &
