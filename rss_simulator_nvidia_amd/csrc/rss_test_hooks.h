@@ -1,8 +1,9 @@
 // rss_test_hooks.h -- entry points of the TEST-HOOKS build only (librss_toeplitz_hooks.so,
 // rss_toeplitz.hip compiled with -DRSS_TEST_HOOKS).  Not part of the product ABI
 // (include/rss_toeplitz.h): the product library librss_toeplitz.so exports none of these and
-// reads no environment; the tests load the hooks build to force the paths a launch takes
-// when scratch memory runs short and to measure the guarded bins' in-flight margin.
+// its hashing path reads no environment; the tests load the hooks build to force the paths a
+// launch takes when scratch memory runs short, to fail a launch on purpose and to measure
+// the guarded bins' in-flight margin.
 #pragma once
 #include <stdint.h>
 

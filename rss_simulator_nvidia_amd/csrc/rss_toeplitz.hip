@@ -1015,7 +1015,7 @@ KernelFn pick_queue(int qmode, int hist, int qwidth, int vec4) {
 // tests force the other paths (the ones a launch takes when memory runs short, and the
 // recount of a guarded pass) through a test-hooks build of this file (-DRSS_TEST_HOOKS:
 // librss_toeplitz_hooks.so, loaded by tests/ only, rss_test_set_option in rss_test_hooks.h).
-// In the product library these are constants: it reads no environment.
+// In the product library these are constants: its hashing path reads no environment.
 struct Options {
     int recount = 0;          // guarded passes: 1 poisons every pass (the recount takes it), 2 runs
                               // no gate and no recount (counts from the bins and moves alone)

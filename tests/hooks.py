@@ -1,7 +1,7 @@
 """Test-only access to the TEST-HOOKS build of the engine (``librss_toeplitz_hooks.so``:
 ``csrc/rss_toeplitz.hip`` compiled with ``-DRSS_TEST_HOOKS``, declared in
-``csrc/rss_test_hooks.h``).  The product library reads no environment and exports no
-switches; these tests force the paths a launch takes when scratch memory runs short (u16
+``csrc/rss_test_hooks.h``).  The product library's hashing path reads no environment, and
+the library exports no switches; these tests force the paths a launch takes when scratch memory runs short (u16
 bins instead of u8, the 12-bit tables, the scratch column instead of residual lists, the
 narrow passes, the static walk, a refused scratch block: alloc_fail), the recount of a
 guarded pass and a launch that fails part-way through a host call (fail_launch) through this
