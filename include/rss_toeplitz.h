@@ -407,7 +407,8 @@ int rss_key_search_host(rss_ctx* ctx, const rss_key* keys, size_t nkeys,
                         const rss_tuple4* h_tuples, size_t n, uint32_t htable,
                         uint32_t nqueues, uint64_t* h_counts);
 
-/* rss_hash6_device on host buffers (synchronous). */
+/* rss_hash6_device on host buffers: rss_hash_host's contract and path (the same staging,
+ * small-batch path, pipeline and direct DMA of page-locked buffers), 36-byte tuples. */
 int rss_hash6_host(rss_ctx* ctx, const rss_key6* key, const rss_tuple6* h_tuples, size_t n,
                    uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
                    uint64_t* h_counts, uint32_t flags);

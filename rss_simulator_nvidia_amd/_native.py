@@ -276,11 +276,13 @@ def ptr(a):
     return a.ctypes.data if a is not None else None
 
 
-def _host_batch(tuples, nqueues, want_hash, want_queue, want_counts, out):
-    """Packed tuples as a contiguous array + the (hash, queue, counts) outputs to fill."""
+def _host_batch(tuples, nqueues, want_hash, want_queue, want_counts, out, ipv6=False):
+    """Packed tuples (IPv4, or IPv6 with ``ipv6``) as a contiguous array + the (hash, queue,
+    counts) outputs to fill."""
     arr = np.ascontiguousarray(tuples)
-    if arr.dtype != TUPLE_DTYPE:
-        arr = np.ascontiguousarray(arr, dtype=np.uint32).reshape(-1, 3)
+    dtype, words = (TUPLE6_DTYPE, 9) if ipv6 else (TUPLE_DTYPE, 3)
+    if arr.dtype != dtype:
+        arr = np.ascontiguousarray(arr, dtype=np.uint32).reshape(-1, words)
     n = len(arr)
     if out is not None:
         h, q = out
@@ -422,17 +424,13 @@ class HostContext:
 
 
     def hash6(self, key6, tuples6, htable, nqueues, want_hash=True, want_queue=True,
-              want_counts=True, reta=None):
-        """IPv6 batch (``TUPLE6_DTYPE`` or uint32 (n, 9)) -> (hash, queue, counts);
-        ``reta`` as for :meth:`hash`."""
+              want_counts=True, reta=None, out=None):
+        """IPv6 batch (``TUPLE6_DTYPE`` or uint32 (n, 9)) -> (hash, queue, counts) through
+        the same staging, small-batch path and pipeline as :meth:`hash`; ``reta`` and
+        ``out`` (page-locked arrays skip the staging copies) as there."""
         htable, nqueues = queue_modulus(htable, nqueues, reta is not None)
-        arr = np.ascontiguousarray(tuples6)
-        if arr.dtype != TUPLE6_DTYPE:
-            arr = np.ascontiguousarray(arr, dtype=np.uint32).reshape(-1, 9)
-        n = len(arr)
-        h = np.empty(n, dtype=np.uint32) if want_hash else None
-        q = np.empty(n, dtype=np.uint32) if want_queue else None
-        c = np.zeros(nqueues, dtype=np.uint64) if want_counts else None
+        arr, n, h, q, c = _host_batch(tuples6, nqueues, want_hash, want_queue, want_counts, out,
+                                      ipv6=True)
         if reta is None:
             _check(self._lib.rss_hash6_host(self._ctx, ctypes.byref(key6), ptr(arr), n, htable,
                                             nqueues, ptr(h), ptr(q), ptr(c), 0), "rss_hash6_host")

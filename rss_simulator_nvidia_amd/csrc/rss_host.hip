@@ -158,75 +158,6 @@ int rss_hash6_device_reta(const rss_key6* key, const rss_tuple6* d_tuples, size_
                              static_cast<hipStream_t>(stream), reta);
 }
 
-static int hash6_host_impl(rss_ctx* ctx, const rss_key6* key, const rss_tuple6* h_tuples, size_t n,
-                           uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
-                           uint64_t* h_counts, uint32_t flags, const uint32_t* reta);
-
-int rss_hash6_host(rss_ctx* ctx, const rss_key6* key, const rss_tuple6* h_tuples, size_t n,
-                   uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
-                   uint64_t* h_counts, uint32_t flags) {
-    return hash6_host_impl(ctx, key, h_tuples, n, htable, nqueues, h_hash, h_queue, h_counts,
-                           flags, nullptr);
-}
-
-int rss_hash6_host_reta(rss_ctx* ctx, const rss_key6* key, const rss_tuple6* h_tuples, size_t n,
-                        uint32_t htable, const uint32_t* reta, uint32_t nqueues, uint32_t* h_hash,
-                        uint32_t* h_queue, uint64_t* h_counts, uint32_t flags) {
-    if (!reta) return rss_set_error(RSS_EINVAL, "rss_hash6_host_reta: reta is NULL");
-    return hash6_host_impl(ctx, key, h_tuples, n, htable, nqueues, h_hash, h_queue, h_counts,
-                           flags, reta);
-}
-
-static int hash6_host_impl(rss_ctx* ctx, const rss_key6* key, const rss_tuple6* h_tuples, size_t n,
-                           uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
-                           uint64_t* h_counts, uint32_t flags, const uint32_t* reta) {
-    if (!ctx) return rss_set_error(RSS_EINVAL, "rss_hash6_host: ctx is NULL");
-    if (n && !h_tuples) return rss_set_error(RSS_EINVAL, "rss_hash6_host: tuples is NULL");
-    std::lock_guard<std::mutex> lock(ctx->mu);  // (struct rss_ctx)
-    RSS_HIP_CHECK(hipSetDevice(ctx->device));
-    hipStream_t s = ctx->stream[0];
-    rss_tuple6* d_t = nullptr;
-    uint32_t *d_h = nullptr, *d_q = nullptr;
-    uint64_t* d_c = nullptr;
-    auto cleanup = [&] {
-        (void)hipStreamSynchronize(s);  // nothing in flight may touch the freed buffers
-        (void)hipFree(d_t);
-        (void)hipFree(d_h);
-        (void)hipFree(d_q);
-        (void)hipFree(d_c);
-    };
-    hipError_t e = hipSuccess;
-    if (n) e = hipMalloc(&d_t, n * sizeof(rss_tuple6));
-    if (e == hipSuccess && n && h_hash) e = hipMalloc(&d_h, n * 4);
-    if (e == hipSuccess && n && h_queue) e = hipMalloc(&d_q, n * 4);
-    if (e == hipSuccess && h_counts) e = hipMalloc(&d_c, nqueues * 8);
-    if (e == hipSuccess && n)
-        e = hipMemcpyAsync(d_t, h_tuples, n * sizeof(rss_tuple6), hipMemcpyHostToDevice, s);
-    if (e != hipSuccess) {
-        cleanup();
-        return rss_set_error(e == hipErrorOutOfMemory ? RSS_ENOMEM : RSS_EIO, "rss_hash6_host: %s",
-                             hipGetErrorString(e));
-    }
-    int rc = rss::launch_hash6(key, d_t, n, htable, nqueues, d_h, d_q, d_c,
-                               0u, s, reta);  // device counts start at 0; accumulation on the host
-    if (rc == RSS_OK) {
-        if (d_h) e = hipMemcpyAsync(h_hash, d_h, n * 4, hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess && d_q) e = hipMemcpyAsync(h_queue, d_q, n * 4, hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess && d_c) {
-            std::vector<uint64_t> tmp(nqueues);
-            e = hipMemcpyAsync(tmp.data(), d_c, nqueues * 8, hipMemcpyDeviceToHost, s);
-            if (e == hipSuccess) e = hipStreamSynchronize(s);
-            if (e == hipSuccess)
-                for (uint32_t q = 0; q < nqueues; ++q)
-                    h_counts[q] = (flags & RSS_FLAG_ACCUMULATE ? h_counts[q] : 0) + tmp[q];
-        }
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess) rc = rss_set_error(RSS_EIO, "rss_hash6_host: %s", hipGetErrorString(e));
-    }
-    cleanup();
-    return rc;
-}
-
 int rss_device_count(int* out) {
     if (!out) return rss_set_error(RSS_EINVAL, "rss_device_count: NULL argument");
     *out = 0;
@@ -339,30 +270,41 @@ int rss_ctx_create(int device, rss_ctx** out) {
     return RSS_OK;
 }
 
-static int ctx_reserve(rss_ctx* ctx, size_t chunk, uint32_t nqueues) {
-    if (ctx->chunk < chunk) {
+}  // extern "C"
+
+// Grows the context's staging to `chunk` output tuples, `in_bytes` of input per slot and
+// `nqueues` counts (never shrinks).
+static int ctx_reserve(rss_ctx* ctx, size_t chunk, size_t in_bytes, uint32_t nqueues) {
+    if (ctx->in_cap < in_bytes) {
         for (int b = 0; b < 2; ++b) {
             (void)hipFree(ctx->d_in[b]);
+            (void)hipHostFree(ctx->h_in[b]);
+            ctx->d_in[b] = ctx->h_in[b] = nullptr;
+        }
+        ctx->in_cap = 0;
+        for (int b = 0; b < 2; ++b) {
+            RSS_HIP_CHECK(hipMalloc(&ctx->d_in[b], in_bytes));
+            RSS_HIP_CHECK(hipHostMalloc(&ctx->h_in[b], in_bytes, hipHostMallocDefault));
+        }
+        RSS_HIP_CHECK(hipHostGetDevicePointer(&ctx->alias_in, ctx->h_in[0], 0));
+        ctx->in_cap = in_bytes;
+    }
+    if (ctx->chunk < chunk) {
+        for (int b = 0; b < 2; ++b) {
             (void)hipFree(ctx->d_hash[b]);
             (void)hipFree(ctx->d_queue[b]);
-            (void)hipHostFree(ctx->h_in[b]);
             (void)hipHostFree(ctx->h_hash[b]);
             (void)hipHostFree(ctx->h_queue[b]);
-            ctx->d_in[b] = nullptr;
             ctx->d_hash[b] = ctx->d_queue[b] = nullptr;
-            ctx->h_in[b] = nullptr;
             ctx->h_hash[b] = ctx->h_queue[b] = nullptr;
         }
         ctx->chunk = 0;
         for (int b = 0; b < 2; ++b) {
-            RSS_HIP_CHECK(hipMalloc(&ctx->d_in[b], chunk * sizeof(rss_tuple4)));
             RSS_HIP_CHECK(hipMalloc(&ctx->d_hash[b], chunk * sizeof(uint32_t)));
             RSS_HIP_CHECK(hipMalloc(&ctx->d_queue[b], chunk * sizeof(uint32_t)));
-            RSS_HIP_CHECK(hipHostMalloc(&ctx->h_in[b], chunk * sizeof(rss_tuple4), hipHostMallocDefault));
             RSS_HIP_CHECK(hipHostMalloc(&ctx->h_hash[b], chunk * sizeof(uint32_t), hipHostMallocDefault));
             RSS_HIP_CHECK(hipHostMalloc(&ctx->h_queue[b], chunk * sizeof(uint32_t), hipHostMallocDefault));
         }
-        RSS_HIP_CHECK(hipHostGetDevicePointer(&ctx->alias_in, ctx->h_in[0], 0));
         RSS_HIP_CHECK(hipHostGetDevicePointer(&ctx->alias_hash, ctx->h_hash[0], 0));
         RSS_HIP_CHECK(hipHostGetDevicePointer(&ctx->alias_queue, ctx->h_queue[0], 0));
         ctx->chunk = chunk;
@@ -383,6 +325,30 @@ static int ctx_reserve(rss_ctx* ctx, size_t chunk, uint32_t nqueues) {
     return RSS_OK;
 }
 
+// The two tuple layouts share the host path -- staging, small batches, the pipeline --
+// and differ in their tuple, key and launcher.
+struct Ipv4 {
+    using Tuple = rss_tuple4;
+    using Key = rss_key;
+    static constexpr const char* kWho = "rss_hash_host";
+    static int launch(const Key* key, const Tuple* t, size_t n, uint32_t htable, uint32_t nqueues,
+                      uint32_t* hash, void* queue, uint64_t* counts, uint32_t flags, hipStream_t s,
+                      const uint32_t* reta) {
+        return rss::launch_hash(key, t, n, htable, nqueues, hash, queue, counts, flags, s, reta);
+    }
+};
+
+struct Ipv6 {
+    using Tuple = rss_tuple6;
+    using Key = rss_key6;
+    static constexpr const char* kWho = "rss_hash6_host";
+    static int launch(const Key* key, const Tuple* t, size_t n, uint32_t htable, uint32_t nqueues,
+                      uint32_t* hash, void* queue, uint64_t* counts, uint32_t flags, hipStream_t s,
+                      const uint32_t* reta) {
+        return rss::launch_hash6(key, t, n, htable, nqueues, hash, queue, counts, flags, s, reta);
+    }
+};
+
 // Small host batches -- a reference-style caller hashing one row per call
 // (Toeplitz.compute_hash from Simulator.__calc_entry_hash, simulator.py:80-92) -- are
 // bound by per-call overhead, not bytes: one stream, no pointer-attribute queries, the
@@ -391,17 +357,21 @@ static int ctx_reserve(rss_ctx* ctx, size_t chunk, uint32_t nqueues) {
 // one synchronisation.  Same kernel and results as the pipelined path.
 constexpr size_t kSmallBatch = (size_t)1 << 14;
 
-static int hash_host_small(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples, size_t n,
-                           uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
+template <class L>
+static int hash_host_small(rss_ctx* ctx, const typename L::Key* key,
+                           const typename L::Tuple* h_tuples, size_t n, uint32_t htable,
+                           uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
                            uint64_t* h_counts, uint32_t flags, const uint32_t* reta) {
-    int rc = ctx_reserve(ctx, std::max(ctx->chunk, kSmallBatch), h_counts ? nqueues : 1);
+    using Tuple = typename L::Tuple;
+    int rc = ctx_reserve(ctx, std::max(ctx->chunk, kSmallBatch), kSmallBatch * sizeof(Tuple),
+                         h_counts ? nqueues : 1);
     if (rc) return rc;
     hipStream_t s = ctx->stream[0];
-    memcpy(ctx->h_in[0], h_tuples, n * sizeof(rss_tuple4));
-    rc = rss::launch_hash(key, static_cast<const rss_tuple4*>(ctx->alias_in), n, htable, nqueues,
-                          h_hash ? static_cast<uint32_t*>(ctx->alias_hash) : nullptr,
-                          h_queue ? ctx->alias_queue : nullptr, h_counts ? ctx->d_counts[0] : nullptr,
-                          0, s, reta);
+    memcpy(ctx->h_in[0], h_tuples, n * sizeof(Tuple));
+    rc = L::launch(key, static_cast<const Tuple*>(ctx->alias_in), n, htable, nqueues,
+                   h_hash ? static_cast<uint32_t*>(ctx->alias_hash) : nullptr,
+                   h_queue ? ctx->alias_queue : nullptr, h_counts ? ctx->d_counts[0] : nullptr, 0,
+                   s, reta);
     if (rc) return rc;
     if (h_counts)
         RSS_HIP_CHECK(hipMemcpyAsync(ctx->h_counts, ctx->d_counts[0], sizeof(uint64_t) * nqueues,
@@ -416,82 +386,12 @@ static int hash_host_small(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h
     return RSS_OK;
 }
 
-static int hash_host_impl(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples, size_t n,
-                          uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
-                          uint64_t* h_counts, uint32_t flags, const uint32_t* reta);
-static int hash_host_pipeline(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples, size_t n,
-                              uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
-                              uint64_t* h_counts, uint32_t flags, const uint32_t* reta);
-
-int rss_hash_host(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples, size_t n,
-                  uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
-                  uint64_t* h_counts, uint32_t flags) {
-    return hash_host_impl(ctx, key, h_tuples, n, htable, nqueues, h_hash, h_queue, h_counts, flags,
-                          nullptr);
-}
-
-int rss_hash_host_reta(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples, size_t n,
-                       uint32_t htable, const uint32_t* reta, uint32_t nqueues, uint32_t* h_hash,
-                       uint32_t* h_queue, uint64_t* h_counts, uint32_t flags) {
-    if (!reta) return rss_set_error(RSS_EINVAL, "rss_hash_host_reta: reta is NULL");
-    return hash_host_impl(ctx, key, h_tuples, n, htable, nqueues, h_hash, h_queue, h_counts, flags,
-                          reta);
-}
-
-int rss_hash_host_multi(rss_ctx* const* ctxs, int nctx, const rss_key* key,
-                        const rss_tuple4* h_tuples, size_t n, uint32_t htable,
-                        const uint32_t* reta, uint32_t nqueues, uint32_t* h_hash,
-                        uint32_t* h_queue, uint64_t* h_counts, uint32_t flags) {
-    if (!ctxs || nctx < 1 || !key)
-        return rss_set_error(RSS_EINVAL, "rss_hash_host_multi: NULL argument or no contexts");
-    for (int i = 0; i < nctx; ++i) {
-        if (!ctxs[i]) return rss_set_error(RSS_EINVAL, "rss_hash_host_multi: context %d is NULL", i);
-        for (int j = 0; j < i; ++j)
-            if (ctxs[j] == ctxs[i])
-                return rss_set_error(RSS_EINVAL, "rss_hash_host_multi: contexts %d and %d are the same",
-                                     j, i);
-    }
-    if (n && !h_tuples) return rss_set_error(RSS_EINVAL, "rss_hash_host_multi: tuples is NULL");
-    if (htable < 1 || nqueues < 1)
-        return rss_set_error(RSS_EINVAL, "rss_hash_host_multi: htable (%u) and nqueues (%u) must be >= 1",
-                             htable, nqueues);
-    // contiguous ranges, exactly sharding.shard_range's: n / nctx each, the first n % nctx
-    // ranges one longer
-    const size_t base = n / (size_t)nctx, extra = n % (size_t)nctx;
-    std::vector<std::vector<uint64_t>> part(nctx, std::vector<uint64_t>(h_counts ? nqueues : 0));
-    std::vector<int> rcs(nctx, RSS_OK);
-    std::vector<std::string> errs(nctx);
-    auto work = [&](int i) {
-        const size_t a = base * (size_t)i + std::min((size_t)i, extra);
-        const size_t b = a + base + ((size_t)i < extra ? 1 : 0);
-        const int rc = hash_host_impl(ctxs[i], key, h_tuples ? h_tuples + a : nullptr, b - a, htable,
-                                      nqueues, h_hash ? h_hash + a : nullptr,
-                                      h_queue ? h_queue + a : nullptr,
-                                      h_counts ? part[i].data() : nullptr, 0, reta);
-        if (rc) {
-            rcs[i] = rc;
-            errs[i] = g_last_error;  // thread-local: carried back to the calling thread
-        }
-    };
-    std::vector<std::thread> pool;
-    for (int i = 1; i < nctx; ++i) pool.emplace_back(work, i);
-    work(0);
-    for (auto& t : pool) t.join();
-    for (int i = 0; i < nctx; ++i)
-        if (rcs[i]) return rss_set_error(rcs[i], "rss_hash_host_multi: context %d: %s", i, errs[i].c_str());
-    if (h_counts) {
-        if (!(flags & RSS_FLAG_ACCUMULATE)) memset(h_counts, 0, sizeof(uint64_t) * nqueues);
-        for (int i = 0; i < nctx; ++i)
-            for (uint32_t q = 0; q < nqueues; ++q) h_counts[q] += part[i][q];
-    }
-    return RSS_OK;
-}
-
-// memcpy split over up to 8 threads: the pinned staging copies, not PCIe or the kernel,
-// bound rss_hash_host (one thread moves ~10 GB/s; a 4M-tuple slot is 80 MB each way)
+// memcpy split over up to 8 threads, 1 MiB or more each, from 4 MiB on (below that a thread
+// start costs more than it saves): the pinned staging copies, not PCIe or the kernel, bound
+// rss_hash_host (one thread moves ~10 GB/s; a 4M-tuple slot is 80 MB each way)
 static void par_memcpy(void* dst, const void* src, size_t bytes) {
-    constexpr size_t kPerThread = (size_t)4 << 20;
-    const size_t nt = std::min<size_t>(8, bytes / kPerThread);
+    constexpr size_t kPerThread = (size_t)1 << 20, kSplitFrom = (size_t)4 << 20;
+    const size_t nt = bytes < kSplitFrom ? 1 : std::min<size_t>(8, bytes / kPerThread);
     if (nt <= 1) {
         memcpy(dst, src, bytes);
         return;
@@ -522,31 +422,22 @@ static bool host_pinned(const void* p, size_t bytes) {
     return true;
 }
 
-static int hash_host_impl(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples, size_t n,
-                          uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
-                          uint64_t* h_counts, uint32_t flags, const uint32_t* reta) {
-    if (!ctx) return rss_set_error(RSS_EINVAL, "rss_hash_host: ctx is NULL");
-    if (n && !h_tuples) return rss_set_error(RSS_EINVAL, "rss_hash_host: tuples is NULL");
-    if (htable < 1 || nqueues < 1)
-        return rss_set_error(RSS_EINVAL, "rss_hash_host: htable (%u) and nqueues (%u) must be >= 1",
-                             htable, nqueues);
-    std::lock_guard<std::mutex> lock(ctx->mu);  // (struct rss_ctx)
-    RSS_HIP_CHECK(hipSetDevice(ctx->device));
-    const int rc = n > 0 && n <= kSmallBatch
-                       ? hash_host_small(ctx, key, h_tuples, n, htable, nqueues, h_hash, h_queue,
-                                         h_counts, flags, reta)
-                       : hash_host_pipeline(ctx, key, h_tuples, n, htable, nqueues, h_hash, h_queue,
-                                            h_counts, flags, reta);
-    if (rc != RSS_OK) rss_ctx_quiesce(ctx);
-    return rc;
-}
-
-static int hash_host_pipeline(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples, size_t n,
-                              uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
+template <class L>
+static int hash_host_pipeline(rss_ctx* ctx, const typename L::Key* key,
+                              const typename L::Tuple* h_tuples, size_t n, uint32_t htable,
+                              uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
                               uint64_t* h_counts, uint32_t flags, const uint32_t* reta) {
-    constexpr size_t kChunkMax = (size_t)1 << 22;  // 4M tuples: 48 MB in + 32 MB out per slot
-    const size_t chunk = n < kChunkMax ? (n ? n : 1) : kChunkMax;
-    int rc = ctx_reserve(ctx, chunk, nqueues);
+    using Tuple = typename L::Tuple;
+    // 48 MB of input per slot, in 64K-tuple steps: 4M IPv4 tuples (+ 32 MB out), 1.38M IPv6
+    // tuples (+ 11 MB out)
+    constexpr size_t kChunkMax = (((size_t)48 << 20) / sizeof(Tuple)) & ~(size_t)0xFFFF;
+    // at least four chunks once a batch has 1M tuples, so that copies and the kernel overlap
+    // from the second chunk on
+    constexpr size_t kStep = (size_t)1 << 16, kChunkMin = (size_t)1 << 18;
+    const size_t quarter = ((n + 3) / 4 + kStep - 1) / kStep * kStep;
+    const size_t chunk = n <= kChunkMin ? (n ? n : 1)
+                                        : std::min(kChunkMax, std::max(kChunkMin, quarter));
+    int rc = ctx_reserve(ctx, chunk, chunk * sizeof(Tuple), nqueues);
     if (rc) return rc;
     for (int b = 0; b < 2; ++b)
         RSS_HIP_CHECK(hipMemsetAsync(ctx->d_counts[b], 0, sizeof(uint64_t) * nqueues, ctx->stream[b]));
@@ -555,7 +446,7 @@ static int hash_host_pipeline(rss_ctx* ctx, const rss_key* key, const rss_tuple4
     // stream, the host fills the other slot's pinned input and drains its output.
     // Caller buffers that are already page-locked skip the staging copy: the copy
     // engines move them directly, so only PCIe bounds the pipeline.
-    const bool in_direct = host_pinned(h_tuples, n * sizeof(rss_tuple4));
+    const bool in_direct = host_pinned(h_tuples, n * sizeof(Tuple));
     const bool hash_direct = host_pinned(h_hash, h_hash ? n * 4 : 0);
     const bool queue_direct = host_pinned(h_queue, h_queue ? n * 4 : 0);
     const size_t nchunks = (n + chunk - 1) / chunk;
@@ -582,16 +473,15 @@ static int hash_host_pipeline(rss_ctx* ctx, const rss_key* key, const rss_tuple4
             rc = drain(b);
             if (rc) return rc;
         }
-        const rss_tuple4* up = h_tuples + off;
+        const void* up = h_tuples + off;
         if (!in_direct) {
-            par_memcpy(ctx->h_in[b], up, len * sizeof(rss_tuple4));
+            par_memcpy(ctx->h_in[b], up, len * sizeof(Tuple));
             up = ctx->h_in[b];
         }
-        RSS_HIP_CHECK(hipMemcpyAsync(ctx->d_in[b], up, len * sizeof(rss_tuple4),
-                                     hipMemcpyHostToDevice, s));
-        rc = rss::launch_hash(key, ctx->d_in[b], len, htable, nqueues, h_hash ? ctx->d_hash[b] : nullptr,
-                              h_queue ? ctx->d_queue[b] : nullptr, ctx->d_counts[b],
-                              RSS_FLAG_ACCUMULATE, s, reta);  // u32 queues on the host path
+        RSS_HIP_CHECK(hipMemcpyAsync(ctx->d_in[b], up, len * sizeof(Tuple), hipMemcpyHostToDevice, s));
+        rc = L::launch(key, static_cast<const Tuple*>(ctx->d_in[b]), len, htable, nqueues,
+                       h_hash ? ctx->d_hash[b] : nullptr, h_queue ? ctx->d_queue[b] : nullptr,
+                       ctx->d_counts[b], RSS_FLAG_ACCUMULATE, s, reta);  // u32 queues on the host path
         if (rc) return rc;
         if (h_hash)
             RSS_HIP_CHECK(hipMemcpyAsync(hash_direct ? h_hash + off : ctx->h_hash[b],
@@ -614,6 +504,111 @@ static int hash_host_pipeline(rss_ctx* ctx, const rss_key* key, const rss_tuple4
                                     hipMemcpyDeviceToHost));
             for (uint32_t q = 0; q < nqueues; ++q) h_counts[q] += tmp[q];
         }
+    }
+    return RSS_OK;
+}
+
+// Every host-memory entry point: argument checks, the context's lock for the whole call
+// (struct rss_ctx), the small-batch path or the pipeline, and on failure the wait for
+// whatever the call left in flight (rss_ctx_quiesce) before the lock is released.
+template <class L>
+static int hash_host_locked(rss_ctx* ctx, const typename L::Key* key,
+                            const typename L::Tuple* h_tuples, size_t n, uint32_t htable,
+                            uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
+                            uint64_t* h_counts, uint32_t flags, const uint32_t* reta) {
+    if (!ctx) return rss_set_error(RSS_EINVAL, "%s: ctx is NULL", L::kWho);
+    if (n && !h_tuples) return rss_set_error(RSS_EINVAL, "%s: tuples is NULL", L::kWho);
+    if (htable < 1 || nqueues < 1)
+        return rss_set_error(RSS_EINVAL, "%s: htable (%u) and nqueues (%u) must be >= 1", L::kWho,
+                             htable, nqueues);
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    RSS_HIP_CHECK(hipSetDevice(ctx->device));
+    const int rc = n > 0 && n <= kSmallBatch
+                       ? hash_host_small<L>(ctx, key, h_tuples, n, htable, nqueues, h_hash,
+                                            h_queue, h_counts, flags, reta)
+                       : hash_host_pipeline<L>(ctx, key, h_tuples, n, htable, nqueues, h_hash,
+                                               h_queue, h_counts, flags, reta);
+    if (rc != RSS_OK) rss_ctx_quiesce(ctx);
+    return rc;
+}
+
+extern "C" {
+
+int rss_hash_host(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples, size_t n,
+                  uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
+                  uint64_t* h_counts, uint32_t flags) {
+    return hash_host_locked<Ipv4>(ctx, key, h_tuples, n, htable, nqueues, h_hash, h_queue,
+                                  h_counts, flags, nullptr);
+}
+
+int rss_hash_host_reta(rss_ctx* ctx, const rss_key* key, const rss_tuple4* h_tuples, size_t n,
+                       uint32_t htable, const uint32_t* reta, uint32_t nqueues, uint32_t* h_hash,
+                       uint32_t* h_queue, uint64_t* h_counts, uint32_t flags) {
+    if (!reta) return rss_set_error(RSS_EINVAL, "rss_hash_host_reta: reta is NULL");
+    return hash_host_locked<Ipv4>(ctx, key, h_tuples, n, htable, nqueues, h_hash, h_queue,
+                                  h_counts, flags, reta);
+}
+
+int rss_hash6_host(rss_ctx* ctx, const rss_key6* key, const rss_tuple6* h_tuples, size_t n,
+                   uint32_t htable, uint32_t nqueues, uint32_t* h_hash, uint32_t* h_queue,
+                   uint64_t* h_counts, uint32_t flags) {
+    return hash_host_locked<Ipv6>(ctx, key, h_tuples, n, htable, nqueues, h_hash, h_queue,
+                                  h_counts, flags, nullptr);
+}
+
+int rss_hash6_host_reta(rss_ctx* ctx, const rss_key6* key, const rss_tuple6* h_tuples, size_t n,
+                        uint32_t htable, const uint32_t* reta, uint32_t nqueues, uint32_t* h_hash,
+                        uint32_t* h_queue, uint64_t* h_counts, uint32_t flags) {
+    if (!reta) return rss_set_error(RSS_EINVAL, "rss_hash6_host_reta: reta is NULL");
+    return hash_host_locked<Ipv6>(ctx, key, h_tuples, n, htable, nqueues, h_hash, h_queue,
+                                  h_counts, flags, reta);
+}
+
+int rss_hash_host_multi(rss_ctx* const* ctxs, int nctx, const rss_key* key,
+                        const rss_tuple4* h_tuples, size_t n, uint32_t htable,
+                        const uint32_t* reta, uint32_t nqueues, uint32_t* h_hash,
+                        uint32_t* h_queue, uint64_t* h_counts, uint32_t flags) {
+    if (!ctxs || nctx < 1 || !key)
+        return rss_set_error(RSS_EINVAL, "rss_hash_host_multi: NULL argument or no contexts");
+    for (int i = 0; i < nctx; ++i) {
+        if (!ctxs[i]) return rss_set_error(RSS_EINVAL, "rss_hash_host_multi: context %d is NULL", i);
+        for (int j = 0; j < i; ++j)
+            if (ctxs[j] == ctxs[i])
+                return rss_set_error(RSS_EINVAL, "rss_hash_host_multi: contexts %d and %d are the same",
+                                     j, i);
+    }
+    if (n && !h_tuples) return rss_set_error(RSS_EINVAL, "rss_hash_host_multi: tuples is NULL");
+    if (htable < 1 || nqueues < 1)
+        return rss_set_error(RSS_EINVAL, "rss_hash_host_multi: htable (%u) and nqueues (%u) must be >= 1",
+                             htable, nqueues);
+    // contiguous ranges, exactly sharding.shard_range's: n / nctx each, the first n % nctx
+    // ranges one longer
+    const size_t base = n / (size_t)nctx, extra = n % (size_t)nctx;
+    std::vector<std::vector<uint64_t>> part(nctx, std::vector<uint64_t>(h_counts ? nqueues : 0));
+    std::vector<int> rcs(nctx, RSS_OK);
+    std::vector<std::string> errs(nctx);
+    auto work = [&](int i) {
+        const size_t a = base * (size_t)i + std::min((size_t)i, extra);
+        const size_t b = a + base + ((size_t)i < extra ? 1 : 0);
+        const int rc = hash_host_locked<Ipv4>(ctxs[i], key, h_tuples ? h_tuples + a : nullptr, b - a,
+                                              htable, nqueues, h_hash ? h_hash + a : nullptr,
+                                              h_queue ? h_queue + a : nullptr,
+                                              h_counts ? part[i].data() : nullptr, 0, reta);
+        if (rc) {
+            rcs[i] = rc;
+            errs[i] = g_last_error;  // thread-local: carried back to the calling thread
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int i = 1; i < nctx; ++i) pool.emplace_back(work, i);
+    work(0);
+    for (auto& t : pool) t.join();
+    for (int i = 0; i < nctx; ++i)
+        if (rcs[i]) return rss_set_error(rcs[i], "rss_hash_host_multi: context %d: %s", i, errs[i].c_str());
+    if (h_counts) {
+        if (!(flags & RSS_FLAG_ACCUMULATE)) memset(h_counts, 0, sizeof(uint64_t) * nqueues);
+        for (int i = 0; i < nctx; ++i)
+            for (uint32_t q = 0; q < nqueues; ++q) h_counts[q] += part[i][q];
     }
     return RSS_OK;
 }

@@ -17,7 +17,7 @@ typedef struct ihipStream_t* hipStream_t;
 typedef struct ihipEvent_t* hipEvent_t;
 
 // Host-pipeline context (rss_ctx_create): device, streams and staging buffers of
-// rss_hash_host, plus the host output buffer of rss_csv_hash_text.
+// rss_hash_host / rss_hash6_host, plus the host output buffer of rss_csv_hash_text.
 //
 // Every entry point that takes a context holds `mu` for the whole call (the staging
 // buffers, streams and scratch below are one caller's at a time): the reference-compatible
@@ -27,14 +27,15 @@ typedef struct ihipEvent_t* hipEvent_t;
 struct rss_ctx {
     std::mutex mu;
     int device = 0;
-    size_t chunk = 0;  // tuples per staging buffer
+    size_t chunk = 0;   // tuples per output staging buffer (hash, queue)
+    size_t in_cap = 0;  // bytes per input staging buffer (IPv4 or IPv6 tuples)
     hipStream_t stream[2] = {nullptr, nullptr};
-    rss_tuple4* d_in[2] = {nullptr, nullptr};
+    void* d_in[2] = {nullptr, nullptr};
     uint32_t* d_hash[2] = {nullptr, nullptr};
     uint32_t* d_queue[2] = {nullptr, nullptr};
     uint64_t* d_counts[2] = {nullptr, nullptr};
     uint32_t counts_cap = 0;
-    rss_tuple4* h_in[2] = {nullptr, nullptr};
+    void* h_in[2] = {nullptr, nullptr};
     uint32_t* h_hash[2] = {nullptr, nullptr};
     uint32_t* h_queue[2] = {nullptr, nullptr};
     // small batches (rss_hash_host, n <= kSmallBatch): device aliases of slot 0's pinned

@@ -102,3 +102,70 @@ def test_host_path_and_reference_api(native, oracle_lib, example_key):
         h, q, c = tz.compute_queues6(host, H, Q, devices=devices)
         for got, want in ((h, ho), (q, qo), (c, co)):
             np.testing.assert_array_equal(got, want)
+
+
+IPV6_CHUNK = 21 * 65536  # rss_hash6_host's slot: 48 MB of 36-byte tuples, rounded down to 64K
+
+
+@pytest.mark.parametrize("pin_in,pin_out", [(False, False), (True, True), (True, False),
+                                            (False, True)])
+def test_host_pipeline_chunks_and_pinned_buffers(native, oracle_lib, example_key, pin_in,
+                                                 pin_out):
+    """rss_hash6_host runs the IPv4 host path's pipeline: three 1.38M-tuple chunks with a
+    ragged tail through two staging slots and two streams, or straight from / into
+    page-locked caller buffers, every element equal to the oracle's; then an indirection
+    table on the same context."""
+    n, H, Q = 2 * IPV6_CHUNK + 12345, 128, 24
+    host = _words(31, n)
+    ho, qo, co = oracle_lib.run_words(example_key, host, H, Q)
+    src = host
+    if pin_in:
+        src = native.pinned_empty(host.shape, np.uint32)
+        src[:] = host
+    alloc = native.pinned_empty if pin_out else (lambda k, t: np.empty(k, t))
+    out = (alloc(n, np.uint32), alloc(n, np.uint32))
+    out[0].fill(0xDEADBEEF)
+    ctx = native.HostContext(0)
+    key6 = native.prepare_key6(example_key)
+    h, q, c = ctx.hash6(key6, src, H, Q, out=out)
+    assert h is out[0] and q is out[1]
+    for got, want in ((h, ho), (q, qo), (c, co)):
+        np.testing.assert_array_equal(got, want)
+    table = (np.arange(H, dtype=np.uint32) * 7) % 5
+    _, q2, c2 = ctx.hash6(key6, src, H, 5, want_hash=False, reta=table)
+    np.testing.assert_array_equal(q2, table[ho % H])
+    np.testing.assert_array_equal(c2, np.bincount(table[ho % H], minlength=5).astype(np.uint64))
+    ctx.close()
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 255, 16383, 16384, 16385, 70001])
+def test_host_small_batches_and_switch(native, oracle_lib, example_key, n):
+    """Batches around the small-batch switch (16384 tuples: the kernel reads the mapped
+    staging in place) and one past it, IPv4 and IPv6 calls alternating on one context so
+    each grows and reuses the other's staging."""
+    ctx = native.HostContext(0)
+    key6, key4 = native.prepare_key6(example_key), native.prepare_key(example_key)
+    w6 = _words(n + 1, n)
+    w4 = oracle_lib.generate(n + 2, 0, n)
+    for _ in range(2):
+        h, q, c = ctx.hash6(key6, w6, 100, 7)
+        ho, qo, co = oracle_lib.run_words(example_key, w6, 100, 7)
+        for got, want in ((h, ho), (q, qo), (c, co)):
+            np.testing.assert_array_equal(got, want)
+        h, q, c = ctx.hash(key4, w4, 100, 7)
+        ho, qo, co = oracle_lib.run(example_key, w4, 100, 7)
+        for got, want in ((h, ho), (q, qo), (c, co)):
+            np.testing.assert_array_equal(got, want)
+    ctx.close()
+
+
+def test_compute_queues6_one_tuple_per_call(native, oracle_lib, example_key):
+    """The reference-style per-row use of compute_queues6: single tuples on the small path,
+    one call each, against the oracle (per-call time: tools/host6_probe.py)."""
+    from rss_simulator_nvidia_amd.toeplitz import Toeplitz
+    tz = Toeplitz(example_key)
+    w = _words(9, 300)
+    ho, qo, _ = oracle_lib.run_words(example_key, w, 128, 24)
+    for i in range(len(w)):
+        h, q, c = tz.compute_queues6(w[i:i + 1], 128, 24)
+        assert int(h[0]) == int(ho[i]) and int(q[0]) == int(qo[i]) and int(c.sum()) == 1
