@@ -1,6 +1,6 @@
 """rss_hash_host on page-locked buffers: the direct-DMA pipeline (no staging copies)
 must give exactly what the staged pipeline and the oracle give, for every mix of
-pinned / pageable input and outputs, over several 4M-tuple chunks with a ragged tail; and a call whose launch fails part-way
+pinned / pageable input and outputs, over several chunks with a ragged tail; and a call whose launch fails part-way
 leaves nothing in flight."""
 import time
 
@@ -28,7 +28,10 @@ def ctx(native):
     return native.HostContext(0)
 
 
-N = (9 << 20) + 5  # three chunks of the 4M-tuple pipeline, the last one ragged
+N = (9 << 20) + 5  # four chunks of the pipeline, the last one ragged
+# the pipeline's chunk for N (rss_host.hip, hash_host_pipeline): a quarter of the batch in
+# 64K-tuple steps, between 256K tuples and the 48 MB slot (4M IPv4 tuples)
+CHUNK = min(4 << 20, max(1 << 18, (-(-N // 4) + 65535) // 65536 * 65536))
 
 
 @pytest.fixture(scope="module")
@@ -129,7 +132,7 @@ def test_multi_context_small_and_ragged(native, oracle_lib, example_key, n):
 @pytest.mark.parametrize("pinned", [True, False])
 def test_failed_chunk_leaves_nothing_in_flight(native, example_key, expected, fail_at, pinned):
     """A launch that fails part-way through a host call (hooks fail_launch: the first, second
-    or third 4M-tuple chunk) reports the error, and the call has waited out the earlier
+    or third chunk) reports the error, and the call has waited out the earlier
     chunks' copies before returning: the caller's page-locked outputs stop changing the
     moment it returns, and the next call on the same context gives the oracle's results."""
     tup, ho, qo, co = expected
@@ -148,8 +151,10 @@ def test_failed_chunk_leaves_nothing_in_flight(native, example_key, expected, fa
         snap = out[0].copy()
         time.sleep(0.05)
         np.testing.assert_array_equal(out[0], snap)
-        if pinned and fail_at > 1:  # chunks before the failed one were written directly
-            np.testing.assert_array_equal(out[0][:4 << 20], ho[:4 << 20])
+        if pinned:  # chunks before the failed one were written directly, none after
+            done = CHUNK * (fail_at - 1)
+            np.testing.assert_array_equal(out[0][:done], ho[:done])
+            assert (out[0][done:] == 0xDEADBEEF).all()
         h, q, c = hctx.hash(key, src, 128, 24, out=out)
         np.testing.assert_array_equal(h, ho)
         np.testing.assert_array_equal(q, qo)
