@@ -542,24 +542,25 @@ class MultiHostContext:
         return h, q, c
 
     def hash6(self, key6, tuples6, htable, nqueues, want_hash=True, want_queue=True,
-              want_counts=True, reta=None):
+              want_counts=True, reta=None, out=None):
         """IPv6 counterpart of :meth:`hash`: the same contiguous ranges as
         ``rss_hash_host_multi`` (``sharding.shard_range``), one host thread per context
-        (ctypes releases the GIL), counts summed here."""
-        arr = np.ascontiguousarray(tuples6)
-        if arr.dtype != TUPLE6_DTYPE:
-            arr = np.ascontiguousarray(arr, dtype=np.uint32).reshape(-1, 9)
-        n, k = len(arr), len(self.contexts)
+        (ctypes releases the GIL) writing its range of the outputs in place (``out`` as for
+        :meth:`hash`), counts summed here."""
+        qn = queue_modulus(htable, nqueues, reta is not None)[1]
+        arr, n, h, q, _ = _host_batch(tuples6, qn, want_hash, want_queue, False, out, ipv6=True)
+        k = len(self.contexts)
         base, extra = divmod(n, k)
         bounds = [base * i + min(i, extra) for i in range(k + 1)]
-        parts = [None] * k
+        counts = [None] * k
         errors = []
 
         def work(i):
+            a, b = bounds[i], bounds[i + 1]
             try:
-                parts[i] = self.contexts[i].hash6(key6, arr[bounds[i]:bounds[i + 1]], htable,
-                                                  nqueues, want_hash, want_queue, want_counts,
-                                                  reta)
+                part = (None if h is None else h[a:b], None if q is None else q[a:b])
+                counts[i] = self.contexts[i].hash6(key6, arr[a:b], htable, nqueues, want_hash,
+                                                   want_queue, want_counts, reta, out=part)[2]
             except Exception as err:  # re-raised on the calling thread
                 errors.append(err)
 
@@ -571,9 +572,7 @@ class MultiHostContext:
             w.join()
         if errors:
             raise errors[0]
-        h = np.concatenate([p[0] for p in parts]) if want_hash else None
-        q = np.concatenate([p[1] for p in parts]) if want_queue else None
-        c = np.sum([p[2] for p in parts], axis=0, dtype=np.uint64) if want_counts else None
+        c = np.sum(counts, axis=0, dtype=np.uint64) if want_counts else None
         return h, q, c
 
 

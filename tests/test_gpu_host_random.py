@@ -2,9 +2,9 @@
 and their ``_reta`` forms) against the C oracle: per seed a batch size anywhere from 0 to 6M
 tuples (so every path -- empty, the small-batch path, one chunk, two to many pipeline chunks
 with a ragged tail -- and the chunk rule's edges come up), IPv4 or IPv6, a random (H, Q) or an
-indirection table, page-locked or pageable tuples and outputs, any subset of the outputs,
-accumulation onto given counts, and one context reused across the seeds (its staging grows
-and is reused in every order).  ``RSS_HOST_SWEEP_CASES`` / ``RSS_HOST_SWEEP_SEED0`` widen it."""
+indirection table, page-locked or pageable tuples and outputs, any subset of the outputs, one
+context reused across the seeds (its staging grows and is reused in every order) or two /
+three contexts splitting the batch (``MultiHostContext``).  ``RSS_HOST_SWEEP_CASES`` / ``RSS_HOST_SWEEP_SEED0`` widen it."""
 import os
 
 import numpy as np
@@ -33,6 +33,15 @@ def ctx(native):
     c.close()
 
 
+@pytest.fixture(scope="module")
+def multi(native):
+    """Several contexts on cuda:0 (rss_hash_host_multi / MultiHostContext.hash6 ranges)."""
+    m = {k: native.MultiHostContext([0] * k) for k in (2, 3)}
+    yield m
+    for c in m.values():
+        c.close()
+
+
 def _size(rng):
     kind = rng.integers(0, 6)
     if kind == 0:
@@ -47,7 +56,7 @@ def _size(rng):
 
 
 @pytest.mark.parametrize("seed", range(SEED0, SEED0 + CASES))
-def test_random_host_batch_matches_oracle(native, ctx, oracle_lib, example_key, seed):
+def test_random_host_batch_matches_oracle(native, ctx, multi, oracle_lib, example_key, seed):
     rng = np.random.default_rng(0x4057 + seed)
     n = _size(rng)
     ipv6 = bool(rng.integers(0, 2))
@@ -78,7 +87,9 @@ def test_random_host_batch_matches_oracle(native, ctx, oracle_lib, example_key, 
         out = (native.pinned_empty(n, np.uint32) if want_hash else None,
                native.pinned_empty(n, np.uint32) if want_queue else None)
     key = native.prepare_key6(example_key) if ipv6 else native.prepare_key(example_key)
-    call = ctx.hash6 if ipv6 else ctx.hash
+    nctx = int(rng.choice([1, 1, 2, 3]))
+    target = ctx if nctx == 1 else multi[nctx]
+    call = target.hash6 if ipv6 else target.hash
     h, q, c = call(key, src, H, Q, want_hash=want_hash, want_queue=want_queue,
                    want_counts=want_counts, reta=table, out=out)
     if want_hash:

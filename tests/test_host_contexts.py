@@ -1,6 +1,6 @@
 """Host-side logic of the multi-GPU option of the reference API (CPU, no device): the
 IPv6 split of ``MultiHostContext.hash6`` (the contiguous ranges of ``rss_hash_host_multi``
-/ ``sharding.shard_range``, outputs concatenated in order, counts summed, a worker's error
+/ ``sharding.shard_range``, each range written in place, counts summed, a worker's error
 re-raised on the caller), ``host_context``'s routing and caching, and the ``devices=``
 plumbing of ``Simulator`` / ``Toeplitz``.  The device results are checked against the
 oracle in ``tests/test_gpu_concurrency.py``."""
@@ -21,15 +21,21 @@ class _FakeCtx:
         self.threads = set()
 
     def hash6(self, key6, arr, htable, nqueues, want_hash=True, want_queue=True,
-              want_counts=True, reta=None):
+              want_counts=True, reta=None, out=None):
         self.threads.add(threading.get_ident())
         if self.fail:
             raise _native.DeviceError("boom")
         self.calls.append(len(arr))
         h = arr.view(np.uint32).reshape(len(arr), 9).astype(np.uint64).sum(axis=1).astype(np.uint32)
         q = h % nqueues
-        return (h if want_hash else None, q if want_queue else None,
-                np.bincount(q, minlength=nqueues).astype(np.uint64) if want_counts else None)
+        counts = np.bincount(q, minlength=nqueues).astype(np.uint64) if want_counts else None
+        if out is not None:  # written in place, like HostContext.hash6
+            for dst, src in zip(out, (h, q)):
+                if dst is not None:
+                    assert dst.shape == src.shape and dst.flags.c_contiguous
+                    dst[:] = src
+            return out[0], out[1], counts
+        return h if want_hash else None, q if want_queue else None, counts
 
 
 def _multi(ctxs):
